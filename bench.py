@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""Benchmark: FasterRCNN_R50_FPN forward+loss img/s (BASELINE.json metric, config 2).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One process per GPU, 2 images per GPU (imgs_per_gpu=2), synthetic 600x1000
+images padded to 608x1024, VOC ground-truth boxes (tests/golden/voc_gts.npz),
+random-init weights.  A step = CascadeRCNN(1 stage).forward_train on the
+GPU's batch: backbone+FPN+RPN convs (PyTorch-ROCm), then the HIP detection
+path (anchor targets, proposals+NMS, RCNN targets, RoIAlign) and the losses.
+Images are independent units: ranks share nothing on the data path
+("scaling": "weak"); the forward+loss metric has no collective.
+
+The JSON line carries the RoIAlign forward roofline (HIP events around every
+launch in the timed region, algorithmic bytes per SURVEY §8(d)) and a CPU
+baseline: the same forward+loss on the host, with the hot path run by the
+oracle's C restatement (oracle/pipeline.py), on a bounded 1-image sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'pytorch-faster-rcnn_amd'))
+sys.path.insert(0, os.path.join(REPO, 'tests', 'golden'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIG = os.path.join(REPO, 'pytorch-faster-rcnn_amd', 'configs', 'faster_rcnn_r50_fpn.py')
+IMG_SHAPE, PAD_SHAPE = (600, 1000), (608, 1024)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def img_meta():
+    return {'img_shape': IMG_SHAPE + (3,), 'pad_shape': PAD_SHAPE + (3,), 'scale_factor': 1.6,
+            'ori_shape': (375, 625, 3)}
+
+
+def voc_gts():
+    z = np.load(os.path.join(REPO, 'tests', 'golden', 'voc_gts.npz'))
+    return [(z['boxes_{}'.format(i)], z['labels_{}'.format(i)]) for i in range(int(z['n']))]
+
+
+def make_batch(dev, batch, seed, rank=0):
+    g = torch.Generator(device='cpu').manual_seed(seed + 1000 * rank)
+    imgs = torch.randn(batch, 3, PAD_SHAPE[0], PAD_SHAPE[1], generator=g).to(dev)
+    gts = voc_gts()
+    sel = [gts[(rank * batch + i) % len(gts)] for i in range(batch)]
+    boxes = [torch.from_numpy(b).to(dev) for b, _ in sel]
+    labels = [torch.from_numpy(l).to(dev) for _, l in sel]
+    return imgs, boxes, labels, [img_meta() for _ in range(batch)]
+
+
+def make_model(dev, seed=0, config=CONFIG):
+    from frcnn_amd.config import Config
+    from frcnn_amd.builder import build_module
+    cfg = Config.fromfile(config)
+    torch.manual_seed(seed)
+    model = build_module(cfg.model, train_cfg=cfg.train_cfg, test_cfg=cfg.test_cfg)
+    model.init_weights()
+    model.train()
+    return model.to(dev), cfg
+
+
+def make_model_and_batch(dev, batch=2, seed=0, rank=0):
+    model, _ = make_model(dev, seed)
+    return model, make_batch(dev, batch, seed, rank)
+
+
+def roi_align_bytes(rec):
+    """Algorithmic bytes of one RoIAlign forward launch:
+    4*C*(sum_K ph*pw + sum_img sum_{levels with >=1 roi} H_l*W_l) + 20*K."""
+    _, _, rois, levels, shapes, (ph, pw) = rec
+    K = rois.shape[0]
+    C = shapes[0][1]
+    bidx = rois[:, 0].long()
+    lv = levels if levels is not None else torch.zeros_like(bidx)
+    used = torch.unique(bidx * 64 + lv).cpu().tolist()
+    feat_elems = sum(shapes[u % 64][2] * shapes[u % 64][3] for u in used)
+    return 4 * C * (K * ph * pw + feat_elems) + 20 * K
+
+
+def cpu_baseline(seed, max_s):
+    """Same forward+loss on the host: torch CPU convs + the oracle's C hot path, 1 image."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import pipeline  # oracle/pipeline.py (test infrastructure)
+    threads = torch.get_num_threads()
+    model, cfg = make_model(torch.device('cpu'), seed)
+    imgs, boxes, labels, metas = make_batch(torch.device('cpu'), 1, seed)
+    t0 = time.time()
+    n = 0
+    while True:
+        pipeline.forward_train_cpu(model, cfg, imgs, boxes, labels, metas)
+        n += 1
+        if time.time() - t0 > max_s or n >= 3:
+            break
+    dt = time.time() - t0
+    return {'value': n / dt, 'unit': 'img/s', 'cores': threads, 'kind': 'port',
+            'sample': '{} x 1-image forward+loss of the cfg2 model on CPU (torch CPU convs + oracle C hot path, '
+                      '{} threads)'.format(n, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=2, help='images per GPU (imgs_per_gpu=2 in cfg2)')
+    ap.add_argument('--sampler', default='device', choices=['device', 'numpy'])
+    ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    import frcnn_amd
+    from frcnn_amd import ops
+    frcnn_amd.set_sampler_mode(args.sampler, seed=1234 + rank)
+    np.random.seed(rank)
+
+    model, cfg = make_model(dev, seed=0)
+    batch = make_batch(dev, args.batch, seed=0, rank=rank)
+
+    def step():
+        losses = model.forward_train(*batch)
+        return sum(losses.values())
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    ops.ROI_ALIGN_PROFILE['records'].clear()
+    ops.ROI_ALIGN_PROFILE['on'] = True
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ops.ROI_ALIGN_PROFILE['on'] = False
+    assert torch.isfinite(loss).all()
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+
+    recs = ops.ROI_ALIGN_PROFILE['records']
+    ms = [r[0].elapsed_time(r[1]) for r in recs]
+    bytes_per = [roi_align_bytes(r) for r in recs]
+    avg_ms = float(np.mean(ms)) if ms else float('nan')
+    avg_bytes = float(np.mean(bytes_per)) if bytes_per else float('nan')
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if ms else None
+
+    traffic = None
+    pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json')
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+
+    if rank == 0:
+        imgs_total = world * args.batch * args.steps
+        out = {
+            'metric': 'img/s FasterRCNN_R50_FPN 1000x600 fwd+loss',
+            'value': imgs_total / t_max,
+            'unit': 'img/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': 1e3 * t_max / args.steps,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic images N(0,1) [B,3,608,1024], VOC07 trainval gt boxes, random-init weights',
+            'config': {'workload': 'configs/faster_rcnn_r50_fpn.py (BASELINE config 2) forward_train',
+                       'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
+                       'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
+                       'sampler': args.sampler},
+            'roofline': {'kernel': 'roi_align_fwd_kernel', 'bound': 'hbm',
+                         'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': traffic,
+                         'avg_launch_us': avg_ms * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,
+                         'launches': len(ms)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out['cpu_baseline'] = cpu_baseline(0, args.cpu_baseline_seconds)
+            except Exception as e:  # the baseline must never hide the GPU number
+                out['cpu_baseline'] = {'value': None, 'error': repr(e)[:200]}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,269 @@
+/*
+ * frcnn_amd.h — C-ABI of the MI355X (gfx950) Faster R-CNN detection hot path.
+ *
+ * Every entry point replaces one function/type of the reference
+ * (pengfeidip/pytorch-faster-rcnn, cited as path:line) or of the third-party
+ * torchvision kernels the reference calls.  Conventions:
+ *   - plain device pointers + sizes; no framework types.  Boxes are
+ *     coordinate-major "[4, n]" float32 (row k = coordinate k, row stride `ld`
+ *     elements), exactly the reference's channel-first layout, unless a
+ *     parameter says "[n,4]" (row-major xyxy, torchvision layout).
+ *   - `stream` is a hipStream_t; every call is asynchronous on it and never
+ *     synchronises, allocates or frees (capturable into a hipGraph).
+ *   - scratch memory comes from the caller through (workspace, ws_bytes);
+ *     each op has a *_workspace() size query.  The library keeps no global
+ *     mutable state: reentrant and thread-safe per stream.
+ *   - variable-size results are written into caller-sized maxima plus a
+ *     device-side int32 count.
+ *   - return 0 on success, a negative FRH_E* code otherwise;
+ *     frh_last_error() gives a thread-local message.
+ */
+#ifndef FRCNN_AMD_H
+#define FRCNN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRH_ABI_VERSION 1
+
+#define FRH_OK 0
+#define FRH_EINVAL (-1)
+#define FRH_EUNSUPPORTED (-2)
+#define FRH_ELAUNCH (-3)
+
+#define FRH_MAX_LEVELS 8
+
+int32_t frh_abi_version(void);
+const char* frh_last_error(void);
+
+/* ---- a1: AnchorCreator.__call__ over all FPN levels in one launch ------------
+ * Replaces lib/anchor.py:107-129 (called per level from
+ * lib/heads/anchor_head.py:66-67).  Level l has grid (grid_hw[2l], grid_hw[2l+1]),
+ * stride strides[l] and per-anchor sizes ws/hs[l*num_anchors + a] (the f32
+ * casts of the reference's float64 base*s*sqrt(ar), anchor.py:92-97).
+ * Output: [4, ld] with level l occupying columns [off_l, off_l + A*H*W) in
+ * the reference's [4, A, H, W].view(4,-1) order, off_l = sum of earlier levels. */
+int32_t frh_anchor_grid(int32_t num_levels, const int32_t* grid_hw, const float* strides,
+                        const float* ws, const float* hs, int32_t num_anchors,
+                        int32_t center_lt, float* out, int64_t ld, void* stream);
+
+/* ---- a2: inside_anchor_mask & inside_grid_mask --------------------------------
+ * Replaces lib/region.py:10-29 as combined in lib/heads/anchor_head.py:93-99.
+ * in_hw[2l..] = min(grid, int(img/stride)+1) computed by the caller in double
+ * exactly as region.py:12-13.  allowed_border < 0 disables the image test. */
+int32_t frh_inside_mask(const float* anchors, int64_t ld, int32_t num_levels,
+                        const int32_t* grid_hw, const int32_t* in_hw, int32_t num_anchors,
+                        int32_t img_h, int32_t img_w, int32_t allowed_border,
+                        uint8_t* mask, void* stream);
+
+/* ---- a3: calc_iou / elem_iou ----------------------------------------------------
+ * calc_iou: lib/utils.py:151-172 -> out[n, k] (row-major), bit-exact.
+ * elem_iou: lib/utils.py:174-182 (no +1) -> out[n]. */
+int32_t frh_iou_table(const float* a, int64_t lda, int64_t n, const float* b, int64_t ldb,
+                      int64_t k, float* out, void* stream);
+int32_t frh_elem_iou(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n,
+                     float* out, void* stream);
+
+/* ---- a4: MaxIoUAssigner.__call__, batched over segments (images) -------------
+ * Replaces lib/region.py:60-107.  Segment s: boxes at boxes + s*box_seg_stride
+ * ([4, box_ld]), count num_boxes[s] (device), optional validity mask
+ * valid + s*valid_seg_stride (nullptr = all valid; invalid boxes get label -1
+ * and take no part in the per-gt maxima), gts at gts + s*gt_seg_stride
+ * ([4, gt_ld]), count num_gts[s] (device).  Labels are int64:
+ * -1 ignore, 0 negative, g+1 positive for gt g; max_iou f32.  Thresholds are
+ * compared in f32 like the reference (`f32 tensor < python float`).
+ * max_boxes / max_gts bound the launch (host-known maxima of the counts). */
+size_t frh_maxiou_assign_workspace(int32_t num_segs, int32_t max_gts);
+int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
+                          int64_t box_seg_stride, const int32_t* num_boxes,
+                          const uint8_t* valid, int64_t valid_seg_stride,
+                          const float* gts, int64_t gt_ld, int64_t gt_seg_stride,
+                          const int32_t* num_gts, float pos_iou, float neg_iou,
+                          float min_pos_iou, int64_t* labels, int64_t label_seg_stride,
+                          float* max_iou, int64_t iou_seg_stride, int64_t max_boxes,
+                          int32_t max_gts, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a5: RandomSampler / random_sample_label ----------------------------------
+ * Replaces lib/region.py:43-57,112-126.  Two modes:
+ *  (1) reference-RNG parity: frh_sample_candidates lists, per segment and in
+ *      ascending box order, the positive (label>0) and negative (label==0)
+ *      boxes plus their counts ([S,2] device int32).  The host draws the
+ *      reference's numpy permutation, then frh_sample_apply keeps the chosen
+ *      list positions (keep_pos/keep_neg [S, keep_ld] device, counts in
+ *      keep_counts [S,2]) and writes labels_out (-1 for everything else).
+ *  (2) device RNG: frh_sample_random keeps min(npos,pos_num) positives and
+ *      min(nneg, max_num-kept_pos) negatives, each chosen uniformly without
+ *      replacement by the smallest 32-bit hash(seed, seg, box) keys. */
+size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes);
+int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
+                              const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
+                              int32_t* neg_list, int64_t list_seg_stride, int32_t* counts,
+                              void* workspace, size_t ws_bytes, void* stream);
+int32_t frh_sample_apply(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
+                         const int32_t* num_boxes, int64_t max_boxes, const int32_t* pos_list,
+                         const int32_t* neg_list, int64_t list_seg_stride,
+                         const int32_t* keep_pos, const int32_t* keep_neg, int64_t keep_ld,
+                         const int32_t* keep_counts, int64_t* labels_out, void* stream);
+int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
+                          const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
+                          int32_t pos_num, uint64_t seed, int64_t* labels_out,
+                          void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a6: anchor_target (lib/anchor.py:11-76) after assign+sample -------------
+ * Chosen = boxes with sampled label >= 0, ascending.  Segment outputs are
+ * concatenated in segment order (the reference's per-image results followed
+ * by torch.cat in anchor_head.py:189-192); out_counts[s] = chosen count of s,
+ * out_counts[num_segs] = total.  Outputs (column j of the concatenation):
+ *   chosen_idx[j] (int64, index into the per-segment box space),
+ *   seg_of[j] (int32), tar_labels[j] (int64: gt_label[g] or 0 for negatives;
+ *   gt_label == nullptr => 1/0), tar_anchors/tar_bbox/tar_param [4, out_ld].
+ * tar_param = (bbox2param(anchor, gt) - means) / stds (anchor.py:69-73). */
+int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
+                          const int32_t* num_boxes, int64_t max_boxes, const float* anchors,
+                          int64_t anchor_ld, int64_t anchor_seg_stride, const float* gts,
+                          int64_t gt_ld, int64_t gt_seg_stride, const int64_t* gt_labels,
+                          int64_t gt_label_seg_stride, const float* means, const float* stds,
+                          int64_t max_out_per_seg, int64_t* chosen_idx, int32_t* seg_of,
+                          int64_t* tar_labels, float* tar_anchors, float* tar_bbox,
+                          float* tar_param, int64_t out_ld, int32_t* out_counts,
+                          void* workspace, size_t ws_bytes, void* stream);
+size_t frh_anchor_target_workspace(int32_t num_segs, int64_t max_boxes);
+
+/* gather of per-level head outputs at chosen anchors (anchor.py:51-56) and its
+ * adjoint (autograd backward).  Level l tensor: [B, C*A, H, W] contiguous
+ * viewed per image as [C, A*H*W] (anchor_head.py:82); level_off[l] = first
+ * flat index of the level.  out: [C, out_ld]. */
+int32_t frh_gather_level_outputs(int32_t num_levels, const float* const* level_ptrs,
+                                 const int64_t* level_off, const int64_t* level_hw_a,
+                                 int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                 const int32_t* seg_of, float* out, int64_t out_ld,
+                                 void* stream);
+int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
+                                const int64_t* level_off, const int64_t* level_hw_a,
+                                int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                const int32_t* seg_of, const float* grad, int64_t grad_ld,
+                                void* stream);
+
+/* ---- a12: bbox_target (lib/bbox.py:6-82) ------------------------------------
+ * frh_prepend_gt_labels builds the reference's candidate list
+ * [gts ; proposals] (bbox.py:27-29): rows_out[s, j] = j+1 for j < G_s, else
+ * prop_labels[s, j-G_s]; num_rows[s] = G_s + n_s.  After sampling those rows,
+ * frh_bbox_target (labels = the sampled rows, num_rows from the prepend)
+ * gathers the chosen rows (ascending) into concatenated
+ * outputs: tar_props/tar_bbox/tar_param [4, out_ld], tar_label (int64, gt
+ * class or 0), tar_is_gt (int64 0/1), out_counts[S+1] as in frh_anchor_target. */
+int32_t frh_prepend_gt_labels(int32_t num_segs, const int64_t* prop_labels,
+                              int64_t prop_label_seg_stride, const int32_t* num_props,
+                              const int32_t* num_gts, int64_t max_rows, int64_t* rows_out,
+                              int64_t rows_seg_stride, int32_t* num_rows, void* stream);
+size_t frh_bbox_target_workspace(int32_t num_segs, int64_t max_rows);
+int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
+                        const int32_t* num_rows, const int32_t* num_gts, int64_t max_rows,
+                        const float* props, int64_t prop_ld, int64_t prop_seg_stride,
+                        const float* gts, int64_t gt_ld, int64_t gt_seg_stride,
+                        const int64_t* gt_labels, int64_t gt_label_seg_stride,
+                        const float* means, const float* stds, int64_t max_out_per_seg,
+                        float* tar_props, float* tar_bbox, int64_t* tar_label,
+                        float* tar_param, int64_t* tar_is_gt, int64_t out_ld,
+                        int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a7/a8: bbox2param / param2bbox (+clamp_bbox) ----------------------------
+ * lib/utils.py:47-70 and 83-144.  param2bbox handles the batched
+ * [4*ncls, n] layout of batched_param2bbox (utils.py:96-106): class c of
+ * coordinate k is row k*ncls + c, output in the same layout.  clamp != 0
+ * clamps x to [0, img_w-1] and y to [0, img_h-1] (utils.py:109-120). */
+int32_t frh_bbox2param(const float* base, int64_t ldb, const float* bbox, int64_t ldx,
+                       int64_t n, const float* means, const float* stds, float* out,
+                       int64_t ldo, void* stream);
+int32_t frh_param2bbox(const float* base, int64_t ldb, const float* param, int64_t ldp,
+                       int64_t n, int32_t ncls, const float* means, const float* stds,
+                       int32_t clamp, float img_h, float img_w, float* out, int64_t ldo,
+                       void* stream);
+
+/* ---- a9/a10: RPNHead.predict_single_image, all images x levels ----------------
+ * lib/heads/rpn_head.py:68-120 with torchvision.ops.nms semantics.  Per
+ * (image, level): score = sigmoid(cls) (use_sigmoid) or softmax(cls)[1];
+ * top pre_nms by (score desc, index asc); decode+clamp (param2bbox); drop
+ * boxes with w+1 < min_size or h+1 < min_size when min_size > 0; greedy NMS
+ * (IoU > nms_iou in double); first post_nms.  Then per image the levels are
+ * concatenated and, if more than max_num survive, the max_num best are kept
+ * in (score desc, concat order) order.  cls level l: [B, C*A, H_l, W_l],
+ * reg level l: [B, 4*A, H_l, W_l]; anchors [4, anchor_ld] from
+ * frh_anchor_grid.  img_hw / min_size are host arrays [B*2] / [B].
+ * Outputs: boxes [B, 4, max_num], scores [B, max_num], counts [B] (device). */
+size_t frh_rpn_proposals_workspace(int32_t num_imgs, int32_t num_levels,
+                                   const int32_t* grid_hw, int32_t num_anchors,
+                                   int32_t pre_nms);
+int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                          const float* const* reg_ptrs, const int32_t* grid_hw,
+                          int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                          int64_t anchor_ld, const float* means, const float* stds,
+                          const float* img_hw, const float* min_size, int32_t pre_nms,
+                          int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                          float* out_scores, int32_t* out_counts, void* workspace,
+                          size_t ws_bytes, void* stream);
+
+/* ---- a10: torchvision.ops.nms on pre-sorted segments --------------------------
+ * boxes [S, n_max, 4] row-major xyxy, already in descending-score order
+ * (stable); count[s] valid rows.  keep[s, :] = kept row positions (ascending
+ * = score order), keep_counts[s].  max_keep >= 0 stops after that many. */
+size_t frh_nms_workspace(int32_t num_segs, int32_t n_max);
+int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride,
+                       const int32_t* counts, int32_t n_max, double iou_thr, int32_t max_keep,
+                       int32_t* keep, int64_t keep_seg_stride, int32_t* keep_counts,
+                       void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- a13/a14: BasicRoIExtractor.map_rois_to_levels + RoIAlign ----------------
+ * level = clamp(floor(log2(sqrt((x2-x1+1)(y2-y1+1))/finest_scale + 1e-6)),
+ * 0, L-1) (lib/region.py:256-264).  rois [K,5] = (batch_idx, x1, y1, x2, y2)
+ * (torchvision convention).  roi_levels == nullptr => every roi on level 0.
+ * RoIAlign = torchvision legacy aligned=False semantics (lib/builder.py:9,
+ * used at lib/region.py:250-276); feats[l] is [B, C, H_l, W_l] NCHW
+ * (layout 0) or NHWC (layout 1, i.e. channels_last strides); out [K, C, ph, pw]. */
+int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float finest_scale,
+                          int32_t num_levels, int64_t* levels, void* stream);
+int32_t frh_roi_align_fwd(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                          const float* scales, int32_t batch, int32_t channels, int32_t layout,
+                          const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                          int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                          int32_t aligned, float* out, void* stream);
+int32_t frh_roi_align_bwd(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
+                          const float* scales, int32_t batch, int32_t channels, int32_t layout,
+                          const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                          int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                          int32_t aligned, const float* grad_out, void* stream);
+/* Same ops with explicit per-level element strides strides[4l..4l+3] =
+ * (batch, channel, y, x): any dense or strided feature view (NCHW,
+ * channels_last, the FPN's P5[..., ::2, ::2] extra level). */
+int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
+                                  const int32_t* feat_hw, const int64_t* strides,
+                                  const float* scales, int32_t batch, int32_t channels,
+                                  const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                  int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                                  int32_t aligned, float* out, void* stream);
+int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
+                                  const int32_t* feat_hw, const int64_t* strides,
+                                  const float* scales, int32_t batch, int32_t channels,
+                                  const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                  int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                                  int32_t aligned, const float* grad_out, void* stream);
+
+/* ---- RoIPool (torchvision.ops.RoIPool; C4 config configs/faster_rcnn_r50.py:26) --
+ * feat [B, C, H, W] with element strides strides[0..3] = (b, c, y, x); rois
+ * [K, 5]; out [K, C, ph, pw] + int32 argmax (flat y*W+x, -1 for empty bins). */
+int32_t frh_roi_pool_fwd(const float* feat, const int64_t* strides, int32_t height, int32_t width,
+                         int32_t channels, float spatial_scale, const float* rois, int64_t num_rois,
+                         int32_t pooled_h, int32_t pooled_w, float* out, int32_t* argmax,
+                         void* stream);
+int32_t frh_roi_pool_bwd(float* grad_feat, const int64_t* strides, int32_t height, int32_t width,
+                         int32_t channels, const float* rois, int64_t num_rois, int32_t pooled_h,
+                         int32_t pooled_w, const float* grad_out, const int32_t* argmax, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRCNN_AMD_H */

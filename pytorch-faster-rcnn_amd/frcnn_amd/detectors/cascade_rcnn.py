@@ -1,0 +1,104 @@
+"""CascadeRCNN detector graph (reference lib/detectors/cascade_rcnn.py).
+Faster R-CNN is the 1-stage case.  Same forward_train / forward_test flow;
+every detection primitive underneath runs batched on the HIP kernels."""
+import torch
+from torch import nn
+
+from .. import utils
+
+
+class CascadeRCNN(nn.Module):
+    def __init__(self, num_stages=3, backbone=None, neck=None, rpn_head=None, roi_extractor=None, shared_head=None,
+                 rcnn_head=None, train_cfg=None, test_cfg=None):
+        super().__init__()
+        from ..builder import build_module
+        if num_stages <= 0:
+            raise AssertionError('num_stages must be positive')
+        self.num_stages = num_stages
+        self.backbone = build_module(backbone)
+        self.with_neck = neck is not None
+        if self.with_neck:
+            self.neck = nn.Sequential(*[build_module(c) for c in neck]) if isinstance(neck, list) else \
+                build_module(neck)
+        self.rpn_head = build_module(rpn_head)
+        cfgs = roi_extractor if isinstance(roi_extractor, list) else [roi_extractor] * num_stages
+        if len(cfgs) < num_stages:
+            raise AssertionError('not enough roi extractors')
+        self.roi_extractors = nn.ModuleList([build_module(cfgs[i]) for i in range(num_stages)])
+        self.with_shared_head = shared_head is not None
+        if self.with_shared_head:
+            self.shared_head = build_module(shared_head)
+        if isinstance(rcnn_head, list):
+            if len(rcnn_head) < num_stages:
+                raise AssertionError('not enough rcnn heads')
+            heads = [build_module(rcnn_head[i]) for i in range(num_stages)]
+        else:
+            if num_stages != 1:
+                raise AssertionError('rcnn_head must be consistent with num_stages')
+            heads = [build_module(rcnn_head)]
+        self.rcnn_head = nn.ModuleList(heads)
+        self.train_cfg = train_cfg
+        self.test_cfg = test_cfg
+
+    def init_weights(self):
+        self.backbone.init_weights()
+        self.rpn_head.init_weights()
+        if self.with_neck:
+            for nk in (self.neck if isinstance(self.neck, nn.Sequential) else [self.neck]):
+                nk.init_weights()
+        for h in self.rcnn_head:
+            h.init_weights()
+        if self.with_shared_head:
+            self.shared_head.init_weights()
+
+    def extract_feat(self, x):
+        x = self.backbone(x)
+        return self.neck(x) if self.with_neck else x
+
+    def forward_train(self, img_data, gt_bboxes, gt_labels, img_metas):
+        """cascade_rcnn.py:90-154."""
+        losses = {}
+        feats = self.extract_feat(img_data)
+        cfg = self.train_cfg
+        rpn_gt_labels = [torch.ones_like(g) for g in gt_labels]
+        rpn_cls, rpn_reg = self.rpn_head(feats)
+        l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
+        losses['rpn_cls_loss'] = l_cls
+        losses['rpn_reg_loss'] = l_reg
+        props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
+        for i in range(self.num_stages):
+            head, extractor, scfg = self.rcnn_head[i], self.roi_extractors[i], cfg.rcnn[i]
+            tar_props, tar_bboxes, tar_labels, tar_params, tar_is_gts = head.bbox_targets(
+                props, gt_bboxes, gt_labels, scfg)
+            roi_outs = extractor(feats, tar_props)
+            if self.with_shared_head:
+                raise NotImplementedError('multi-image shared head is not implemented for CascadeRCNN')
+            cls_outs, reg_outs = head(roi_outs)
+            c_loss, r_loss = head.calc_loss(cls_outs, reg_outs, tar_labels, tar_params, scfg)
+            losses['rcnn_{}_cls_loss'.format(i)] = c_loss * cfg.stage_loss_weight[i]
+            losses['rcnn_{}_reg_loss'.format(i)] = r_loss * cfg.stage_loss_weight[i]
+            if i < self.num_stages - 1:
+                with torch.no_grad():
+                    props = head.refine_bboxes(tar_props, tar_labels, reg_outs, tar_is_gts, img_metas)
+        return losses
+
+    def forward_test(self, img_data, img_metas):
+        """cascade_rcnn.py:157-203."""
+        cfg = self.test_cfg
+        feats = self.extract_feat(img_data)
+        props = list(self.rpn_head.predict_bboxes(feats, img_metas, cfg.rpn)[0])
+        img_sizes = [m['img_shape'][:2] for m in img_metas]
+        stage_cls = []
+        for i in range(self.num_stages):
+            head = self.rcnn_head[i]
+            cls_outs, reg_outs = head(self.roi_extractors[i](feats, props))
+            stage_cls.append(list(cls_outs))
+            if i < self.num_stages - 1:
+                labels = [c.argmax(1) for c in cls_outs]
+                if head.use_sigmoid:
+                    labels = [l + 1 for l in labels]
+                props = head.refine_bboxes(props, labels, list(reg_outs), None, img_metas)
+        per_img = utils.unpack_multi_result(stage_cls)
+        mean_cls = [sum(c) / self.num_stages for c in per_img]
+        return utils.unpack_multi_result(utils.multi_apply(self.rcnn_head[-1].predict_bboxes_single_image, props,
+                                                           mean_cls, list(reg_outs), img_sizes, cfg.rcnn))

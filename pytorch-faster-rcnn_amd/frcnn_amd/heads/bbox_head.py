@@ -1,0 +1,93 @@
+"""BBoxHead base (reference lib/heads/bbox_head.py) with batched targets."""
+import logging
+
+import torch
+from torch import nn
+
+from .. import losses, utils
+from ..bbox import bbox_targets_batched
+
+
+class BBoxHead(nn.Module):
+    def __init__(self, num_classes, target_means=(0.0, 0.0, 0.0, 0.0), target_stds=(0.1, 0.1, 0.2, 0.2),
+                 reg_class_agnostic=False, loss_cls=None, loss_bbox=None):
+        super().__init__()
+        from ..builder import build_module
+        self.num_classes = num_classes
+        self.target_means = list(target_means)
+        self.target_stds = list(target_stds)
+        self.reg_class_agnostic = reg_class_agnostic
+        self.loss_cls = build_module(loss_cls) if isinstance(loss_cls, dict) else loss_cls
+        self.loss_bbox = build_module(loss_bbox) if isinstance(loss_bbox, dict) else loss_bbox
+        self.use_sigmoid = loss_cls.get('use_sigmoid', False) if isinstance(loss_cls, dict) else \
+            getattr(self.loss_cls, 'use_sigmoid', False)
+        self.cls_channels = num_classes - 1 if self.use_sigmoid else num_classes
+
+    def bbox_targets(self, img_props, gt_bboxes, gt_labels, train_cfg):
+        """Per image (tar_props, tar_bbox, tar_label, tar_param, tar_is_gt) lists (bbox_head.py:47-52),
+        computed for the whole batch at once."""
+        r = bbox_targets_batched(img_props, gt_bboxes, gt_labels, train_cfg.assigner, train_cfg.sampler,
+                                 tuple(self.target_means), tuple(self.target_stds))
+        return r['tar_props'], r['tar_bbox'], r['tar_label'], r['tar_param'], r['tar_is_gt']
+
+    def calc_loss_all(self, cls_out, reg_out, tar_label, tar_param, train_cfg):
+        """bbox_head.py:56-80."""
+        dev = cls_out.device
+        cls_loss, reg_loss = losses.zero_loss(dev), losses.zero_loss(dev)
+        pos = tar_label > 0
+        n = len(tar_label)
+        avg_factor = pos.sum() if 'sampler' not in train_cfg else n
+        if avg_factor == 0:
+            logging.warning('return zero loss due to zero avg_factor')
+            return cls_loss, reg_loss
+        if tar_label.numel() != 0:
+            cls_loss = self.loss_cls(cls_out, tar_label) / avg_factor
+            if not self.reg_class_agnostic:
+                reg_out = reg_out.view(-1, 4, self.num_classes)
+                reg_out = reg_out[torch.arange(n, device=dev), :, tar_label]
+            if pos.sum() == 0:
+                logging.warning('BBoxHead recieves no positive samples to train')
+            else:
+                reg_loss = self.loss_bbox(reg_out[pos, :], tar_param[:, pos].t()) / avg_factor
+        return cls_loss, reg_loss
+
+    def calc_loss(self, cls_outs, reg_outs, tar_labels, tar_params, train_cfg):
+        flat = getattr(cls_outs, 'flat', None)
+        cls_out = flat[0] if flat is not None else torch.cat(cls_outs, 0)
+        reg_out = flat[1] if flat is not None else torch.cat(reg_outs, 0)
+        return self.calc_loss_all(cls_out, reg_out, torch.cat(tar_labels), torch.cat(tar_params, 1), train_cfg)
+
+    def refine_bboxes(self, props, labels, reg_outs, is_gts=None, img_metas=None):
+        return utils.multi_apply(self.refine_bboxes_single_image, props, labels, reg_outs,
+                                 is_gts if is_gts is not None else [None] * len(props),
+                                 img_metas if img_metas is not None else [None] * len(props))
+
+    def refine_bboxes_single_image(self, props, label, reg_out, is_gt=None, img_meta=None):
+        """bbox_head.py:100-120: decode the predicted deltas of the labelled class, dropping gt rows."""
+        if is_gt is None:
+            is_gt = torch.zeros_like(label)
+        if not (props.shape[1] == reg_out.shape[0] == is_gt.numel()):
+            raise AssertionError('props / reg_out / is_gt size mismatch')
+        n = len(label)
+        if not self.reg_class_agnostic:
+            reg_out = reg_out.view(-1, 4, self.num_classes)[torch.arange(n, device=reg_out.device), :, label]
+        keep = ~is_gt.bool()
+        return utils.param2bbox(props[:, keep], reg_out.t()[:, keep], self.target_means, self.target_stds,
+                                img_meta['img_shape'] if img_meta is not None else None)
+
+    def predict_bboxes_single_image(self, props, cls_out, reg_out, img_size=None, cfg=None):
+        """bbox_head.py:122-146: softmax, per-class decode, multiclass NMS."""
+        with torch.no_grad():
+            if self.use_sigmoid:
+                raise NotImplementedError('Need to be implemented')
+            score = cls_out.softmax(dim=1)
+            preds = utils.batched_param2bbox(props, reg_out.t(), self.target_means, self.target_stds, img_size)
+            preds, score, label = utils.multiclass_nms(preds.t(), score, range(1, self.num_classes), cfg.nms_iou,
+                                                       cfg.min_score, cfg.max_per_img,
+                                                       mode=cfg.get('nms_type', 'official'))
+        return preds.t(), score, label
+
+
+class HeadOutputs(list):
+    """Per-image head outputs plus the unsplit batch tensor (`flat`)."""
+    flat = None

@@ -1,0 +1,114 @@
+"""Detection losses (reference lib/losses.py), PyTorch autograd, sum reductions.
+
+These run after the HIP target kernels; fusing them into the gather kernels
+is SURVEY §8(f-1), the next row after the hot path.  Semantics follow the
+reference, including its quirk that FocalLoss ignores the configured
+alpha/gamma/loss_weight (losses.py:106-109).
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import utils
+
+
+def zero_loss(device):
+    return torch.tensor(0.0, device=device, requires_grad=True)
+
+
+def smooth_l1_loss_v2(x, y, beta):
+    """losses.py:77-83: sum of 0.5 d^2 / beta (d < beta) or d - 0.5 beta."""
+    if beta <= 0 or x.shape != y.shape:
+        raise AssertionError('bad smooth-l1 arguments')
+    d = torch.abs(x - y)
+    small = (d < beta).float()
+    return (small * (d ** 2) / (2 * beta) + (1 - small) * (d - 0.5 * beta)).sum()
+
+
+def sigmoid_focal_loss(pred, target, alpha=0.25, gamma=2.0, fix_alpha=False):
+    """losses.py:33-61: pred [n, C] logits, target [n] in 0..C (0 = background)."""
+    n, c = pred.shape
+    onehot = utils.one_hot_embedding(target, c + 1)[:, 1:].to(pred.dtype)
+    p = pred.sigmoid()
+    pt = p * onehot + (1 - p) * (1 - onehot)
+    w = alpha if fix_alpha else alpha * onehot + (1 - alpha) * (1 - onehot)
+    w = w * (1 - pt).pow(gamma)
+    return (F.binary_cross_entropy_with_logits(pred, onehot, reduction='none') * w).sum()
+
+
+def giou_loss(a, b):
+    """losses.py:13-30: 1 - GIoU on [4, n] boxes (no +1 widths)."""
+    tl = torch.max(a[:2], b[:2])
+    br = torch.min(a[2:], b[2:])
+    area_i = torch.prod(br - tl, dim=0) * (tl < br).all(0).float()
+    area_a = torch.prod(a[2:] - a[:2], dim=0)
+    area_b = torch.prod(b[2:] - b[:2], dim=0)
+    area_u = area_a + area_b - area_i
+    iou = area_i / area_u
+    lo = torch.min(a[:2], b[:2])
+    hi = torch.max(a[2:], b[2:])
+    area_c = torch.prod(hi - lo, dim=0)
+    return 1 - (iou - (area_c - area_u) / area_c)
+
+
+class FocalLoss(nn.Module):
+    def __init__(self, alpha=0.25, gamma=2.0, use_sigmoid=True, loss_weight=1.0):
+        if not use_sigmoid:
+            raise AssertionError('FocalLoss for non sigmoid is not implemented')
+        super().__init__()
+        self.use_sigmoid = True
+        self.alpha, self.gamma, self.loss_weight = 0.25, 2.0, 1.0  # reference ignores the cfg values
+
+    def forward(self, pred, target):
+        return self.loss_weight * sigmoid_focal_loss(pred, target, self.alpha, self.gamma)
+
+
+class SmoothL1Loss(nn.Module):
+    def __init__(self, beta=1.0, loss_weight=1.0):
+        super().__init__()
+        self.beta, self.loss_weight = beta, loss_weight
+
+    def forward(self, x, y):
+        return self.loss_weight * smooth_l1_loss_v2(x, y, self.beta)
+
+
+class CrossEntropyLoss(nn.Module):
+    def __init__(self, use_sigmoid=False, loss_weight=1.0):
+        super().__init__()
+        self.use_sigmoid, self.loss_weight = use_sigmoid, loss_weight
+
+    def forward(self, pred, label):
+        c = pred.shape[1]
+        if self.use_sigmoid:
+            if c == 1:
+                tgt = label.view(-1, 1).float()
+            else:
+                tgt = utils.one_hot_embedding(label, c + 1)[:, 1:].to(pred.dtype)
+            return F.binary_cross_entropy_with_logits(pred, tgt, reduction='none').sum() * self.loss_weight
+        return F.cross_entropy(pred, label, reduction='none').sum() * self.loss_weight
+
+
+class GIoULoss(nn.Module):
+    def __init__(self, loss_weight=1.0):
+        super().__init__()
+        self.loss_weight = loss_weight
+
+    def forward(self, a, b, weight=None, avg_factor=1.0):
+        loss = giou_loss(a, b)
+        if weight is not None:
+            loss = loss * weight
+        return loss.sum() * self.loss_weight / avg_factor
+
+
+class IoULoss(nn.Module):
+    def __init__(self, loss_weight=1.0):
+        super().__init__()
+        self.loss_weight = loss_weight
+
+    def forward(self, a, b, weight=None, avg_factor=None):
+        loss = -utils.elem_iou(a, b).log()
+        if weight is not None:
+            loss = loss * weight
+        if avg_factor is not None:
+            loss = loss / avg_factor
+        return loss.sum() * self.loss_weight

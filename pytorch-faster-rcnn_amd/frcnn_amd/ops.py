@@ -1,0 +1,506 @@
+"""Tensor-level wrappers of the HIP kernels (one function per C-ABI entry).
+
+These take/return torch tensors resident on the HIP device, allocate outputs
+and workspaces with the caching allocator and launch on the current stream.
+The reference-API modules (anchor, region, bbox, utils, heads) are built on
+these.  The torchvision drop-ins the reference imports (`nms`, `roi_align`,
+`RoIAlign`, `RoIPool`) live here too.
+"""
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import call, ptr, stream_of, i32_array, i64_array, f32_array, ptr_array, workspace
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('frcnn_amd: HIP device tensors required (got {})'.format(t.device))
+
+
+def _f32(t):
+    return t if t.dtype == torch.float32 else t.float()
+
+
+# ---------------------------------------------------------------- anchors (a1/a2)
+def anchor_grid(grid_sizes, strides, ws, hs, num_anchors, center_lt, device):
+    """All levels' anchors as one [4, N] tensor (reference AnchorCreator per level, concatenated)."""
+    L = len(grid_sizes)
+    n = sum(num_anchors * int(h) * int(w) for h, w in grid_sizes)
+    out = torch.empty(4, max(n, 1), dtype=torch.float32, device=device)[:, :n]
+    ws_t = torch.tensor(ws, dtype=torch.float32, device=device)
+    hs_t = torch.tensor(hs, dtype=torch.float32, device=device)
+    hw = i32_array([v for g in grid_sizes for v in (int(g[0]), int(g[1]))])
+    call('frh_anchor_grid', L, hw, f32_array(strides), ptr(ws_t), ptr(hs_t), num_anchors,
+         int(bool(center_lt)), ptr(out), out.stride(0), stream_of(out))
+    return out
+
+
+def inside_mask(anchors, grid_sizes, in_sizes, num_anchors, img_h, img_w, allowed_border):
+    _need_cuda(anchors)
+    n = anchors.shape[1]
+    mask = torch.empty(n, dtype=torch.uint8, device=anchors.device)
+    hw = i32_array([v for g in grid_sizes for v in (int(g[0]), int(g[1]))])
+    ihw = i32_array([v for g in in_sizes for v in (int(g[0]), int(g[1]))])
+    call('frh_inside_mask', ptr(anchors), anchors.stride(0), len(grid_sizes), hw, ihw, num_anchors,
+         int(img_h), int(img_w), int(allowed_border), ptr(mask), stream_of(anchors))
+    return mask
+
+
+# ---------------------------------------------------------------- IoU (a3)
+def iou_table(a, b):
+    _need_cuda(a, b)
+    a, b = _f32(a), _f32(b)
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    if b.stride(1) != 1:
+        b = b.contiguous()
+    n, k = a.shape[1], b.shape[1]
+    out = torch.empty(n, k, dtype=torch.float32, device=a.device)
+    call('frh_iou_table', ptr(a), a.stride(0), n, ptr(b), b.stride(0), k, ptr(out), stream_of(a))
+    return out
+
+
+def elem_iou(a, b):
+    _need_cuda(a, b)
+    a, b = _f32(a).contiguous(), _f32(b).contiguous()
+    n = a.shape[1]
+    out = torch.empty(n, dtype=torch.float32, device=a.device)
+    call('frh_elem_iou', ptr(a), a.stride(0), ptr(b), b.stride(0), n, ptr(out), stream_of(a))
+    return out
+
+
+# ---------------------------------------------------------------- packing helpers
+def pack_boxes(box_list, device, min_cols=1):
+    """list of [4, n_i] -> ([S, 4, n_max] f32, counts int32 device, n_max)."""
+    S = len(box_list)
+    nmax = max([int(b.shape[1]) for b in box_list] + [min_cols])
+    out = torch.zeros(S, 4, nmax, dtype=torch.float32, device=device)
+    for s, b in enumerate(box_list):
+        if b.shape[1]:
+            out[s, :, :b.shape[1]] = b
+    counts = torch.tensor([int(b.shape[1]) for b in box_list], dtype=torch.int32, device=device)
+    return out, counts, nmax
+
+
+def pack_labels(label_list, nmax, device):
+    S = len(label_list)
+    out = torch.zeros(S, max(nmax, 1), dtype=torch.int64, device=device)
+    for s, l in enumerate(label_list):
+        if l.numel():
+            out[s, :l.numel()] = l.to(torch.int64)
+    return out
+
+
+# ---------------------------------------------------------------- MaxIoU assignment (a4)
+def maxiou_assign(boxes, box_seg_stride, num_boxes, max_boxes, gts, gt_counts, max_gts, pos_iou, neg_iou,
+                  min_pos_iou, valid=None, valid_seg_stride=0, num_segs=None):
+    """Batched MaxIoUAssigner: boxes [.., 4, ld] (segment stride given), gts [S, 4, Gmax]."""
+    _need_cuda(boxes, gts)
+    S = num_segs if num_segs is not None else gts.shape[0]
+    dev = boxes.device
+    labels = torch.empty(S, max(max_boxes, 1), dtype=torch.int64, device=dev)
+    max_iou = torch.empty(S, max(max_boxes, 1), dtype=torch.float32, device=dev)
+    ws = workspace(_lib.query('frh_maxiou_assign_workspace', S, max(max_gts, 1)), dev)
+    call('frh_maxiou_assign', S, ptr(boxes), boxes.stride(-2), box_seg_stride, ptr(num_boxes),
+         ptr(valid), valid_seg_stride, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_counts),
+         float(pos_iou), float(neg_iou), float(min_pos_iou), ptr(labels), labels.stride(0), ptr(max_iou),
+         max_iou.stride(0), max_boxes, max_gts, ptr(ws), ws.numel(), stream_of(boxes))
+    return labels, max_iou
+
+
+# ---------------------------------------------------------------- sampling (a5)
+_SAMPLER = {'mode': 'numpy', 'seed': 0x5eed, 'calls': 0}
+
+
+def set_sampler_mode(mode, seed=None):
+    """'numpy' = the reference's np.random stream (exact parity, host round trip);
+    'device' = on-device hash RNG (same distribution, no sync)."""
+    if mode not in ('numpy', 'device'):
+        raise ValueError("sampler mode must be 'numpy' or 'device'")
+    _SAMPLER['mode'] = mode
+    if seed is not None:
+        _SAMPLER['seed'] = int(seed)
+        _SAMPLER['calls'] = 0
+
+
+def sampler_mode():
+    return _SAMPLER['mode']
+
+
+def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None):
+    """Batched RandomSampler over labels [S, >=max_boxes] (region.py:43-57,112-126)."""
+    mode = mode or _SAMPLER['mode']
+    S = labels.shape[0]
+    dev = labels.device
+    out = torch.empty_like(labels)
+    if mode == 'device':
+        ws = workspace(_lib.query('frh_sample_workspace', S, max(max_boxes, 1)), dev)
+        _SAMPLER['calls'] += 1
+        seed = (_SAMPLER['seed'] * 0x9E3779B97F4A7C15 + _SAMPLER['calls']) & 0xFFFFFFFFFFFFFFFF
+        call('frh_sample_random', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, int(max_num),
+             int(pos_num), seed, ptr(out), ptr(ws), ws.numel(), stream_of(labels))
+        return out
+    ld = max(max_boxes, 1)
+    pos_list = torch.empty(S, ld, dtype=torch.int32, device=dev)
+    neg_list = torch.empty(S, ld, dtype=torch.int32, device=dev)
+    counts = torch.empty(S, 2, dtype=torch.int32, device=dev)
+    ws = workspace(_lib.query('frh_sample_workspace', S, ld), dev)
+    call('frh_sample_candidates', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, ptr(pos_list),
+         ptr(neg_list), ld, ptr(counts), ptr(ws), ws.numel(), stream_of(labels))
+    cnt = counts.cpu().numpy()  # host round trip, as the reference's .cpu().numpy() (region.py:48,55)
+    keep_ld = max(int(max_num), 1)
+    keep = np.zeros((2, S, keep_ld), dtype=np.int32)
+    kc = np.zeros((S, 2), dtype=np.int32)
+    for s in range(S):
+        npos, nneg = int(cnt[s, 0]), int(cnt[s, 1])
+        kp = _numpy_keep(npos, pos_num)
+        kneg = _numpy_keep(nneg, max_num - min(npos, pos_num))
+        kc[s, 0], kc[s, 1] = len(kp), len(kneg)
+        keep[0, s, :len(kp)] = kp
+        keep[1, s, :len(kneg)] = kneg
+    keep_t = torch.from_numpy(keep).to(dev, non_blocking=False)
+    kc_t = torch.from_numpy(kc).to(dev)
+    call('frh_sample_apply', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, ptr(pos_list),
+         ptr(neg_list), ld, ptr(keep_t[0]), ptr(keep_t[1]), keep_ld, ptr(kc_t), ptr(out), stream_of(labels))
+    return out
+
+
+def _numpy_keep(n, cap):
+    """Positions kept by `np.random.choice(cands, n - cap, replace=False)` discarding.
+
+    numpy's legacy choice(replace=False) is permutation(n)[:size]; the kept
+    positions are the rest of that permutation, and the global RNG advances
+    exactly as in the reference."""
+    if n <= cap:
+        return np.arange(n, dtype=np.int32)
+    perm = np.random.permutation(n)
+    return np.sort(perm[n - cap:]).astype(np.int32)
+
+
+# ---------------------------------------------------------------- target gathers (a6/a12)
+def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, max_out_per_seg):
+    S = labels.shape[0]
+    dev = labels.device
+    cap = max(int(max_out_per_seg), 1)
+    T = S * cap
+    chosen_idx = torch.empty(T, dtype=torch.int64, device=dev)
+    seg_of = torch.empty(T, dtype=torch.int32, device=dev)
+    tar_labels = torch.empty(T, dtype=torch.int64, device=dev)
+    tars = torch.empty(3, 4, T, dtype=torch.float32, device=dev)
+    counts = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    ws = workspace(_lib.query('frh_anchor_target_workspace', S, max(max_boxes, 1)), dev)
+    m = f32_array(means) if means is not None else None
+    sd = f32_array(stds) if stds is not None else None
+    call('frh_anchor_target', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, ptr(anchors),
+         anchors.stride(0), 0, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_labels),
+         gt_labels.stride(0) if gt_labels is not None else 0, m, sd, cap, ptr(chosen_idx), ptr(seg_of),
+         ptr(tar_labels), ptr(tars[0]), ptr(tars[1]), ptr(tars[2]), T, ptr(counts), ptr(ws), ws.numel(),
+         stream_of(labels))
+    cnt = counts.cpu().tolist()  # output sizes are data dependent: one sync per batch
+    n = cnt[S]
+    return dict(chosen_idx=chosen_idx[:n], seg_of=seg_of[:n], tar_labels=tar_labels[:n],
+                tar_anchors=tars[0][:, :n], tar_bbox=tars[1][:, :n], tar_param=tars[2][:, :n], counts=cnt[:S])
+
+
+class _GatherLevels(torch.autograd.Function):
+    """tar = cat_l(level_out.view(C, -1))[:, chosen] per image, with its adjoint scatter."""
+
+    @staticmethod
+    def forward(ctx, chosen_idx, seg_of, channels, *levels):
+        levels = [l.contiguous() for l in levels]
+        n = chosen_idx.numel()
+        offs, hwa = _level_offsets(levels, channels)
+        out = torch.empty(channels, n, dtype=torch.float32, device=chosen_idx.device)
+        if n:
+            call('frh_gather_level_outputs', len(levels), ptr_array(levels), i64_array(offs), i64_array(hwa),
+                 channels, n, ptr(chosen_idx), ptr(seg_of), ptr(out), out.stride(0), stream_of(out))
+        ctx.save_for_backward(chosen_idx, seg_of)
+        ctx.shapes = [l.shape for l in levels]
+        ctx.channels = channels
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        chosen_idx, seg_of = ctx.saved_tensors
+        grads = [torch.zeros(s, dtype=torch.float32, device=grad.device) for s in ctx.shapes]
+        grad = grad.contiguous()
+        n = chosen_idx.numel()
+        offs, hwa = _level_offsets(grads, ctx.channels)
+        if n:
+            call('frh_scatter_level_grads', len(grads), ptr_array(grads), i64_array(offs), i64_array(hwa),
+                 ctx.channels, n, ptr(chosen_idx), ptr(seg_of), ptr(grad), grad.stride(0), stream_of(grad))
+        return (None, None, None) + tuple(grads)
+
+
+def _level_offsets(levels, channels):
+    offs, hwa, acc = [], [], 0
+    for l in levels:
+        per = l.shape[1] * l.shape[2] * l.shape[3] // channels
+        offs.append(acc)
+        hwa.append(per)
+        acc += per
+    return offs, hwa
+
+
+def gather_level_outputs(levels, chosen_idx, seg_of, channels):
+    _need_cuda(chosen_idx)
+    return _GatherLevels.apply(chosen_idx, seg_of, channels, *levels)
+
+
+def prepend_gt_labels(prop_labels, num_props, num_gts, max_rows):
+    S = prop_labels.shape[0]
+    rows = torch.empty(S, max(max_rows, 1), dtype=torch.int64, device=prop_labels.device)
+    num_rows = torch.empty(S, dtype=torch.int32, device=prop_labels.device)
+    call('frh_prepend_gt_labels', S, ptr(prop_labels), prop_labels.stride(0), ptr(num_props), ptr(num_gts),
+         max_rows, ptr(rows), rows.stride(0), ptr(num_rows), stream_of(prop_labels))
+    return rows, num_rows
+
+
+def bbox_target_batched(rows, num_rows, num_gts, max_rows, props, prop_seg_stride, gts, gt_labels, means, stds,
+                        max_out_per_seg):
+    S = rows.shape[0]
+    dev = rows.device
+    cap = max(int(max_out_per_seg), 1)
+    T = S * cap
+    tars = torch.empty(3, 4, T, dtype=torch.float32, device=dev)
+    lab = torch.empty(2, T, dtype=torch.int64, device=dev)
+    counts = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    ws = workspace(_lib.query('frh_bbox_target_workspace', S, max(max_rows, 1)), dev)
+    m = f32_array(means) if means is not None else None
+    sd = f32_array(stds) if stds is not None else None
+    call('frh_bbox_target', S, ptr(rows), rows.stride(0), ptr(num_rows), ptr(num_gts), max_rows, ptr(props),
+         props.stride(-2), prop_seg_stride, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_labels),
+         gt_labels.stride(0), m, sd, cap, ptr(tars[0]), ptr(tars[1]), ptr(lab[0]), ptr(tars[2]), ptr(lab[1]), T,
+         ptr(counts), ptr(ws), ws.numel(), stream_of(rows))
+    cnt = counts.cpu().tolist()
+    n = cnt[S]
+    return dict(tar_props=tars[0][:, :n], tar_bbox=tars[1][:, :n], tar_label=lab[0][:n], tar_param=tars[2][:, :n],
+                tar_is_gt=lab[1][:n], counts=cnt[:S])
+
+
+# ---------------------------------------------------------------- encode / decode (a7/a8)
+def bbox2param(base, bbox, means=None, stds=None):
+    _need_cuda(base, bbox)
+    base, bbox = _f32(base), _f32(bbox)
+    if base.stride(1) != 1:
+        base = base.contiguous()
+    if bbox.stride(1) != 1:
+        bbox = bbox.contiguous()
+    n = base.shape[1]
+    out = torch.empty(4, n, dtype=torch.float32, device=base.device)
+    call('frh_bbox2param', ptr(base), base.stride(0), ptr(bbox), bbox.stride(0), n,
+         f32_array(means) if means is not None else None, f32_array(stds) if stds is not None else None,
+         ptr(out), out.stride(0), stream_of(base))
+    return out
+
+
+def param2bbox(base, param, means, stds, img_size=None):
+    """base [4, n]; param [4*ncls, n] (coordinate-major classes); out like param."""
+    _need_cuda(base, param)
+    base, param = _f32(base), _f32(param)
+    if base.stride(1) != 1:
+        base = base.contiguous()
+    if param.stride(1) != 1:
+        param = param.contiguous()
+    n = base.shape[1]
+    ncls = param.shape[0] // 4
+    out = torch.empty(param.shape[0], n, dtype=torch.float32, device=base.device)
+    h, w = (float(img_size[0]), float(img_size[1])) if img_size is not None else (0.0, 0.0)
+    call('frh_param2bbox', ptr(base), base.stride(0), ptr(param), param.stride(0), n, ncls, f32_array(means),
+         f32_array(stds), int(img_size is not None), h, w, ptr(out), out.stride(0), stream_of(base))
+    return out
+
+
+# ---------------------------------------------------------------- RPN proposals (a9)
+def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means, stds, img_hw, min_sizes, pre_nms,
+                  post_nms, max_num, nms_iou):
+    """All images x levels; returns (boxes [B, 4, cap], scores [B, cap], counts int32 device [B])."""
+    cls_outs = [c.contiguous() for c in cls_outs]
+    reg_outs = [r.contiguous() for r in reg_outs]
+    _need_cuda(*cls_outs)
+    B, L = cls_outs[0].shape[0], len(cls_outs)
+    grid = [v for c in cls_outs for v in (c.shape[2], c.shape[3])]
+    grid_a = i32_array(grid)
+    per_level = [num_anchors * c.shape[2] * c.shape[3] for c in cls_outs]
+    P = max(min(pre_nms, n) if pre_nms > 0 else n for n in per_level)
+    post = min(post_nms, P) if post_nms > 0 else P
+    cap = max_num if max_num > 0 else post * L
+    dev = cls_outs[0].device
+    boxes = torch.empty(B, 4, cap, dtype=torch.float32, device=dev)
+    scores = torch.empty(B, cap, dtype=torch.float32, device=dev)
+    counts = torch.empty(B, dtype=torch.int32, device=dev)
+    wsb = _lib.query('frh_rpn_proposals_workspace', B, L, grid_a, num_anchors, int(pre_nms))
+    ws = workspace(wsb, dev)
+    call('frh_rpn_proposals', B, L, ptr_array(cls_outs), ptr_array(reg_outs), grid_a, num_anchors, cls_channels,
+         ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
+         f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
+         int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(),
+         stream_of(boxes))
+    return boxes, scores, counts
+
+
+# ---------------------------------------------------------------- NMS (a10)
+def nms_sorted(boxes_rows, counts, n_max, iou_thr, max_keep=-1):
+    """boxes_rows [S, n_max, 4] pre-sorted; returns keep [S, n_max] int32 positions + counts [S]."""
+    S = boxes_rows.shape[0]
+    dev = boxes_rows.device
+    keep = torch.empty(S, max(n_max, 1), dtype=torch.int32, device=dev)
+    kc = torch.empty(S, dtype=torch.int32, device=dev)
+    ws = workspace(_lib.query('frh_nms_workspace', S, max(n_max, 1)), dev)
+    call('frh_nms_sorted', S, ptr(boxes_rows), boxes_rows.stride(0), ptr(counts), n_max, float(iou_thr),
+         int(max_keep), ptr(keep), keep.stride(0), ptr(kc), ptr(ws), ws.numel(), stream_of(boxes_rows))
+    return keep, kc
+
+
+def nms(boxes, scores, iou_threshold):
+    """Drop-in for torchvision.ops.nms(boxes[N,4], scores[N], thr) -> int64 keep (score order)."""
+    _need_cuda(boxes, scores)
+    n = boxes.shape[0]
+    if n == 0:
+        return torch.empty(0, dtype=torch.int64, device=boxes.device)
+    order = torch.sort(scores, descending=True, stable=True)[1]
+    rows = _f32(boxes).index_select(0, order).contiguous().view(1, n, 4)
+    counts = torch.full((1,), n, dtype=torch.int32, device=boxes.device)
+    keep, kc = nms_sorted(rows, counts, n, iou_threshold)
+    k = int(kc.item())
+    return order[keep[0, :k].long()]
+
+
+# ---------------------------------------------------------------- RoI level map + RoIAlign (a13/a14)
+def roi_level_map(rois, finest_scale, num_levels):
+    _need_cuda(rois)
+    rois = _f32(rois).contiguous()
+    lv = torch.empty(rois.shape[0], dtype=torch.int64, device=rois.device)
+    call('frh_roi_level_map', ptr(rois), rois.shape[0], float(finest_scale), int(num_levels), ptr(lv),
+         stream_of(rois))
+    return lv
+
+
+def _feat_desc(feats):
+    hw = i32_array([v for f in feats for v in (f.shape[2], f.shape[3])])
+    st = i64_array([v for f in feats for v in f.stride()])
+    return hw, st
+
+
+# Optional live timing of the RoIAlign forward launches (bench.py roofline):
+# HIP events recorded on the launch stream around each call.
+ROI_ALIGN_PROFILE = {'on': False, 'records': []}
+
+
+class _RoIAlignMulti(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rois, levels, scales, output_size, sampling_ratio, aligned, *feats):
+        _need_cuda(rois, *feats)
+        feats = [_f32(f) for f in feats]
+        K = rois.shape[0]
+        C = feats[0].shape[1]
+        ph, pw = output_size
+        out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
+        hw, st = _feat_desc(feats)
+        prof = ROI_ALIGN_PROFILE['on']
+        if prof:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales),
+             feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
+             ptr(out), stream_of(out))
+        if prof:
+            e1.record()
+            ROI_ALIGN_PROFILE['records'].append((e0, e1, rois, levels, [tuple(f.shape) for f in feats], (ph, pw)))
+        ctx.save_for_backward(rois, levels)
+        ctx.cfg = (list(scales), output_size, sampling_ratio, aligned, [f.shape for f in feats])
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        rois, levels = ctx.saved_tensors
+        scales, (ph, pw), sr, aligned, shapes = ctx.cfg
+        grads = [torch.zeros(s, dtype=torch.float32, device=grad.device) for s in shapes]
+        grad = grad.contiguous()
+        hw, st = _feat_desc(grads)
+        call('frh_roi_align_bwd_strided', len(grads), ptr_array(grads), hw, st, f32_array(scales),
+             shapes[0][0], shapes[0][1], ptr(rois), ptr(levels), rois.shape[0], ph, pw, int(sr),
+             int(bool(aligned)), ptr(grad), stream_of(grad))
+        return (None, None, None, None, None, None) + tuple(grads)
+
+
+def roi_align_multilevel(feats, rois, levels, scales, output_size, sampling_ratio, aligned=False):
+    rois = _f32(rois).contiguous()
+    return _RoIAlignMulti.apply(rois, levels, tuple(scales), tuple(output_size), sampling_ratio, aligned, *feats)
+
+
+def _pair(v):
+    return (int(v), int(v)) if isinstance(v, int) else tuple(int(x) for x in v)
+
+
+def roi_align(input, boxes, output_size, spatial_scale=1.0, sampling_ratio=-1, aligned=False):
+    """Drop-in for torchvision.ops.roi_align with [K, 5] rois."""
+    if isinstance(boxes, (list, tuple)):
+        raise NotImplementedError('roi_align takes [K, 5] rois')
+    return roi_align_multilevel([input], boxes, None, [spatial_scale], _pair(output_size), sampling_ratio, aligned)
+
+
+class RoIAlign(nn.Module):
+    """Drop-in for torchvision.ops.RoIAlign (reference registry lib/builder.py:9,22)."""
+
+    def __init__(self, output_size, spatial_scale, sampling_ratio, aligned=False):
+        super().__init__()
+        self.output_size = _pair(output_size)
+        self.spatial_scale = spatial_scale
+        self.sampling_ratio = sampling_ratio
+        self.aligned = aligned
+
+    def forward(self, input, rois):
+        return roi_align(input, rois, self.output_size, self.spatial_scale, self.sampling_ratio, self.aligned)
+
+    def __repr__(self):
+        return '{}(output_size={}, spatial_scale={}, sampling_ratio={}, aligned={})'.format(
+            type(self).__name__, self.output_size, self.spatial_scale, self.sampling_ratio, self.aligned)
+
+
+class _RoIPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, output_size, spatial_scale):
+        _need_cuda(feat, rois)
+        feat = _f32(feat)
+        rois = _f32(rois).contiguous()
+        K, C = rois.shape[0], feat.shape[1]
+        ph, pw = output_size
+        out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=feat.device)
+        argmax = torch.empty(K, C, ph, pw, dtype=torch.int32, device=feat.device)
+        call('frh_roi_pool_fwd', ptr(feat), i64_array(feat.stride()), feat.shape[2], feat.shape[3], C,
+             float(spatial_scale), ptr(rois), K, ph, pw, ptr(out), ptr(argmax), stream_of(out))
+        ctx.save_for_backward(rois, argmax)
+        ctx.shape = feat.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        rois, argmax = ctx.saved_tensors
+        g = torch.zeros(ctx.shape, dtype=torch.float32, device=grad.device)
+        grad = grad.contiguous()
+        call('frh_roi_pool_bwd', ptr(g), i64_array(g.stride()), g.shape[2], g.shape[3], g.shape[1], ptr(rois),
+             rois.shape[0], grad.shape[2], grad.shape[3], ptr(grad), ptr(argmax), stream_of(grad))
+        return g, None, None, None
+
+
+def roi_pool(input, boxes, output_size, spatial_scale=1.0):
+    """Drop-in for torchvision.ops.roi_pool with [K, 5] rois."""
+    return _RoIPoolFn.apply(input, boxes, _pair(output_size), spatial_scale)
+
+
+class RoIPool(nn.Module):
+    """Drop-in for torchvision.ops.RoIPool.  Accepts and ignores `sampling_ratio`, which the
+    reference's C4 config passes (configs/faster_rcnn_r50.py:26) and torchvision rejects
+    (documented deviation Q9)."""
+
+    def __init__(self, output_size, spatial_scale, sampling_ratio=None):
+        super().__init__()
+        self.output_size = _pair(output_size)
+        self.spatial_scale = spatial_scale
+
+    def forward(self, input, rois):
+        return roi_pool(input, rois, self.output_size, self.spatial_scale)

@@ -1,0 +1,317 @@
+"""Generate golden vectors by running the REFERENCE's own code (this container only).
+
+    python -B tests/golden/gen_golden.py
+
+Imports /root/reference/lib with sys.modules stubs for the dependencies that
+are absent here (torchvision, mmcv, mmdet, PIL-free transforms), runs the
+reference's hot-path functions on the deterministic inputs of inputs.py and
+writes small .npz fixtures next to this file.  torchvision's nms / RoIAlign
+are stubbed with the oracle's restatements (oracle/oracle.py), so fixtures
+that pass through them pin everything *around* those two kernels; the
+kernels themselves stay "parity unpinned" (no reference or torchvision
+outputs exist for them).  Exits cleanly (code 0, message) when the
+reference is not present.  Never writes into /root/reference (bytecode off).
+"""
+import hashlib
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get('FRCNN_REFERENCE', '/root/reference')
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, 'oracle'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import inputs  # noqa: E402
+import oracle  # noqa: E402
+
+
+def install_shims():
+    """sys.modules stubs for torchvision / mmcv / mmdet (absent in this image)."""
+    tv = types.ModuleType('torchvision')
+    tr = types.ModuleType('torchvision.transforms')
+
+    class _Noop(object):
+        def __init__(self, *a, **k):
+            pass
+
+        def __call__(self, x):
+            return x
+
+    tr.Compose = tr.ToTensor = tr.Normalize = _Noop
+    ops = types.ModuleType('torchvision.ops')
+
+    def nms(boxes, scores, thr):
+        keep = oracle.nms(boxes.detach().cpu().numpy(), scores.detach().cpu().numpy(), thr)
+        return torch.from_numpy(np.asarray(keep, np.int64))
+
+    class RoIAlign(torch.nn.Module):
+        def __init__(self, output_size, spatial_scale, sampling_ratio, aligned=False):
+            super().__init__()
+            self.output_size = output_size if isinstance(output_size, tuple) else (output_size, output_size)
+            self.spatial_scale, self.sampling_ratio, self.aligned = spatial_scale, sampling_ratio, aligned
+
+        def forward(self, x, rois):
+            out = oracle.roi_align([x.detach().numpy()], rois.detach().numpy(), None, [self.spatial_scale],
+                                   self.output_size, self.sampling_ratio, self.aligned)
+            return torch.from_numpy(out)
+
+    class RoIPool(torch.nn.Module):
+        def __init__(self, output_size, spatial_scale):
+            super().__init__()
+
+    ops.nms, ops.RoIAlign, ops.RoIPool = nms, RoIAlign, RoIPool
+    ops.roi_align = ops.roi_pool = None
+    models = types.ModuleType('torchvision.models')
+
+    def _nope(*a, **k):
+        raise RuntimeError('pretrained torchvision models are unavailable offline')
+
+    models.resnet50 = models.resnet101 = models.resnet152 = models.vgg16 = _nope
+    tv.transforms, tv.ops, tv.models = tr, ops, models
+    sys.modules.update({'torchvision': tv, 'torchvision.transforms': tr, 'torchvision.ops': ops,
+                        'torchvision.models': models})
+    mmcv = types.ModuleType('mmcv')
+    cnn = types.ModuleType('mmcv.cnn')
+
+    def normal_init(m, mean=0, std=1, bias=0):
+        torch.nn.init.normal_(m.weight, mean, std)
+        if getattr(m, 'bias', None) is not None:
+            torch.nn.init.constant_(m.bias, bias)
+
+    def xavier_init(m, gain=1, bias=0, distribution='normal'):
+        torch.nn.init.xavier_uniform_(m.weight, gain)
+        if getattr(m, 'bias', None) is not None:
+            torch.nn.init.constant_(m.bias, bias)
+
+    def constant_init(m, val, bias=0):
+        torch.nn.init.constant_(m.weight, val)
+        if getattr(m, 'bias', None) is not None:
+            torch.nn.init.constant_(m.bias, bias)
+
+    cnn.normal_init, cnn.xavier_init, cnn.constant_init = normal_init, xavier_init, constant_init
+    mmcv.cnn = cnn
+    mmcv.ProgressBar = object
+    mmdet = types.ModuleType('mmdet')
+    mops = types.ModuleType('mmdet.ops')
+    dcn = types.ModuleType('mmdet.ops.dcn')
+    dcn.DeformConv = None
+    sys.modules.update({'mmcv': mmcv, 'mmcv.cnn': cnn, 'mmdet': mmdet, 'mmdet.ops': mops, 'mmdet.ops.dcn': dcn})
+
+
+class CD(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+
+def cd(d):
+    return CD({k: cd(v) if isinstance(v, dict) else v for k, v in d.items()})
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print('wrote', name, os.path.getsize(path), 'bytes')
+
+
+def gen_voc_gts(n=64):
+    d = json.load(open(os.path.join(REF, 'data', 'voc2007_trainval_no_difficult.json')))
+    imgs = sorted(d['images'], key=lambda x: x['id'])[:n]
+    by = {}
+    for a in d['annotations']:
+        by.setdefault(a['image_id'], []).append(a)
+    out = {'n': np.int64(len(imgs))}
+    for i, im in enumerate(imgs):
+        sx, sy = 1000.0 / im['width'], 600.0 / im['height']
+        anns = by.get(im['id'], [])
+        b = np.array([[a['bbox'][0] * sx, a['bbox'][1] * sy, (a['bbox'][0] + a['bbox'][2] - 1) * sx,
+                       (a['bbox'][1] + a['bbox'][3] - 1) * sy] for a in anns], np.float64).T
+        out['boxes_{}'.format(i)] = b.astype(np.float32).reshape(4, -1)
+        out['labels_{}'.format(i)] = np.array([a['category_id'] for a in anns], np.int64)
+    save('voc_gts.npz', **out)
+
+
+def gen_anchors(lib_anchor):
+    res = {}
+    cases = {
+        'fpn': (inputs.FPN_STRIDES, inputs.FPN_GRIDS, [8], [0.5, 1.0, 2.0]),
+        'retina': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [4 * 2 ** (i / 3) for i in range(3)], [0.5, 1.0, 2.0]),
+        'atss': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [8], [1.0]),
+        'c4': ([16], inputs.C4_GRIDS, [4, 8, 16, 32], [0.5, 1.0, 2.0]),
+    }
+    for name, (strides, grids, scales, ratios) in cases.items():
+        for l, (s, g) in enumerate(zip(strides, grids)):
+            ac = lib_anchor.AnchorCreator(base=s, scales=scales, aspect_ratios=ratios)
+            a = ac(s, g).numpy()
+            res['{}_{}_sha'.format(name, l)] = np.array(sha(a))
+            res['{}_{}_head'.format(name, l)] = a.reshape(4, -1)[:, :64].copy()
+    save('anchors.npz', **res)
+
+
+def _fpn_anchors(lib_anchor, strides, grids, scales, ratios):
+    out = []
+    for s, g in zip(strides, grids):
+        out.append(lib_anchor.AnchorCreator(base=s, scales=scales, aspect_ratios=ratios)(s, g).view(4, -1))
+    return torch.cat(out, 1)
+
+
+def gen_assign(lib_anchor, region, utils):
+    gts = inputs.voc_gts()
+    anchors = _fpn_anchors(lib_anchor, inputs.FPN_STRIDES, inputs.FPN_GRIDS, [8], [0.5, 1.0, 2.0])
+    A = 3
+    ingrid = torch.cat([region.inside_grid_mask(A, inputs.IMG_SHAPE, g, s)
+                        for g, s in zip(inputs.FPN_GRIDS, inputs.FPN_STRIDES)]).bool()
+    inimg = region.inside_anchor_mask(anchors, inputs.IMG_SHAPE, 0)
+    mask = (ingrid & inimg)
+    res = {'mask_sha': np.array(sha(mask.numpy().astype(np.uint8))), 'mask_count': np.int64(mask.sum())}
+    in_anchors = anchors[:, mask]
+    for i in range(8):
+        gb = torch.from_numpy(gts[i][0])
+        for tag, thr in (('rpn', (0.7, 0.3, 0.3)), ('rcnn', (0.5, 0.5, 0.5)), ('retina', (0.5, 0.4, 0.0))):
+            lab, miou = region.MaxIoUAssigner(*thr)(in_anchors, gb)
+            res['{}_{}_labels'.format(tag, i)] = lab.numpy().astype(np.int8)
+            res['{}_{}_miou_sha'.format(tag, i)] = np.array(sha(miou.numpy()))
+        if i < 2:
+            tab = utils.calc_iou(in_anchors, gb).numpy()
+            res['iou_{}_sha'.format(i)] = np.array(sha(tab))
+            res['iou_{}_head'.format(i)] = tab[:4096].copy()
+    # random boxes vs random boxes (ties, degenerate widths)
+    a = torch.from_numpy(inputs.random_boxes(11, 3000))
+    b = torch.from_numpy(inputs.random_boxes(12, 40))
+    res['rand_iou'] = utils.calc_iou(a, b).numpy()
+    lab, miou = region.MaxIoUAssigner(0.5, 0.4, 0.0)(a, b)
+    res['rand_labels'], res['rand_miou'] = lab.numpy(), miou.numpy()
+    res['rand_elem_iou'] = utils.elem_iou(a[:, :40], b).numpy()
+    save('assign.npz', **res)
+
+
+def gen_targets(lib_anchor, region, anchor_mod, bbox_mod, utils):
+    gts = inputs.voc_gts()
+    anchors = _fpn_anchors(lib_anchor, inputs.FPN_STRIDES, inputs.FPN_GRIDS, [8], [0.5, 1.0, 2.0])
+    ingrid = torch.cat([region.inside_grid_mask(3, inputs.IMG_SHAPE, g, s)
+                        for g, s in zip(inputs.FPN_GRIDS, inputs.FPN_STRIDES)]).bool()
+    mask = ingrid & region.inside_anchor_mask(anchors, inputs.IMG_SHAPE, 0)
+    in_anchors = anchors[:, mask]
+    res = {}
+    for i in range(4):
+        cls, reg = inputs.head_outputs(100 + i, inputs.FPN_GRIDS, 3, 1)
+        cls_out = torch.cat([torch.from_numpy(c[0]).view(1, -1) for c in cls], 1)
+        reg_out = torch.cat([torch.from_numpy(r[0]).view(4, -1) for r in reg], 1)
+        gb = torch.from_numpy(gts[i][0])
+        np.random.seed(1000 + i)
+        out = anchor_mod.anchor_target(cls_out, reg_out, 1, in_anchors, mask, gb, torch.ones(gb.shape[1]).long(),
+                                       region.MaxIoUAssigner(0.7, 0.3, 0.3), region.RandomSampler(256, 128),
+                                       [0.0] * 4, [1.0] * 4)
+        for k, v in zip(('tar_cls_out', 'tar_reg_out', 'tar_labels', 'tar_anchors', 'tar_bbox', 'tar_param'), out):
+            res['rpn_{}_{}'.format(i, k)] = v.numpy()
+        res['rpn_{}_rng_after'.format(i)] = np.random.randint(0, 2 ** 31 - 1)
+    # RCNN bbox_target on random proposals (the RPN fixture's props are pinned separately)
+    for i in range(4):
+        props = torch.from_numpy(inputs.random_boxes(200 + i, 2000, min_wh=8, max_wh=300))
+        gb, gl = torch.from_numpy(gts[i][0]), torch.from_numpy(gts[i][1])
+        np.random.seed(2000 + i)
+        out = bbox_mod.bbox_target(props, gb, gl, region.MaxIoUAssigner(0.5, 0.5, 0.5),
+                                   region.RandomSampler(512, 128), (0.0,) * 4, (0.1, 0.1, 0.2, 0.2))
+        for k, v in zip(('tar_props', 'tar_bbox', 'tar_label', 'tar_param', 'tar_is_gt'), out):
+            res['rcnn_{}_{}'.format(i, k)] = v.numpy()
+    # encode / decode
+    base = torch.from_numpy(inputs.random_boxes(300, 1000))
+    box = torch.from_numpy(inputs.random_boxes(301, 1000))
+    res['enc'] = utils.bbox2param(base, box).numpy()
+    res['enc_norm'] = utils.bbox2param(base, box, [0.0] * 4, [0.1, 0.1, 0.2, 0.2]).numpy()
+    delta = torch.from_numpy(np.random.default_rng(302).standard_normal((4 * 21, 1000)).astype(np.float32) * 0.5)
+    res['dec'] = utils.param2bbox(base, delta[:4], [0.0] * 4, [0.1, 0.1, 0.2, 0.2], inputs.IMG_SHAPE).numpy()
+    res['dec_batched'] = utils.batched_param2bbox(base, delta, [0.0] * 4, [0.1, 0.1, 0.2, 0.2],
+                                                  inputs.IMG_SHAPE).numpy()
+    res['dec_noclamp'] = utils.param2bbox(base, delta[:4]).numpy()
+    save('targets.npz', **res)
+
+
+def gen_rpn(lib_anchor, rpn_head_mod):
+    res = {}
+    anchors = [lib_anchor.AnchorCreator(base=s, scales=[8], aspect_ratios=[0.5, 1.0, 2.0])(s, g)
+               for s, g in zip(inputs.FPN_STRIDES, inputs.FPN_GRIDS)]
+    head = rpn_head_mod.RPNHead(256, 256, loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True),
+                                loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0))
+    for tag, cfg in (('train', dict(pre_nms=2000, post_nms=2000, max_num=2000, nms_iou=0.7, min_bbox_size=0)),
+                     ('test', dict(pre_nms=1000, post_nms=1000, max_num=1000, nms_iou=0.7, min_bbox_size=0.0)),
+                     ('minsz', dict(pre_nms=1000, post_nms=300, max_num=1000, nms_iou=0.5, min_bbox_size=16))):
+        for i in range(2):
+            cls, reg = inputs.head_outputs(500 + i, inputs.FPN_GRIDS, 3, 1, reg_scale=0.5)
+            b, s, _ = head.predict_single_image([torch.from_numpy(c[0]) for c in cls],
+                                                [torch.from_numpy(r[0]) for r in reg], anchors, inputs.img_meta(),
+                                                cd(cfg))
+            res['{}_{}_boxes'.format(tag, i)] = b.numpy()
+            res['{}_{}_scores'.format(tag, i)] = s.numpy()
+    save('rpn.npz', **res)
+
+
+def gen_levels(region):
+    ex = region.BasicRoIExtractor.__new__(region.BasicRoIExtractor)
+    ex.finest_scale = 56
+    rng = np.random.default_rng(400)
+    sides = np.concatenate([rng.uniform(4, 900, 4000), 56.0 * 2.0 ** np.arange(0, 5) - 1.0,
+                            56.0 * 2.0 ** np.arange(0, 5) - 1.0 + 1e-3, 56.0 * 2.0 ** np.arange(0, 5) - 1.0 - 1e-3])
+    x1 = rng.uniform(0, 50, len(sides))
+    y1 = rng.uniform(0, 50, len(sides))
+    rois = np.stack([x1, y1, x1 + sides - 1, y1 + sides - 1]).astype(np.float32)
+    lv = ex.map_rois_to_levels(torch.from_numpy(rois), 4).numpy()
+    save('levels.npz', rois=rois, levels=lv)
+
+
+def gen_rpn_loss(rpn_head_mod):
+    gts = inputs.voc_gts()
+    head = rpn_head_mod.RPNHead(256, 256, loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0),
+                                loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0, loss_weight=1.0))
+    cfg = cd(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.7, neg_iou=0.3, min_pos_iou=0.3),
+                  sampler=dict(type='RandomSampler', max_num=256, pos_num=128), allowed_border=0))
+    res = {}
+    for i in range(2):
+        cls, reg = inputs.head_outputs(700 + i, inputs.FPN_GRIDS, 3, 1, batch=2)
+        np.random.seed(3000 + i)
+        c, r = head.loss([torch.from_numpy(x) for x in cls], [torch.from_numpy(x) for x in reg],
+                         [torch.from_numpy(gts[2 * i + j][0]) for j in range(2)],
+                         [torch.ones(gts[2 * i + j][0].shape[1]).long() for j in range(2)],
+                         [inputs.img_meta(), inputs.img_meta()], cfg)
+        res['loss_{}'.format(i)] = np.array([float(c), float(r)], np.float64)
+    save('rpn_loss.npz', **res)
+
+
+def main():
+    if not os.path.isdir(os.path.join(REF, 'lib')):
+        print('reference not found at {}: nothing to generate (fixtures are committed)'.format(REF))
+        return 0
+    install_shims()
+    sys.path.insert(0, REF)
+    import lib.anchor as lib_anchor
+    import lib.region as region
+    import lib.bbox as bbox_mod
+    import lib.utils as utils
+    import lib.heads.rpn_head as rpn_head_mod
+    torch.set_num_threads(8)
+    if '--voc' in sys.argv or not os.path.exists(os.path.join(HERE, 'voc_gts.npz')):
+        gen_voc_gts()
+    gen_anchors(lib_anchor)
+    gen_assign(lib_anchor, region, utils)
+    gen_targets(lib_anchor, region, lib_anchor, bbox_mod, utils)
+    gen_rpn(lib_anchor, rpn_head_mod)
+    gen_levels(region)
+    gen_rpn_loss(rpn_head_mod)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -1,0 +1,63 @@
+"""Deterministic synthetic inputs shared by the golden generator and the tests.
+
+Everything here is numpy (PCG64 `default_rng`, stable across platforms) so the
+GPU box regenerates bit-identical inputs without the reference present; the
+only stored inputs are the VOC ground-truth boxes (tests/golden/voc_gts.npz).
+"""
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+IMG_SHAPE = (600, 1000)
+PAD_SHAPE = (608, 1024)
+# cfg2/cfg4 FPN: strides 4..64; P6 = P5[::2, ::2]
+FPN_STRIDES = [4, 8, 16, 32, 64]
+FPN_GRIDS = [(152, 256), (76, 128), (38, 64), (19, 32), (10, 16)]
+# cfg3 / cfg5: strides 8..128 (P3..P7)
+RETINA_STRIDES = [8, 16, 32, 64, 128]
+RETINA_GRIDS = [(76, 128), (38, 64), (19, 32), (10, 16), (5, 8)]
+# cfg1 C4: one level, stride 16
+C4_GRIDS = [(38, 64)]
+
+
+def img_meta(scale_factor=1.6):
+    return {'img_shape': IMG_SHAPE + (3,), 'pad_shape': PAD_SHAPE + (3,), 'scale_factor': scale_factor,
+            'ori_shape': (375, 625, 3)}
+
+
+def voc_gts():
+    """[(boxes [4, G] f32 xyxy in the 1000x600 frame, labels int64 [G])] from the committed fixture."""
+    z = np.load(os.path.join(HERE, 'voc_gts.npz'))
+    out = []
+    for i in range(int(z['n'])):
+        out.append((z['boxes_{}'.format(i)].astype(np.float32), z['labels_{}'.format(i)].astype(np.int64)))
+    return out
+
+
+def head_outputs(seed, grids, num_anchors, cls_channels, batch=1, cls_scale=1.0, reg_scale=0.1):
+    """Per-level (cls [B, C*A, H, W], reg [B, 4*A, H, W]) f32 arrays."""
+    rng = np.random.default_rng(seed)
+    cls, reg = [], []
+    for h, w in grids:
+        cls.append((rng.standard_normal((batch, cls_channels * num_anchors, h, w)) * cls_scale).astype(np.float32))
+        reg.append((rng.standard_normal((batch, 4 * num_anchors, h, w)) * reg_scale).astype(np.float32))
+    return cls, reg
+
+
+def random_boxes(seed, n, img=IMG_SHAPE, min_wh=2.0, max_wh=400.0):
+    """[4, n] f32 xyxy boxes inside the image."""
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(min_wh, max_wh, n)
+    h = rng.uniform(min_wh, max_wh, n)
+    x1 = rng.uniform(0, img[1] - 1, n)
+    y1 = rng.uniform(0, img[0] - 1, n)
+    x2 = np.minimum(x1 + w, img[1] - 1)
+    y2 = np.minimum(y1 + h, img[0] - 1)
+    return np.stack([x1, y1, x2, y2]).astype(np.float32)
+
+
+def feature_maps(seed, grids, channels, batch):
+    rng = np.random.default_rng(seed)
+    return [rng.standard_normal((batch, channels, h, w)).astype(np.float32) for h, w in grids]

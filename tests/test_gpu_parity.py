@@ -1,0 +1,417 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the reference's
+golden vectors and the CPU oracle, on the same seeded inputs.
+
+Bars: bit-exact for anchors, masks, IoU tables, assignment labels/IoUs,
+sampling (numpy-parity mode), chosen indices and NMS keep lists; float
+tolerances are stated per test (encode/decode log/exp, RoIAlign 1e-5)."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+import inputs
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def T(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+def canon_ties(boxes, scores):
+    order = np.lexsort((boxes[3], boxes[2], boxes[1], boxes[0], -scores.astype(np.float64)))
+    return boxes[:, order]
+
+
+ANCHOR_CASES = {
+    'fpn': (inputs.FPN_STRIDES, inputs.FPN_GRIDS, [8], [0.5, 1.0, 2.0]),
+    'retina': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [4 * 2 ** (i / 3) for i in range(3)], [0.5, 1.0, 2.0]),
+    'atss': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [8], [1.0]),
+    'c4': ([16], inputs.C4_GRIDS, [4, 8, 16, 32], [0.5, 1.0, 2.0]),
+}
+
+
+def fpn_setup(dev):
+    from frcnn_amd.heads.rpn_head import RPNHead
+    head = RPNHead(256, 256, loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0),
+                   loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0, loss_weight=1.0)).to(dev)
+    anchors = head._flat_anchors(inputs.FPN_GRIDS, dev)
+    return head, anchors
+
+
+# ----------------------------------------------------------------- a1/a2
+@pytest.mark.parametrize('name', sorted(ANCHOR_CASES))
+def test_anchor_grid_bit_exact(dev, golden, name):
+    from frcnn_amd.anchor import AnchorCreator
+    g = golden('anchors.npz')
+    strides, grids, scales, ratios = ANCHOR_CASES[name]
+    for l, (s, grid) in enumerate(zip(strides, grids)):
+        a = AnchorCreator(base=s, scales=scales, aspect_ratios=ratios, device=dev)(s, grid)
+        assert tuple(a.shape) == (4, len(scales) * len(ratios)) + tuple(grid)
+        assert sha(a.cpu().numpy()) == str(g['{}_{}_sha'.format(name, l)]), (name, l)
+
+
+def test_inside_mask_bit_exact(dev, golden):
+    g = golden('assign.npz')
+    head, anchors = fpn_setup(dev)
+    m = head._valid_masks(anchors, inputs.FPN_GRIDS, [inputs.img_meta()], 0)[0]
+    assert int(m.sum()) == int(g['mask_count'])
+    assert sha(m.cpu().numpy()) == str(g['mask_sha'])
+
+
+# ----------------------------------------------------------------- a3
+def test_iou_bit_exact(dev, golden):
+    from frcnn_amd import utils
+    g = golden('assign.npz')
+    a, b = T(inputs.random_boxes(11, 3000), dev), T(inputs.random_boxes(12, 40), dev)
+    np.testing.assert_array_equal(utils.calc_iou(a, b).cpu().numpy(), g['rand_iou'])
+    np.testing.assert_array_equal(utils.elem_iou(a[:, :40], b).cpu().numpy(), g['rand_elem_iou'])
+    head, anchors = fpn_setup(dev)
+    m = head._valid_masks(anchors, inputs.FPN_GRIDS, [inputs.img_meta()], 0)[0].bool()
+    ina = anchors[:, m]
+    gts = inputs.voc_gts()
+    for i in range(2):
+        t = utils.calc_iou(ina, T(gts[i][0], dev)).cpu().numpy()
+        assert sha(t) == str(g['iou_{}_sha'.format(i)])
+
+
+# ----------------------------------------------------------------- a4
+@pytest.mark.parametrize('tag,thr', [('rpn', (0.7, 0.3, 0.3)), ('rcnn', (0.5, 0.5, 0.5)), ('retina', (0.5, 0.4, 0.0))])
+def test_assign_batched_bit_exact(dev, golden, tag, thr):
+    """All 8 images in ONE fused launch over the full anchor set with validity masks."""
+    from frcnn_amd import ops
+    g = golden('assign.npz')
+    head, anchors = fpn_setup(dev)
+    masks = head._valid_masks(anchors, inputs.FPN_GRIDS, [inputs.img_meta()] * 8, 0)
+    gts = inputs.voc_gts()[:8]
+    gb, gc, gm = ops.pack_boxes([T(x[0], dev) for x in gts], dev)
+    N = anchors.shape[1]
+    num = torch.full((8,), N, dtype=torch.int32, device=dev)
+    labels, miou = ops.maxiou_assign(anchors, 0, num, N, gb, gc, gm, *thr, valid=masks,
+                                     valid_seg_stride=masks.stride(0))
+    m0 = masks[0].bool()
+    for i in range(8):
+        lab = labels[i][m0].cpu().numpy()
+        np.testing.assert_array_equal(lab.astype(np.int8), g['{}_{}_labels'.format(tag, i)])
+        assert sha(miou[i][m0].cpu().numpy()) == str(g['{}_{}_miou_sha'.format(tag, i)])
+        assert bool((labels[i][~m0] == -1).all())
+
+
+def test_assigner_api_random_boxes(dev, golden):
+    from frcnn_amd.region import MaxIoUAssigner
+    g = golden('assign.npz')
+    lab, miou = MaxIoUAssigner(0.5, 0.4, 0.0)(T(inputs.random_boxes(11, 3000), dev),
+                                             T(inputs.random_boxes(12, 40), dev))
+    np.testing.assert_array_equal(lab.cpu().numpy(), g['rand_labels'])
+    np.testing.assert_array_equal(miou.cpu().numpy(), g['rand_miou'])
+
+
+def test_assign_ties_and_nan_free_edges(dev):
+    """Identical boxes (all tie at a gt's max), boxes touching gts, far-away boxes."""
+    from frcnn_amd.region import MaxIoUAssigner
+    gts = np.array([[10, 10, 50, 50], [100, 100, 140, 180], [10, 10, 50, 50]], np.float32).T
+    boxes = np.concatenate([np.tile(gts[:, :1], (1, 5)), np.array([[51, 51, 90, 90], [500, 500, 600, 600],
+                                                                  [100, 100, 140, 180]], np.float32).T,
+                            inputs.random_boxes(7, 500)], 1)
+    for thr in ((0.7, 0.3, 0.3), (0.5, 0.4, 0.0), (0.5, 0.5, 0.5)):
+        lab, miou = MaxIoUAssigner(*thr)(T(boxes, dev), T(gts, dev))
+        rl, ri = oracle.maxiou_assign(boxes, gts, *thr)
+        np.testing.assert_array_equal(lab.cpu().numpy(), rl)
+        np.testing.assert_array_equal(miou.cpu().numpy(), ri)
+
+
+# ----------------------------------------------------------------- a5/a6 anchor targets (numpy-parity sampler)
+def test_anchor_target_single_image_vs_reference(dev, golden):
+    from frcnn_amd import anchor as A
+    from frcnn_amd.region import MaxIoUAssigner, RandomSampler
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('numpy')
+    g = golden('targets.npz')
+    head, anchors = fpn_setup(dev)
+    m = head._valid_masks(anchors, inputs.FPN_GRIDS, [inputs.img_meta()], 0)[0].bool()
+    ina = anchors[:, m]
+    gts = inputs.voc_gts()
+    for i in range(4):
+        cls, reg = inputs.head_outputs(100 + i, inputs.FPN_GRIDS, 3, 1)
+        cls_out = T(np.concatenate([c[0].reshape(1, -1) for c in cls], 1), dev)
+        reg_out = T(np.concatenate([r[0].reshape(4, -1) for r in reg], 1), dev)
+        np.random.seed(1000 + i)
+        out = A.anchor_target(cls_out, reg_out, 1, ina, m, T(gts[i][0], dev),
+                              torch.ones(gts[i][0].shape[1], dtype=torch.long, device=dev),
+                              MaxIoUAssigner(0.7, 0.3, 0.3), RandomSampler(256, 128), [0.0] * 4, [1.0] * 4)
+        names = ('tar_cls_out', 'tar_reg_out', 'tar_labels', 'tar_anchors', 'tar_bbox')
+        for k, v in zip(names, out[:5]):
+            np.testing.assert_array_equal(v.cpu().numpy(), g['rpn_{}_{}'.format(i, k)], err_msg=k)
+        np.testing.assert_allclose(out[5].cpu().numpy(), g['rpn_{}_tar_param'.format(i)], rtol=1e-5, atol=1e-5)
+        assert np.random.randint(0, 2 ** 31 - 1) == int(g['rpn_{}_rng_after'.format(i)])
+
+
+def test_rpn_targets_batched_equal_per_image_oracle(dev):
+    """B=4 batched targets == per-image oracle results concatenated (one numpy stream)."""
+    from frcnn_amd.config import wrap
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('numpy')
+    head, anchors = fpn_setup(dev)
+    gts = inputs.voc_gts()[10:14]
+    cls, reg = inputs.head_outputs(900, inputs.FPN_GRIDS, 3, 1, batch=4)
+    cfg = wrap(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.7, neg_iou=0.3, min_pos_iou=0.3),
+                    sampler=dict(type='RandomSampler', max_num=256, pos_num=128), allowed_border=0))
+    np.random.seed(77)
+    tc, tr, tl, tp = head.targets_batched([T(c, dev) for c in cls], [T(r, dev) for r in reg],
+                                          [T(x[0], dev) for x in gts],
+                                          [torch.ones(x[0].shape[1], dtype=torch.long, device=dev) for x in gts],
+                                          [inputs.img_meta()] * 4, cfg)
+    anc = anchors.cpu().numpy()
+    mask = head._valid_masks(anchors, inputs.FPN_GRIDS, [inputs.img_meta()], 0)[0].bool().cpu().numpy()
+    np.random.seed(77)
+    ref = {k: [] for k in range(6)}
+    for b in range(4):
+        co = np.concatenate([c[b].reshape(1, -1) for c in cls], 1)
+        ro = np.concatenate([r[b].reshape(4, -1) for r in reg], 1)
+        out = oracle.anchor_target(co, ro, 1, anc[:, mask], mask, gts[b][0], np.ones(gts[b][0].shape[1], np.int64),
+                                   (0.7, 0.3, 0.3), (256, 128), [0.0] * 4, [1.0] * 4)
+        for k in range(6):
+            ref[k].append(out[k])
+    np.testing.assert_array_equal(tc.detach().cpu().numpy(), np.concatenate(ref[0], 1))
+    np.testing.assert_array_equal(tr.detach().cpu().numpy(), np.concatenate(ref[1], 1))
+    np.testing.assert_array_equal(tl.cpu().numpy(), np.concatenate(ref[2]))
+    np.testing.assert_allclose(tp.cpu().numpy(), np.concatenate(ref[5], 1), rtol=1e-5, atol=1e-5)
+
+
+def test_rpn_loss_vs_reference(dev, golden):
+    from frcnn_amd.config import wrap
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('numpy')
+    g = golden('rpn_loss.npz')
+    head, _ = fpn_setup(dev)
+    gts = inputs.voc_gts()
+    cfg = wrap(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.7, neg_iou=0.3, min_pos_iou=0.3),
+                    sampler=dict(type='RandomSampler', max_num=256, pos_num=128), allowed_border=0))
+    for i in range(2):
+        cls, reg = inputs.head_outputs(700 + i, inputs.FPN_GRIDS, 3, 1, batch=2)
+        np.random.seed(3000 + i)
+        c, r = head.loss([T(x, dev) for x in cls], [T(x, dev) for x in reg],
+                         [T(gts[2 * i + j][0], dev) for j in range(2)],
+                         [torch.ones(gts[2 * i + j][0].shape[1], dtype=torch.long, device=dev) for j in range(2)],
+                         [inputs.img_meta()] * 2, cfg)
+        np.testing.assert_allclose([float(c), float(r)], g['loss_{}'.format(i)], rtol=2e-5)
+
+
+def test_device_sampler_properties(dev):
+    from frcnn_amd import ops
+    rng = np.random.default_rng(3)
+    S, n = 3, 130000
+    lab = rng.choice([-1, 0, 0, 0, 1, 2], size=(S, n), p=[0.3, 0.2, 0.2, 0.2, 0.05, 0.05]).astype(np.int64)
+    lab[2, :] = np.where(lab[2] > 0, 0, lab[2])  # a segment with no positives
+    lt = T(lab, dev)
+    num = torch.tensor([n, n - 5, 1000], dtype=torch.int32, device=dev)
+    out = ops.sample_labels(lt, num, n, 256, 128, mode='device').cpu().numpy()
+    for s in range(S):
+        ns = int(num[s])
+        src, o = lab[s, :ns], out[s, :ns]
+        npos, nneg = int((src > 0).sum()), int((src == 0).sum())
+        kp = min(npos, 128)
+        assert int((o > 0).sum()) == kp
+        assert int((o == 0).sum()) == min(nneg, 256 - kp)
+        kept = o >= 0
+        np.testing.assert_array_equal(o[kept], src[kept])  # kept rows keep their labels
+    # fresh draws differ, and a fixed (seed, call) reproduces
+    out2 = ops.sample_labels(lt, num, n, 256, 128, mode='device').cpu().numpy()
+    assert not np.array_equal(out, out2)
+
+
+# ----------------------------------------------------------------- a12
+def test_bbox_target_vs_reference(dev, golden):
+    from frcnn_amd import bbox as B
+    from frcnn_amd.region import MaxIoUAssigner, RandomSampler
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('numpy')
+    g = golden('targets.npz')
+    gts = inputs.voc_gts()
+    for i in range(4):
+        props = T(inputs.random_boxes(200 + i, 2000, min_wh=8, max_wh=300), dev)
+        np.random.seed(2000 + i)
+        out = B.bbox_target(props, T(gts[i][0], dev), T(gts[i][1], dev), MaxIoUAssigner(0.5, 0.5, 0.5),
+                            RandomSampler(512, 128), (0.0,) * 4, (0.1, 0.1, 0.2, 0.2))
+        for k, v in zip(('tar_props', 'tar_bbox', 'tar_label'), out[:3]):
+            np.testing.assert_array_equal(v.cpu().numpy(), g['rcnn_{}_{}'.format(i, k)], err_msg=k)
+        np.testing.assert_allclose(out[3].cpu().numpy(), g['rcnn_{}_tar_param'.format(i)], rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(out[4].cpu().numpy(), g['rcnn_{}_tar_is_gt'.format(i)])
+
+
+# ----------------------------------------------------------------- a7/a8
+def test_encode_decode(dev, golden):
+    from frcnn_amd import utils
+    g = golden('targets.npz')
+    base, box = T(inputs.random_boxes(300, 1000), dev), T(inputs.random_boxes(301, 1000), dev)
+    delta = T(np.random.default_rng(302).standard_normal((4 * 21, 1000)).astype(np.float32) * 0.5, dev)
+    sd = [0.1, 0.1, 0.2, 0.2]
+    np.testing.assert_allclose(utils.bbox2param(base, box).cpu().numpy(), g['enc'], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(utils.bbox2param(base, box, [0.0] * 4, sd).cpu().numpy(), g['enc_norm'], rtol=1e-5,
+                               atol=1e-5)
+    np.testing.assert_allclose(utils.param2bbox(base, delta[:4], [0.0] * 4, sd, inputs.IMG_SHAPE).cpu().numpy(),
+                               g['dec'], rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(utils.batched_param2bbox(base, delta, [0.0] * 4, sd, inputs.IMG_SHAPE).cpu().numpy(),
+                               g['dec_batched'], rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(utils.param2bbox(base, delta[:4]).cpu().numpy(), g['dec_noclamp'], rtol=1e-5,
+                               atol=1e-3)
+
+
+# ----------------------------------------------------------------- a9/a10
+@pytest.mark.parametrize('tag,cfg', [('train', (2000, 2000, 2000, 0.7, 0.0)), ('test', (1000, 1000, 1000, 0.7, 0.0)),
+                                     ('minsz', (1000, 300, 1000, 0.5, 16.0))])
+def test_rpn_proposals_vs_reference(dev, golden, tag, cfg):
+    from frcnn_amd.config import wrap
+    g = golden('rpn.npz')
+    pre, post, mx, thr, minb = cfg
+    head, _ = fpn_setup(dev)
+    tcfg = wrap(dict(pre_nms=pre, post_nms=post, max_num=mx, nms_iou=thr, min_bbox_size=minb))
+    cls_l, reg_l = [], []
+    for i in range(2):
+        cls, reg = inputs.head_outputs(500 + i, inputs.FPN_GRIDS, 3, 1, reg_scale=0.5)
+        cls_l.append(cls)
+        reg_l.append(reg)
+    cls_b = [T(np.concatenate([cls_l[0][l], cls_l[1][l]], 0), dev) for l in range(5)]
+    reg_b = [T(np.concatenate([reg_l[0][l], reg_l[1][l]], 0), dev) for l in range(5)]
+    props, scores, _ = head.predict_bboxes_from_output(cls_b, reg_b, [inputs.img_meta()] * 2, tcfg)
+    for i in range(2):
+        rb, rs = g['{}_{}_boxes'.format(tag, i)], g['{}_{}_scores'.format(tag, i)]
+        b, s = props[i].cpu().numpy(), scores[i].cpu().numpy()
+        assert b.shape == rb.shape, (b.shape, rb.shape)
+        np.testing.assert_allclose(s, rs, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(canon_ties(b, s), canon_ties(rb, rs), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize('n,thr', [(2000, 0.7), (1000, 0.5), (5000, 0.3), (12000, 0.7), (1, 0.5), (63, 0.5),
+                                   (64, 0.5), (65, 0.5)])
+def test_nms_keep_bit_exact(dev, n, thr):
+    from frcnn_amd import ops
+    rng = np.random.default_rng(n)
+    boxes = inputs.random_boxes(n, n, min_wh=5, max_wh=200).T.copy()
+    boxes[::17] = boxes[::17][:, [0, 1, 2, 3]]  # duplicates
+    if n > 10:
+        boxes[5] = boxes[3]
+    scores = rng.random(n).astype(np.float32)
+    scores[::7] = scores[0]  # ties resolved by input order (stable)
+    keep = ops.nms(T(boxes, dev), T(scores, dev), thr).cpu().numpy()
+    np.testing.assert_array_equal(keep, oracle.nms(boxes, scores, thr))
+
+
+def test_nms_empty_and_batched(dev):
+    from frcnn_amd import ops, utils
+    e = ops.nms(torch.zeros(0, 4, device=dev), torch.zeros(0, device=dev), 0.5)
+    assert e.numel() == 0
+    boxes = inputs.random_boxes(3, 3000, min_wh=5, max_wh=100).T.copy()
+    scores = np.random.default_rng(4).random(3000).astype(np.float32)
+    labels = np.random.default_rng(5).integers(1, 21, 3000)
+    kb, ks, kl = utils.batched_nms(T(boxes, dev), T(scores, dev), T(labels, dev), 0.5)
+    off = boxes + (labels.astype(np.float32) * np.float32(boxes.max()))[:, None]
+    k = oracle.nms(off, scores, 0.5)
+    np.testing.assert_array_equal(kl.cpu().numpy(), labels[k])
+    np.testing.assert_array_equal(ks.cpu().numpy(), scores[k])
+
+
+# ----------------------------------------------------------------- a13/a14
+def test_roi_level_map(dev, golden):
+    from frcnn_amd import ops
+    g = golden('levels.npz')
+    r = g['rois']
+    r5 = np.concatenate([np.zeros((1, r.shape[1]), np.float32), r], 0).T.copy()
+    np.testing.assert_array_equal(ops.roi_level_map(T(r5, dev), 56, 4).cpu().numpy(), g['levels'])
+
+
+def _rois(seed, n, batch):
+    b = inputs.random_boxes(seed, n, min_wh=1.0, max_wh=500.0)
+    b[:, :8] = np.array([[-20, -20, 10, 10], [990, 590, 1200, 700], [0, 0, 0, 0], [5, 5, 5.5, 5.2],
+                         [998.9, 598.9, 999, 599], [-300, -300, -200, -100], [0, 0, 999, 599],
+                         [100.25, 200.75, 101.0, 260.5]], np.float32).T
+    bi = np.random.default_rng(seed + 1).integers(0, batch, n).astype(np.float32)
+    return np.concatenate([bi[None], b], 0).T.copy()
+
+
+@pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
+@pytest.mark.parametrize('sampling', [2, 0])
+def test_roi_align_multilevel_vs_oracle(dev, layout, sampling):
+    from frcnn_amd import ops
+    grids = [(76, 128), (38, 64), (19, 32), (10, 16)]
+    feats = inputs.feature_maps(40, grids, 64, 2)
+    rois = _rois(41, 300, 2)
+    levels = oracle.roi_level_map(rois, 56.0, 4)
+    scales = [1 / 8, 1 / 16, 1 / 32, 1 / 64]
+    ref = oracle.roi_align(feats, rois, levels, scales, (7, 7), sampling)
+    ft = [T(f, dev) for f in feats]
+    if layout == 'nhwc':
+        ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), sampling).cpu().numpy()
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_roi_align_module_and_strided_view(dev):
+    from frcnn_amd.ops import RoIAlign
+    f = inputs.feature_maps(50, [(40, 60)], 32, 2)[0]
+    ft = T(f, dev)[:, :, ::2, ::2]  # non-contiguous (FPN P6 style)
+    rois = _rois(51, 200, 2)
+    out = RoIAlign((7, 7), 0.25, 2)(ft, T(rois, dev)).cpu().numpy()
+    ref = oracle.roi_align([np.ascontiguousarray(f[:, :, ::2, ::2])], rois, None, [0.25], (7, 7), 2)
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_roi_align_backward_vs_oracle(dev):
+    from frcnn_amd import ops
+    grids = [(38, 64), (19, 32)]
+    feats = inputs.feature_maps(60, grids, 16, 2)
+    rois = _rois(61, 120, 2)
+    levels = oracle.roi_level_map(rois, 56.0, 2)
+    scales = [1 / 16, 1 / 32]
+    g = np.random.default_rng(62).standard_normal((120, 16, 7, 7)).astype(np.float32)
+    ft = [T(f, dev).requires_grad_(True) for f in feats]
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2)
+    out.backward(T(g, dev))
+    ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, 2)
+    for a, r in zip(ft, ref):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), r, rtol=1e-4, atol=1e-5)
+
+
+def test_roi_pool_vs_oracle(dev):
+    from frcnn_amd.ops import RoIPool
+    f = inputs.feature_maps(70, [(38, 64)], 32, 2)[0]
+    rois = _rois(71, 150, 2)
+    out = RoIPool((7, 7), 1 / 16, sampling_ratio=2)(T(f, dev), T(rois, dev)).cpu().numpy()
+    ref, _ = oracle.roi_pool(f, rois, (7, 7), 1 / 16)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_basic_roi_extractor_matches_reference_flow(dev):
+    """Level mapping + per-level RoIAlign + scatter back (region.py:280-296) in one launch."""
+    from frcnn_amd.region import BasicRoIExtractor
+    ex = BasicRoIExtractor([dict(type='RoIAlign', spatial_scale=1 / s, sampling_ratio=2) for s in (4, 8, 16, 32)],
+                           output_size=(7, 7))
+    grids = [(152, 256), (76, 128), (38, 64), (19, 32)]
+    feats = inputs.feature_maps(80, grids, 32, 2)
+    props = [inputs.random_boxes(81, 300, min_wh=4, max_wh=599), inputs.random_boxes(82, 200, min_wh=4, max_wh=599)]
+    outs = ex([T(f, dev) for f in feats], [T(p, dev) for p in props])
+    for b, p in enumerate(props):
+        r5 = np.concatenate([np.full((1, p.shape[1]), b, np.float32), p], 0).T.copy()
+        lv = oracle.roi_level_map(r5, 56.0, 4)
+        ref = oracle.roi_align(feats, r5, lv, [1 / 4, 1 / 8, 1 / 16, 1 / 32], (7, 7), 2)
+        np.testing.assert_allclose(outs[b].cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------- end to end (cfg2 shapes)
+def test_faster_rcnn_fpn_forward_train_runs(dev):
+    import bench
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('numpy')
+    model, batch = bench.make_model_and_batch(dev, batch=2, seed=0)
+    losses = model.forward_train(*batch)
+    assert set(losses) == {'rpn_cls_loss', 'rpn_reg_loss', 'rcnn_0_cls_loss', 'rcnn_0_reg_loss'}
+    for k, v in losses.items():
+        assert torch.isfinite(v).all(), k
+    sum(losses.values()).backward()

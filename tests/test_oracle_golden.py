@@ -1,0 +1,179 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/gen_golden.py).  CPU only; these are what make the oracle a
+trustworthy checker for the GPU parity tests."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import inputs
+import oracle
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def fpn_anchors(strides=inputs.FPN_STRIDES, grids=inputs.FPN_GRIDS, scales=(8,), ratios=(0.5, 1.0, 2.0)):
+    return np.concatenate([oracle.anchor_grid(s, scales, ratios, s, g).reshape(4, -1) for s, g in zip(strides, grids)],
+                          1)
+
+
+def fpn_in_mask(anchors):
+    ingrid = np.concatenate([oracle.inside_grid_mask(3, inputs.IMG_SHAPE, g, s)
+                             for g, s in zip(inputs.FPN_GRIDS, inputs.FPN_STRIDES)]).astype(bool)
+    return ingrid & oracle.inside_anchor_mask(anchors, inputs.IMG_SHAPE, 0)
+
+
+def canon_ties(boxes, scores):
+    """Reorder columns so that runs of equal scores are sorted by coordinates."""
+    order = np.lexsort((boxes[3], boxes[2], boxes[1], boxes[0], -scores.astype(np.float64)))
+    return boxes[:, order]
+
+
+CASES = {
+    'fpn': (inputs.FPN_STRIDES, inputs.FPN_GRIDS, [8], [0.5, 1.0, 2.0]),
+    'retina': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [4 * 2 ** (i / 3) for i in range(3)], [0.5, 1.0, 2.0]),
+    'atss': (inputs.RETINA_STRIDES, inputs.RETINA_GRIDS, [8], [1.0]),
+    'c4': ([16], inputs.C4_GRIDS, [4, 8, 16, 32], [0.5, 1.0, 2.0]),
+}
+
+
+@pytest.mark.parametrize('name', sorted(CASES))
+def test_anchor_grid_bit_exact(golden, name):
+    g = golden('anchors.npz')
+    strides, grids, scales, ratios = CASES[name]
+    for l, (s, grid) in enumerate(zip(strides, grids)):
+        a = oracle.anchor_grid(s, scales, ratios, s, grid)
+        assert sha(a) == str(g['{}_{}_sha'.format(name, l)]), (name, l)
+
+
+def test_inside_mask(golden):
+    g = golden('assign.npz')
+    m = fpn_in_mask(fpn_anchors())
+    assert int(m.sum()) == int(g['mask_count'])
+    assert sha(m.astype(np.uint8)) == str(g['mask_sha'])
+
+
+def test_iou_table_bit_exact(golden):
+    g = golden('assign.npz')
+    a = inputs.random_boxes(11, 3000)
+    b = inputs.random_boxes(12, 40)
+    np.testing.assert_array_equal(oracle.calc_iou(a, b), g['rand_iou'])
+    np.testing.assert_array_equal(oracle.elem_iou(a[:, :40], b), g['rand_elem_iou'])
+    anc = fpn_anchors()
+    ina = anc[:, fpn_in_mask(anc)]
+    gts = inputs.voc_gts()
+    for i in range(2):
+        t = oracle.calc_iou(ina, gts[i][0])
+        assert sha(t) == str(g['iou_{}_sha'.format(i)])
+
+
+@pytest.mark.parametrize('tag,thr', [('rpn', (0.7, 0.3, 0.3)), ('rcnn', (0.5, 0.5, 0.5)), ('retina', (0.5, 0.4, 0.0))])
+def test_maxiou_assign_bit_exact(golden, tag, thr):
+    g = golden('assign.npz')
+    anc = fpn_anchors()
+    ina = anc[:, fpn_in_mask(anc)]
+    gts = inputs.voc_gts()
+    for i in range(8):
+        lab, miou = oracle.maxiou_assign(ina, gts[i][0], *thr)
+        np.testing.assert_array_equal(lab.astype(np.int8), g['{}_{}_labels'.format(tag, i)])
+        assert sha(miou) == str(g['{}_{}_miou_sha'.format(tag, i)])
+
+
+def test_assign_random_boxes(golden):
+    g = golden('assign.npz')
+    lab, miou = oracle.maxiou_assign(inputs.random_boxes(11, 3000), inputs.random_boxes(12, 40), 0.5, 0.4, 0.0)
+    np.testing.assert_array_equal(lab, g['rand_labels'])
+    np.testing.assert_array_equal(miou, g['rand_miou'])
+
+
+def test_numpy_choice_is_permutation_prefix():
+    """The device sampler's numpy-parity mode relies on legacy
+    choice(replace=False) == permutation(n)[:size] with identical RNG use."""
+    for n, size in ((10, 3), (1000, 744), (130000, 129872)):
+        a = np.arange(n) * 7 + 3
+        np.random.seed(5)
+        c = np.random.choice(a, size=size, replace=False)
+        after_c = np.random.randint(1 << 30)
+        np.random.seed(5)
+        p = np.random.permutation(n)
+        after_p = np.random.randint(1 << 30)
+        np.testing.assert_array_equal(c, a[p[:size]])
+        assert after_c == after_p
+
+
+def test_anchor_target_rpn(golden):
+    g = golden('targets.npz')
+    anc = fpn_anchors()
+    mask = fpn_in_mask(anc)
+    ina = anc[:, mask]
+    gts = inputs.voc_gts()
+    for i in range(4):
+        cls, reg = inputs.head_outputs(100 + i, inputs.FPN_GRIDS, 3, 1)
+        cls_out = np.concatenate([c[0].reshape(1, -1) for c in cls], 1)
+        reg_out = np.concatenate([r[0].reshape(4, -1) for r in reg], 1)
+        np.random.seed(1000 + i)
+        out = oracle.anchor_target(cls_out, reg_out, 1, ina, mask, gts[i][0], np.ones(gts[i][0].shape[1], np.int64),
+                                   (0.7, 0.3, 0.3), (256, 128), [0.0] * 4, [1.0] * 4)
+        for k, v in zip(('tar_cls_out', 'tar_reg_out', 'tar_labels', 'tar_anchors', 'tar_bbox'), out[:5]):
+            np.testing.assert_array_equal(v, g['rpn_{}_{}'.format(i, k)], err_msg=k)
+        np.testing.assert_allclose(out[5], g['rpn_{}_tar_param'.format(i)], rtol=1e-6, atol=1e-6)
+        assert np.random.randint(0, 2 ** 31 - 1) == int(g['rpn_{}_rng_after'.format(i)])
+
+
+def test_bbox_target_rcnn(golden):
+    g = golden('targets.npz')
+    gts = inputs.voc_gts()
+    for i in range(4):
+        props = inputs.random_boxes(200 + i, 2000, min_wh=8, max_wh=300)
+        np.random.seed(2000 + i)
+        out = oracle.bbox_target(props, gts[i][0], gts[i][1], (0.5, 0.5, 0.5), (512, 128), (0.0,) * 4,
+                                 (0.1, 0.1, 0.2, 0.2))
+        for k, v in zip(('tar_props', 'tar_bbox', 'tar_label'), out[:3]):
+            np.testing.assert_array_equal(v, g['rcnn_{}_{}'.format(i, k)], err_msg=k)
+        np.testing.assert_allclose(out[3], g['rcnn_{}_tar_param'.format(i)], rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(out[4], g['rcnn_{}_tar_is_gt'.format(i)])
+
+
+def test_encode_decode(golden):
+    g = golden('targets.npz')
+    base = inputs.random_boxes(300, 1000)
+    box = inputs.random_boxes(301, 1000)
+    delta = (np.random.default_rng(302).standard_normal((4 * 21, 1000)).astype(np.float32) * 0.5)
+    np.testing.assert_allclose(oracle.bbox2param(base, box), g['enc'], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(oracle.bbox2param(base, box, [0.0] * 4, [0.1, 0.1, 0.2, 0.2]), g['enc_norm'],
+                               rtol=1e-6, atol=1e-5)
+    sd = [0.1, 0.1, 0.2, 0.2]
+    np.testing.assert_allclose(oracle.param2bbox(base, delta[:4], [0.0] * 4, sd, inputs.IMG_SHAPE), g['dec'],
+                               rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(oracle.param2bbox(base, delta, [0.0] * 4, sd, inputs.IMG_SHAPE), g['dec_batched'],
+                               rtol=1e-6, atol=1e-4)
+    np.testing.assert_allclose(oracle.param2bbox(base, delta[:4]), g['dec_noclamp'], rtol=1e-6, atol=1e-4)
+
+
+def test_roi_level_map(golden):
+    g = golden('levels.npz')
+    rois = g['rois']
+    r5 = np.concatenate([np.zeros((1, rois.shape[1]), np.float32), rois], 0).T
+    np.testing.assert_array_equal(oracle.roi_level_map(r5, 56.0, 4), g['levels'])
+
+
+@pytest.mark.parametrize('tag,cfg', [('train', (2000, 2000, 2000, 0.7, 0.0)), ('test', (1000, 1000, 1000, 0.7, 0.0)),
+                                     ('minsz', (1000, 300, 1000, 0.5, 16.0))])
+def test_rpn_proposals(golden, tag, cfg):
+    """Pins the oracle's selection/decode/ordering around NMS (NMS itself unpinned)."""
+    g = golden('rpn.npz')
+    pre, post, mx, thr, minb = cfg
+    anchors = [oracle.anchor_grid(s, [8], [0.5, 1.0, 2.0], s, gr) for s, gr in zip(inputs.FPN_STRIDES, inputs.FPN_GRIDS)]
+    for i in range(2):
+        cls, reg = inputs.head_outputs(500 + i, inputs.FPN_GRIDS, 3, 1, reg_scale=0.5)
+        b, s = oracle.rpn_predict_single_image([c[0] for c in cls], [r[0] for r in reg], anchors, inputs.IMG_SHAPE,
+                                               1.6 * minb, pre, post, mx, thr)
+        rb, rs = g['{}_{}_boxes'.format(tag, i)], g['{}_{}_scores'.format(tag, i)]
+        assert b.shape == rb.shape
+        np.testing.assert_allclose(s, rs, rtol=1e-6, atol=1e-7)
+        # torch.topk orders exactly tied scores in an implementation-defined way:
+        # compare with each tie group in canonical (coordinate) order
+        b, rb = canon_ties(b, s), canon_ties(rb, rs)
+        np.testing.assert_allclose(b, rb, rtol=1e-5, atol=1e-3)
