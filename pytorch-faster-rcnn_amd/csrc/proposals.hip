@@ -9,7 +9,7 @@
 //  2. NMS mask + scan over all segments (nms.hip), keep <= post_nms.
 //  3. merge   (1 block per image): concatenate the levels' survivors and, if
 //     more than max_num, keep the best max_num by (score desc, concat order).
-#include "block_ops.h"
+#include "seg_topk.h"
 
 namespace frh {
 
@@ -55,26 +55,42 @@ __device__ __forceinline__ float score_of(const float* cls, int64_t hwa, int C, 
   return e1 / (e0 + e1);
 }
 
-__global__ void __launch_bounds__(kPropThreads) rpn_select_kernel(PropArgs p, ImgArgs ia) {
+// keys = order-preserving u32 of the score; also seeds the top-k state
+__global__ void rpn_keys_kernel(PropArgs p, uint32_t* keys, int64_t kld, int32_t* state) {
+  const int seg = blockIdx.y;
+  const int b = seg / p.L, l = seg % p.L;
+  const int64_t hwa = (int64_t)p.A * p.h[l] * p.w[l];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    int n = (int)hwa;
+    state[seg * TK_WORDS + TK_N] = n;
+    state[seg * TK_WORDS + TK_K] = (p.pre_nms > 0 && p.pre_nms < n) ? p.pre_nms : n;
+  }
+  if (i >= hwa) return;
+  const float* cls = p.cls[l] + (int64_t)b * p.C * hwa;
+  keys[(int64_t)seg * kld + i] = float_key(score_of(cls, hwa, p.C, i));
+}
+
+// one 1024-thread block per segment: order the selected anchors by
+// (score desc, index asc), decode + clamp, min-size filter (order preserving)
+__global__ void __launch_bounds__(kPropThreads) rpn_sort_decode_kernel(PropArgs p, ImgArgs ia, const uint32_t* keys,
+                                                                       int64_t kld, const int32_t* state,
+                                                                       const int32_t* sel, int64_t sel_ld) {
   extern __shared__ uint64_t skeys[];
-  __shared__ TopkSmem sm;
   __shared__ int wave_tot[kPropThreads / 64];
   const int seg = blockIdx.x;
   const int b = seg / p.L, l = seg % p.L;
   const int64_t hwa = (int64_t)p.A * p.h[l] * p.w[l];
-  const int n = (int)hwa;
-  const float* cls = p.cls[l] + (int64_t)b * p.C * hwa;
   const float* reg = p.reg[l] + (int64_t)b * 4 * hwa;
-  const int k = (p.pre_nms > 0 && p.pre_nms < n) ? p.pre_nms : n;
-  int32_t* sel = p.sel_idx + (int64_t)seg * p.P;
-  auto key_of = [&](int i) -> uint32_t { return float_key(score_of(cls, hwa, p.C, i)); };
-  const int m = block_topk_select(key_of, n, k, sel, sm);
+  const int m = state[seg * TK_WORDS + TK_K];
   const int P2 = next_pow2(m > 1 ? m : 1);
+  const uint32_t* kk = keys + (int64_t)seg * kld;
+  const int32_t* sl = sel + (int64_t)seg * sel_ld;
   for (int j = threadIdx.x; j < P2; j += blockDim.x) {
     uint64_t key = 0;
     if (j < m) {
-      int i = sel[j];
-      key = ((uint64_t)key_of(i) << 32) | (uint32_t)(~(uint32_t)i);
+      int i = sl[j];
+      key = ((uint64_t)kk[i] << 32) | (uint32_t)(~(uint32_t)i);
     }
     skeys[j] = key;
   }
@@ -144,73 +160,67 @@ struct MergeArgs {
   int32_t* out_counts;
 };
 
-__global__ void __launch_bounds__(kPropThreads) rpn_merge_kernel(MergeArgs p) {
-  extern __shared__ uint64_t skeys[];
-  __shared__ int lvl_off[FRH_MAX_LEVELS + 1];
-  const int b = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int l = 0; l < p.L; ++l) {
-      lvl_off[l] = acc;
-      acc += p.keep_count[b * p.L + l];
-    }
-    lvl_off[p.L] = acc;
+// Cross-level top-k as a merge: each level's survivors are already in
+// (score desc) order, so the rank of survivor j of level l among all levels
+// (score desc, concatenation order on ties) is j + sum over other levels of
+// a binary search (upper bound for earlier levels, lower bound for later).
+// Grid: (survivor chunks of 256, level, image); no sort, no LDS.
+__device__ __forceinline__ float kept_score(const MergeArgs& p, int seg, int j) {
+  return p.sel_scores[(int64_t)seg * p.P + p.keep[(int64_t)seg * p.P + j]];
+}
+
+__global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
+  const int b = blockIdx.z, l = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int seg = b * p.L + l;
+  const int cnt = p.keep_count[seg];
+  int total = 0, base = 0;
+  for (int q = 0; q < p.L; ++q) {
+    int c = p.keep_count[b * p.L + q];
+    base += q < l ? c : 0;
+    total += c;
   }
-  __syncthreads();
-  const int total = lvl_off[p.L];
-  auto locate = [&](int qpos, int* seg, int* pos) {
-    int l = 0;
-    while (l + 1 < p.L && qpos >= lvl_off[l + 1]) ++l;
-    *seg = b * p.L + l;
-    *pos = p.keep[(int64_t)(*seg) * p.P + (qpos - lvl_off[l])];
-  };
-  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
-  float* os = p.out_scores + (int64_t)b * p.out_cap;
-  if (p.max_num > 0 && total > p.max_num) {  // rpn_head.py:112-118
-    const int P2 = next_pow2(total);
-    for (int q = threadIdx.x; q < P2; q += blockDim.x) {
-      uint64_t key = 0;
-      if (q < total) {
-        int seg, pos;
-        locate(q, &seg, &pos);
-        key = ((uint64_t)float_key(p.sel_scores[(int64_t)seg * p.P + pos]) << 32) | (uint32_t)(~(uint32_t)q);
+  const bool cut = p.max_num > 0 && total > p.max_num;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && l == 0) p.out_counts[b] = cut ? p.max_num : total;
+  if (j >= cnt) return;
+  const int pos = p.keep[(int64_t)seg * p.P + j];
+  const float s = p.sel_scores[(int64_t)seg * p.P + pos];
+  int rank = base + j;
+  if (cut) {
+    rank = j;
+    for (int q = 0; q < p.L; ++q) {
+      if (q == l) continue;
+      const int oseg = b * p.L + q;
+      int lo = 0, hi = p.keep_count[oseg];
+      // count of survivors of level q ordered before (s, this level)
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        float o = kept_score(p, oseg, mid);
+        bool before = q < l ? (o >= s) : (o > s);
+        if (before)
+          lo = mid + 1;
+        else
+          hi = mid;
       }
-      skeys[q] = key;
+      rank += lo;
     }
-    __syncthreads();
-    block_bitonic_sort_desc(skeys, P2);
-    for (int j = threadIdx.x; j < p.max_num; j += blockDim.x) {
-      int q = (int)(~(uint32_t)skeys[j]);
-      int seg, pos;
-      locate(q, &seg, &pos);
-      float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + pos];
-      ob[j] = bx.x;
-      ob[p.out_cap + j] = bx.y;
-      ob[2 * p.out_cap + j] = bx.z;
-      ob[3 * p.out_cap + j] = bx.w;
-      os[j] = p.sel_scores[(int64_t)seg * p.P + pos];
-    }
-    if (threadIdx.x == 0) p.out_counts[b] = p.max_num;
-  } else {
-    for (int q = threadIdx.x; q < total; q += blockDim.x) {
-      int seg, pos;
-      locate(q, &seg, &pos);
-      float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + pos];
-      ob[q] = bx.x;
-      ob[p.out_cap + q] = bx.y;
-      ob[2 * p.out_cap + q] = bx.z;
-      ob[3 * p.out_cap + q] = bx.w;
-      os[q] = p.sel_scores[(int64_t)seg * p.P + pos];
-    }
-    if (threadIdx.x == 0) p.out_counts[b] = total;
+    if (rank >= p.max_num) return;
   }
+  float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + pos];
+  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
+  ob[rank] = bx.x;
+  ob[p.out_cap + rank] = bx.y;
+  ob[2 * p.out_cap + rank] = bx.z;
+  ob[3 * p.out_cap + rank] = bx.w;
+  p.out_scores[(int64_t)b * p.out_cap + rank] = s;
 }
 
 static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, cnt, keep, kcnt, mask, total;
+  size_t boxes, scores, idx, cnt, keep, kcnt, mask, keys, hist, state, cand, total;
+  int64_t nmax;
 };
 
 static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int32_t A, int32_t pre_nms) {
@@ -222,6 +232,12 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
     if (k > P) P = (int)k;
   }
   z.P = P;
+  int64_t nmax = 1;
+  for (int l = 0; l < L; ++l) {
+    int64_t n = (int64_t)A * grid_hw[2 * l] * grid_hw[2 * l + 1];
+    if (n > nmax) nmax = n;
+  }
+  z.nmax = nmax;
   const size_t S = (size_t)B * L;
   z.boxes = 0;
   z.scores = z.boxes + al(S * P * 4 * sizeof(float));
@@ -230,7 +246,11 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
   z.keep = z.cnt + al(S * sizeof(int32_t));
   z.kcnt = z.keep + al(S * P * sizeof(int32_t));
   z.mask = z.kcnt + al(S * sizeof(int32_t));
-  z.total = z.mask + al(nms_mask_bytes((int32_t)S, P));
+  z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
+  z.hist = z.keys + al(S * (size_t)nmax * sizeof(uint32_t));
+  z.state = z.hist + al(tk_hist_bytes((int)S));
+  z.cand = z.state + al(tk_state_bytes((int)S));
+  z.total = z.cand + al(tk_cand_bytes((int)S));
   return z;
 }
 
@@ -298,11 +318,20 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
     ia.min_size[b] = min_size[b];
   }
   const int S = num_imgs * num_levels;
+  // 1. keys + top-k state, 2. segmented top-k, 3. order + decode + min-size
+  uint32_t* keys = reinterpret_cast<uint32_t*>(ws + z.keys);
+  TopkBuffers tb{keys, z.nmax, reinterpret_cast<uint32_t*>(ws + z.hist), reinterpret_cast<int32_t*>(ws + z.state),
+                 p.sel_idx, z.P, reinterpret_cast<int32_t*>(ws + z.cand), S};
+  FRH_HIP(hipMemsetAsync(ws + z.hist, 0, z.cand - z.hist, st));  // hist + state
+  hipLaunchKernelGGL(rpn_keys_kernel, dim3((unsigned)((z.nmax + 255) / 256), (unsigned)S), dim3(256), 0, st, p, keys,
+                     z.nmax, tb.state);
+  tk_launch(tb, z.nmax, st);
   const size_t lds_sel = (size_t)next_pow2(z.P) * sizeof(uint64_t);
   if (lds_sel > 65536)
-    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_select_kernel),
+    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_sort_decode_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sel));
-  hipLaunchKernelGGL(rpn_select_kernel, dim3(S), dim3(kPropThreads), lds_sel, st, p, ia);
+  hipLaunchKernelGGL(rpn_sort_decode_kernel, dim3(S), dim3(kPropThreads), lds_sel, st, p, ia, keys, z.nmax,
+                     tb.state, p.sel_idx, (int64_t)z.P);
   int32_t r = check_launch("rpn_select");
   if (r) return r;
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);
@@ -312,10 +341,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   if (r) return r;
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};
-  const size_t lds_merge = (size_t)next_pow2((int)(post * num_levels)) * sizeof(uint64_t);
-  if (lds_merge > 65536)
-    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_merge_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_merge));
-  hipLaunchKernelGGL(rpn_merge_kernel, dim3(num_imgs), dim3(kPropThreads), lds_merge, st, mp);
+  dim3 mg((unsigned)((post + 255) / 256), (unsigned)num_levels, (unsigned)num_imgs);
+  hipLaunchKernelGGL(rpn_merge_kernel, mg, dim3(256), 0, st, mp);
   return check_launch("rpn_merge");
 }

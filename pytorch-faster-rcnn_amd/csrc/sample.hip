@@ -5,7 +5,7 @@
 // chunk block adds the counts of its preceding chunks and ranks its own
 // elements with wave ballots (coalesced: round r of a chunk reads elements
 // base + r*256 + tid).
-#include "block_ops.h"
+#include "seg_topk.h"
 
 namespace frh {
 
@@ -118,30 +118,56 @@ __global__ void sample_apply_kernel(const int64_t* lab_in, int64_t label_seg_str
   lab_out[(int64_t)s * label_seg_stride + box] = lab_in[(int64_t)s * label_seg_stride + box];
 }
 
-// device-RNG sampler: one 1024-thread block per (segment, pos|neg)
-constexpr int kSelThreads = 1024;
-__global__ void __launch_bounds__(kSelThreads)
-    sample_random_kernel(const int64_t* lab_in, int64_t label_seg_stride, const int32_t* pos_list,
-                         const int32_t* neg_list, int64_t list_seg_stride, const int32_t* counts,
-                         int max_num, int pos_num, uint64_t seed, int32_t* sel_scratch,
-                         int64_t* lab_out) {
-  __shared__ TopkSmem sm;
-  const int s = blockIdx.x;
-  const int which = blockIdx.y;
-  const int npos = counts[s * 2 + 0], nneg = counts[s * 2 + 1];
-  const int kpos = npos < pos_num ? npos : pos_num;
-  const int nslots = max_num - kpos;
-  const int k = which == 0 ? kpos : (nneg < nslots ? nneg : nslots);
-  const int n = which == 0 ? npos : nneg;
-  const int32_t* list = (which == 0 ? pos_list : neg_list) + (int64_t)s * list_seg_stride;
-  int32_t* sel = sel_scratch + ((int64_t)s * 2 + which) * list_seg_stride;
-  const uint32_t salt = (uint32_t)(s * 2 + which);
-  auto key_of = [&](int i) -> uint32_t { return ~hash_u32(seed, salt, (uint32_t)list[i]); };
-  int m = block_topk_select(key_of, n, k, sel, sm);
-  for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    int64_t box = list[sel[j]];
-    lab_out[(int64_t)s * label_seg_stride + box] = lab_in[(int64_t)s * label_seg_stride + box];
+// device-RNG sampler: virtual top-k segment v = 2s (positives) / 2s+1
+// (negatives); key = candidate ? (~hash(seed, v, box) | 1) : 0, so the k
+// largest keys are a uniform k-subset of the candidates.  Also resets
+// labels_out to -1 and counts the candidates.
+__global__ void sampler_keys_kernel(const int64_t* lab_in, int64_t lstride, const int32_t* num, uint64_t seed,
+                                    uint32_t* keys, int64_t kld, int32_t* counts, int64_t* lab_out) {
+  __shared__ int scratch[4];
+  const int s = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = num[s];
+  bool pos = false, neg = false;
+  if (i < n) {
+    int64_t l = lab_in[(int64_t)s * lstride + i];
+    pos = l > 0;
+    neg = l == 0;
+    lab_out[(int64_t)s * lstride + i] = -1;
   }
+  if (i < kld) {
+    keys[(int64_t)(2 * s) * kld + i] = pos ? ((~hash_u32(seed, 2 * s, (uint32_t)i)) | 1u) : 0u;
+    keys[(int64_t)(2 * s + 1) * kld + i] = neg ? ((~hash_u32(seed, 2 * s + 1, (uint32_t)i)) | 1u) : 0u;
+  }
+  int cp = block_sum(pos ? 1 : 0, scratch);
+  int cn = block_sum(neg ? 1 : 0, scratch);
+  if (threadIdx.x == 0) {
+    if (cp) atomicAdd(&counts[2 * s], cp);
+    if (cn) atomicAdd(&counts[2 * s + 1], cn);
+  }
+}
+
+__global__ void sampler_k_kernel(const int32_t* num, const int32_t* counts, int S, int max_num, int pos_num,
+                                 int32_t* state) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  int npos = counts[2 * s], nneg = counts[2 * s + 1];
+  int kp = npos < pos_num ? npos : pos_num;
+  int slots = max_num - kp;
+  int kn = nneg < slots ? nneg : slots;
+  state[(2 * s) * TK_WORDS + TK_N] = num[s];
+  state[(2 * s) * TK_WORDS + TK_K] = kp;
+  state[(2 * s + 1) * TK_WORDS + TK_N] = num[s];
+  state[(2 * s + 1) * TK_WORDS + TK_K] = kn;
+}
+
+__global__ void sampler_apply_topk_kernel(const int64_t* lab_in, int64_t lstride, const int32_t* state,
+                                          const int32_t* sel, int64_t sel_ld, int64_t* lab_out) {
+  const int v = blockIdx.y, s = v >> 1;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= state[v * TK_WORDS + TK_K]) return;
+  int64_t box = sel[(int64_t)v * sel_ld + j];
+  lab_out[(int64_t)s * lstride + box] = lab_in[(int64_t)s * lstride + box];
 }
 
 int32_t launch_compact_lists(int32_t S, const int64_t* labels, int64_t label_seg_stride,
@@ -165,13 +191,30 @@ size_t compact_workspace(int32_t S, int64_t max_n) {
 
 using namespace frh;
 
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct SampLayout {
+  size_t keys, hist, state, counts, cand, sel, total;
+};
+
+static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
+  SampLayout z{};
+  const size_t n = (size_t)(max_boxes > 0 ? max_boxes : 1);
+  const int V = 2 * S;
+  z.keys = 0;
+  z.hist = z.keys + al256((size_t)V * n * sizeof(uint32_t));
+  z.state = z.hist + al256(tk_hist_bytes(V));
+  z.counts = z.state + al256(tk_state_bytes(V));
+  z.cand = z.counts + al256((size_t)V * sizeof(int32_t));
+  z.sel = z.cand + al256(tk_cand_bytes(V));
+  z.total = z.sel + al256((size_t)V * n * sizeof(int32_t));
+  return z;
+}
+
 extern "C" size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes) {
-  size_t a = compact_workspace(num_segs, max_boxes);
-  a = (a + 255) & ~(size_t)255;
-  size_t lists = (size_t)num_segs * 2 * (size_t)(max_boxes > 0 ? max_boxes : 1) * sizeof(int32_t);  // pos/neg
-  size_t sel = lists;
-  size_t cnt = (size_t)num_segs * 2 * sizeof(int32_t);
-  return a + ((lists + 255) & ~(size_t)255) + ((sel + 255) & ~(size_t)255) + cnt;
+  size_t a = al256(compact_workspace(num_segs, max_boxes));
+  size_t b = samp_layout(num_segs, max_boxes).total;
+  return a > b ? a : b;
 }
 
 extern "C" int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
@@ -224,24 +267,23 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
   FRH_REQUIRE(workspace && ws_bytes >= frh_sample_workspace(num_segs, max_boxes), "workspace too small");
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
-  size_t a = (compact_workspace(num_segs, max_boxes) + 255) & ~(size_t)255;
-  int32_t* chunk_counts = reinterpret_cast<int32_t*>(ws);
-  int32_t* lists = reinterpret_cast<int32_t*>(ws + a);
-  size_t lists_b = ((size_t)num_segs * 2 * max_boxes * sizeof(int32_t) + 255) & ~(size_t)255;
-  int32_t* sel = reinterpret_cast<int32_t*>(ws + a + lists_b);
-  int32_t* counts = reinterpret_cast<int32_t*>(ws + a + 2 * lists_b);
-  int32_t* pos_list = lists;
-  int32_t* neg_list = lists + (int64_t)num_segs * max_boxes;
-  int preds[2] = {kPos, kNeg};
-  int32_t* lp[2] = {pos_list, neg_list};
-  int32_t r = launch_compact_lists(num_segs, labels_in, label_seg_stride, num_boxes, max_boxes, 2, preds, lp,
-                                   max_boxes, counts, chunk_counts, st);
-  if (r) return r;
+  SampLayout z = samp_layout(num_segs, max_boxes);
+  const int V = 2 * num_segs;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(ws + z.keys);
+  int32_t* state = reinterpret_cast<int32_t*>(ws + z.state);
+  int32_t* counts = reinterpret_cast<int32_t*>(ws + z.counts);
+  int32_t* sel = reinterpret_cast<int32_t*>(ws + z.sel);
+  FRH_HIP(hipMemsetAsync(ws + z.hist, 0, z.cand - z.hist, st));  // hist + state + counts
   dim3 g1((unsigned)((max_boxes + 255) / 256), (unsigned)num_segs);
-  hipLaunchKernelGGL(fill_i64_kernel, g1, dim3(256), 0, st, labels_out, label_seg_stride, num_boxes,
-                     max_boxes, (int64_t)-1);
-  hipLaunchKernelGGL(sample_random_kernel, dim3((unsigned)num_segs, 2), dim3(kSelThreads), 0, st, labels_in,
-                     label_seg_stride, pos_list, neg_list, (int64_t)max_boxes, counts, max_num, pos_num, seed,
-                     sel, labels_out);
+  hipLaunchKernelGGL(sampler_keys_kernel, g1, dim3(256), 0, st, labels_in, label_seg_stride, num_boxes, seed, keys,
+                     max_boxes, counts, labels_out);
+  hipLaunchKernelGGL(sampler_k_kernel, dim3((unsigned)((num_segs + 63) / 64)), dim3(64), 0, st, num_boxes, counts,
+                     num_segs, max_num, pos_num, state);
+  TopkBuffers tb{keys, max_boxes, reinterpret_cast<uint32_t*>(ws + z.hist), state, sel, max_boxes,
+                 reinterpret_cast<int32_t*>(ws + z.cand), V};
+  tk_launch(tb, max_boxes, st);
+  dim3 g2((unsigned)((max_num + 255) / 256), (unsigned)V);
+  hipLaunchKernelGGL(sampler_apply_topk_kernel, g2, dim3(256), 0, st, labels_in, label_seg_stride, state, sel,
+                     (int64_t)max_boxes, labels_out);
   return check_launch("frh_sample_random");
 }
