@@ -76,7 +76,7 @@ def make_model_and_batch(dev, batch=2, seed=0, rank=0):
 def roi_align_bytes(rec):
     """Algorithmic bytes of one RoIAlign forward launch:
     4*C*(sum_K ph*pw + sum_img sum_{levels with >=1 roi} H_l*W_l) + 20*K."""
-    _, _, rois, levels, shapes, (ph, pw) = rec
+    _, _, rois, levels, shapes, (ph, pw) = rec[:6]
     K = rois.shape[0]
     C = shapes[0][1]
     bidx = rois[:, 0].long()

@@ -169,6 +169,496 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_kernel(RoiLevels lv
   }
 }
 
+// Staged variant (fixed sampling ratio): the RoI's bilinear taps all fall in
+// the window [y0, y1] x [x0, x1] of its level (<= ~30x30 cells after FPN level
+// mapping).  The workgroup copies that window for as many channels as fit in
+// 48 KB of LDS with row-contiguous (coalesced) loads, then evaluates the
+// 16 taps of every output element from LDS.  Same arithmetic order as the
+// direct kernel, so outputs are identical.
+constexpr int kStageTaps = 64;
+constexpr int kStageFloats = 12288;
+
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_staged_kernel(RoiLevels lv, RoiCfg c,
+                                                                           float* __restrict__ out) {
+  __shared__ Tap ty[kStageTaps], tx[kStageTaps];
+  __shared__ float win[kStageFloats];
+  __shared__ int wb[4];
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int ny = c.ph * g.gh, nx = c.pw * g.gw;
+  for (int e = threadIdx.x; e < ny + nx; e += blockDim.x) {
+    if (e < ny) {
+      int p = e / g.gh, i = e - p * g.gh;
+      ty[e] = make_tap(sample_y(g, p, i), H);
+    } else {
+      int q = e - ny, p = q / g.gw, i = q - p * g.gw;
+      tx[q] = make_tap(sample_x(g, p, i), W);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
+    for (int e = 0; e < ny; ++e)
+      if (ty[e].valid) {
+        y0 = min(y0, ty[e].lo);
+        y1 = max(y1, ty[e].hi);
+      }
+    for (int e = 0; e < nx; ++e)
+      if (tx[e].valid) {
+        x0 = min(x0, tx[e].lo);
+        x1 = max(x1, tx[e].hi);
+      }
+    wb[0] = y0;
+    wb[1] = y1;
+    wb[2] = x0;
+    wb[3] = x1;
+  }
+  __syncthreads();
+  const int y0 = wb[0], x0 = wb[2];
+  const int WH = wb[1] - y0 + 1, WW = wb[3] - x0 + 1;
+  const int area = (wb[1] >= 0 && wb[3] >= 0) ? WH * WW : 0;
+  const int nbins = c.ph * c.pw;
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* o = out + (k * c.C + c0) * nbins;
+  int csub = area > 0 ? min(nch, kStageFloats / area) : nch;
+  if (csub == 0) {
+    // window too large for LDS (only for tiny pooled sizes on huge RoIs): direct gather
+    for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
+      const int cl = item / nbins, bin = item - cl * nbins;
+      const int py = bin / c.pw, px = bin - py * c.pw;
+      const float* f = base + (int64_t)(c0 + cl) * scs;
+      float acc = 0.0f;
+      for (int iy = 0; iy < g.gh; ++iy) {
+        const Tap a = ty[py * g.gh + iy];
+        for (int ix = 0; ix < g.gw; ++ix) {
+          const Tap bx = tx[px * g.gw + ix];
+          float val = 0.0f;
+          if (a.valid && bx.valid) {
+            float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
+            val = ((w1 * f[a.lo * sy + bx.lo * sx] + w2 * f[a.lo * sy + bx.hi * sx]) +
+                   w3 * f[a.hi * sy + bx.lo * sx]) + w4 * f[a.hi * sy + bx.hi * sx];
+          }
+          acc = acc + val;
+        }
+      }
+      o[item] = acc / g.count;
+    }
+    return;
+  }
+  for (int cc = 0; cc < nch; cc += csub) {
+    const int cn = min(csub, nch - cc);
+    const int total = cn * area;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      int ch = e / area, rem = e - ch * area;
+      int r = rem / WW, col = rem - r * WW;
+      win[e] = base[(int64_t)(c0 + cc + ch) * scs + (int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx];
+    }
+    __syncthreads();
+    for (int item = threadIdx.x; item < cn * nbins; item += blockDim.x) {
+      const int cl = item / nbins, bin = item - cl * nbins;
+      const int py = bin / c.pw, px = bin - py * c.pw;
+      const float* w = win + cl * area;
+      float acc = 0.0f;
+      for (int iy = 0; iy < g.gh; ++iy) {
+        const Tap a = ty[py * g.gh + iy];
+        for (int ix = 0; ix < g.gw; ++ix) {
+          const Tap bx = tx[px * g.gw + ix];
+          float val = 0.0f;
+          if (a.valid && bx.valid) {
+            const int ylo = (a.lo - y0) * WW, yhi = (a.hi - y0) * WW;
+            const int xlo = bx.lo - x0, xhi = bx.hi - x0;
+            float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
+            val = ((w1 * w[ylo + xlo] + w2 * w[ylo + xhi]) + w3 * w[yhi + xlo]) + w4 * w[yhi + xhi];
+          }
+          acc = acc + val;
+        }
+      }
+      o[(cc + cl) * nbins + bin] = acc / g.count;
+    }
+    __syncthreads();
+  }
+}
+
+// Register-tap variant (sampling ratio 2, any pooled size with ph*pw <= 256):
+// thread t owns ONE output bin (t % nbins) for a fixed channel residue
+// (t / nbins), so its 2x2 sample taps (rows and columns: low/high index +
+// weights) are computed once into registers; the thread then walks the
+// channels of its chunk with stride (threads / nbins), issuing the 16 tap
+// loads of each channel back to back.  No LDS, no per-item division.
+template <int SR>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_regtap_kernel(RoiLevels lv, RoiCfg c,
+                                                                           float* __restrict__ out) {
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int groups = kRoiThreads / nbins;
+  const int t = threadIdx.x;
+  if (t >= groups * nbins) return;
+  const int bin = t % nbins, cg = t / nbins;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  // per-sample offsets and weights (invalid samples contribute exactly 0)
+  int32_t off[SR][SR][4];  // offsets within one channel plane fit in 32 bits
+  float wt[SR][SR][4];
+  bool ok[SR][SR];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      off[iy][ix][0] = (int32_t)(a.lo * sy + b.lo * sx);
+      off[iy][ix][1] = (int32_t)(a.lo * sy + b.hi * sx);
+      off[iy][ix][2] = (int32_t)(a.hi * sy + b.lo * sx);
+      off[iy][ix][3] = (int32_t)(a.hi * sy + b.hi * sx);
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
+  float* o = out + (k * c.C + c0) * nbins + bin;
+  for (int ch = cg; ch < nch; ch += groups) {
+    const float* f = base + (int64_t)ch * scs;
+    float v[SR][SR][4];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[iy][ix][q] = f[off[iy][ix][q]];  // invalid taps point at (0,0)
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    o[(int64_t)ch * nbins] = acc / g.count;
+  }
+}
+
+__device__ __forceinline__ float pick4(const float4& v, int i) {
+  const float a = (i & 1) ? v.y : v.x;
+  const float b = (i & 1) ? v.w : v.z;
+  return (i & 2) ? b : a;
+}
+
+// Row-vector variant (sampling ratio 2, unit x stride, ph*pw <= 256).
+// After FPN level mapping a bin spans <= ~4 feature cells, so the x taps of a
+// bin's two x-samples (x_lo0 .. x_hi1) fall inside 4 consecutive cells: ONE
+// 16-byte load per tap row (rows y_lo/y_hi of the two y-samples) fetches all
+// of them -> 4 vector loads per (bin, channel) instead of 16 dword gathers.
+// The window start xb = min(x_lo0, W - 4) keeps the load inside the row (the
+// KFD runs gfx9+ queues in unaligned mode, so xb need not be 4-aligned).
+// Bins whose taps do not fit (huge clamped RoIs, maps narrower than 4) use
+// the dword gather.  Arithmetic identical to the reference order.
+template <int U>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_vec4_kernel(RoiLevels lv, RoiCfg c,
+                                                                         float* __restrict__ out) {
+  constexpr int SR = 2;
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int groups = kRoiThreads / nbins;
+  const int t = threadIdx.x;
+  if (t >= groups * nbins) return;
+  const int bin = t % nbins, cg = t / nbins;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  int xmin = 1 << 30, xmax = -1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i)
+    if (tx[i].valid) {
+      xmin = min(xmin, tx[i].lo);
+      xmax = max(xmax, tx[i].hi);
+    }
+  const int xb = min(xmin, W - 4);
+  const bool fit = sx == 1 && W >= 4 && xmax >= 0 && xmax - xb <= 3;
+  int cl[SR], chh[SR], rowo[SR][2];
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    cl[i] = tx[i].valid ? tx[i].lo - xb : 0;
+    chh[i] = tx[i].valid ? tx[i].hi - xb : 0;
+    rowo[i][0] = ty[i].valid ? (int)(ty[i].lo * sy) : 0;
+    rowo[i][1] = ty[i].valid ? (int)(ty[i].hi * sy) : 0;
+  }
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
+  float* o = out + (k * c.C + c0) * nbins + bin;
+  if (fit) {
+    const float* bx = base + xb;
+    auto bin_value = [&](const float4 (&rv)[SR][2]) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const float v1 = pick4(rv[iy][0], cl[ix]), v2 = pick4(rv[iy][0], chh[ix]);
+          const float v3 = pick4(rv[iy][1], cl[ix]), v4 = pick4(rv[iy][1], chh[ix]);
+          float val = ((wt[iy][ix][0] * v1 + wt[iy][ix][1] * v2) + wt[iy][ix][2] * v3) + wt[iy][ix][3] * v4;
+          acc = acc + (ok[iy][ix] ? val : 0.0f);
+        }
+      return acc / g.count;
+    };
+    int ch = cg;
+    // U channels per step: all 4U row loads are issued before any is consumed
+    for (; ch + (U - 1) * groups < nch; ch += U * groups) {
+      float4 rv[U][SR][2];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float* f = bx + (int64_t)(ch + u * groups) * scs;
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy) {
+          rv[u][iy][0] = *reinterpret_cast<const float4*>(f + rowo[iy][0]);
+          rv[u][iy][1] = *reinterpret_cast<const float4*>(f + rowo[iy][1]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) o[(int64_t)(ch + u * groups) * nbins] = bin_value(rv[u]);
+    }
+    for (; ch < nch; ch += groups) {
+      const float* f = bx + (int64_t)ch * scs;
+      float4 rv[SR][2];
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy) {
+        rv[iy][0] = *reinterpret_cast<const float4*>(f + rowo[iy][0]);
+        rv[iy][1] = *reinterpret_cast<const float4*>(f + rowo[iy][1]);
+      }
+      o[(int64_t)ch * nbins] = bin_value(rv);
+    }
+  } else {
+    for (int ch = cg; ch < nch; ch += groups) {
+      const float* f = base + (int64_t)ch * scs;
+      float acc = 0.0f;
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const int64_t q0 = ok[iy][ix] ? (int64_t)tx[ix].lo * sx : 0, q1 = ok[iy][ix] ? (int64_t)tx[ix].hi * sx : 0;
+          const float v1 = f[rowo[iy][0] + q0], v2 = f[rowo[iy][0] + q1];
+          const float v3 = f[rowo[iy][1] + q0], v4 = f[rowo[iy][1] + q1];
+          float val = ((wt[iy][ix][0] * v1 + wt[iy][ix][1] * v2) + wt[iy][ix][2] * v3) + wt[iy][ix][3] * v4;
+          acc = acc + (ok[iy][ix] ? val : 0.0f);
+        }
+      o[(int64_t)ch * nbins] = acc / g.count;
+    }
+  }
+}
+
+// Staged + register-tap variant (sampling ratio SR, ph*pw <= 256).
+// After FPN level mapping a RoI covers few feature cells (random-init cfg2:
+// median side ~5 cells on P2), so its 16*ph*pw taps per channel hit a small
+// window many times over.  Thread (bin, channel group) keeps its bin's tap
+// offsets (relative to the window) and weights in registers; the workgroup
+// stages the window rows of a channel sub-chunk in LDS with row-contiguous
+// loads, then every output element is 16 LDS reads + the reference's
+// arithmetic.  Identical results to the direct kernel.
+constexpr int kWinFloats = 12288;  // 48 KB window buffer
+
+template <int SR>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_winreg_kernel(RoiLevels lv, RoiCfg c,
+                                                                           float* __restrict__ out) {
+  __shared__ float win[kWinFloats];
+  __shared__ int wb[4];
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int groups = kRoiThreads / nbins;
+  const int t = threadIdx.x;
+  const bool active = t < groups * nbins;
+  const int bin = active ? t % nbins : 0, cg = active ? t / nbins : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  if (t == 0) {
+    wb[0] = 1 << 30;
+    wb[1] = -1;
+    wb[2] = 1 << 30;
+    wb[3] = -1;
+  }
+  __syncthreads();
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  if (active) {
+    int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+      if (ty[i].valid) {
+        ylo = min(ylo, ty[i].lo);
+        yhi = max(yhi, ty[i].hi);
+      }
+      if (tx[i].valid) {
+        xlo = min(xlo, tx[i].lo);
+        xhi = max(xhi, tx[i].hi);
+      }
+    }
+    if (yhi >= 0 && xhi >= 0) {
+      atomicMin(&wb[0], ylo);
+      atomicMax(&wb[1], yhi);
+      atomicMin(&wb[2], xlo);
+      atomicMax(&wb[3], xhi);
+    }
+  }
+  __syncthreads();
+  const int y0 = wb[0], x0 = wb[2];
+  const bool empty = wb[1] < 0;
+  const int WH = empty ? 0 : wb[1] - y0 + 1, WW = empty ? 0 : wb[3] - x0 + 1;
+  const int area = WH * WW;
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
+  float* o = out + (k * c.C + c0) * nbins + bin;
+  int woff[SR][SR][4];
+  float wt[SR][SR][4];
+  bool ok[SR][SR];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      const int rl = ok[iy][ix] ? (a.lo - y0) * WW : 0, rh = ok[iy][ix] ? (a.hi - y0) * WW : 0;
+      const int cl = ok[iy][ix] ? b.lo - x0 : 0, ch = ok[iy][ix] ? b.hi - x0 : 0;
+      woff[iy][ix][0] = rl + cl;
+      woff[iy][ix][1] = rl + ch;
+      woff[iy][ix][2] = rh + cl;
+      woff[iy][ix][3] = rh + ch;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  if (empty) {
+    if (active)
+      for (int chn = cg; chn < nch; chn += groups) o[(int64_t)chn * nbins] = 0.0f / g.count;
+    return;
+  }
+  const int csub = min(nch, kWinFloats / area);
+  if (csub == 0) {
+    // window larger than the LDS buffer: gather straight from global memory
+    if (!active) return;
+    for (int chn = cg; chn < nch; chn += groups) {
+      const float* f = base + (int64_t)chn * scs;
+      float acc = 0.0f;
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const Tap a = ty[iy], b = tx[ix];
+          const int64_t r0 = (int64_t)a.lo * sy, r1 = (int64_t)a.hi * sy;
+          const int64_t q0 = (int64_t)b.lo * sx, q1 = (int64_t)b.hi * sx;
+          float val = ((wt[iy][ix][0] * f[r0 + q0] + wt[iy][ix][1] * f[r0 + q1]) + wt[iy][ix][2] * f[r1 + q0]) +
+                      wt[iy][ix][3] * f[r1 + q1];
+          acc = acc + (ok[iy][ix] ? val : 0.0f);
+        }
+      o[(int64_t)chn * nbins] = acc / g.count;
+    }
+    return;
+  }
+  // staging: the window image [cn][WH][WW] is filled in flat order (lanes
+  // along the row), 8 independent loads in flight per lane before the LDS
+  // stores, so the copy is bandwidth- not latency-bound.
+  constexpr int kUnroll = 8;
+  // flat element e = (chn*WH + r)*WW + col advanced by the block size with
+  // carries (no per-element integer division)
+  const int st_col = kRoiThreads % WW, st_r = (kRoiThreads / WW) % WH, st_ch = kRoiThreads / area;
+  const int t_ch = t / area, t_rem = t - t_ch * area, t_r = t_rem / WW, t_col = t_rem - t_r * WW;
+  for (int cc = 0; cc < nch; cc += csub) {
+    const int cn = min(csub, nch - cc);
+    const int total = cn * area;
+    int chn = t_ch, r = t_r, col = t_col;
+    const float* cbase = base + (int64_t)cc * scs;
+    for (int e0 = 0; e0 < total; e0 += kUnroll * kRoiThreads) {
+      float v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const bool in = e0 + u * kRoiThreads + t < total;
+        const int64_t a = in ? (int64_t)chn * scs + (int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx : 0;
+        v[u] = cbase[a];
+        col += st_col;
+        r += st_r;
+        chn += st_ch;
+        if (col >= WW) {
+          col -= WW;
+          ++r;
+        }
+        if (r >= WH) {
+          r -= WH;
+          ++chn;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int e = e0 + u * kRoiThreads + t;
+        if (e < total) win[e] = v[u];
+      }
+    }
+    __syncthreads();
+    if (active) {
+      for (int chn = cg; chn < cn; chn += groups) {
+        const float* w = win + chn * area;
+        float acc = 0.0f;
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix) {
+            float val = ((wt[iy][ix][0] * w[woff[iy][ix][0]] + wt[iy][ix][1] * w[woff[iy][ix][1]]) +
+                         wt[iy][ix][2] * w[woff[iy][ix][2]]) +
+                        wt[iy][ix][3] * w[woff[iy][ix][3]];
+            acc = acc + (ok[iy][ix] ? val : 0.0f);
+          }
+        o[(int64_t)(cc + chn) * nbins] = acc / g.count;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
                                                                     const float* __restrict__ gout) {
   __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];
@@ -264,11 +754,14 @@ static int32_t roi_common_checks(int32_t batch, int32_t channels, int64_t num_ro
   return FRH_OK;
 }
 
-extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                                             const int64_t* strides, const float* scales, int32_t batch,
-                                             int32_t channels, const float* rois, const int64_t* roi_levels,
-                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
-                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
+// variant: 0 = direct gather, 1 = LDS-staged window, -1 = best available.
+// Exported for the kernel micro-benchmarks (tools/bench_roi_align.py).
+extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
+                                             const int32_t* feat_hw, const int64_t* strides, const float* scales,
+                                             int32_t batch, int32_t channels, const float* rois,
+                                             const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
+                                             int32_t pooled_w, int32_t sampling_ratio, int32_t aligned, float* out,
+                                             void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
   FRH_REQUIRE((feats && out) || num_rois == 0, "null pointer argument");
@@ -278,8 +771,36 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  const bool staged_ok = sampling_ratio > 0 && pooled_h * sampling_ratio <= kStageTaps &&
+                         pooled_w * sampling_ratio <= kStageTaps;
+  const bool regtap_ok = sampling_ratio == 2 && pooled_h * pooled_w <= kRoiThreads;
+  if (variant < 0) variant = regtap_ok ? 4 : 0;
+  FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok),
+              "roi_align variant %d unsupported here", variant);
+  if (variant == 4)
+    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 5)
+    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 6)
+    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<4>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 3)
+    hipLaunchKernelGGL(roi_align_fwd_winreg_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 2)
+    hipLaunchKernelGGL(roi_align_fwd_regtap_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 1)
+    hipLaunchKernelGGL(roi_align_fwd_staged_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else
+    hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   return check_launch("frh_roi_align_fwd");
+}
+
+extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                                             const int64_t* strides, const float* scales, int32_t batch,
+                                             int32_t channels, const float* rois, const int64_t* roi_levels,
+                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
+  return frh_roi_align_fwd_variant(-1, num_levels, feats, feat_hw, strides, scales, batch, channels, rois,
+                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, stream);
 }
 
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,

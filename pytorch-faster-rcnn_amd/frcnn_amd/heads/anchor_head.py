@@ -112,7 +112,10 @@ class AnchorHead(nn.Module):
                                     [gt_bbox], [gt_label] if gt_label is not None else None, [img_meta], train_cfg)
 
     def calc_loss(self, tar_cls_out, tar_reg_out, tar_labels, tar_param, train_cfg):
-        """anchor_head.py:113-139."""
+        """anchor_head.py:113-139.  The regression loss over the positive columns is
+        computed as a masked sum (zeroed negative columns contribute exactly 0 to the
+        reference's sum-reduced losses), which avoids the host synchronisation of
+        boolean indexing; with no positives it is 0 as in the reference."""
         dev = tar_cls_out.device
         cls_loss, reg_loss = losses.zero_loss(dev), losses.zero_loss(dev)
         sampling = 'sampler' in train_cfg
@@ -120,10 +123,9 @@ class AnchorHead(nn.Module):
         avg_factor = len(tar_labels) if sampling else pos.sum()
         if tar_labels.numel() != 0:
             cls_loss = self.loss_cls(tar_cls_out.t(), tar_labels) / avg_factor
-            if pos.sum() == 0:
-                logging.warning('%s recieved no positive samples to train', type(self).__name__)
-            else:
-                reg_loss = self.loss_bbox(tar_reg_out[:, pos], tar_param[:, pos]) / avg_factor
+            m = pos.view(1, -1)
+            z = tar_reg_out.new_zeros(())
+            reg_loss = self.loss_bbox(torch.where(m, tar_reg_out, z), torch.where(m, tar_param, z)) / avg_factor
         else:
             logging.warning('%s recieved no samples to train, return dummy zero losses', type(self).__name__)
         return cls_loss, reg_loss

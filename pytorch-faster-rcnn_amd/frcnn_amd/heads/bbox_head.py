@@ -45,10 +45,10 @@ class BBoxHead(nn.Module):
             if not self.reg_class_agnostic:
                 reg_out = reg_out.view(-1, 4, self.num_classes)
                 reg_out = reg_out[torch.arange(n, device=dev), :, tar_label]
-            if pos.sum() == 0:
-                logging.warning('BBoxHead recieves no positive samples to train')
-            else:
-                reg_loss = self.loss_bbox(reg_out[pos, :], tar_param[:, pos].t()) / avg_factor
+            # masked sum over positive rows (see AnchorHead.calc_loss): no host sync
+            m = pos.view(-1, 1)
+            z = reg_out.new_zeros(())
+            reg_loss = self.loss_bbox(torch.where(m, reg_out, z), torch.where(m, tar_param.t(), z)) / avg_factor
         return cls_loss, reg_loss
 
     def calc_loss(self, cls_outs, reg_outs, tar_labels, tar_params, train_cfg):

@@ -13,7 +13,7 @@ from . import utils
 
 
 def zero_loss(device):
-    return torch.tensor(0.0, device=device, requires_grad=True)
+    return torch.zeros((), device=device, requires_grad=True)
 
 
 def smooth_l1_loss_v2(x, y, beta):

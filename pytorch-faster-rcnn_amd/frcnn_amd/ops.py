@@ -73,6 +73,15 @@ def elem_iou(a, b):
 
 
 # ---------------------------------------------------------------- packing helpers
+def device_ints(vals, device, dtype=torch.int32):
+    """Small host list -> device tensor without a stream synchronisation
+    (pinned staging + non_blocking copy; a pageable copy would block)."""
+    t = torch.tensor(list(vals), dtype=dtype)
+    if device.type != 'cuda':
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def pack_boxes(box_list, device, min_cols=1):
     """list of [4, n_i] -> ([S, 4, n_max] f32, counts int32 device, n_max)."""
     S = len(box_list)
@@ -81,7 +90,7 @@ def pack_boxes(box_list, device, min_cols=1):
     for s, b in enumerate(box_list):
         if b.shape[1]:
             out[s, :, :b.shape[1]] = b
-    counts = torch.tensor([int(b.shape[1]) for b in box_list], dtype=torch.int32, device=device)
+    counts = device_ints([int(b.shape[1]) for b in box_list], device)
     return out, counts, nmax
 
 
@@ -409,7 +418,8 @@ class _RoIAlignMulti(torch.autograd.Function):
              ptr(out), stream_of(out))
         if prof:
             e1.record()
-            ROI_ALIGN_PROFILE['records'].append((e0, e1, rois, levels, [tuple(f.shape) for f in feats], (ph, pw)))
+            ROI_ALIGN_PROFILE['records'].append((e0, e1, rois, levels, [tuple(f.shape) for f in feats], (ph, pw),
+                                                 feats, tuple(scales), sampling_ratio))
         ctx.save_for_backward(rois, levels)
         ctx.cfg = (list(scales), output_size, sampling_ratio, aligned, [f.shape for f in feats])
         return out

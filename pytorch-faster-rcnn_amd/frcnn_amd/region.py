@@ -126,7 +126,7 @@ class BasicRoIExtractor(nn.Module):
         if self._fusable():
             boxes = torch.cat([r.float() for r in rois_list], 1) if rois_list else torch.zeros(4, 0, device=dev)
             bidx = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.float32),
-                                           torch.tensor(counts, device=dev))
+                                           ops.device_ints(counts, dev, torch.int64), output_size=sum(counts))
             rois = torch.cat([bidx.view(1, -1), boxes], 0).t().contiguous()
             levels = ops.roi_level_map(rois, self.finest_scale, n_lvls) if n_lvls > 1 else None
             first = self.roi_layers[0]
@@ -149,7 +149,7 @@ class BasicRoIExtractor(nn.Module):
         dev = level_feats[0].device
         boxes = torch.cat([r.float() for r in rois_list], 1)
         bidx = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.float32),
-                                       torch.tensor(counts, device=dev))
+                                       ops.device_ints(counts, dev, torch.int64), output_size=sum(counts))
         rois = torch.cat([bidx.view(1, -1), boxes], 0).t().contiguous()
         C = level_feats[0].shape[1]
         out = level_feats[0].new_zeros((rois.shape[0], C) + tuple(self.output_size))

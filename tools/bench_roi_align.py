@@ -1,0 +1,63 @@
+"""Micro-benchmark of RoIAlign forward variants on the RoIs of a real cfg2 forward pass.
+
+    python tools/bench_roi_align.py [--iters 50]
+Prints per-variant average launch time (HIP events), algorithmic GB/s (SURVEY §8(d)
+bytes) and the max |difference| to variant 0."""
+import argparse, ctypes, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+import numpy as np, torch
+import bench
+from frcnn_amd import ops, _lib, set_sampler_mode
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--variants', default='0,1')
+    args = ap.parse_args()
+    dev = torch.device('cuda', 0)
+    set_sampler_mode('device', seed=1)
+    model, batch = bench.make_model_and_batch(dev, batch=2)
+    ops.ROI_ALIGN_PROFILE['on'] = True
+    model.forward_train(*batch)
+    ops.ROI_ALIGN_PROFILE['on'] = False
+    rec = ops.ROI_ALIGN_PROFILE['records'][-1]
+    _, _, rois, levels, shapes, (ph, pw), feats, scales, sr = rec
+    nbytes = bench.roi_align_bytes(rec)
+    lv = levels.cpu().numpy()
+    r = rois.cpu().numpy()
+    side = np.sqrt((r[:, 3] - r[:, 1] + 1) * (r[:, 4] - r[:, 2] + 1))
+    print('rois', r.shape[0], 'level hist', np.bincount(lv, minlength=4).tolist(),
+          'side px p10/50/90', np.percentile(side, [10, 50, 90]).round(1).tolist(), 'bytes', nbytes)
+    lib = _lib.load()
+    fn = lib.frh_roi_align_fwd_variant
+    fn.restype = ctypes.c_int32
+    K, C = rois.shape[0], shapes[0][1]
+    hw, st = ops._feat_desc(feats)
+    outs = {}
+    for v in [int(x) for x in args.variants.split(',')]:
+        out = torch.empty(K, C, ph, pw, device=dev)
+        def launch():
+            s = fn(v, len(feats), _lib.ptr_array(feats), hw, st, _lib.f32_array(scales), shapes[0][0], C,
+                   _lib.ptr(rois), _lib.ptr(levels), ctypes.c_int64(K), ph, pw, sr, 0, _lib.ptr(out),
+                   _lib.stream_of(out))
+            assert s == 0, lib.frh_last_error()
+        for _ in range(5):
+            launch()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.iters):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(); launch(); e1.record()
+            ts.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = np.array([a.elapsed_time(b) for a, b in ts])
+        outs[v] = out
+        d = float((out - outs[min(outs)]).abs().max())
+        print('variant {}: {:8.1f} us (min {:7.1f})  {:7.1f} GB/s algorithmic  max|diff| {:.3g}'.format(
+            v, ms.mean() * 1e3, ms.min() * 1e3, nbytes / (ms.mean() * 1e-3) / 1e9, d), flush=True)
+
+
+if __name__ == '__main__':
+    main()
