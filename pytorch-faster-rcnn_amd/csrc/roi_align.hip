@@ -485,6 +485,160 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_vec4_kernel(RoiLeve
   }
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, n, 0x00020000);
+}
+
+// Buffer-descriptor variant (sampling ratio 2, ph*pw <= 256; the default).
+// Lane (bin, channel group cg) keeps its bin's 16 tap offsets in VGPRs as
+// 32-bit byte offsets into a descriptor over this (image, level, channel
+// chunk) slice; the channel walk moves only the wave-uniform soffset, so the
+// loop carries no per-lane address arithmetic.  When every x-sample of the
+// wave has x_hi = x_lo + 1 (all but right-border clamped samples) the taps of
+// a sample row are one 8-byte load: 8 loads per (bin, channel) instead of 16.
+// The 1/count of SR=2 is an exact power of two, so acc * 0.25 == acc / 4.
+// Results identical to the direct kernel.
+template <int U>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevels lv, RoiCfg c,
+                                                                        float* __restrict__ out) {
+  constexpr int SR = 2;
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int groups = kRoiThreads / nbins;
+  const int t = threadIdx.x;
+  if (t >= groups * nbins) return;
+  const int bin = t % nbins, cg = t / nbins;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
+  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + c0) * nbins, (int64_t)nch * nbins * 4);
+  const int cstep = groups * scs * 4, ostep = groups * nbins * 4;
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+  int row[SR][2], col[SR][2];
+  bool pair = sx == 1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    row[i][0] = (cg * scs + (ty[i].valid ? ty[i].lo * sy : 0)) * 4;
+    row[i][1] = (cg * scs + (ty[i].valid ? ty[i].hi * sy : 0)) * 4;
+    col[i][0] = tx[i].valid ? tx[i].lo * sx * 4 : 0;
+    col[i][1] = tx[i].valid ? tx[i].hi * sx * 4 : 0;
+    pair = pair && (!tx[i].valid || tx[i].hi == tx[i].lo + 1);
+  }
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  auto bin_value = [&](const float (&v)[SR][SR][4]) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    return acc * 0.25f;
+  };
+  // wave-uniform trip counts (soffset must stay scalar): every lane has a
+  // channel in the first nch / groups steps, the tail step is lane-guarded
+  const int full = nch / groups, iters = (nch + groups - 1) / groups;
+  const bool tail_ok = cg + full * groups < nch;
+  if (__all(pair)) {
+    int off[SR][2][SR];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) off[iy][r][ix] = row[iy][r] + col[ix][0];
+    int it = 0;
+    for (; it + U <= full; it += U) {
+      u32x2 rv[U][SR][2][SR];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int ix = 0; ix < SR; ++ix)
+              rv[u][iy][r][ix] = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][r][ix], (it + u) * cstep, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float v[SR][SR][4];
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix) {
+            v[iy][ix][0] = __uint_as_float(rv[u][iy][0][ix].x);
+            v[iy][ix][1] = __uint_as_float(rv[u][iy][0][ix].y);
+            v[iy][ix][2] = __uint_as_float(rv[u][iy][1][ix].x);
+            v[iy][ix][3] = __uint_as_float(rv[u][iy][1][ix].y);
+          }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, (it + u) * ostep, 0);
+      }
+    }
+    for (; it < iters; ++it) {
+      if (it == full && !tail_ok) break;
+      float v[SR][SR][4];
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][0][ix], it * cstep, 0);
+          const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][1][ix], it * cstep, 0);
+          v[iy][ix][0] = __uint_as_float(a.x);
+          v[iy][ix][1] = __uint_as_float(a.y);
+          v[iy][ix][2] = __uint_as_float(b.x);
+          v[iy][ix][3] = __uint_as_float(b.y);
+        }
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
+    }
+  } else {
+    for (int it = 0; it < iters; ++it) {
+      if (it == full && !tail_ok) break;
+      float v[SR][SR][4];
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[iy][ix][q] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(fr, row[iy][q >> 1] + col[ix][q & 1], it * cstep, 0));
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
+    }
+  }
+}
+
 // Staged + register-tap variant (sampling ratio SR, ph*pw <= 256).
 // After FPN level mapping a RoI covers few feature cells (random-init cfg2:
 // median side ~5 cells on P2), so its 16*ph*pw taps per channel hit a small
@@ -774,10 +928,22 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   const bool staged_ok = sampling_ratio > 0 && pooled_h * sampling_ratio <= kStageTaps &&
                          pooled_w * sampling_ratio <= kStageTaps;
   const bool regtap_ok = sampling_ratio == 2 && pooled_h * pooled_w <= kRoiThreads;
-  if (variant < 0) variant = regtap_ok ? 4 : 0;
-  FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok),
+  // the descriptor variant addresses one (image, level) slice with 32-bit byte offsets
+  bool buf_ok = regtap_ok;
+  for (int l = 0; l < lv.L; ++l) {
+    const int64_t ext = ((int64_t)(channels - 1) * lv.sc[l] + (int64_t)(lv.h[l] - 1) * lv.sy[l] +
+                         (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
+    buf_ok = buf_ok && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
+  }
+  if (variant < 0) variant = buf_ok ? 8 : 0;
+  FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok) ||
+                  (variant >= 7 && variant <= 8 && buf_ok),
               "roi_align variant %d unsupported here", variant);
-  if (variant == 4)
+  if (variant == 7)
+    hipLaunchKernelGGL(roi_align_fwd_buf_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 8)
+    hipLaunchKernelGGL(roi_align_fwd_buf_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 4)
     hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   else if (variant == 5)
     hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);

@@ -11,12 +11,41 @@ import bench
 from frcnn_amd import ops, _lib, set_sampler_mode
 
 
+def calibrate(variants, dev):
+    """Known-byte calibration of the FETCH_SIZE counter for this kernel's access pattern
+    (MI355X_MICROARCH.md: only 16-B/lane streaming reads are calibrated).  One RoI over a
+    29x29 map with 65536 channels: the 2x2-sampled 7x7 bins touch rows/cols 1..28 of every
+    channel plane, i.e. every 128-B line of the 220 MB feature tensor (but the first of
+    each plane's 3364 B), exactly once.  Run under rocprofv3 --pmc FETCH_SIZE."""
+    lib = _lib.load()
+    fn = lib.frh_roi_align_fwd_variant
+    fn.restype = ctypes.c_int32
+    C, S = 65536, 29
+    rois = torch.tensor([[0.0, 0.0, 0.0, 28.0, 28.0]], device=dev)
+    levels = torch.zeros(1, dtype=torch.int64, device=dev)
+    print('calibration: feature bytes', C * S * S * 4, 'output bytes', C * 49 * 4, flush=True)
+    for v in variants:
+        feats = [torch.randn(1, C, S, S, device=dev)]  # fresh tensor per variant: no reuse across runs
+        hw, st = ops._feat_desc(feats)
+        out = torch.empty(1, C, 7, 7, device=dev)
+        torch.cuda.synchronize()
+        s = fn(v, 1, _lib.ptr_array(feats), hw, st, _lib.f32_array([1.0]), 1, C, _lib.ptr(rois), _lib.ptr(levels),
+               ctypes.c_int64(1), 7, 7, 2, 0, _lib.ptr(out), _lib.stream_of(out))
+        assert s == 0, lib.frh_last_error()
+        torch.cuda.synchronize()
+        print('variant', v, 'done', flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--variants', default='0,1')
+    ap.add_argument('--calib', action='store_true', help='known-byte FETCH_SIZE calibration launches only')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
+    if args.calib:
+        calibrate([int(x) for x in args.variants.split(',')], dev)
+        return
     set_sampler_mode('device', seed=1)
     model, batch = bench.make_model_and_batch(dev, batch=2)
     ops.ROI_ALIGN_PROFILE['on'] = True

@@ -1,0 +1,59 @@
+"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes.
+
+    python tools/pmc_summary.py --fetch DIR --write DIR --kernel roi_align_fwd_buf \
+        [--calib-fetch DIR --calib-bytes N] --out profiles/roi_align_pmc.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (MI355X_MICROARCH.md, HBM section).  The
+guide's x2 FETCH correction is calibrated only for 16-B/lane streaming reads; this kernel
+issues 8-B gathers, so the FETCH scale is measured on a known-byte launch of the SAME kernel
+(tools/bench_roi_align.py --calib) when --calib-fetch is given: scale = known bytes / FETCH.
+"""
+import argparse, csv, glob, json, os
+
+
+def counter_rows(d, name):
+    rows = []
+    for p in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+        for r in csv.DictReader(open(p)):
+            if r['Counter_Name'] == name:
+                rows.append(r)
+    return rows
+
+
+def per_launch(d, name, kernel):
+    vals = [float(r['Counter_Value']) for r in counter_rows(d, name) if kernel in r['Kernel_Name']]
+    if not vals:
+        raise SystemExit('no {} rows for kernel matching {!r} under {}'.format(name, kernel, d))
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--fetch', required=True)
+    ap.add_argument('--write', required=True)
+    ap.add_argument('--kernel', required=True)
+    ap.add_argument('--calib-fetch')
+    ap.add_argument('--calib-kernel')
+    ap.add_argument('--calib-bytes', type=float)
+    ap.add_argument('--out', required=True)
+    a = ap.parse_args()
+    fkb, nf = per_launch(a.fetch, 'FETCH_SIZE', a.kernel)
+    wkb, nw = per_launch(a.write, 'WRITE_SIZE', a.kernel)
+    res = {'kernel': a.kernel, 'fetch_kib_per_launch': fkb, 'write_kib_per_launch': wkb,
+           'launches_fetch_pass': nf, 'launches_write_pass': nw}
+    scale, how = 1.0, 'raw FETCH_SIZE (uncalibrated access width)'
+    if a.calib_fetch:
+        ckb, _ = per_launch(a.calib_fetch, 'FETCH_SIZE', a.calib_kernel or a.kernel)
+        scale = a.calib_bytes / (ckb * 1024.0)
+        how = 'FETCH_SIZE x {:.3f}: known-byte calibration launch ({:.0f} B read, {:.0f} KiB counted)'.format(
+            scale, a.calib_bytes, ckb)
+        res['calibration'] = {'known_bytes': a.calib_bytes, 'fetch_kib': ckb}
+    res['fetch_scale'] = scale
+    res['fetch_correction'] = how
+    res['hbm_bytes_per_launch'] = fkb * 1024.0 * scale + wkb * 1024.0
+    json.dump(res, open(a.out, 'w'), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()
