@@ -16,6 +16,8 @@
 // views (FPN P6 = P5[..., ::2, ::2]) all run the same kernel.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace frh {
@@ -505,12 +507,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
 // The 1/count of SR=2 is an exact power of two, so acc * 0.25 == acc / 4.
 // Results identical to the direct kernel.
 template <int U>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevels lv, RoiCfg c,
-                                                                        float* __restrict__ out) {
+__device__ __forceinline__ void fwd_buf_block(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out,
+                                              int64_t k, int c0, const RoiGeom& g) {
   constexpr int SR = 2;
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
   const int nbins = c.ph * c.pw;
@@ -636,6 +635,196 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevel
                 __builtin_amdgcn_raw_buffer_load_b32(fr, row[iy][q >> 1] + col[ix][q & 1], it * cstep, 0));
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
     }
+  }
+}
+
+template <int U>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevels lv, RoiCfg c,
+                                                                        float* __restrict__ out) {
+  const int64_t k = blockIdx.x;
+  fwd_buf_block<U>(lv, c, out, k, blockIdx.y * kRoiChanChunk, roi_geom(c, lv, k));
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Wave-staged variant (sampling ratio 2, ph*pw <= 64, 2*ph and 2*pw <= 64).
+// Every tap of a RoI lies in the window [y0, y1] x [x0, x1] of its level;
+// after FPN level mapping that window is a few to ~30 cells per side.  Each
+// wave owns 16 channels of the RoI and, per channel, copies the window into
+// its own LDS slab with lane-contiguous loads (every feature line fetched
+// once per RoI-channel, instead of 8 gathers per bin hitting the same lines),
+// then lane = bin reads its 16 taps from LDS.  The loads of channel i+1 are
+// in flight while channel i is evaluated.  The slab row has one extra column
+// holding a copy of the window's last feature column, so a right-border
+// clamped tap (x_lo = x_hi = W-1) reads (x_lo, x_lo + 1) like every other
+// sample.  No block barriers: waves are independent.  Windows above
+// kWinMax floats take the per-wave gather path.  Results identical to the
+// direct kernel.
+constexpr int kWinMax = 1024;
+constexpr int kWinR = kWinMax / kWave;
+constexpr int kWaveChans = kRoiChanChunk / (kRoiThreads / kWave);
+
+template <int kStageMax>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
+                                                                        float* __restrict__ out) {
+  constexpr int SR = 2;
+  __shared__ float slab_all[kRoiThreads / kWave][kWinMax];
+  const int64_t k = blockIdx.x;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kWaveChans;
+  const int nch = min(kWaveChans, c.C - cw0);
+  float* slab = slab_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  // window of the valid taps: lane i evaluates y sample i and x sample i
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  if (lane < c.ph * SR) {
+    const Tap t = make_tap(sample_y(g, lane / SR, lane % SR), H);
+    if (t.valid) ylo = t.lo, yhi = t.hi;
+  }
+  if (lane < c.pw * SR) {
+    const Tap t = make_tap(sample_x(g, lane / SR, lane % SR), W);
+    if (t.valid) xlo = t.lo, xhi = t.hi;
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  const bool any = y1 >= y0 && x1 >= x0;
+  // odd slab row stride: the 4 tap rows of a wave's bins spread over the LDS banks
+  const int ws = (x1 - x0 + 2) | 1, n = any ? (y1 - y0 + 1) * ws : 0;
+  if (n > kStageMax) {  // uniform over the block (one RoI): large windows take the block gather path
+    fwd_buf_block<2>(lv, c, out, k, blockIdx.y * kRoiChanChunk, g);
+    return;
+  }
+  if (nch <= 0) return;
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)nch * nbins * 4);
+  const int cstep = scs * 4, ostep = nbins * 4;
+  // this lane's bin: taps, weights, validity
+  const int bin = lane < nbins ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  auto bin_value = [&](const float (&v)[SR][SR][4]) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    return acc * 0.25f;
+  };
+  const bool active = lane < nbins;
+  if (n <= kStageMax) {
+    // slab addresses of this bin's sample rows (x_lo, x_lo + 1 pairs)
+    int sa[SR][2][SR];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const bool v = ok[iy][ix];
+        sa[iy][0][ix] = v ? (ty[iy].lo - y0) * ws + (tx[ix].lo - x0) : 0;
+        sa[iy][1][ix] = v ? (ty[iy].hi - y0) * ws + (tx[ix].lo - x0) : 0;
+      }
+    // staging: slab element e = lane + 64 j  <-  feature (y0 + e / ws, min(x0 + e % ws, W - 1));
+    // the j loop is specialised on RB = 64-element rounds (1, 2, 4, 8, 16) so it unrolls branch-free
+    auto run = [&](auto rb) {
+      constexpr int RB = decltype(rb)::value, D = kWinR / RB;  // D channel windows per round, 16 loads/lane
+      int goff[RB];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int e = lane + j * kWave;
+        const int r = e / ws, cc = e - r * ws;
+        // lanes past the window re-read its first element: no extra cache line per round
+        goff[j] = e < n ? ((y0 + r) * sy + min(x0 + cc, W - 1) * sx) * 4 : (y0 * sy + x0 * sx) * 4;
+      }
+      float st[D][RB];
+      auto issue = [&](int c0r) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+          for (int j = 0; j < RB; ++j)
+            st[d][j] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(fr, goff[j], min(c0r + d, nch - 1) * cstep, 0));
+      };
+      issue(0);
+      for (int i = 0; i < nch; i += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+          for (int j = 0; j < RB; ++j) slab[(d * RB + j) * kWave + lane] = st[d][j];  // [n, 64 RB) junk, unread
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (i + D < nch) issue(i + D);
+        if (active) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            if (i + d < nch) {
+              const float* sl = slab + d * RB * kWave;
+              float v[SR][SR][4];
+#pragma unroll
+              for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+                for (int ix = 0; ix < SR; ++ix) {
+                  v[iy][ix][0] = sl[sa[iy][0][ix]];
+                  v[iy][ix][1] = sl[sa[iy][0][ix] + 1];
+                  v[iy][ix][2] = sl[sa[iy][1][ix]];
+                  v[iy][ix][3] = sl[sa[iy][1][ix] + 1];
+                }
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, lane * 4, (i + d) * ostep, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    };
+    const int R = (n + kWave - 1) / kWave;
+    if (R <= 1)
+      run(std::integral_constant<int, 1>{});
+    else if (R <= 2 || kStageMax <= 2 * kWave)
+      run(std::integral_constant<int, 2>{});
+    else if (R <= 4 || kStageMax <= 4 * kWave)
+      run(std::integral_constant<int, 4>{});
+    else if (R <= 8 || kStageMax <= 8 * kWave)
+      run(std::integral_constant<int, 8>{});
+    else
+      run(std::integral_constant<int, kWinR>{});
   }
 }
 
@@ -935,11 +1124,20 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                          (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
     buf_ok = buf_ok && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
   }
-  if (variant < 0) variant = buf_ok ? 8 : 0;
+  const bool lds_ok = buf_ok && pooled_h * pooled_w <= 64 && 2 * pooled_h <= 64 && 2 * pooled_w <= 64;
+  if (variant < 0) variant = lds_ok ? 10 : buf_ok ? 8 : 0;
   FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok) ||
-                  (variant >= 7 && variant <= 8 && buf_ok),
+                  (variant >= 7 && variant <= 8 && buf_ok) || (variant >= 9 && variant <= 12 && lds_ok),
               "roi_align variant %d unsupported here", variant);
-  if (variant == 7)
+  if (variant == 9)
+    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<kWinMax>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 10)
+    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 11)
+    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<128>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 12)
+    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<64>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 7)
     hipLaunchKernelGGL(roi_align_fwd_buf_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   else if (variant == 8)
     hipLaunchKernelGGL(roi_align_fwd_buf_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);

@@ -11,17 +11,19 @@ import bench
 from frcnn_amd import ops, _lib, set_sampler_mode
 
 
-def calibrate(variants, dev):
+def calibrate(variants, dev, small=False):
     """Known-byte calibration of the FETCH_SIZE counter for this kernel's access pattern
     (MI355X_MICROARCH.md: only 16-B/lane streaming reads are calibrated).  One RoI over a
     29x29 map with 65536 channels: the 2x2-sampled 7x7 bins touch rows/cols 1..28 of every
     channel plane, i.e. every 128-B line of the 220 MB feature tensor (but the first of
-    each plane's 3364 B), exactly once.  Run under rocprofv3 --pmc FETCH_SIZE."""
+    each plane's 3364 B), exactly once.  small=True: a 12x12 map of 262144 channels (151 MB)
+    whose 12x13-float window takes the LDS-staged path of the default kernel; the large map
+    takes its block-gather path.  Run under rocprofv3 --pmc FETCH_SIZE."""
     lib = _lib.load()
     fn = lib.frh_roi_align_fwd_variant
     fn.restype = ctypes.c_int32
-    C, S = 65536, 29
-    rois = torch.tensor([[0.0, 0.0, 0.0, 28.0, 28.0]], device=dev)
+    C, S = (65536, 29) if small is False else (262144, 12)
+    rois = torch.tensor([[0.0, 0.0, 0.0, S - 1.0, S - 1.0]], device=dev)
     levels = torch.zeros(1, dtype=torch.int64, device=dev)
     print('calibration: feature bytes', C * S * S * 4, 'output bytes', C * 49 * 4, flush=True)
     for v in variants:
@@ -41,10 +43,12 @@ def main():
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--variants', default='0,1')
     ap.add_argument('--calib', action='store_true', help='known-byte FETCH_SIZE calibration launches only')
+    ap.add_argument('--calib-small', action='store_true', help='calibration on the staged (small-window) path')
+    ap.add_argument('--dump', help='save the RoIs / levels / level shapes of the recorded launch to this .npz')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     if args.calib:
-        calibrate([int(x) for x in args.variants.split(',')], dev)
+        calibrate([int(x) for x in args.variants.split(',')], dev, args.calib_small)
         return
     set_sampler_mode('device', seed=1)
     model, batch = bench.make_model_and_batch(dev, batch=2)
@@ -59,6 +63,8 @@ def main():
     side = np.sqrt((r[:, 3] - r[:, 1] + 1) * (r[:, 4] - r[:, 2] + 1))
     print('rois', r.shape[0], 'level hist', np.bincount(lv, minlength=4).tolist(),
           'side px p10/50/90', np.percentile(side, [10, 50, 90]).round(1).tolist(), 'bytes', nbytes)
+    if args.dump:
+        np.savez(args.dump, rois=r, levels=lv, shapes=np.array(shapes), scales=np.array(scales))
     lib = _lib.load()
     fn = lib.frh_roi_align_fwd_variant
     fn.restype = ctypes.c_int32

@@ -32,9 +32,9 @@ def main():
     ap.add_argument('--fetch', required=True)
     ap.add_argument('--write', required=True)
     ap.add_argument('--kernel', required=True)
-    ap.add_argument('--calib-fetch')
+    ap.add_argument('--calib-fetch', nargs='*', default=[])
     ap.add_argument('--calib-kernel')
-    ap.add_argument('--calib-bytes', type=float)
+    ap.add_argument('--calib-bytes', nargs='*', type=float, default=[])
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
     fkb, nf = per_launch(a.fetch, 'FETCH_SIZE', a.kernel)
@@ -43,11 +43,18 @@ def main():
            'launches_fetch_pass': nf, 'launches_write_pass': nw}
     scale, how = 1.0, 'raw FETCH_SIZE (uncalibrated access width)'
     if a.calib_fetch:
-        ckb, _ = per_launch(a.calib_fetch, 'FETCH_SIZE', a.calib_kernel or a.kernel)
-        scale = a.calib_bytes / (ckb * 1024.0)
-        how = 'FETCH_SIZE x {:.3f}: known-byte calibration launch ({:.0f} B read, {:.0f} KiB counted)'.format(
-            scale, a.calib_bytes, ckb)
-        res['calibration'] = {'known_bytes': a.calib_bytes, 'fetch_kib': ckb}
+        cal = []
+        for d, nbytes in zip(a.calib_fetch, a.calib_bytes):
+            ckb, _ = per_launch(d, 'FETCH_SIZE', a.calib_kernel or a.kernel)
+            cal.append({'dir': d, 'known_bytes': nbytes, 'fetch_kib': ckb, 'scale': nbytes / (ckb * 1024.0)})
+        scales = [c['scale'] for c in cal]
+        res['calibration'] = cal
+        if max(scales) / min(scales) < 1.1:  # both access paths agree: apply their mean
+            scale = sum(scales) / len(scales)
+            how = 'FETCH_SIZE x {:.3f}: mean of known-byte calibration launches {}'.format(
+                scale, ['{:.3f}'.format(x) for x in scales])
+        else:
+            how = 'raw FETCH_SIZE: calibration launches disagree ({})'.format(['{:.3f}'.format(x) for x in scales])
     res['fetch_scale'] = scale
     res['fetch_correction'] = how
     res['hbm_bytes_per_launch'] = fkb * 1024.0 * scale + wkb * 1024.0
