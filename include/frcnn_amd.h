@@ -263,6 +263,27 @@ int32_t frh_roi_pool_bwd(float* grad_feat, const int64_t* strides, int32_t heigh
                          int32_t channels, const float* rois, int64_t num_rois, int32_t pooled_h,
                          int32_t pooled_w, const float* grad_out, const int32_t* argmax, void* stream);
 
+/* ---------------------------------------------------------------- a16 ATSS / LTRB targets
+ * Replaces FCOSHead.single_image_targets_atss (lib/heads/fcos_head.py:283-368) with
+ * topk_by_center (:106-116, row index by floor division), bbox2ltrb (:78-87),
+ * positive_ltrb (:51-53), centerness (:56-59) and paint_value (:90-94), for all
+ * images of a batch.  Levels: grid_hw[2l..2l+1] = (H_l, W_l), strides[l] (host arrays);
+ * anchors [4, anchor_ld] f32 = one anchor per cell, levels concatenated (AnchorCreator
+ * scale atss_cfg.scale, ratio 1).  gts [B][4][max_gts] f32 (segment stride gt_seg_stride),
+ * num_gts [B] (device), gt_labels [B][max_gts] i64, img_hw [B][2] (device, img_shape h, w).
+ * Outputs over the N level-concatenated cells: cls [B][N] i64 (-1 outside the painted
+ * image, 0 background, label), reg [B][N][4] f32 ltrb (-1 when not positive),
+ * ctr [B][N] f32 (-1 / 0 / centerness).  topk <= 16, num_levels <= 16.  Top-k ties
+ * break by ascending cell index; the per-gt IoU mean / unbiased std use double sums. */
+size_t frh_atss_workspace(int32_t batch, int32_t max_gts, int32_t num_levels, int32_t topk,
+                          int64_t num_cells);
+int32_t frh_atss_assign(int32_t batch, int32_t num_levels, const int32_t* grid_hw,
+                        const float* strides, const float* anchors, int64_t anchor_ld,
+                        const float* gts, int64_t gt_seg_stride, const int32_t* num_gts,
+                        const int64_t* gt_labels, int32_t max_gts, const int32_t* img_hw,
+                        int32_t topk, int64_t* cls, float* reg, float* ctr, void* workspace,
+                        size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,7 @@
  *   roi_align fwd/bwd   torchvision legacy RoIAlign (aligned=False) CPU
  *                       kernel semantics (lib/builder.py:9, lib/region.py:276)
  *   roi_pool            torchvision RoIPool semantics
+ *   atss targets        lib/heads/fcos_head.py:51-116,283-368
  * torchvision is not vendored in the reference and not installed here: the
  * nms / roi_align / roi_pool rows are "parity unpinned" (SURVEY §8c).
  */
@@ -360,4 +361,110 @@ void orc_roi_pool_fwd(const float* feat, const int64_t* st, int H, int W, int C,
           argmax[o] = mi;
         }
   }
+}
+
+/* ATSS targets of one image: FCOSHead.single_image_targets_atss
+ * (lib/heads/fcos_head.py:283-368) with its helpers topk_by_center (:106-116,
+ * row index by floor division), bbox2ltrb (:78-87), positive_ltrb (:51-53),
+ * centerness (:56-59), paint_value (:90-94), calc_iou (lib/utils.py:151-172).
+ * Level l has a gh[l] x gw[l] grid, stride strides[l] and one anchor per cell
+ * (anchors[l]: [4, gh*gw]).  Outputs cover the level-concatenated cells:
+ * cls[N] (-1 outside the painted image area, 0 background, label), reg[N*4]
+ * (ltrb, -1 where not positive), ctr[N] (-1 / 0 / centerness).
+ * Top-k ties are broken by ascending cell index; the IoU mean / unbiased std
+ * are accumulated in double and rounded to f32 (torch's f32 reduction order
+ * can differ by an ulp: only an IoU within an ulp of mean+std could flip). */
+static int cmp_dist(const void* a, const void* b) {
+  const float* x = (const float*)a;
+  const float* y = (const float*)b;
+  if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
+  return x[1] < y[1] ? -1 : (x[1] > y[1] ? 1 : 0);
+}
+
+void orc_atss_targets(int L, const int32_t* gh, const int32_t* gw, const float* strides,
+                      const float* const* anchors, const float* gts, int64_t G, const int64_t* labels, int img_h,
+                      int img_w, int topk, int64_t* cls, float* reg, float* ctr) {
+  int64_t off[17], N = 0;
+  for (int l = 0; l < L; ++l) {
+    off[l] = N;
+    N += (int64_t)gh[l] * gw[l];
+  }
+  float* maxiou = (float*)calloc((size_t)N, sizeof(float));
+  for (int64_t i = 0; i < N; ++i) {
+    cls[i] = -1;
+    ctr[i] = -1.0f;
+    reg[4 * i] = reg[4 * i + 1] = reg[4 * i + 2] = reg[4 * i + 3] = -1.0f;
+  }
+  for (int l = 0; l < L; ++l) {  /* paint_value([0, 0, img_w, img_h] * (1/stride)) */
+    const float sc = (float)(1.0 / (double)strides[l]);
+    const int x2 = (int)rintf((float)img_w * sc), y2 = (int)rintf((float)img_h * sc);
+    for (int y = 0; y <= y2 && y < gh[l]; ++y)
+      for (int x = 0; x <= x2 && x < gw[l]; ++x) {
+        cls[off[l] + (int64_t)y * gw[l] + x] = 0;
+        ctr[off[l] + (int64_t)y * gw[l] + x] = 0.0f;
+      }
+  }
+  int64_t maxhw = 0;
+  for (int l = 0; l < L; ++l) maxhw = (int64_t)gh[l] * gw[l] > maxhw ? (int64_t)gh[l] * gw[l] : maxhw;
+  float* dist = (float*)malloc((size_t)maxhw * 2 * sizeof(float));
+  int64_t* cidx = (int64_t*)malloc((size_t)L * topk * sizeof(int64_t));
+  float* ciou = (float*)malloc((size_t)L * topk * sizeof(float));
+  int* cnum = (int*)malloc((size_t)L * sizeof(int));
+  for (int64_t g = 0; g < G; ++g) {
+    const float b[4] = {gts[g], gts[G + g], gts[2 * G + g], gts[3 * G + g]};
+    const float bcx = (b[2] + b[0]) / 2.0f, bcy = (b[3] + b[1]) / 2.0f;
+    int tot = 0;
+    for (int l = 0; l < L; ++l) {
+      const int64_t hw = (int64_t)gh[l] * gw[l];
+      const float* a = anchors[l];
+      for (int64_t i = 0; i < hw; ++i) {
+        const float acx = (a[2 * hw + i] + a[i]) / 2.0f, acy = (a[3 * hw + i] + a[hw + i]) / 2.0f;
+        const float dx = acx - bcx, dy = acy - bcy;
+        dist[2 * i] = sqrtf(dx * dx + dy * dy);
+        dist[2 * i + 1] = (float)i;  /* exact: hw < 2^24 */
+      }
+      qsort(dist, (size_t)hw, 2 * sizeof(float), cmp_dist);
+      const int k = (int64_t)topk < hw ? topk : (int)hw;
+      for (int j = 0; j < k; ++j) {
+        const int64_t i = (int64_t)dist[2 * j + 1];
+        cidx[tot + j] = i;
+        ciou[tot + j] = iou_p1(a, hw, i, b, 1, 0);
+      }
+      cnum[l] = k;
+      tot += k;
+    }
+    double s = 0.0, ss = 0.0;
+    for (int j = 0; j < tot; ++j) s += ciou[j];
+    const double mean = s / tot;
+    for (int j = 0; j < tot; ++j) ss += ((double)ciou[j] - mean) * ((double)ciou[j] - mean);
+    const float thr = (float)mean + (float)sqrt(ss / (tot - 1));
+    int j0 = 0;
+    for (int l = 0; l < L; ++l) {
+      for (int j = j0; j < j0 + cnum[l]; ++j) {
+        const int64_t i = cidx[j];
+        const int x = (int)(i % gw[l]), y = (int)(i / gw[l]);
+        const float cx = (float)x * strides[l] + strides[l] / 2.0f, cy = (float)y * strides[l] + strides[l] / 2.0f;
+        const float lt[4] = {cx - b[0], cy - b[1], b[2] - cx, b[3] - cy};
+        const int pos_ltrb = lt[0] > 0 && lt[1] > 0 && lt[2] > 0 && lt[3] > 0;
+        const int64_t c = off[l] + i;
+        if (ciou[j] >= maxiou[c] && ciou[j] > thr && pos_ltrb) {
+          cls[c] = labels[g];
+          for (int q = 0; q < 4; ++q) reg[4 * c + q] = lt[q];
+          maxiou[c] = ciou[j];
+        }
+      }
+      j0 += cnum[l];
+    }
+  }
+  for (int64_t c = 0; c < N; ++c)
+    if (cls[c] > 0) {
+      const float l = reg[4 * c] + 1e-6f, t = reg[4 * c + 1] + 1e-6f;
+      const float r = reg[4 * c + 2] + 1e-6f, bb = reg[4 * c + 3] + 1e-6f;
+      ctr[c] = sqrtf(((l < r ? l : r) / (l > r ? l : r)) * ((t < bb ? t : bb) / (t > bb ? t : bb)));
+    }
+  free(maxiou);
+  free(dist);
+  free(cidx);
+  free(ciou);
+  free(cnum);
 }

@@ -334,3 +334,24 @@ def rpn_predict_single_image(level_cls, level_reg, level_anchors, img_size, min_
         idx = np.argsort(-s, kind='stable')[:max_num]
         s, b = s[idx], b[:, idx]
     return b, s
+
+
+def atss_targets(anchors, grids, strides, gts, labels, img_shape, topk=9):
+    """FCOSHead.single_image_targets_atss (fcos_head.py:283-368) for one image.
+    anchors: per-level [4, H*W] f32 (one anchor per cell); gts [4, G]; labels [G].
+    Returns level-concatenated (cls int64 [N], reg f32 [N, 4], ctr f32 [N])."""
+    L = len(grids)
+    gh = np.array([g[0] for g in grids], np.int32)
+    gw = np.array([g[1] for g in grids], np.int32)
+    N = int((gh.astype(np.int64) * gw).sum())
+    an = [np.ascontiguousarray(a, np.float32).reshape(4, -1) for a in anchors]
+    ap = (ctypes.c_void_p * L)(*[a.ctypes.data for a in an])
+    g = np.ascontiguousarray(gts, np.float32).reshape(4, -1)
+    lab = np.ascontiguousarray(labels, np.int64)
+    cls = np.empty(N, np.int64)
+    reg = np.empty((N, 4), np.float32)
+    ctr = np.empty(N, np.float32)
+    lib().orc_atss_targets(L, gh.ctypes.data_as(_I32), gw.ctypes.data_as(_I32), _f(_c32(strides)), ap, _f(g),
+                           ctypes.c_int64(g.shape[1]), lab.ctypes.data_as(_I64), int(img_shape[0]),
+                           int(img_shape[1]), int(topk), cls.ctypes.data_as(_I64), _f(reg), _f(ctr))
+    return cls, reg, ctr

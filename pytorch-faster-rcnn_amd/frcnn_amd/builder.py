@@ -10,14 +10,15 @@ from torch.optim import SGD
 from .backbones import ResNet, ResLayerC5
 from .necks import FPN
 from .region import MaxIoUAssigner, RandomSampler, BasicRoIExtractor
-from .losses import FocalLoss, SmoothL1Loss, CrossEntropyLoss, GIoULoss, IoULoss
-from .heads import RPNHead, RCNNHead, RetinaHead
-from .detectors import CascadeRCNN, RetinaNet
+from .losses import (FocalLoss, SmoothL1Loss, CrossEntropyLoss, GIoULoss, IoULoss, QualityFocalLoss,
+                     DistributionFocalLoss)
+from .heads import RPNHead, RCNNHead, RetinaHead, FCOSHead
+from .detectors import CascadeRCNN, RetinaNet, FCOS
 from .ops import RoIAlign, RoIPool
 
-_MODULE_LIST = [RetinaNet, CascadeRCNN, ResNet, ResLayerC5, FPN, RetinaHead, RPNHead, RCNNHead, CrossEntropyLoss,
-                SmoothL1Loss, FocalLoss, GIoULoss, IoULoss, BasicRoIExtractor, RoIAlign, RoIPool, SGD,
-                MaxIoUAssigner, RandomSampler]
+_MODULE_LIST = [RetinaNet, CascadeRCNN, FCOS, ResNet, ResLayerC5, FPN, RetinaHead, RPNHead, RCNNHead, FCOSHead,
+                CrossEntropyLoss, SmoothL1Loss, FocalLoss, GIoULoss, IoULoss, QualityFocalLoss, DistributionFocalLoss,
+                BasicRoIExtractor, RoIAlign, RoIPool, SGD, MaxIoUAssigner, RandomSampler]
 
 MODULES = {cls.__name__: cls for cls in _MODULE_LIST}
 

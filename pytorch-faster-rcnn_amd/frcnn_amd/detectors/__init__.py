@@ -1,4 +1,5 @@
 from .cascade_rcnn import CascadeRCNN
 from .retinanet import RetinaNet
+from .fcos import FCOS
 
-__all__ = ['CascadeRCNN', 'RetinaNet']
+__all__ = ['CascadeRCNN', 'RetinaNet', 'FCOS']

@@ -112,3 +112,54 @@ class IoULoss(nn.Module):
         if avg_factor is not None:
             loss = loss / avg_factor
         return loss.sum() * self.loss_weight
+
+
+def generalized_focal_loss(pred, tar, beta=2.0):
+    """losses.py:221-224 (elementwise, logits pred)."""
+    focal_weight = (tar - pred.sigmoid()).abs().pow(beta)
+    return focal_weight * F.binary_cross_entropy_with_logits(pred, tar, reduction='none')
+
+
+class QualityFocalLoss(nn.Module):
+    """losses.py:226-249: pred [n, C] logits, quality [n], label [n] in 0..C."""
+
+    def __init__(self, beta=2.0, use_sigmoid=True, loss_weight=1.0):
+        if not use_sigmoid:
+            raise AssertionError('QualityFocalLoss only support sigmoid activation')
+        super().__init__()
+        self.use_sigmoid, self.beta, self.loss_weight = use_sigmoid, beta, loss_weight
+
+    def forward(self, pred, quality, label, weight=None, avg_factor=1.0):
+        n, n_cls = pred.shape
+        tar = pred.new_zeros((n, n_cls + 1))
+        tar[torch.arange(n, device=pred.device), label] = quality
+        loss = generalized_focal_loss(pred, tar[:, 1:], beta=self.beta)
+        if weight is not None:
+            loss = loss * weight
+        return loss.sum() * self.loss_weight / avg_factor
+
+
+def log_softmax_with_logits(logits):
+    """losses.py:251-254: row-wise stable log-softmax."""
+    c, _ = logits.detach().max(1)
+    s = logits - c.unsqueeze(1)
+    return s - s.exp().sum(1).log().unsqueeze(1)
+
+
+class DistributionFocalLoss(nn.Module):
+    """losses.py:256-285: pred [n, cls_channels] logits, y [n], left_idx [n]."""
+
+    def __init__(self, cls_channels, stride, norm_prob, loss_weight=1.0):
+        super().__init__()
+        self.cls_channels, self.stride, self.norm_prob, self.loss_weight = cls_channels, stride, norm_prob, loss_weight
+
+    def forward(self, pred, y, left_idx, weight=None, avg_factor=1.0):
+        n = pred.shape[0]
+        ar = torch.arange(n, device=pred.device)
+        log_sigma = log_softmax_with_logits(pred)
+        right_idx = left_idx + 1
+        y_left, y_right = left_idx * self.stride, right_idx * self.stride
+        loss = (y_right - y) * log_sigma[ar, left_idx] + (y - y_left) * log_sigma[ar, right_idx]
+        if self.norm_prob:
+            loss = loss / self.stride
+        return -loss.sum() * self.loss_weight / avg_factor

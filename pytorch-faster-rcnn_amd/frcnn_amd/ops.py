@@ -527,3 +527,31 @@ class RoIPool(nn.Module):
 
     def forward(self, input, rois):
         return roi_pool(input, rois, self.output_size, self.spatial_scale)
+
+
+# ---------------------------------------------------------------- ATSS / LTRB targets (a16)
+def atss_assign(anchors, grid_sizes, strides, gt_list, label_list, img_shapes, topk=9):
+    """Batched FCOSHead.single_image_targets_atss (fcos_head.py:283-368).
+    anchors: [4, N] f32 (one per cell, levels concatenated); gt_list: per image [4, G_i];
+    label_list: per image [G_i]; img_shapes: per image (h, w).
+    Returns cls i64 [B, N], reg f32 [B, N, 4] (ltrb), ctr f32 [B, N]."""
+    _need_cuda(anchors)
+    dev = anchors.device
+    B = len(gt_list)
+    L = len(grid_sizes)
+    N = sum(int(h) * int(w) for h, w in grid_sizes)
+    if anchors.shape[1] != N or anchors.stride(1) != 1:
+        raise AssertionError('anchors must be a [4, N] row-contiguous tensor with one anchor per cell')
+    gts, gcnt, gmax = pack_boxes([g.float() for g in gt_list], dev)
+    labels = pack_labels(label_list, gmax, dev)
+    img_hw = device_ints([int(v) for s in img_shapes for v in s[:2]], dev)
+    cls = torch.empty(B, N, dtype=torch.int64, device=dev)
+    reg = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+    ctr = torch.empty(B, N, dtype=torch.float32, device=dev)
+    ws_n = _lib.query('frh_atss_workspace', B, gmax, L, int(topk), N)
+    ws = workspace(ws_n, dev)
+    hw = i32_array([int(v) for g in grid_sizes for v in g])
+    call('frh_atss_assign', B, L, hw, f32_array(strides), ptr(anchors), anchors.stride(0), ptr(gts), gts.stride(0),
+         ptr(gcnt), ptr(labels), gmax, ptr(img_hw), int(topk), ptr(cls), ptr(reg), ptr(ctr), ptr(ws), ws_n,
+         stream_of(cls))
+    return cls, reg, ctr

@@ -188,3 +188,22 @@ def init_module_normal(m, mean=0.0, std=1.0):
             p.data.normal_(mean, std)
         if 'bias' in name:
             p.data.zero_()
+
+
+def full_index(size):
+    """utils.py:338-341: [*size, len(size)] long tensor of every index (row-major)."""
+    grids = torch.meshgrid(*[torch.arange(int(s)) for s in size], indexing='ij')
+    return torch.stack(grids, dim=-1)
+
+
+def sort_bbox(bbox, labels=None, descending=False):
+    """utils.py:362-366: boxes [4, n] sorted by (w+1)(h+1) area."""
+    w, h = wh_from_xyxy(bbox)
+    _, idx = (w * h).sort(descending=descending)
+    return bbox[:, idx], labels[idx] if labels is not None else None
+
+
+def concate_grid_result(grid_res, last=True):
+    """utils.py:372-374: per-level grid tensors flattened and concatenated."""
+    grid_res = [x.reshape(-1, x.shape[-1]) if last else x.reshape(x.shape[0], -1) for x in grid_res]
+    return torch.cat(grid_res, dim=0 if last else -1)

@@ -290,6 +290,42 @@ def gen_rpn_loss(rpn_head_mod):
     save('rpn_loss.npz', **res)
 
 
+def gen_atss(fcos_head_mod):
+    """FCOSHead.single_image_targets_atss (fcos_head.py:283-368) on the cfg5 geometry.
+    The reference's topk_by_center (fcos_head.py:106-116) computes the row index with `/`,
+    which on current torch yields float indices that cannot index; it is run here with `//`
+    (its evident intent)."""
+    def topk_by_center(anchors, bbox, k):
+        h, w = anchors.shape[-2:]
+        flat = anchors.view(4, -1)
+        ctr = torch.stack(list(fcos_head_mod.utils.center_of(flat)))
+        bctr = torch.stack(list(fcos_head_mod.utils.center_of(bbox))).view(-1, 1)
+        l2 = (ctr - bctr).norm(dim=0)
+        _, k_inds = l2.topk(k, largest=False)
+        return k_inds % w, k_inds // w, flat[:, k_inds], k_inds.numel()
+
+    fcos_head_mod.topk_by_center = topk_by_center
+    head = fcos_head_mod.FCOSHead(
+        num_classes=21, in_channels=256, stacked_convs=1, feat_channels=8, strides=inputs.RETINA_STRIDES,
+        reg_std=1200, reg_mean=0, atss_cfg=cd(dict(topk=9, scale=8)),
+        loss_cls=cd(dict(type='FocalLoss', use_sigmoid=True, loss_weight=1.0)),
+        loss_bbox=cd(dict(type='GIoULoss', loss_weight=2.0)),
+        loss_centerness=cd(dict(type='CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0)))
+    import lib.anchor as lib_anchor
+    anchors = [lib_anchor.AnchorCreator(base=s, scales=[8], aspect_ratios=[1.0])(s, g).squeeze()
+               for s, g in zip(inputs.RETINA_STRIDES, inputs.RETINA_GRIDS)]
+    dummy = [torch.zeros(20, h, w) for h, w in inputs.RETINA_GRIDS]
+    res = {}
+    for i, (b, l) in enumerate(inputs.atss_cases()):
+        cls, reg, ctr = head.single_image_targets_atss(dummy, dummy, dummy, anchors, torch.from_numpy(b),
+                                                       torch.from_numpy(l), inputs.img_meta(), None)
+        res['cls_{}'.format(i)] = torch.cat([c.view(-1) for c in cls]).numpy().astype(np.int8)
+        res['reg_{}'.format(i)] = torch.cat([r.view(-1, 4) for r in reg]).numpy()
+        res['ctr_{}'.format(i)] = torch.cat([c.view(-1) for c in ctr]).numpy()
+    res['n'] = np.int64(len(inputs.atss_cases()))
+    save('atss.npz', **res)
+
+
 def main():
     if not os.path.isdir(os.path.join(REF, 'lib')):
         print('reference not found at {}: nothing to generate (fixtures are committed)'.format(REF))
@@ -304,12 +340,18 @@ def main():
     torch.set_num_threads(8)
     if '--voc' in sys.argv or not os.path.exists(os.path.join(HERE, 'voc_gts.npz')):
         gen_voc_gts()
+    if '--only-atss' in sys.argv:
+        import lib.heads.fcos_head as fcos_head_mod
+        gen_atss(fcos_head_mod)
+        return 0
     gen_anchors(lib_anchor)
     gen_assign(lib_anchor, region, utils)
     gen_targets(lib_anchor, region, lib_anchor, bbox_mod, utils)
     gen_rpn(lib_anchor, rpn_head_mod)
     gen_levels(region)
     gen_rpn_loss(rpn_head_mod)
+    import lib.heads.fcos_head as fcos_head_mod
+    gen_atss(fcos_head_mod)
     return 0
 
 

@@ -61,3 +61,19 @@ def random_boxes(seed, n, img=IMG_SHAPE, min_wh=2.0, max_wh=400.0):
 def feature_maps(seed, grids, channels, batch):
     rng = np.random.default_rng(seed)
     return [rng.standard_normal((batch, channels, h, w)).astype(np.float32) for h, w in grids]
+
+
+def atss_cases():
+    """(gt boxes [4, G] f32, labels [G] i64) cases for the ATSS fixtures: 8 VOC images plus
+    synthetic sets (many boxes, tiny boxes, border boxes, one box)."""
+    gts = voc_gts()
+    cases = [gts[i] for i in range(8)]
+    rng = np.random.default_rng(77)
+    b = random_boxes(21, 40)
+    cases.append((b, rng.integers(1, 21, 40).astype(np.int64)))
+    b = random_boxes(22, 12, min_wh=1.0, max_wh=12.0)
+    cases.append((b, rng.integers(1, 21, 12).astype(np.int64)))
+    b = np.array([[0, 0, 40, 30], [950, 560, 999, 599], [0, 300, 999, 599], [480, 0, 520, 599]], np.float32).T
+    cases.append((b.copy(), np.array([3, 7, 11, 15], np.int64)))
+    cases.append((np.array([[100.5], [200.25], [300.75], [260.0]], np.float32), np.array([9], np.int64)))
+    return cases

@@ -415,3 +415,102 @@ def test_faster_rcnn_fpn_forward_train_runs(dev):
     for k, v in losses.items():
         assert torch.isfinite(v).all(), k
     sum(losses.values()).backward()
+
+
+# ----------------------------------------------------------------- a16 ATSS / LTRB
+def _atss_anchor_flat(dev):
+    from frcnn_amd import ops
+    from frcnn_amd.anchor import AnchorCreator
+    parts = []
+    for s, g in zip(inputs.RETINA_STRIDES, inputs.RETINA_GRIDS):
+        c = AnchorCreator(base=s, scales=[8], aspect_ratios=[1.0])
+        parts.append(ops.anchor_grid([g], [float(s)], c.ws, c.hs, 1, False, dev))
+    return torch.cat(parts, 1).contiguous()
+
+
+def test_atss_assign_batched_vs_oracle(dev):
+    """All ATSS cases as ONE batch (ragged gt counts 1..40): labels, ltrb and centerness
+    bit-exact against the oracle (both use correctly rounded f32 sqrt/div)."""
+    from frcnn_amd import ops
+    cases = inputs.atss_cases()
+    anchors = _atss_anchor_flat(dev)
+    o_anchors = [oracle.anchor_grid(s, [8], [1.0], s, g).reshape(4, -1)
+                 for s, g in zip(inputs.RETINA_STRIDES, inputs.RETINA_GRIDS)]
+    assert np.array_equal(anchors.cpu().numpy(), np.concatenate(o_anchors, 1))
+    cls, reg, ctr = ops.atss_assign(anchors, inputs.RETINA_GRIDS, [float(s) for s in inputs.RETINA_STRIDES],
+                                    [T(b, dev) for b, _ in cases], [T(l, dev) for _, l in cases],
+                                    [inputs.IMG_SHAPE] * len(cases), 9)
+    cls, reg, ctr = cls.cpu().numpy(), reg.cpu().numpy(), ctr.cpu().numpy()
+    for i, (b, l) in enumerate(cases):
+        c, r, t = oracle.atss_targets(o_anchors, inputs.RETINA_GRIDS, inputs.RETINA_STRIDES, b, l, inputs.IMG_SHAPE)
+        assert np.array_equal(cls[i], c), (i, np.nonzero(cls[i] != c)[0][:10])
+        assert np.array_equal(reg[i], r), i
+        assert np.array_equal(ctr[i], t), i
+
+
+def test_atss_head_single_image_and_edges(dev):
+    """FCOSHead.single_image_targets_atss (reference signature, per-level [H, W, k] outputs),
+    an image with no gts, and a smaller img_shape (paint region)."""
+    from frcnn_amd import ops
+    from frcnn_amd.heads.fcos_head import FCOSHead
+    head = FCOSHead(num_classes=21, in_channels=8, stacked_convs=1, feat_channels=8,
+                    strides=inputs.RETINA_STRIDES, reg_std=1200, atss_cfg=dict(topk=9, scale=8),
+                    loss_cls=dict(type='FocalLoss', use_sigmoid=True, loss_weight=1.0),
+                    loss_bbox=dict(type='GIoULoss', loss_weight=2.0),
+                    loss_centerness=dict(type='CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0)).to(dev)
+    b, l = inputs.atss_cases()[0]
+    outs = [torch.zeros(20, h, w, device=dev) for h, w in inputs.RETINA_GRIDS]
+    cls_t, reg_t, ctr_t = head.single_image_targets_atss(outs, outs, outs, [None] * 5, T(b, dev), T(l, dev),
+                                                        {'img_shape': (600, 1000, 3)}, None)
+    o_anchors = [oracle.anchor_grid(s, [8], [1.0], s, g).reshape(4, -1)
+                 for s, g in zip(inputs.RETINA_STRIDES, inputs.RETINA_GRIDS)]
+    c, r, t = oracle.atss_targets(o_anchors, inputs.RETINA_GRIDS, inputs.RETINA_STRIDES, b, l, inputs.IMG_SHAPE)
+    assert [tuple(x.shape) for x in cls_t] == [(h, w, 1) for h, w in inputs.RETINA_GRIDS]
+    assert np.array_equal(torch.cat([x.reshape(-1) for x in cls_t]).cpu().numpy(), c)
+    assert np.array_equal(torch.cat([x.reshape(-1, 4) for x in reg_t]).cpu().numpy(), r)
+    assert np.array_equal(torch.cat([x.reshape(-1) for x in ctr_t]).cpu().numpy(), t)
+    # no gts + a small image: only painting
+    anchors = _atss_anchor_flat(dev)
+    empty = torch.zeros(4, 0, device=dev)
+    cls, reg, ctr = ops.atss_assign(anchors, inputs.RETINA_GRIDS, [float(s) for s in inputs.RETINA_STRIDES],
+                                    [empty, T(b, dev)], [torch.zeros(0, dtype=torch.int64, device=dev), T(l, dev)],
+                                    [(300, 500), (300, 500)], 9)
+    c0, _, _ = oracle.atss_targets(o_anchors, inputs.RETINA_GRIDS, inputs.RETINA_STRIDES, np.zeros((4, 0), np.float32),
+                                   np.zeros(0, np.int64), (300, 500))
+    c1, r1, t1 = oracle.atss_targets(o_anchors, inputs.RETINA_GRIDS, inputs.RETINA_STRIDES, b, l, (300, 500))
+    assert np.array_equal(cls[0].cpu().numpy(), c0) and (c0 > 0).sum() == 0 and (c0 == -1).sum() > 0
+    assert np.array_equal(cls[1].cpu().numpy(), c1)
+    assert np.array_equal(reg[1].cpu().numpy(), r1) and np.array_equal(ctr[1].cpu().numpy(), t1)
+
+
+def test_fcos_atss_forward_train_loss(dev):
+    """cfg5 head forward+loss through the HIP targets equals the same losses computed from the
+    oracle's targets (reference calc_loss, fcos_head.py:418-534)."""
+    from frcnn_amd.heads.fcos_head import FCOSHead
+    torch.manual_seed(0)
+    head = FCOSHead(num_classes=21, in_channels=16, stacked_convs=1, feat_channels=16,
+                    strides=inputs.RETINA_STRIDES, reg_std=1200, atss_cfg=dict(topk=9, scale=8),
+                    loss_cls=dict(type='FocalLoss', use_sigmoid=True, loss_weight=1.0),
+                    loss_bbox=dict(type='GIoULoss', loss_weight=2.0),
+                    loss_centerness=dict(type='CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0)).to(dev)
+    head.init_weights()
+    feats = [torch.randn(2, 16, h, w, device=dev) for h, w in inputs.RETINA_GRIDS]
+    cases = inputs.atss_cases()[:2]
+    metas = [inputs.img_meta(), inputs.img_meta()]
+    losses = head.forward_train(feats, [T(b, dev) for b, _ in cases], [T(l, dev) for _, l in cases], metas, None)
+    assert set(losses) == {'cls_loss', 'ctr_loss', 'bbox_loss'}
+    o_anchors = [oracle.anchor_grid(s, [8], [1.0], s, g).reshape(4, -1)
+                 for s, g in zip(inputs.RETINA_STRIDES, inputs.RETINA_GRIDS)]
+    tars = [oracle.atss_targets(o_anchors, inputs.RETINA_GRIDS, inputs.RETINA_STRIDES, b, l, inputs.IMG_SHAPE)
+            for b, l in cases]
+    with torch.no_grad():
+        co, ro, to = head.forward(feats)
+    flat = lambda xs: torch.cat([x.reshape(2, x.shape[1], -1) for x in xs], -1).permute(1, 0, 2).reshape(
+        xs[0].shape[1], -1)
+    ref = head.calc_loss_flat(flat(co), flat(ro), flat(to), T(np.concatenate([t[0] for t in tars]), dev),
+                              T(np.concatenate([t[1] for t in tars]), dev), T(np.concatenate([t[2] for t in tars]), dev))
+    for k in losses:
+        assert torch.isfinite(losses[k]).all()
+        torch.testing.assert_close(losses[k].detach(), ref[k], rtol=1e-6, atol=0)
+    sum(losses.values()).backward()
+    assert head.fcos_cls.weight.grad is not None
