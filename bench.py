@@ -52,7 +52,7 @@ def make_batch(dev, batch, seed, rank=0):
     g = torch.Generator(device='cpu').manual_seed(seed + 1000 * rank)
     imgs = torch.randn(batch, 3, PAD_SHAPE[0], PAD_SHAPE[1], generator=g).to(dev)
     gts = voc_gts()
-    sel = [gts[(rank * batch + i) % len(gts)] for i in range(batch)]
+    sel = [gts[i] for i in shard_images(None, rank, batch)]
     boxes = [torch.from_numpy(b).to(dev) for b, _ in sel]
     labels = [torch.from_numpy(l).to(dev) for _, l in sel]
     return imgs, boxes, labels, [img_meta() for _ in range(batch)]
@@ -107,6 +107,20 @@ def cpu_baseline(seed, max_s):
                       '{} threads)'.format(n, threads)}
 
 
+def max_over_ranks(elapsed, dev, world):
+    """Job time = the slowest rank's (weak scaling: every rank has its own shard)."""
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_images(world, rank, batch):
+    """VOC gt indices of this rank's images: disjoint per rank, ranks x batch in total."""
+    n = len(voc_gts())
+    return [(rank * batch + i) % n for i in range(batch)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -156,10 +170,7 @@ def main():
     ops.ROI_ALIGN_PROFILE['on'] = False
     assert torch.isfinite(loss).all()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
+    t_max = max_over_ranks(elapsed, dev, world)
 
     recs = ops.ROI_ALIGN_PROFILE['records']
     ms = [r[0].elapsed_time(r[1]) for r in recs]  # per-launch event pairs inside the steps

@@ -10,6 +10,8 @@
 //        readlane'd diagonal words (pure register/SALU work), then all
 //        waves OR the kept rows' words into the LDS suppression bitmap with
 //        8 independent loads per lane in flight.
+#include <stdlib.h>
+
 #include "block_ops.h"
 
 namespace frh {
@@ -51,6 +53,12 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
   uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -122,14 +130,218 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   if (tid == 0) kcounts[s] = s_nkeep;
 }
 
+// Pipelined scan: the resolve chain of one segment never waits on memory.
+//  wave 0 (resolver), per 64-row block b: suppression word remv[b] | own,
+//    resolve the 64 candidates by visiting only unsuppressed ones (lowest set
+//    bit of the complement, readlane of the diagonal word), publish the kept
+//    bits, and OR the kept rows' word b+1 itself (wave-wide OR) -> `own` for
+//    the next block.  Its diagonal / next-word tiles come from an LDS ring.
+//  wave 1 (loader): stages the diagonal and next-word tiles of blocks ahead
+//    of the resolver into a kNmsRing-deep LDS ring.
+//  waves 2..3 (helpers), per block j: prefetch rows of block j for words
+//    >= j+2 BEFORE its kept bits exist, then OR the kept rows into remv with
+//    LDS atomics and publish their own progress (one counter per wave).  The resolver needs block j's
+//    helpers only at block j+2: one block of slack.
+// Wave hand-off is through LDS counters (release/acquire, workgroup scope).
+constexpr int kNmsHelpers = 2;
+constexpr int kNmsRing = 8;
+constexpr int kNmsRowGroups = kNmsHelpers * kWave / 32;  // 4 row groups x 32 word lanes
+constexpr int kNmsRowsPer = 64 / kNmsRowGroups;
+
+// OR over the 64 lanes with DPP row ops (no LDS round trip); uniform result.
+__device__ __forceinline__ uint32_t wave_or_u32_dpp(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);  // row_mirror
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint64_t wave_or_u64_dpp(uint64_t v) {
+  return ((uint64_t)wave_or_u32_dpp((uint32_t)(v >> 32)) << 32) | wave_or_u32_dpp((uint32_t)v);
+}
+
+__device__ __forceinline__ int lds_acquire(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), o, kWave) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)v, o, kWave);
+    v |= w;
+  }
+  return v;
+}
+
+template <int kParallel>
+__global__ void __launch_bounds__(256) nms_scan_pipe_kernel(const uint64_t* __restrict__ mask,
+                                                            const int32_t* __restrict__ counts, int64_t n_max,
+                                                            int nbw, int max_keep, int32_t* __restrict__ keep,
+                                                            int64_t kstride, int32_t* __restrict__ kcounts,
+                                                            uint64_t* __restrict__ dbg) {
+  __shared__ uint64_t remv[kMaxNmsWords];
+  __shared__ uint64_t kbs[kMaxNmsWords];
+  __shared__ uint64_t ring_diag[kNmsRing][kWave], ring_next[kNmsRing][kWave];
+  __shared__ int s_resolved, s_tiles, s_stop;
+  __shared__ int s_applied[kNmsHelpers];  // per helper wave: blocks applied (a shared count could hide a laggard)
+  const int s = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
+  const int n = counts[s];
+  const int nb = (n + 63) >> 6;
+  for (int w = tid; w < nb; w += blockDim.x) remv[w] = 0;
+  if (tid < kNmsHelpers) s_applied[tid] = 0;
+  if (tid == 0) {
+    s_resolved = 0;
+    s_tiles = 0;
+    s_stop = nb;
+  }
+  __syncthreads();
+  const uint64_t* M = mask + (int64_t)s * n_max * nbw;
+  if (wave == 0) {
+    int32_t* K = keep + (int64_t)s * kstride;
+    int nk = 0;
+    uint64_t own = 0;
+    for (int b = 0; b < nb; ++b) {
+      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b] = wall_clock64();
+      while (lds_acquire(&s_tiles) < b + 1) __builtin_amdgcn_s_sleep(1);
+      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 1] = wall_clock64();
+      if (b >= 2)
+        for (int hw = 0; hw < kNmsHelpers; ++hw)
+          while (lds_acquire(&s_applied[hw]) < b - 1) __builtin_amdgcn_s_sleep(1);
+      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 2] = wall_clock64();
+      const uint64_t diag = ring_diag[b % kNmsRing][lane], nxt = ring_next[b % kNmsRing][lane];
+      // r / kb / todo are wave-uniform: readfirstlane makes that provable, so the
+      // visit loop runs on the scalar unit (s_ff1, s_or) with one readlane pair each
+      uint64_t r = readfirstlane64(remv[b] | own);
+      const int valid = n - b * 64;
+      if (valid < 64) r |= (~0ull) << valid;
+      // Bit-parallel greedy: an undecided candidate with no undecided suppressor
+      // before it is kept; the victims of the newly kept are dropped; repeat.
+      // Same keep set as the one-by-one greedy (the lowest undecided index is
+      // always decided, so it terminates), in rounds = suppression-chain depth.
+      uint64_t kb = 0, und = ~r;
+      if (kParallel == 1) {
+        while (und) {
+          const uint64_t sup = wave_or_u64_dpp(((und >> lane) & 1ull) ? diag : 0ull);
+          const uint64_t nk = und & ~sup;
+          kb |= nk;
+          const uint64_t vic = wave_or_u64_dpp(((nk >> lane) & 1ull) ? diag : 0ull);
+          und &= ~(nk | vic);
+        }
+      } else if (kParallel == 2) {
+        while (und) {
+          const uint64_t sup = readfirstlane64(wave_or_u64(((und >> lane) & 1ull) ? diag : 0ull));
+          const uint64_t nk = und & ~sup;
+          kb |= nk;
+          const uint64_t vic = readfirstlane64(wave_or_u64(((nk >> lane) & 1ull) ? diag : 0ull));
+          und &= ~(nk | vic);
+        }
+      } else {
+        while (und) {
+          const int i = __builtin_ctzll(und);
+          kb |= 1ull << i;
+          r |= readlane64(diag, i);
+          und = ~r & ((i == 63) ? 0ull : (~0ull << (i + 1)));
+        }
+      }
+      bool stop = false;
+      if (max_keep >= 0) {
+        const int room = max_keep - nk;
+        while (__popcll(kb) > room) kb &= ~(1ull << (63 - __clzll(kb)));  // drop lowest-score extras
+        stop = nk + __popcll(kb) >= max_keep;
+      }
+      if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
+      nk += __popcll(kb);
+      own = wave_or_u64_dpp(((kb >> lane) & 1ull) ? nxt : 0ull);
+      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 3] = wall_clock64();
+      if (lane == 0) {
+        kbs[b] = kb;
+        if (stop) s_stop = b;
+        lds_release(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1);
+      }
+      if (stop) break;
+    }
+    if (lane == 0) kcounts[s] = nk;
+  } else if (wave == 1) {
+    for (int j = 0; j < nb; ++j) {
+      const int row = j * 64 + lane, rc = row < n ? row : n - 1;
+      const uint64_t d = M[(int64_t)rc * nbw + j];
+      const uint64_t x = M[(int64_t)rc * nbw + (j + 1 < nbw ? j + 1 : j)];
+      while (lds_acquire(&s_resolved) < j - kNmsRing + 1) __builtin_amdgcn_s_sleep(1);
+      if (s_stop < j) break;
+      ring_diag[j % kNmsRing][lane] = row < n ? d : 0ull;
+      ring_next[j % kNmsRing][lane] = (row < n && j + 1 < nb) ? x : 0ull;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) lds_release(&s_tiles, j + 1);
+    }
+  } else {
+    const int h = tid - 2 * kWave;   // 0 .. 127
+    const int q = h & 31, rg = h >> 5;  // word lane, row group
+    // rows of block j, first word chunk (word j + 2 + q), loaded one block ahead
+    auto load = [&](int j, uint64_t (&v)[kNmsRowsPer]) {
+      const int wq = j + 2 + q, wc = wq < nbw ? wq : nbw - 1;
+#pragma unroll
+      for (int t = 0; t < kNmsRowsPer; ++t) {
+        const int rowj = j * 64 + rg + kNmsRowGroups * t;
+        v[t] = M[(int64_t)(rowj < n ? rowj : n - 1) * nbw + wc];
+      }
+    };
+    uint64_t v[kNmsRowsPer], vn[kNmsRowsPer];
+    load(0, v);
+    for (int j = 0; j < nb; ++j) {
+      const int wq = j + 2 + q;
+      load(j + 1 < nb ? j + 1 : j, vn);  // unconditional: keeps the vmcnt accounting exact
+      while (lds_acquire(&s_resolved) < j + 1) __builtin_amdgcn_s_sleep(1);
+      if (s_stop < j) break;
+      const uint64_t kb = kbs[j];
+      for (int w = wq; w < nb; w += 32) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int t = 0; t < kNmsRowsPer; ++t) {
+          const int rr = rg + kNmsRowGroups * t, rowj = j * 64 + rr;
+          if (((kb >> rr) & 1ull) && rowj < n) acc |= (w == wq) ? v[t] : M[(int64_t)rowj * nbw + w];
+        }
+        if (acc) atomicOr((unsigned long long*)&remv[w], (unsigned long long)acc);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) lds_release(&s_applied[wave - 2], j + 1);
+#pragma unroll
+      for (int t = 0; t < kNmsRowsPer; ++t) v[t] = vn[t];
+    }
+  }
+}
+
+// tools/bench_nms.py hooks (not part of the public header): scan variant 0 = legacy
+// block-synchronous scan, 1 = pipelined; optional per-block resolver timestamps.
+static int g_nms_scan_variant = -1;
+static uint64_t* g_nms_dbg = nullptr;
+
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                           uint64_t* mask, hipStream_t st) {
   const int nbw = (n_max + 63) / 64;
   dim3 g(nbw, nbw, S);
   hipLaunchKernelGGL(nms_mask_kernel, g, dim3(64), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw, thr, mask);
-  hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw, max_keep, keep,
-                     kstride, kcounts);
+  if (g_nms_scan_variant < 0) g_nms_scan_variant = getenv("FRH_NMS_SCAN_LEGACY") ? 0 : 1;
+  if (g_nms_scan_variant == 0)
+    hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw, max_keep, keep,
+                       kstride, kcounts);
+  else if (g_nms_scan_variant == 3)
+    hipLaunchKernelGGL(nms_scan_pipe_kernel<2>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
+                       max_keep, keep, kstride, kcounts, g_nms_dbg);
+  else if (g_nms_scan_variant == 2)
+    hipLaunchKernelGGL(nms_scan_pipe_kernel<0>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
+                       max_keep, keep, kstride, kcounts, g_nms_dbg);
+  else
+    hipLaunchKernelGGL(nms_scan_pipe_kernel<1>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
+                       max_keep, keep, kstride, kcounts, g_nms_dbg);
   return check_launch("nms");
 }
 
@@ -141,6 +353,11 @@ size_t nms_mask_bytes(int32_t S, int32_t n_max) {
 }  // namespace frh
 
 using namespace frh;
+
+extern "C" void frh_nms_scan_debug(int32_t variant, void* timestamps) {
+  g_nms_scan_variant = variant;
+  g_nms_dbg = reinterpret_cast<uint64_t*>(timestamps);
+}
 
 extern "C" size_t frh_nms_workspace(int32_t num_segs, int32_t n_max) {
   return nms_mask_bytes(num_segs, n_max > 0 ? n_max : 1);
