@@ -355,3 +355,43 @@ def atss_targets(anchors, grids, strides, gts, labels, img_shape, topk=9):
                            ctypes.c_int64(g.shape[1]), lab.ctypes.data_as(_I64), int(img_shape[0]),
                            int(img_shape[1]), int(topk), cls.ctypes.data_as(_I64), _f(reg), _f(ctr))
     return cls, reg, ctr
+
+
+def multiclass_nms(bbox, score, nms_channel, nms_iou, min_score=-1, max_num=None, score_factor=None,
+                   mode='official'):
+    """utils.multiclass_nms (lib/utils.py:224-269) + batched_nms (:211-221) in numpy f32:
+    candidate (box, class) pairs, coordinate offset label * max(candidate coords), one
+    greedy nms (this module's `nms`, torchvision semantics), first max_num."""
+    bbox = np.asarray(bbox, np.float32)
+    score = np.asarray(score, np.float32)
+    n, ncls = score.shape
+    simple = bbox.shape[1] == 4
+    chans = np.zeros(ncls, bool)
+    chans[list(nms_channel)] = True
+    if mode == 'official':
+        label = np.where(chans[None, :], np.arange(ncls)[None, :], -1).repeat(n, 0)
+        boxes = np.repeat(bbox[:, :, None], ncls, 2) if simple else bbox.reshape(n, 4, ncls)
+        boxes = boxes.transpose(0, 2, 1)
+        chosen = (score >= np.float32(min_score)) & (label != -1)
+        if score_factor is not None:
+            sf = np.asarray(score_factor, np.float32)
+            score = score * (sf[:, None] if sf.ndim == 1 else sf)
+        nb, ns, nl = boxes[chosen], score[chosen], label[chosen]
+    else:
+        lab = score.argmax(1)
+        sc = score[np.arange(n), lab]
+        if not simple:
+            bbox = bbox.reshape(n, 4, ncls)[np.arange(n), :, lab]
+        chosen = (sc >= np.float32(min_score)) & chans[lab]
+        if score_factor is not None:
+            sc = sc * np.asarray(score_factor, np.float32)
+        nb, ns, nl = bbox[chosen], sc[chosen], lab[chosen]
+    if ns.size == 0:
+        return nb, ns, nl
+    mx = nb.max()
+    off = nb + (nl.astype(np.float32) * mx).astype(np.float32)[:, None]
+    keep = np.asarray(nms(off, ns, nms_iou), np.int64)
+    kb, ks, kl = nb[keep], ns[keep], nl[keep]
+    if max_num is not None and ks.size > max_num:
+        kb, ks, kl = kb[:max_num], ks[:max_num], kl[:max_num]
+    return kb, ks, kl

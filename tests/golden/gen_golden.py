@@ -326,6 +326,56 @@ def gen_atss(fcos_head_mod):
     save('atss.npz', **res)
 
 
+def gen_multiclass_nms(utils):
+    """utils.multiclass_nms (utils.py:224-269), official and strict modes (torchvision nms
+    stubbed by the oracle restatement, see the module docstring)."""
+    res = {}
+    for i, (mode, n, ncls, per_class, factor) in enumerate(inputs.MCNMS_CASES):
+        bbox, score, sf, channels = inputs.mcnms_inputs(i)
+        kb, ks, kl = utils.multiclass_nms(torch.from_numpy(bbox), torch.from_numpy(score), channels, 0.5, 0.05, 100,
+                                          torch.from_numpy(sf) if sf is not None else None, mode=mode)
+        res['boxes_{}'.format(i)] = kb.numpy()
+        res['scores_{}'.format(i)] = ks.numpy()
+        res['labels_{}'.format(i)] = kl.numpy()
+    save('mcnms.npz', **res)
+
+
+def gen_retina(retina_mod, bbox_head_mod):
+    """RetinaHead.loss (anchor_head.py:113-199, no sampler, focal + smooth-L1), its
+    predict_single_image (anchor_head.py:207-262, strict NMS) and the cascade refine
+    (bbox_head.py:93-120)."""
+    gts = inputs.voc_gts()
+    head = retina_mod.RetinaHead(21, 256, 1, 8, loss_cls=cd(dict(type='FocalLoss', use_sigmoid=True)),
+                                 loss_bbox=cd(dict(type='SmoothL1Loss', beta=1.0 / 9.0, loss_weight=1.0)))
+    cfg = cd(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.5, neg_iou=0.4, min_pos_iou=0.0),
+                  allowed_border=-1))
+    res = {}
+    for i in range(2):
+        cls, reg = inputs.head_outputs(900 + i, inputs.RETINA_GRIDS, 9, 20, batch=2, cls_scale=1.0, reg_scale=0.2)
+        c, r = head.loss([torch.from_numpy(x) for x in cls], [torch.from_numpy(x) for x in reg],
+                         [torch.from_numpy(gts[2 * i + j][0]) for j in range(2)],
+                         [torch.from_numpy(gts[2 * i + j][1]) for j in range(2)],
+                         [inputs.img_meta(), inputs.img_meta()], cfg)
+        res['loss_{}'.format(i)] = np.array([float(c), float(r)], np.float64)
+    anchors = [a for a in head.create_anchors(inputs.RETINA_GRIDS)]
+    test_cfg = cd(dict(pre_nms=1000, min_bbox_size=0, min_score=0.05, nms_iou=0.5, nms_type='strict',
+                       max_per_img=100))
+    cls, reg = inputs.head_outputs(950, inputs.RETINA_GRIDS, 9, 20, batch=1, cls_scale=2.0, reg_scale=0.2)
+    kb, ks, kl = head.predict_single_image([torch.from_numpy(c[0]) for c in cls], [torch.from_numpy(r[0]) for r in reg],
+                                           anchors, inputs.img_meta(), test_cfg)
+    res['pred_boxes'], res['pred_scores'], res['pred_labels'] = kb.numpy(), ks.numpy(), kl.numpy()
+    bh = bbox_head_mod.BBoxHead.__new__(bbox_head_mod.BBoxHead)
+    torch.nn.Module.__init__(bh)
+    for agnostic in (False, True):
+        bh.reg_class_agnostic, bh.num_classes = agnostic, 21
+        bh.target_means, bh.target_stds = [0.0] * 4, [0.05, 0.05, 0.1, 0.1]
+        props, label, reg_out, is_gt = inputs.refine_inputs(agnostic)
+        out = bh.refine_bboxes_single_image(torch.from_numpy(props), torch.from_numpy(label),
+                                            torch.from_numpy(reg_out), torch.from_numpy(is_gt), inputs.img_meta())
+        res['refine_{}'.format(int(agnostic))] = out.numpy()
+    save('retina.npz', **res)
+
+
 def main():
     if not os.path.isdir(os.path.join(REF, 'lib')):
         print('reference not found at {}: nothing to generate (fixtures are committed)'.format(REF))
@@ -344,6 +394,12 @@ def main():
         import lib.heads.fcos_head as fcos_head_mod
         gen_atss(fcos_head_mod)
         return 0
+    if '--only-new' in sys.argv:
+        import lib.heads.retina_head as retina_mod
+        import lib.heads.bbox_head as bbox_head_mod
+        gen_multiclass_nms(utils)
+        gen_retina(retina_mod, bbox_head_mod)
+        return 0
     gen_anchors(lib_anchor)
     gen_assign(lib_anchor, region, utils)
     gen_targets(lib_anchor, region, lib_anchor, bbox_mod, utils)
@@ -352,6 +408,10 @@ def main():
     gen_rpn_loss(rpn_head_mod)
     import lib.heads.fcos_head as fcos_head_mod
     gen_atss(fcos_head_mod)
+    import lib.heads.retina_head as retina_mod
+    import lib.heads.bbox_head as bbox_head_mod
+    gen_multiclass_nms(utils)
+    gen_retina(retina_mod, bbox_head_mod)
     return 0
 
 

@@ -77,3 +77,45 @@ def atss_cases():
     cases.append((b.copy(), np.array([3, 7, 11, 15], np.int64)))
     cases.append((np.array([[100.5], [200.25], [300.75], [260.0]], np.float32), np.array([9], np.int64)))
     return cases
+
+
+# (mode, n boxes, score channels, class-specific boxes, score factor) for multiclass_nms
+MCNMS_CASES = [('official', 300, 21, False, False), ('official', 400, 21, True, False),
+               ('strict', 500, 20, False, True), ('strict', 300, 21, True, False)]
+
+
+def mcnms_inputs(i):
+    """(bbox [n, 4] or [n, 4*C], score [n, C], score_factor or None, channels) of case i:
+    clustered boxes (heavy overlap) with softmax / sigmoid-like scores."""
+    mode, n, ncls, per_class, factor = MCNMS_CASES[i]
+    rng = np.random.default_rng(1100 + i)
+    ctr = rng.uniform(50, 950, (12, 2))
+    k = rng.integers(0, 12, n)
+    wh = rng.uniform(20, 200, (n, 2))
+    c = ctr[k] + rng.normal(0, 15, (n, 2))
+    base = np.stack([c[:, 0] - wh[:, 0] / 2, c[:, 1] - wh[:, 1] / 2, c[:, 0] + wh[:, 0] / 2, c[:, 1] + wh[:, 1] / 2], 1)
+    if per_class:
+        jit = rng.normal(0, 4, (n, 4, ncls))
+        bbox = (base[:, :, None] + jit).reshape(n, 4 * ncls)
+    else:
+        bbox = base
+    logits = rng.normal(0, 2, (n, ncls))
+    if mode == 'official':
+        e = np.exp(logits - logits.max(1, keepdims=True))
+        score = e / e.sum(1, keepdims=True)
+        channels = list(range(1, ncls))
+    else:
+        score = 1 / (1 + np.exp(-logits))
+        channels = list(range(0, ncls))
+    sf = rng.uniform(0.2, 1.0, n).astype(np.float32) if factor else None
+    return bbox.astype(np.float32), score.astype(np.float32), sf, channels
+
+
+def refine_inputs(agnostic, n=512, ncls=21):
+    """(props [4, n], label [n], reg_out [n, 4] or [n, 4*C], is_gt [n] u8) for BBoxHead.refine."""
+    rng = np.random.default_rng(1200 + int(agnostic))
+    props = random_boxes(1201, n)
+    label = rng.integers(0, ncls, n).astype(np.int64)
+    reg_out = rng.normal(0, 1.0, (n, 4 if agnostic else 4 * ncls)).astype(np.float32)
+    is_gt = (np.arange(n) < 9).astype(np.uint8)
+    return props, label, reg_out, is_gt

@@ -514,3 +514,77 @@ def test_fcos_atss_forward_train_loss(dev):
         torch.testing.assert_close(losses[k].detach(), ref[k], rtol=1e-6, atol=0)
     sum(losses.values()).backward()
     assert head.fcos_cls.weight.grad is not None
+
+
+# ----------------------------------------------------------------- a11 multiclass NMS
+@pytest.mark.parametrize('i', range(len(inputs.MCNMS_CASES)))
+def test_multiclass_nms_vs_reference(dev, golden, i):
+    """utils.multiclass_nms on the HIP NMS (official / strict, class-specific boxes, score
+    factor) against the reference's outputs: bit-exact."""
+    from frcnn_amd import utils
+    g = golden('mcnms.npz')
+    bbox, score, sf, channels = inputs.mcnms_inputs(i)
+    mode = inputs.MCNMS_CASES[i][0]
+    kb, ks, kl = utils.multiclass_nms(T(bbox, dev), T(score, dev), channels, 0.5, 0.05, 100,
+                                      T(sf, dev) if sf is not None else None, mode=mode)
+    np.testing.assert_array_equal(kb.cpu().numpy(), g['boxes_{}'.format(i)])
+    np.testing.assert_array_equal(ks.cpu().numpy(), g['scores_{}'.format(i)])
+    np.testing.assert_array_equal(kl.cpu().numpy(), g['labels_{}'.format(i)])
+
+
+# ----------------------------------------------------------------- a15 Retina dense path, a17 refine
+def _retina_head(dev):
+    from frcnn_amd.heads.retina_head import RetinaHead
+    return RetinaHead(21, 256, 1, 8, loss_cls=dict(type='FocalLoss', use_sigmoid=True),
+                      loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0, loss_weight=1.0)).to(dev)
+
+
+def test_retina_loss_vs_reference(dev, golden):
+    """cfg3 dense path: A=9 anchors, MaxIoU (0.5, 0.4, 0.0), no sampler, focal + smooth-L1,
+    two images batched; f32 sums over ~116k x 20 terms -> rtol 1e-5."""
+    from frcnn_amd.config import ConfigDict
+    g = golden('retina.npz')
+    gts = inputs.voc_gts()
+    head = _retina_head(dev)
+    cfg = ConfigDict(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.5, neg_iou=0.4, min_pos_iou=0.0),
+                          allowed_border=-1))
+    for i in range(2):
+        cls, reg = inputs.head_outputs(900 + i, inputs.RETINA_GRIDS, 9, 20, batch=2, cls_scale=1.0, reg_scale=0.2)
+        c, r = head.loss([T(x, dev) for x in cls], [T(x, dev) for x in reg],
+                         [T(gts[2 * i + j][0], dev) for j in range(2)], [T(gts[2 * i + j][1], dev) for j in range(2)],
+                         [inputs.img_meta(), inputs.img_meta()], cfg)
+        np.testing.assert_allclose([float(c), float(r)], g['loss_{}'.format(i)], rtol=1e-5)
+
+
+def test_retina_predict_vs_reference(dev, golden):
+    """cfg3 test path (anchor_head.py:207-262, strict multiclass NMS).  sigmoid / exp are
+    device math (<= 1 ulp from torch CPU), so boxes/scores to 1e-4 and labels exact."""
+    from frcnn_amd.config import ConfigDict
+    g = golden('retina.npz')
+    head = _retina_head(dev)
+    anchors = head.create_anchors(inputs.RETINA_GRIDS)
+    cfg = ConfigDict(dict(pre_nms=1000, min_bbox_size=0, min_score=0.05, nms_iou=0.5, nms_type='strict',
+                          max_per_img=100))
+    cls, reg = inputs.head_outputs(950, inputs.RETINA_GRIDS, 9, 20, batch=1, cls_scale=2.0, reg_scale=0.2)
+    kb, ks, kl = head.predict_single_image([T(c[0], dev) for c in cls], [T(r[0], dev) for r in reg], anchors,
+                                           inputs.img_meta(), cfg)
+    np.testing.assert_array_equal(kl.cpu().numpy(), g['pred_labels'])
+    np.testing.assert_allclose(ks.cpu().numpy(), g['pred_scores'], rtol=1e-5)
+    np.testing.assert_allclose(kb.cpu().numpy(), g['pred_boxes'], rtol=0, atol=1e-3)
+
+
+@pytest.mark.parametrize('agnostic', [False, True])
+def test_cascade_refine_vs_reference(dev, golden, agnostic):
+    """a17 BBoxHead.refine_bboxes_single_image: class column select, gt rows dropped,
+    decode with cascade stds, clamp (HIP param2bbox; exp within 1 ulp -> atol 1e-3 px)."""
+    from frcnn_amd.heads.bbox_head import BBoxHead
+    g = golden('retina.npz')
+    bh = BBoxHead(21, target_means=(0.0,) * 4, target_stds=(0.05, 0.05, 0.1, 0.1), reg_class_agnostic=agnostic,
+                  loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=False),
+                  loss_bbox=dict(type='SmoothL1Loss', beta=1.0))
+    props, label, reg_out, is_gt = inputs.refine_inputs(agnostic)
+    out = bh.refine_bboxes_single_image(T(props, dev), T(label, dev), T(reg_out, dev), T(is_gt, dev),
+                                        inputs.img_meta())
+    ref = g['refine_{}'.format(int(agnostic))]
+    assert tuple(out.shape) == ref.shape
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=1e-3)

@@ -222,3 +222,15 @@ def test_atss_targets_vs_reference(golden):
         ok[bad] = False
         np.testing.assert_allclose(t[ok], rt[ok], rtol=2.5e-7, atol=0, err_msg=str(i))
         assert (c > 0).sum() > 0
+
+
+# ----------------------------------------------------------------- a11 multiclass NMS
+@pytest.mark.parametrize('i', range(len(inputs.MCNMS_CASES)))
+def test_multiclass_nms_vs_reference(golden, i):
+    g = golden('mcnms.npz')
+    bbox, score, sf, channels = inputs.mcnms_inputs(i)
+    mode = inputs.MCNMS_CASES[i][0]
+    kb, ks, kl = oracle.multiclass_nms(bbox, score, channels, 0.5, 0.05, 100, sf, mode=mode)
+    np.testing.assert_array_equal(kb, g['boxes_{}'.format(i)])
+    np.testing.assert_array_equal(ks, g['scores_{}'.format(i)])
+    np.testing.assert_array_equal(kl, g['labels_{}'.format(i)])
