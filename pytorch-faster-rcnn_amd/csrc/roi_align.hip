@@ -645,16 +645,21 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevel
   fwd_buf_block<U>(lv, c, out, k, blockIdx.y * kRoiChanChunk, roi_geom(c, lv, k));
 }
 
-__device__ __forceinline__ int wave_min_i32(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
-  return v;
+// Wave-wide min / max with DPP row ops (no LDS round trip); result in every lane.
+template <bool kMin>
+__device__ __forceinline__ int wave_minmax_i32(int v) {
+  const int id = kMin ? 0x7fffffff : (int)0x80000000;
+  auto op = [](int a, int b) { return kMin ? min(a, b) : max(a, b); };
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast15
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast31
+  return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, kWave));
-  return v;
-}
+__device__ __forceinline__ int wave_min_i32(int v) { return wave_minmax_i32<true>(v); }
+__device__ __forceinline__ int wave_max_i32(int v) { return wave_minmax_i32<false>(v); }
 
 // Wave-staged variant (sampling ratio 2, ph*pw <= 64, 2*ph and 2*pw <= 64).
 // Every tap of a RoI lies in the window [y0, y1] x [x0, x1] of its level;
@@ -673,15 +678,19 @@ constexpr int kWinMax = 1024;
 constexpr int kWinR = kWinMax / kWave;
 constexpr int kWaveChans = kRoiChanChunk / (kRoiThreads / kWave);
 
-template <int kStageMax>
+// kChunk: channels per workgroup (kChunk / 4 per wave).  kSkip (diagnostics only):
+// 1 = skip staged RoIs, 2 = skip gathered ones.
+template <int kStageMax, int kSkip = 0, int kChunk = kRoiChanChunk>
 __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
                                                                         float* __restrict__ out) {
   constexpr int SR = 2;
   __shared__ float slab_all[kRoiThreads / kWave][kWinMax];
   const int64_t k = blockIdx.x;
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kWaveChans;
-  const int nch = min(kWaveChans, c.C - cw0);
+  // readfirstlane: the wave index is uniform, and the compiler must know it (soffset operands)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  constexpr int kWC = kChunk / (kRoiThreads / kWave);
+  const int cw0 = blockIdx.y * kChunk + wave * kWC;
+  const int nch = min(kWC, c.C - cw0);
   float* slab = slab_all[wave];
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl;
@@ -704,9 +713,12 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_lds_kernel(RoiLevel
   // odd slab row stride: the 4 tap rows of a wave's bins spread over the LDS banks
   const int ws = (x1 - x0 + 2) | 1, n = any ? (y1 - y0 + 1) * ws : 0;
   if (n > kStageMax) {  // uniform over the block (one RoI): large windows take the block gather path
-    fwd_buf_block<2>(lv, c, out, k, blockIdx.y * kRoiChanChunk, g);
+    if (kSkip != 2)
+      for (int cc = 0; cc < kChunk && blockIdx.y * kChunk + cc < c.C; cc += kRoiChanChunk)
+        fwd_buf_block<2>(lv, c, out, k, blockIdx.y * kChunk + cc, g);
     return;
   }
+  if (kSkip == 1) return;
   if (nch <= 0) return;
   const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
   const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
@@ -1127,7 +1139,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   const bool lds_ok = buf_ok && pooled_h * pooled_w <= 64 && 2 * pooled_h <= 64 && 2 * pooled_w <= 64;
   if (variant < 0) variant = lds_ok ? 10 : buf_ok ? 8 : 0;
   FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok) ||
-                  (variant >= 7 && variant <= 8 && buf_ok) || (variant >= 9 && variant <= 12 && lds_ok),
+                  (variant >= 7 && variant <= 8 && buf_ok) || (variant >= 9 && variant <= 16 && lds_ok),
               "roi_align variant %d unsupported here", variant);
   if (variant == 9)
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<kWinMax>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
@@ -1137,6 +1149,18 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<128>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   else if (variant == 12)
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<64>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 13)
+    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 1>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 14)
+    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 2>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  else if (variant == 15)
+    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 256>),
+                       dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0,
+                       as_stream(stream), lv, c, out);
+  else if (variant == 16)
+    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 128>),
+                       dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0,
+                       as_stream(stream), lv, c, out);
   else if (variant == 7)
     hipLaunchKernelGGL(roi_align_fwd_buf_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   else if (variant == 8)
