@@ -1,0 +1,44 @@
+# Faster R-CNN R50-C4 (BASELINE config 1), in the reference's config-file format.
+# Hyper-parameters follow the reference's configs/faster_rcnn_r50.py (single stride-16
+# level, RoIPool); data pipeline / optimiser sections are out of this build's scope.
+
+
+def _loss(kind, **kw):
+    return dict(type=kind, **kw)
+
+
+model = dict(
+    type='CascadeRCNN',
+    num_stages=1,
+    backbone=dict(type='ResNet', depth=50, frozen_stages=1, out_layers=(3,), pretrained=False),
+    neck=None,
+    rpn_head=dict(type='RPNHead', in_channels=1024, feat_channels=256, anchor_scales=[4, 8, 16, 32],
+                  anchor_ratios=[0.5, 1.0, 2.0], anchor_strides=[16],
+                  target_means=[0.0] * 4, target_stds=[1.0] * 4,
+                  loss_cls=_loss('CrossEntropyLoss', use_sigmoid=True, loss_weight=1.0),
+                  loss_bbox=_loss('SmoothL1Loss', beta=1.0 / 9.0, loss_weight=1.0)),
+    roi_extractor=dict(type='BasicRoIExtractor', output_size=(7, 7),
+                       roi_layers=[dict(type='RoIPool', spatial_scale=1.0 / 16.0, sampling_ratio=2)]),
+    rcnn_head=[dict(type='RCNNHead', in_channels=1024, roi_out_size=(7, 7), fc_channels=[1024, 1024],
+                    with_avg_pool=False, num_classes=21, target_means=[0.0] * 4,
+                    target_stds=[0.1, 0.1, 0.2, 0.2], reg_class_agnostic=False,
+                    loss_cls=_loss('CrossEntropyLoss', use_sigmoid=False, loss_weight=1.0),
+                    loss_bbox=_loss('SmoothL1Loss', beta=1.0, loss_weight=1.0))],
+)
+
+train_cfg = dict(
+    rpn=dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.7, neg_iou=0.3, min_pos_iou=0.3),
+             sampler=dict(type='RandomSampler', max_num=256, pos_num=128),
+             allowed_border=0),
+    rpn_proposal=dict(pre_nms=12000, post_nms=2000, max_num=2000, nms_iou=0.7, min_bbox_size=16),
+    rcnn=[dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.5, neg_iou=0.5, min_pos_iou=0.5),
+               sampler=dict(type='RandomSampler', max_num=128, pos_num=32))],
+    stage_loss_weight=[1.0],
+)
+
+test_cfg = dict(
+    rpn=dict(pre_nms=6000, post_nms=300, max_num=300, nms_iou=0.7, min_bbox_size=0.0),
+    rcnn=dict(min_score=0.05, nms_iou=0.3, max_per_img=100),
+)
+
+data = dict(train=dict(imgs_per_gpu=2), test=dict(imgs_per_gpu=2))

@@ -596,3 +596,31 @@ def test_cascade_refine_vs_reference(dev, golden, agnostic):
     ref = g['refine_{}'.format(int(agnostic))]
     assert tuple(out.shape) == ref.shape
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=1e-3)
+
+
+# ----------------------------------------------------------------- all BASELINE configs end to end
+@pytest.mark.parametrize('config', ['faster_rcnn_r50', 'faster_rcnn_r50_fpn', 'retinanet_r50_fpn',
+                                    'cascade_rcnn_r50_fpn', 'fcos_r50_fpn_atss'])
+def test_baseline_config_train_and_test(dev, config):
+    """Every BASELINE.json config builds from its config file through the registry and runs
+    forward_train (+ backward) and forward_test on the HIP path (2 images, 600x1000)."""
+    import os
+    import bench
+    from frcnn_amd import set_sampler_mode
+    set_sampler_mode('device', seed=3)
+    path = os.path.join(bench.REPO, 'pytorch-faster-rcnn_amd', 'configs', config + '.py')
+    model, _ = bench.make_model(dev, seed=0, config=path)
+    imgs, boxes, labels, metas = bench.make_batch(dev, 2, seed=1)
+    losses = model.forward_train(imgs, boxes, labels, metas)
+    assert len(losses) >= 2
+    for k, v in losses.items():
+        assert torch.isfinite(v).all(), (config, k)
+    sum(losses.values()).backward()
+    model.eval()
+    with torch.no_grad():
+        preds = model.forward_test(imgs, metas)
+    assert len(preds) == 3 and len(preds[0]) == 2  # (boxes, scores, labels) per image
+    for b, s, l in zip(*preds):
+        assert b.shape[0] == 4 and b.shape[1] == s.numel() == l.numel() <= 100
+        if s.numel():
+            assert (l >= 1).all() and (l <= 20).all()
