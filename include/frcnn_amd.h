@@ -284,6 +284,16 @@ int32_t frh_atss_assign(int32_t batch, int32_t num_levels, const int32_t* grid_h
                         int32_t topk, int64_t* cls, float* reg, float* ctr, void* workspace,
                         size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- backbone epilogue
+ * Frozen BatchNorm (+ residual) (+ ReLU) of the reference ResNet's bottlenecks
+ * (lib/backbones.py:69-76 keeps every BN in eval mode; torchvision Bottleneck.forward):
+ * y = act(x * s + b (+ skip)), s = gamma / sqrt(var + eps), b = beta - mean * s, per
+ * channel; x / skip / y contiguous NCHW f32 [n, c, hw], 16-byte aligned, hw % 4 == 0;
+ * gamma / beta may be NULL (1 / 0); y may alias x. */
+int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gamma,
+                   const float* beta, const float* mean, const float* var, float eps,
+                   int64_t n, int32_t c, int64_t hw, int32_t relu, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

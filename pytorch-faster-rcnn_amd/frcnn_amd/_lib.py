@@ -73,6 +73,7 @@ SIGNATURES = {
     'frh_roi_pool_bwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,
                                  c_vp]),
     'frh_atss_workspace': (c_size, [c_i32, c_i32, c_i32, c_i32, c_i64]),
+    'frh_bn_act': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_i64, c_i32, c_vp]),
     'frh_atss_assign': (c_i32, [c_i32, c_i32, P(c_i32), P(c_f32), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32,
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }

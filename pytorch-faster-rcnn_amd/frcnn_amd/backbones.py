@@ -16,6 +16,8 @@ import logging
 import torch
 from torch import nn
 
+from .ops import bn_act
+
 # blocks per stage for each depth
 _STAGE_BLOCKS = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
 _STAGE_WIDTH = (64, 256, 512, 1024, 2048)
@@ -42,11 +44,11 @@ class Bottleneck(nn.Module):
             self.downsample = nn.Sequential(*_conv_bn(in_channels, out_channels, 1, stride=stride))
 
     def forward(self, x):
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        skip = self.downsample(x) if self.do_downsample else x
-        return self.relu(y + skip)
+        # frozen BN (+ residual) + ReLU as one HIP epilogue pass per conv (ops.bn_act)
+        y = bn_act(self.conv1(x), self.bn1)
+        y = bn_act(self.conv2(y), self.bn2)
+        skip = bn_act(self.downsample[0](x), self.downsample[1], relu=False) if self.do_downsample else x
+        return bn_act(self.conv3(y), self.bn3, skip=skip)
 
 
 class ResNet(nn.Module):
@@ -68,7 +70,7 @@ class ResNet(nn.Module):
             setattr(self, 'layer{}'.format(s + 1), nn.Sequential(*blocks))
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(bn_act(self.conv1(x), self.bn1))
         outs = []
         for s in range(1, 5):
             x = getattr(self, 'layer{}'.format(s))(x)

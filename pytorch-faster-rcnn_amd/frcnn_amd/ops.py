@@ -555,3 +555,47 @@ def atss_assign(anchors, grid_sizes, strides, gt_list, label_list, img_shapes, t
          ptr(gcnt), ptr(labels), gmax, ptr(img_hw), int(topk), ptr(cls), ptr(reg), ptr(ctr), ptr(ws), ws_n,
          stream_of(cls))
     return cls, reg, ctr
+
+
+# ---------------------------------------------------------------- backbone epilogue (frozen BN + add + ReLU)
+class _FrozenBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, skip, weight, bias, mean, var, eps, relu):
+        n, c, h, w = x.shape
+        x = x.contiguous()
+        skip = skip.contiguous() if skip is not None else None
+        y = torch.empty_like(x)
+        call('frh_bn_act', ptr(x), ptr(skip), ptr(y), ptr(weight), ptr(bias), ptr(mean), ptr(var), float(eps), n, c,
+             h * w, int(bool(relu)), stream_of(x))
+        need_x = weight is not None and weight.requires_grad
+        ctx.save_for_backward(x if need_x else None, y if relu else None, weight, mean, var)
+        ctx.cfg = (eps, relu, skip is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, weight, mean, var = ctx.saved_tensors
+        eps, relu, has_skip = ctx.cfg
+        g = gy * (y > 0) if relu else gy
+        inv = torch.rsqrt(var + eps)
+        s = inv * weight if weight is not None else inv
+        gx = g * s.view(1, -1, 1, 1) if ctx.needs_input_grad[0] else None
+        gskip = g if has_skip and ctx.needs_input_grad[1] else None
+        gw = gb = None
+        if ctx.needs_input_grad[2]:
+            gw = (g * (x - mean.view(1, -1, 1, 1))).sum((0, 2, 3)) * inv
+        if ctx.needs_input_grad[3]:
+            gb = g.sum((0, 2, 3))
+        return gx, gskip, gw, gb, None, None, None, None
+
+
+def bn_act(x, bn, skip=None, relu=True):
+    """act(bn(x) (+ skip)) for an eval-mode BatchNorm2d in one HIP pass (frh_bn_act).
+    A BN in training mode (the reference never trains BN statistics) or CPU tensors take
+    the plain module ops."""
+    if bn.training or not x.is_cuda or x.dtype != torch.float32 or (x.shape[2] * x.shape[3]) % 4:
+        y = bn(x)
+        if skip is not None:
+            y = y + skip
+        return torch.relu_(y) if relu else y
+    return _FrozenBNAct.apply(x, skip, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu)

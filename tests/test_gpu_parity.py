@@ -624,3 +624,31 @@ def test_baseline_config_train_and_test(dev, config):
         assert b.shape[0] == 4 and b.shape[1] == s.numel() == l.numel() <= 100
         if s.numel():
             assert (l >= 1).all() and (l <= 20).all()
+
+
+# ----------------------------------------------------------------- backbone epilogue (frozen BN + add + ReLU)
+@pytest.mark.parametrize('skip,relu,shape', [(False, True, (2, 64, 76, 128)), (True, True, (2, 256, 38, 64)),
+                                             (False, False, (1, 512, 19, 32)), (True, True, (2, 2048, 19, 32))])
+def test_bn_act_matches_torch(dev, skip, relu, shape):
+    """frh_bn_act vs the PyTorch fp32 reference bn(x) (+ skip) (+ relu) in eval mode, forward
+    and backward (f32 ulp-level tolerance: x*s+b vs (x-mean)*inv*gamma+beta)."""
+    from frcnn_amd import ops
+    torch.manual_seed(0)
+    C = shape[1]
+    bn = torch.nn.BatchNorm2d(C).to(dev).eval()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2.0)
+    x = torch.randn(*shape, device=dev, requires_grad=True)
+    sk = torch.randn(*shape, device=dev, requires_grad=True) if skip else None
+    y = ops.bn_act(x, bn, skip=sk, relu=relu)
+    ref = bn(x) + (sk if skip else 0)
+    ref = torch.relu(ref) if relu else ref
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    gy = torch.randn_like(y)
+    grads = torch.autograd.grad(y, [x, bn.weight, bn.bias] + ([sk] if skip else []), gy)
+    rgrads = torch.autograd.grad(ref, [x, bn.weight, bn.bias] + ([sk] if skip else []), gy)
+    for a, b in zip(grads, rgrads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
