@@ -245,6 +245,29 @@ int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, float* out, void* stream);
+/* The grouped forward (opt-in): a one-workgroup planning launch sorts the
+ * RoIs into spatial groups of 8 (same image and level); the main launch
+ * stages the union of each group's tap rows per channel into LDS by LDS-DMA
+ * and evaluates every RoI of the group from it, so a line shared by several
+ * RoIs is fetched once.  Bit-identical to frh_roi_align_fwd_strided, which it
+ * falls back to when the workspace is absent / short, K > 8192, or the shape
+ * is outside (sampling 2, ph*pw <= 64).  workspace: frh_roi_align_workspace(K)
+ * bytes.  Currently slower than the default on cfg2. */
+size_t frh_roi_align_workspace(int64_t num_rois);
+int32_t frh_roi_align_fwd_ws(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                             const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
+                             const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                             int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                             float* out, void* workspace, size_t ws_bytes, void* stream);
+/* Diagnostics / micro-benchmark: a named forward kernel (0 direct gather, 10
+ * per-RoI LDS windows = the default, 50 grouped, 51 grouped with timing stamps
+ * written past the results; -1 = default, -2 = grouped if possible). */
+int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
+                                  const int32_t* feat_hw, const int64_t* strides, const float* scales,
+                                  int32_t batch, int32_t channels, const float* rois,
+                                  const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
+                                  int32_t pooled_w, int32_t sampling_ratio, int32_t aligned, float* out,
+                                  void* workspace, size_t ws_bytes, void* stream);
 int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
                                   const int32_t* feat_hw, const int64_t* strides,
                                   const float* scales, int32_t batch, int32_t channels,

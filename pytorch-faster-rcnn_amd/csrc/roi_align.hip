@@ -1,19 +1,22 @@
 // a13/a14: FPN level mapping + RoIAlign forward/backward over all levels and
-// images in one launch.
+// images.
 // Reference: lib/region.py:243-306 (BasicRoIExtractor: map_rois_to_levels,
 // per-level torchvision RoIAlign(output_size, 1/stride, sampling_ratio=2)),
 // torchvision legacy (aligned=False) RoIAlign semantics.
 //
-// Work decomposition: one 256-thread workgroup per (RoI, chunk of 64
-// channels).  The bilinear sample grid is separable, so the workgroup first
-// tabulates the ph*gh sample rows and pw*gw sample columns (low/high index,
-// fractional weights, validity) in LDS once; every output element then only
-// multiplies table entries and gathers 4 taps per sample.  Output items are
-// mapped channel-major / bin-minor, so a wave writes one contiguous run of
-// the [K, C, ph, pw] output and neighbouring lanes read neighbouring x taps
-// of the same feature row.  Feature tensors are addressed through explicit
-// (batch, channel, y, x) element strides: NCHW, channels_last and strided
-// views (FPN P6 = P5[..., ::2, ::2]) all run the same kernel.
+// Forward kernels (all bit-identical: -ffp-contract=off, reference op order):
+//  * roi_align_fwd_lds_kernel -- the default: per (RoI, 64 channels) workgroup,
+//    each wave copies its RoI's tap window of 16 channels into LDS (windows
+//    <= 256 floats) or gathers per bin (larger windows).
+//  * roi_align_fwd_group_kernel -- opt-in (frh_roi_align_fwd_ws): a
+//    planning launch sorts the RoIs into spatial groups of 8; a workgroup
+//    stages the UNION of its group's tap rows for one channel at a time into
+//    LDS with 16-B LDS-DMA (three-slot ring, one barrier per channel) and its
+//    8 waves evaluate one RoI each.  Overlapping RoIs share each staged line.
+//  * roi_align_fwd_kernel -- direct gather, any pooled size / sampling ratio.
+// Feature tensors are addressed through explicit (batch, channel, y, x)
+// element strides: NCHW, channels_last and strided views (FPN P6 =
+// P5[..., ::2, ::2]) all run.
 #include <math.h>
 
 #include <type_traits>
@@ -171,321 +174,6 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_kernel(RoiLevels lv
   }
 }
 
-// Staged variant (fixed sampling ratio): the RoI's bilinear taps all fall in
-// the window [y0, y1] x [x0, x1] of its level (<= ~30x30 cells after FPN level
-// mapping).  The workgroup copies that window for as many channels as fit in
-// 48 KB of LDS with row-contiguous (coalesced) loads, then evaluates the
-// 16 taps of every output element from LDS.  Same arithmetic order as the
-// direct kernel, so outputs are identical.
-constexpr int kStageTaps = 64;
-constexpr int kStageFloats = 12288;
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_staged_kernel(RoiLevels lv, RoiCfg c,
-                                                                           float* __restrict__ out) {
-  __shared__ Tap ty[kStageTaps], tx[kStageTaps];
-  __shared__ float win[kStageFloats];
-  __shared__ int wb[4];
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int ny = c.ph * g.gh, nx = c.pw * g.gw;
-  for (int e = threadIdx.x; e < ny + nx; e += blockDim.x) {
-    if (e < ny) {
-      int p = e / g.gh, i = e - p * g.gh;
-      ty[e] = make_tap(sample_y(g, p, i), H);
-    } else {
-      int q = e - ny, p = q / g.gw, i = q - p * g.gw;
-      tx[q] = make_tap(sample_x(g, p, i), W);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
-    for (int e = 0; e < ny; ++e)
-      if (ty[e].valid) {
-        y0 = min(y0, ty[e].lo);
-        y1 = max(y1, ty[e].hi);
-      }
-    for (int e = 0; e < nx; ++e)
-      if (tx[e].valid) {
-        x0 = min(x0, tx[e].lo);
-        x1 = max(x1, tx[e].hi);
-      }
-    wb[0] = y0;
-    wb[1] = y1;
-    wb[2] = x0;
-    wb[3] = x1;
-  }
-  __syncthreads();
-  const int y0 = wb[0], x0 = wb[2];
-  const int WH = wb[1] - y0 + 1, WW = wb[3] - x0 + 1;
-  const int area = (wb[1] >= 0 && wb[3] >= 0) ? WH * WW : 0;
-  const int nbins = c.ph * c.pw;
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  float* o = out + (k * c.C + c0) * nbins;
-  int csub = area > 0 ? min(nch, kStageFloats / area) : nch;
-  if (csub == 0) {
-    // window too large for LDS (only for tiny pooled sizes on huge RoIs): direct gather
-    for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
-      const int cl = item / nbins, bin = item - cl * nbins;
-      const int py = bin / c.pw, px = bin - py * c.pw;
-      const float* f = base + (int64_t)(c0 + cl) * scs;
-      float acc = 0.0f;
-      for (int iy = 0; iy < g.gh; ++iy) {
-        const Tap a = ty[py * g.gh + iy];
-        for (int ix = 0; ix < g.gw; ++ix) {
-          const Tap bx = tx[px * g.gw + ix];
-          float val = 0.0f;
-          if (a.valid && bx.valid) {
-            float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
-            val = ((w1 * f[a.lo * sy + bx.lo * sx] + w2 * f[a.lo * sy + bx.hi * sx]) +
-                   w3 * f[a.hi * sy + bx.lo * sx]) + w4 * f[a.hi * sy + bx.hi * sx];
-          }
-          acc = acc + val;
-        }
-      }
-      o[item] = acc / g.count;
-    }
-    return;
-  }
-  for (int cc = 0; cc < nch; cc += csub) {
-    const int cn = min(csub, nch - cc);
-    const int total = cn * area;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
-      int ch = e / area, rem = e - ch * area;
-      int r = rem / WW, col = rem - r * WW;
-      win[e] = base[(int64_t)(c0 + cc + ch) * scs + (int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx];
-    }
-    __syncthreads();
-    for (int item = threadIdx.x; item < cn * nbins; item += blockDim.x) {
-      const int cl = item / nbins, bin = item - cl * nbins;
-      const int py = bin / c.pw, px = bin - py * c.pw;
-      const float* w = win + cl * area;
-      float acc = 0.0f;
-      for (int iy = 0; iy < g.gh; ++iy) {
-        const Tap a = ty[py * g.gh + iy];
-        for (int ix = 0; ix < g.gw; ++ix) {
-          const Tap bx = tx[px * g.gw + ix];
-          float val = 0.0f;
-          if (a.valid && bx.valid) {
-            const int ylo = (a.lo - y0) * WW, yhi = (a.hi - y0) * WW;
-            const int xlo = bx.lo - x0, xhi = bx.hi - x0;
-            float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
-            val = ((w1 * w[ylo + xlo] + w2 * w[ylo + xhi]) + w3 * w[yhi + xlo]) + w4 * w[yhi + xhi];
-          }
-          acc = acc + val;
-        }
-      }
-      o[(cc + cl) * nbins + bin] = acc / g.count;
-    }
-    __syncthreads();
-  }
-}
-
-// Register-tap variant (sampling ratio 2, any pooled size with ph*pw <= 256):
-// thread t owns ONE output bin (t % nbins) for a fixed channel residue
-// (t / nbins), so its 2x2 sample taps (rows and columns: low/high index +
-// weights) are computed once into registers; the thread then walks the
-// channels of its chunk with stride (threads / nbins), issuing the 16 tap
-// loads of each channel back to back.  No LDS, no per-item division.
-template <int SR>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_regtap_kernel(RoiLevels lv, RoiCfg c,
-                                                                           float* __restrict__ out) {
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int groups = kRoiThreads / nbins;
-  const int t = threadIdx.x;
-  if (t >= groups * nbins) return;
-  const int bin = t % nbins, cg = t / nbins;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(sample_y(g, py, i), H);
-    tx[i] = make_tap(sample_x(g, px, i), W);
-  }
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  // per-sample offsets and weights (invalid samples contribute exactly 0)
-  int32_t off[SR][SR][4];  // offsets within one channel plane fit in 32 bits
-  float wt[SR][SR][4];
-  bool ok[SR][SR];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = a.valid && b.valid;
-      off[iy][ix][0] = (int32_t)(a.lo * sy + b.lo * sx);
-      off[iy][ix][1] = (int32_t)(a.lo * sy + b.hi * sx);
-      off[iy][ix][2] = (int32_t)(a.hi * sy + b.lo * sx);
-      off[iy][ix][3] = (int32_t)(a.hi * sy + b.hi * sx);
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
-  float* o = out + (k * c.C + c0) * nbins + bin;
-  for (int ch = cg; ch < nch; ch += groups) {
-    const float* f = base + (int64_t)ch * scs;
-    float v[SR][SR][4];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[iy][ix][q] = f[off[iy][ix][q]];  // invalid taps point at (0,0)
-    float acc = 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
-                    wt[iy][ix][3] * v[iy][ix][3];
-        acc = acc + (ok[iy][ix] ? val : 0.0f);
-      }
-    o[(int64_t)ch * nbins] = acc / g.count;
-  }
-}
-
-__device__ __forceinline__ float pick4(const float4& v, int i) {
-  const float a = (i & 1) ? v.y : v.x;
-  const float b = (i & 1) ? v.w : v.z;
-  return (i & 2) ? b : a;
-}
-
-// Row-vector variant (sampling ratio 2, unit x stride, ph*pw <= 256).
-// After FPN level mapping a bin spans <= ~4 feature cells, so the x taps of a
-// bin's two x-samples (x_lo0 .. x_hi1) fall inside 4 consecutive cells: ONE
-// 16-byte load per tap row (rows y_lo/y_hi of the two y-samples) fetches all
-// of them -> 4 vector loads per (bin, channel) instead of 16 dword gathers.
-// The window start xb = min(x_lo0, W - 4) keeps the load inside the row (the
-// KFD runs gfx9+ queues in unaligned mode, so xb need not be 4-aligned).
-// Bins whose taps do not fit (huge clamped RoIs, maps narrower than 4) use
-// the dword gather.  Arithmetic identical to the reference order.
-template <int U>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_vec4_kernel(RoiLevels lv, RoiCfg c,
-                                                                         float* __restrict__ out) {
-  constexpr int SR = 2;
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int groups = kRoiThreads / nbins;
-  const int t = threadIdx.x;
-  if (t >= groups * nbins) return;
-  const int bin = t % nbins, cg = t / nbins;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(sample_y(g, py, i), H);
-    tx[i] = make_tap(sample_x(g, px, i), W);
-  }
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  int xmin = 1 << 30, xmax = -1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i)
-    if (tx[i].valid) {
-      xmin = min(xmin, tx[i].lo);
-      xmax = max(xmax, tx[i].hi);
-    }
-  const int xb = min(xmin, W - 4);
-  const bool fit = sx == 1 && W >= 4 && xmax >= 0 && xmax - xb <= 3;
-  int cl[SR], chh[SR], rowo[SR][2];
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    cl[i] = tx[i].valid ? tx[i].lo - xb : 0;
-    chh[i] = tx[i].valid ? tx[i].hi - xb : 0;
-    rowo[i][0] = ty[i].valid ? (int)(ty[i].lo * sy) : 0;
-    rowo[i][1] = ty[i].valid ? (int)(ty[i].hi * sy) : 0;
-  }
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
-  float* o = out + (k * c.C + c0) * nbins + bin;
-  if (fit) {
-    const float* bx = base + xb;
-    auto bin_value = [&](const float4 (&rv)[SR][2]) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          const float v1 = pick4(rv[iy][0], cl[ix]), v2 = pick4(rv[iy][0], chh[ix]);
-          const float v3 = pick4(rv[iy][1], cl[ix]), v4 = pick4(rv[iy][1], chh[ix]);
-          float val = ((wt[iy][ix][0] * v1 + wt[iy][ix][1] * v2) + wt[iy][ix][2] * v3) + wt[iy][ix][3] * v4;
-          acc = acc + (ok[iy][ix] ? val : 0.0f);
-        }
-      return acc / g.count;
-    };
-    int ch = cg;
-    // U channels per step: all 4U row loads are issued before any is consumed
-    for (; ch + (U - 1) * groups < nch; ch += U * groups) {
-      float4 rv[U][SR][2];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float* f = bx + (int64_t)(ch + u * groups) * scs;
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy) {
-          rv[u][iy][0] = *reinterpret_cast<const float4*>(f + rowo[iy][0]);
-          rv[u][iy][1] = *reinterpret_cast<const float4*>(f + rowo[iy][1]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) o[(int64_t)(ch + u * groups) * nbins] = bin_value(rv[u]);
-    }
-    for (; ch < nch; ch += groups) {
-      const float* f = bx + (int64_t)ch * scs;
-      float4 rv[SR][2];
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy) {
-        rv[iy][0] = *reinterpret_cast<const float4*>(f + rowo[iy][0]);
-        rv[iy][1] = *reinterpret_cast<const float4*>(f + rowo[iy][1]);
-      }
-      o[(int64_t)ch * nbins] = bin_value(rv);
-    }
-  } else {
-    for (int ch = cg; ch < nch; ch += groups) {
-      const float* f = base + (int64_t)ch * scs;
-      float acc = 0.0f;
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          const int64_t q0 = ok[iy][ix] ? (int64_t)tx[ix].lo * sx : 0, q1 = ok[iy][ix] ? (int64_t)tx[ix].hi * sx : 0;
-          const float v1 = f[rowo[iy][0] + q0], v2 = f[rowo[iy][0] + q1];
-          const float v3 = f[rowo[iy][1] + q0], v4 = f[rowo[iy][1] + q1];
-          float val = ((wt[iy][ix][0] * v1 + wt[iy][ix][1] * v2) + wt[iy][ix][2] * v3) + wt[iy][ix][3] * v4;
-          acc = acc + (ok[iy][ix] ? val : 0.0f);
-        }
-      o[(int64_t)ch * nbins] = acc / g.count;
-    }
-  }
-}
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -495,6 +183,44 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
   const int n = __builtin_amdgcn_readfirstlane((int)bytes);
   void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(q, 0, n, 0x00020000);
+}
+
+// Wave-wide min / max with DPP row ops (no LDS round trip); result in every lane.
+template <bool kMin>
+__device__ __forceinline__ int wave_minmax_i32(int v) {
+  const int id = kMin ? 0x7fffffff : (int)0x80000000;
+  auto op = [](int a, int b) { return kMin ? min(a, b) : max(a, b); };
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast15
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_min_i32(int v) { return wave_minmax_i32<true>(v); }
+__device__ __forceinline__ int wave_max_i32(int v) { return wave_minmax_i32<false>(v); }
+
+// buffer_load_dword{,x4} ... lds: kBytes per lane into LDS at lds + 4*kBytes/4 * lane.
+// The 16-byte form is a gfx950 instruction the host pass of hipcc cannot check,
+// hence the device-pass guard (the host never runs device code).
+template <int kBytes>
+__device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t r, float* lds, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(kBytes == 4 || kBytes == 16, "LDS-DMA width");
+  if constexpr (kBytes == 16)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, soff, 0, 0);
+#endif
+}
+
+// s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding).  The
+// compiler does not wait for LDS-DMA data before ds_reads: these are explicit.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
 // Buffer-descriptor variant (sampling ratio 2, ph*pw <= 256; the default).
@@ -638,28 +364,6 @@ __device__ __forceinline__ void fwd_buf_block(const RoiLevels& lv, const RoiCfg&
   }
 }
 
-template <int U>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_buf_kernel(RoiLevels lv, RoiCfg c,
-                                                                        float* __restrict__ out) {
-  const int64_t k = blockIdx.x;
-  fwd_buf_block<U>(lv, c, out, k, blockIdx.y * kRoiChanChunk, roi_geom(c, lv, k));
-}
-
-// Wave-wide min / max with DPP row ops (no LDS round trip); result in every lane.
-template <bool kMin>
-__device__ __forceinline__ int wave_minmax_i32(int v) {
-  const int id = kMin ? 0x7fffffff : (int)0x80000000;
-  auto op = [](int a, int b) { return kMin ? min(a, b) : max(a, b); };
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xf, 0xf, false));  // row_mirror
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast15
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast31
-  return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ int wave_min_i32(int v) { return wave_minmax_i32<true>(v); }
-__device__ __forceinline__ int wave_max_i32(int v) { return wave_minmax_i32<false>(v); }
 
 // Wave-staged variant (sampling ratio 2, ph*pw <= 64, 2*ph and 2*pw <= 64).
 // Every tap of a RoI lies in the window [y0, y1] x [x0, x1] of its level;
@@ -676,7 +380,6 @@ __device__ __forceinline__ int wave_max_i32(int v) { return wave_minmax_i32<fals
 // direct kernel.
 constexpr int kWinMax = 1024;
 constexpr int kWinR = kWinMax / kWave;
-constexpr int kWaveChans = kRoiChanChunk / (kRoiThreads / kWave);
 
 // kChunk: channels per workgroup (kChunk / 4 per wave).  kSkip (diagnostics only):
 // 1 = skip staged RoIs, 2 = skip gathered ones.
@@ -840,177 +543,588 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_lds_kernel(RoiLevel
   }
 }
 
-// Staged + register-tap variant (sampling ratio SR, ph*pw <= 256).
-// After FPN level mapping a RoI covers few feature cells (random-init cfg2:
-// median side ~5 cells on P2), so its 16*ph*pw taps per channel hit a small
-// window many times over.  Thread (bin, channel group) keeps its bin's tap
-// offsets (relative to the window) and weights in registers; the workgroup
-// stages the window rows of a channel sub-chunk in LDS with row-contiguous
-// loads, then every output element is 16 LDS reads + the reference's
-// arithmetic.  Identical results to the direct kernel.
-constexpr int kWinFloats = 12288;  // 48 KB window buffer
 
-template <int SR>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_winreg_kernel(RoiLevels lv, RoiCfg c,
-                                                                           float* __restrict__ out) {
-  __shared__ float win[kWinFloats];
-  __shared__ int wb[4];
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
+// ---------------------------------------------------------------------------
+// One wave, one RoI, channels [c0, c1): the RoI's tap rows (dense window
+// [y0, y1] when it has <= 4*ph rows, else the (y_lo, y_hi) list of its 2*ph
+// y-samples) x columns [x0 & ~(kV-1), x1] are staged channel by channel into
+// the wave's slab by LDS-DMA (kV floats per lane), two batches in flight with
+// counted vmcnt waits; lane = bin evaluates from LDS.  Slabs beyond kSlab /
+// 2 are gathered per bin.  Used where a group's union does not fit.
+template <int kSlab, int kV>
+__device__ __forceinline__ void roi_segment(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, float* slab,
+                                            int64_t k, int c0, int c1, int lane) {
+  constexpr int SR = 2;
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int groups = kRoiThreads / nbins;
-  const int t = threadIdx.x;
-  const bool active = t < groups * nbins;
-  const int bin = active ? t % nbins : 0, cg = active ? t / nbins : 0;
+  const int nbins = c.ph * c.pw, nsy = c.ph * SR;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
   const int py = bin / c.pw, px = bin - py * c.pw;
-  if (t == 0) {
-    wb[0] = 1 << 30;
-    wb[1] = -1;
-    wb[2] = 1 << 30;
-    wb[3] = -1;
-  }
-  __syncthreads();
   Tap ty[SR], tx[SR];
 #pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(sample_y(g, py, i), H);
-    tx[i] = make_tap(sample_x(g, px, i), W);
+  for (int i = 0; i < SR; ++i) {  // sampling 2: the "/ gh" of the sample position is an exact halving
+    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
   }
-  if (active) {
-    int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
 #pragma unroll
-    for (int i = 0; i < SR; ++i) {
-      if (ty[i].valid) {
-        ylo = min(ylo, ty[i].lo);
-        yhi = max(yhi, ty[i].hi);
-      }
-      if (tx[i].valid) {
-        xlo = min(xlo, tx[i].lo);
-        xhi = max(xhi, tx[i].hi);
-      }
-    }
-    if (yhi >= 0 && xhi >= 0) {
-      atomicMin(&wb[0], ylo);
-      atomicMax(&wb[1], yhi);
-      atomicMin(&wb[2], xlo);
-      atomicMax(&wb[3], xhi);
-    }
+  for (int i = 0; i < SR; ++i) {
+    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
+    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
   }
-  __syncthreads();
-  const int y0 = wb[0], x0 = wb[2];
-  const bool empty = wb[1] < 0;
-  const int WH = empty ? 0 : wb[1] - y0 + 1, WW = empty ? 0 : wb[3] - x0 + 1;
-  const int area = WH * WW;
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
-  float* o = out + (k * c.C + c0) * nbins + bin;
-  int woff[SR][SR][4];
-  float wt[SR][SR][4];
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  const bool any = y1 >= y0 && x1 >= x0;
+  const int xs0 = x0 & ~(kV - 1);
+  const int ws = kV == 1 ? ((x1 - x0 + 1) | 1) : ((x1 - xs0 + kV) & ~(kV - 1));
+  const bool dense = any && y1 - y0 + 1 <= 2 * nsy;
+  const int nrows = !any ? 0 : dense ? y1 - y0 + 1 : 2 * nsy;
+  const int R = (nrows * ws + kV * kWave - 1) / (kV * kWave);
+  const int Rr = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 16;
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + k * c.C * nbins, (int64_t)c.C * nbins * 4);
+  const int cstep = scs * 4, ostep = nbins * 4;
+  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  if (!any) {
+    for (int ch = c0; ch < c1; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
+    return;
+  }
   bool ok[SR][SR];
+  float wt[SR][SR][4];
 #pragma unroll
   for (int iy = 0; iy < SR; ++iy)
 #pragma unroll
     for (int ix = 0; ix < SR; ++ix) {
       const Tap a = ty[iy], b = tx[ix];
       ok[iy][ix] = a.valid && b.valid;
-      const int rl = ok[iy][ix] ? (a.lo - y0) * WW : 0, rh = ok[iy][ix] ? (a.hi - y0) * WW : 0;
-      const int cl = ok[iy][ix] ? b.lo - x0 : 0, ch = ok[iy][ix] ? b.hi - x0 : 0;
-      woff[iy][ix][0] = rl + cl;
-      woff[iy][ix][1] = rl + ch;
-      woff[iy][ix][2] = rh + cl;
-      woff[iy][ix][3] = rh + ch;
       wt[iy][ix][0] = a.h * b.h;
       wt[iy][ix][1] = a.h * b.l;
       wt[iy][ix][2] = a.l * b.h;
       wt[iy][ix][3] = a.l * b.l;
     }
-  if (empty) {
-    if (active)
-      for (int chn = cg; chn < nch; chn += groups) o[(int64_t)chn * nbins] = 0.0f / g.count;
-    return;
-  }
-  const int csub = min(nch, kWinFloats / area);
-  if (csub == 0) {
-    // window larger than the LDS buffer: gather straight from global memory
-    if (!active) return;
-    for (int chn = cg; chn < nch; chn += groups) {
-      const float* f = base + (int64_t)chn * scs;
-      float acc = 0.0f;
+  auto combine = [&](const float (&v)[SR][SR][4]) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    return acc * 0.25f;
+  };
+  if (Rr * kV * kWave * 2 > kSlab) {
+    // window larger than half the slab: per-bin gather, two channels in flight
+    int off[SR][SR][4];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const bool v = ok[iy][ix];
+        const int r0 = v ? ty[iy].lo * sy : 0, r1 = v ? ty[iy].hi * sy : 0;
+        const int q0 = v ? tx[ix].lo * sx : 0, q1 = v ? tx[ix].hi * sx : 0;
+        off[iy][ix][0] = (r0 + q0) * 4;
+        off[iy][ix][1] = (r0 + q1) * 4;
+        off[iy][ix][2] = (r1 + q0) * 4;
+        off[iy][ix][3] = (r1 + q1) * 4;
+      }
+    for (int ch = c0; ch < c1; ch += 2) {
+      const int chb = min(ch + 1, c1 - 1);
+      float va[SR][SR][4], vb[SR][SR][4];
 #pragma unroll
       for (int iy = 0; iy < SR; ++iy)
 #pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          const Tap a = ty[iy], b = tx[ix];
-          const int64_t r0 = (int64_t)a.lo * sy, r1 = (int64_t)a.hi * sy;
-          const int64_t q0 = (int64_t)b.lo * sx, q1 = (int64_t)b.hi * sx;
-          float val = ((wt[iy][ix][0] * f[r0 + q0] + wt[iy][ix][1] * f[r0 + q1]) + wt[iy][ix][2] * f[r1 + q0]) +
-                      wt[iy][ix][3] * f[r1 + q1];
-          acc = acc + (ok[iy][ix] ? val : 0.0f);
-        }
-      o[(int64_t)chn * nbins] = acc / g.count;
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            va[iy][ix][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fr, off[iy][ix][q], ch * cstep, 0));
+            vb[iy][ix][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fr, off[iy][ix][q], chb * cstep, 0));
+          }
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(combine(va)), orr, ovoff, ch * ostep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(combine(vb)), orr, ch + 1 < c1 ? ovoff : 0x40000000,
+                                            (ch + 1) * ostep, 0);
     }
     return;
   }
-  // staging: the window image [cn][WH][WW] is filled in flat order (lanes
-  // along the row), 8 independent loads in flight per lane before the LDS
-  // stores, so the copy is bandwidth- not latency-bound.
-  constexpr int kUnroll = 8;
-  // flat element e = (chn*WH + r)*WW + col advanced by the block size with
-  // carries (no per-element integer division)
-  const int st_col = kRoiThreads % WW, st_r = (kRoiThreads / WW) % WH, st_ch = kRoiThreads / area;
-  const int t_ch = t / area, t_rem = t - t_ch * area, t_r = t_rem / WW, t_col = t_rem - t_r * WW;
-  for (int cc = 0; cc < nch; cc += csub) {
-    const int cn = min(csub, nch - cc);
-    const int total = cn * area;
-    int chn = t_ch, r = t_r, col = t_col;
-    const float* cbase = base + (int64_t)cc * scs;
-    for (int e0 = 0; e0 < total; e0 += kUnroll * kRoiThreads) {
-      float v[kUnroll];
+  // slab byte offsets of this bin's taps: [iy][row lo/hi][ix][col lo/hi]
+  int sa[SR][2][SR][2];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const bool in = e0 + u * kRoiThreads + t < total;
-        const int64_t a = in ? (int64_t)chn * scs + (int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx : 0;
-        v[u] = cbase[a];
-        col += st_col;
-        r += st_r;
-        chn += st_ch;
-        if (col >= WW) {
-          col -= WW;
-          ++r;
-        }
-        if (r >= WH) {
-          r -= WH;
-          ++chn;
-        }
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      const bool v = ok[iy][ix];
+      const int rlo = dense ? a.lo - y0 : 2 * (py * SR + iy), rhi = dense ? a.hi - y0 : 2 * (py * SR + iy) + 1;
+      sa[iy][0][ix][0] = v ? (rlo * ws + (b.lo - xs0)) * 4 : 0;
+      sa[iy][0][ix][1] = v ? (rlo * ws + (b.hi - xs0)) * 4 : 0;
+      sa[iy][1][ix][0] = v ? (rhi * ws + (b.lo - xs0)) * 4 : 0;
+      sa[iy][1][ix][1] = v ? (rhi * ws + (b.hi - xs0)) * 4 : 0;
+    }
+  auto bin_value = [&](const char* sl) {
+    float v[SR][SR][4];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        v[iy][ix][0] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][0]);
+        v[iy][ix][1] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][1]);
+        v[iy][ix][2] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][0]);
+        v[iy][ix][3] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][1]);
       }
+    return combine(v);
+  };
+  // sparse rows: entry 2i / 2i+1 = y_lo / y_hi of y-sample i = ty[i % 2] of lane (i / 2) * pw
+  const int tyl0 = ty[0].valid ? ty[0].lo : y0, tyh0 = ty[0].valid ? ty[0].hi : y0;
+  const int tyl1 = ty[1].valid ? ty[1].lo : y0, tyh1 = ty[1].valid ? ty[1].hi : y0;
+  const int n = nrows * ws;
+  auto run = [&](auto rb) {
+    constexpr int RB = decltype(rb)::value;
+    constexpr int kB0 = kSlab / (2 * RB * kV * kWave);
+    constexpr int kB = kB0 < 1 ? 1 : (kB0 < 16 ? kB0 : 16);  // channels per batch
+    constexpr int F = RB * kV * kWave * 4;                     // slab bytes per channel
+    static_assert(kB * (RB + 1) < 64, "batch too large for vmcnt");
+    if (kB0 < 1) return;  // excluded by the gather test above
+    int goff[RB];
+    {
+      const int step = kV * kWave, dr = step / ws, dc = step - dr * ws;
+      int r = (kV * lane) / ws, col = kV * lane - r * ws;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int e = e0 + u * kRoiThreads + t;
-        if (e < total) win[e] = v[u];
+      for (int j = 0; j < RB; ++j) {
+        const int e = kV * lane + j * step;
+        const int rs = min(r, 2 * nsy - 1), src = (rs >> 2) * c.pw;
+        const int a0 = __shfl(tyl0, src, kWave), a1 = __shfl(tyh0, src, kWave);
+        const int b0 = __shfl(tyl1, src, kWave), b1 = __shfl(tyh1, src, kWave);
+        const int srow = (rs & 2) ? ((rs & 1) ? b1 : b0) : ((rs & 1) ? a1 : a0);
+        const int fy = dense ? y0 + r : srow;
+        // columns past the row end only fill slab cells no tap reads; lanes past the slab
+        // re-read its first element (no extra line)
+        const int fx = kV == 1 ? min(xs0 + col, W - 1) : xs0 + col;
+        goff[j] = e < n ? (fy * sy + fx * sx) * 4 : (y0 * sy + xs0 * sx) * 4;
+        r += dr;
+        col += dc;
+        if (col >= ws) col -= ws, ++r;
       }
     }
-    __syncthreads();
-    if (active) {
-      for (int chn = cg; chn < cn; chn += groups) {
-        const float* w = win + chn * area;
-        float acc = 0.0f;
+    const int nb = (c1 - c0 + kB - 1) / kB;
+    auto issue = [&](int b) {  // batch b -> slot b & 1; channels past c1 re-read the last one
+      const int slot = (b & 1) * kB;
+#pragma unroll
+      for (int s = 0; s < kB; ++s) {
+        const int ch = min(c0 + b * kB + s, c1 - 1);
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+          lds_dma<4 * kV>(fr, slab + (slot + s) * (F / 4) + j * kV * kWave, goff[j], ch * cstep);
+      }
+    };
+    issue(0);
+    if (nb > 1) issue(1);
+    for (int b = 0; b < nb; ++b) {
+      // retire batch b: younger than it are batch b-1's kB stores and batch b+1's DMAs
+      if (b + 1 < nb) {
+        if (b == 0)
+          wait_vmcnt<kB * RB>();
+        else
+          wait_vmcnt<kB * RB + kB>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      const char* sl = reinterpret_cast<const char*>(slab + (b & 1) * kB * (F / 4));
+#pragma unroll
+      for (int s = 0; s < kB; ++s) {
+        const int ch = c0 + b * kB + s;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(sl + s * F)), orr,
+                                              ch < c1 ? ovoff : 0x40000000, ch * ostep, 0);
+      }
+      if (b + 2 < nb) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot b & 1 fully read before it is refilled
+        issue(b + 2);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  if (Rr == 1)
+    run(std::integral_constant<int, 1>{});
+  else if (Rr == 2)
+    run(std::integral_constant<int, 2>{});
+  else if (Rr == 4)
+    run(std::integral_constant<int, 4>{});
+  else if (Rr == 8)
+    run(std::integral_constant<int, 8>{});
+  else
+    run(std::integral_constant<int, 16>{});
+}
+
+// ---------------------------------------------------------------------------
+// Grouped forward (opt-in: frh_roi_align_fwd_ws).  Measured on cfg2 (1024 RoIs):
+// 76-85 us vs 55 us for the per-RoI kernel -- each workgroup is a serial chain
+// of a ~6 us dependent-load prologue plus ~2 us per 4-channel step (DESIGN.md
+// §4); it moves half the L2 lines but does not yet hide the latency.
+//
+// roi_group_plan_kernel (one workgroup, K <= 8192): counting sort of the RoIs
+// by (image, level, 128-px tile of the RoI centre), then the sorted sequence is
+// cut into groups of kGrp consecutive RoIs of one (image, level).  Output:
+// order [K], gstart [ngroups + 1], ngroups.
+//
+// roi_align_fwd_group_kernel: workgroup = (group, 64 channels), wave w = the
+// group's RoI w.  The union of the group's tap rows (a bitmask over feature
+// rows) x the union of their columns is staged per channel into a three-slot
+// LDS ring by LDS-DMA (all 512 threads, fixed per-thread offsets), one barrier
+// per channel; wave w evaluates RoI w's 49 bins from the slot.  A feature line
+// shared by several RoIs of the group is fetched once, not once per RoI (the
+// RoI-by-RoI kernels are bound by the L1-miss line rate: ~3.1M mostly partial
+// lines for cfg2 vs ~1.6M here).  Groups whose union exceeds a slot fall back
+// to roi_segment per wave.  XCD x (= block % 8) takes the x-th eighth of the
+// groups, so neighbouring groups share an L2.
+constexpr int kGrp = 8;                    // RoIs per group = waves per workgroup
+constexpr int kGrpThreads = kGrp * kWave;  // 512
+constexpr int kGrpChans = 64;              // channels per workgroup
+constexpr int kGrpRing = 18432;            // LDS ring floats (72 KB: two workgroups per CU)
+constexpr int kRowWords = 32;              // union row bitmask: feature maps up to 1024 rows
+constexpr int kMaxURows = 512;
+constexpr int kPlanThreads = 1024, kPlanMaxRois = 8192, kPlanBuckets = 4096;
+
+struct GroupPlan {
+  const int32_t* order;    // [K] RoI ids, grouped
+  const int32_t* gstart;   // [maxg + 1]; gstart[ngroups] = K
+  const int32_t* ngroups;  // [1]
+};
+
+// block-wide exclusive scan (sum or max) of one value per thread
+template <bool kMax>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : a + b; };
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc = op(inc, u);
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (int i = 0; i < (int)(blockDim.x / kWave); ++i) {
+    if (i < w) base = op(base, wsum[i]);
+    all = op(all, wsum[i]);
+  }
+  *total = all;
+  __syncthreads();
+  // exclusive: the inclusive value of the previous lane, folded into the earlier waves' total
+  const uint32_t prev = __shfl_up(inc, 1, kWave);
+  return lane == 0 ? base : op(base, prev);
+}
+
+__global__ void __launch_bounds__(kPlanThreads) roi_group_plan_kernel(const float* rois, const int64_t* levels,
+                                                                      int32_t K, int32_t* order, int32_t* gstart,
+                                                                      int32_t* ngroups) {
+  __shared__ uint32_t cnt[kPlanBuckets];
+  __shared__ uint16_t keys[kPlanMaxRois];
+  __shared__ uint16_t pkey[kPlanMaxRois];
+  __shared__ uint32_t wsum[kPlanThreads / kWave];
+  const int t = threadIdx.x;
+  for (int b = t; b < kPlanBuckets; b += kPlanThreads) cnt[b] = 0;
+  __syncthreads();
+  for (int k = t; k < K; k += kPlanThreads) {
+    const float* r = rois + (int64_t)k * 5;
+    const int lvl = levels ? (int)levels[k] : 0;
+    const float xc = 0.5f * (r[1] + r[3]), yc = 0.5f * (r[2] + r[4]);
+    const int ty = yc < 0.0f ? 0 : (yc >= 896.0f ? 7 : (int)(yc * (1.0f / 128.0f)));
+    const int tx = xc < 0.0f ? 0 : (xc >= 896.0f ? 7 : (int)(xc * (1.0f / 128.0f)));
+    const uint16_t key = (uint16_t)((((int)r[0] & 15) << 8) | ((lvl & 3) << 6) | (ty << 3) | tx);
+    keys[k] = key;
+    atomicAdd(&cnt[key], 1u);
+  }
+  __syncthreads();
+  constexpr int P = kPlanBuckets / kPlanThreads;
+  uint32_t loc[P], s = 0, tot;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    loc[i] = s;
+    s += cnt[t * P + i];
+  }
+  const uint32_t base = block_exscan<false>(s, wsum, &tot);
+#pragma unroll
+  for (int i = 0; i < P; ++i) cnt[t * P + i] = base + loc[i];
+  __syncthreads();
+  for (int k = t; k < K; k += kPlanThreads) {
+    const uint32_t pos = atomicAdd(&cnt[keys[k]], 1u);  // order inside a bucket: arbitrary
+    order[pos] = k;
+    pkey[pos] = keys[k];
+  }
+  __syncthreads();
+  // groups: runs of equal (image, level) = pkey >> 6, cut every kGrp positions
+  constexpr int Q = kPlanMaxRois / kPlanThreads;
+  uint32_t segs[Q], lastseg = 0;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int p = t * Q + i;
+    const bool head = p < K && (p == 0 || (pkey[p] >> 6) != (pkey[p - 1] >> 6));
+    if (head) lastseg = (uint32_t)p;
+    segs[i] = lastseg;  // running segment start inside this thread's span (0 = none yet)
+  }
+  const uint32_t carry = block_exscan<true>(lastseg, wsum, &tot);  // latest head before this span
+  uint32_t nhead = 0;
+  bool gflag[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int p = t * Q + i;
+    const uint32_t ss = segs[i] > carry ? segs[i] : carry;
+    gflag[i] = p < K && ((uint32_t)p - ss) % kGrp == 0;
+    nhead += gflag[i];
+  }
+  const uint32_t gbase = block_exscan<false>(nhead, wsum, &tot);
+  uint32_t gid = gbase;
+#pragma unroll
+  for (int i = 0; i < Q; ++i)
+    if (gflag[i]) gstart[gid++] = t * Q + i;
+  if (t == 0) {
+    gstart[tot] = K;
+    ngroups[0] = (int32_t)tot;
+  }
+}
+
+// kDiag (timing diagnostics only, variant 51): thread 0 of every workgroup writes
+// int64 [start, union ready, end, path | U << 8] past the K*C*ph*pw results.
+template <int kV, int kDiag = 0>
+__global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLevels lv, RoiCfg c, GroupPlan gp,
+                                                                          float* __restrict__ out) {
+  const uint64_t t_start = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
+  constexpr int SR = 2;
+  __shared__ float ring[kGrpRing];
+  __shared__ uint32_t umask[kRowWords], upre[kRowWords + 1];
+  __shared__ uint16_t urows[kMaxURows];
+  __shared__ int ux[2];
+  const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t / kWave), lane = t & (kWave - 1);
+  const int ng = __builtin_amdgcn_readfirstlane(gp.ngroups[0]);
+  const int gq = (ng + 7) >> 3;  // groups per XCD slice
+  const int nchunk = (c.C + kGrpChans - 1) / kGrpChans;
+  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+  const int chunk = gq ? j / gq : 0, gi = j - chunk * gq;
+  const int grp = xcd * gq + gi;
+  if (gq == 0 || chunk >= nchunk || grp >= ng) return;  // uniform over the block
+  const int gs = __builtin_amdgcn_readfirstlane(gp.gstart[grp]);
+  const int gn = __builtin_amdgcn_readfirstlane(gp.gstart[grp + 1]) - gs;
+  const bool has = wave < gn;  // waves past the group mirror its first RoI and store nothing
+  const int64_t k = __builtin_amdgcn_readfirstlane(gp.order[gs + (has ? wave : 0)]);
+  const int c0 = chunk * kGrpChans, c1 = min(c.C, c0 + kGrpChans);
+  if (t < kRowWords) umask[t] = 0;
+  if (t == 0) ux[0] = 1 << 30, ux[1] = -1;
+  __syncthreads();
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
+  }
+  // the union: every row a tap reads, and the column span
+  int xlo = 1 << 30, xhi = -1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    if (active && ty[i].valid && ty[i].hi < kRowWords * 32) {
+      atomicOr(&umask[ty[i].lo >> 5], 1u << (ty[i].lo & 31));
+      atomicOr(&umask[ty[i].hi >> 5], 1u << (ty[i].hi & 31));
+    }
+    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
+  }
+  const int wx0 = wave_min_i32(xlo), wx1 = wave_max_i32(xhi);
+  if (lane == 0 && wx1 >= 0) {
+    atomicMin(&ux[0], wx0);
+    atomicMax(&ux[1], wx1);
+  }
+  __syncthreads();
+  if (wave == 0) {  // prefix counts of the row mask, and the union's row list
+    const uint32_t w = lane < kRowWords ? umask[lane] : 0u;
+    uint32_t inc = __popc(w);
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += u;
+    }
+    const uint32_t ex = inc - __popc(w);
+    if (lane < kRowWords) upre[lane] = ex;
+    if (lane == kRowWords - 1) upre[kRowWords] = inc;
+    uint32_t m = w, r = ex;
+    while (m) {
+      const int b = __ffs(m) - 1;
+      if (r < (uint32_t)kMaxURows) urows[r] = (uint16_t)(lane * 32 + b);
+      ++r;
+      m &= m - 1;
+    }
+  }
+  __syncthreads();
+  const uint64_t t_union = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto stamp = [&](int path, int U) {
+    if (kDiag && t == 0) {
+      int64_t* d = reinterpret_cast<int64_t*>(out + c.K * c.C * c.ph * c.pw) + (int64_t)blockIdx.x * 4;
+      d[0] = (int64_t)t_start;
+      d[1] = (int64_t)t_union;
+      d[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      d[3] = path | ((int64_t)U << 8);
+    }
+  };
+  const int nr = (int)upre[kRowWords];
+  const int ux0 = ux[0], ux1 = ux[1];
+  const int xs0 = ux0 & ~(kV - 1);
+  const int uw = kV == 1 ? ((ux1 - ux0 + 1) | 1) : ((ux1 - xs0 + kV) & ~(kV - 1));
+  const int U = nr * uw;
+  bool rows_ok = H <= kRowWords * 32;
+  const int nbig = __builtin_amdgcn_readfirstlane((int)(ux1 < 0 ? 0 : 1));
+  if (nbig == 0 || !rows_ok || nr > kMaxURows || 3 * U > kGrpRing - 2 * kV * kWave * kGrp) {
+    // no valid tap anywhere, or a union too large for three slots: each wave on its own RoI
+    if (has) roi_segment<kGrpRing / kGrp, kV>(lv, c, out, ring + wave * (kGrpRing / kGrp), k, c0, c1, lane);
+    if (kDiag) {
+      __syncthreads();
+      stamp(1, U);
+    }
+    return;
+  }
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+  int sa[SR][2][SR][2];
+  auto ridx = [&](int y) { return (int)upre[y >> 5] + __popc(umask[y >> 5] & ((1u << (y & 31)) - 1u)); };
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy) {
+    const int rl = ty[iy].valid ? ridx(ty[iy].lo) : 0, rh = ty[iy].valid ? ridx(ty[iy].hi) : 0;
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      const bool v = a.valid && b.valid;
+      ok[iy][ix] = v;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+      sa[iy][0][ix][0] = v ? (rl * uw + (b.lo - xs0)) * 4 : 0;
+      sa[iy][0][ix][1] = v ? (rl * uw + (b.hi - xs0)) * 4 : 0;
+      sa[iy][1][ix][0] = v ? (rh * uw + (b.lo - xs0)) * 4 : 0;
+      sa[iy][1][ix][1] = v ? (rh * uw + (b.hi - xs0)) * 4 : 0;
+    }
+  }
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + k * c.C * nbins, (int64_t)c.C * nbins * 4);
+  const int cstep = scs * 4, ostep = nbins * 4;
+  const int ovoff = (has && active) ? lane * 4 : 0x40000000;  // dropped by the range check
+  // Staging: a channel's union is Q wave-instructions of kV*64 floats; instruction q is
+  // issued by wave q % 8 (round q / 8).  Every wave issues the same J rounds per
+  // channel (rounds past Q load a dummy into a junk block), so one counted vmcnt fits
+  // all waves.  A step is B channels (B slots of Q*kV*64 floats); three step buffers,
+  // two steps in flight ahead of the one being read, one barrier per step.
+  constexpr int kPiece = kV * kWave;  // floats per DMA wave-instruction
+  constexpr int kRing = kGrpRing - kPiece;
+  const int Q = (U + kPiece - 1) / kPiece;
+  const int SF = Q * kPiece;
+  float* junk = ring + kRing;
+  auto run = [&](auto jj, auto bb) {
+    constexpr int J = decltype(jj)::value;  // DMA rounds per wave per channel
+    constexpr int B = decltype(bb)::value;  // channels per step
+    static_assert(B * (J + 1) < 64, "vmcnt range");
+    int goff[J], dst[J];
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const int piece = wave + q * kGrp;
+      const int e = kV * lane + piece * kPiece;
+      const int r = e / uw, col = e - r * uw;
+      const int fx = kV == 1 ? min(xs0 + col, W - 1) : xs0 + col;
+      const bool real = piece < Q;
+      goff[q] = real && e < U ? ((int)urows[r] * sy + fx * sx) * 4 : ((int)urows[0] * sy + xs0 * sx) * 4;
+      dst[q] = real ? piece * kPiece : -1;
+    }
+    const int nch = c1 - c0, nst = (nch + B - 1) / B;
+    auto issue = [&](int st) {  // step st: channels c0 + B*st + b (clamped) -> buffer st % 3
+      float* sb = ring + (st % 3) * (B * SF);
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int ch = c0 + min(st * B + b, nch - 1);
+#pragma unroll
+        for (int q = 0; q < J; ++q) lds_dma<4 * kV>(fr, dst[q] >= 0 ? sb + b * SF + dst[q] : junk, goff[q], ch * cstep);
+      }
+    };
+    issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+      // retire step st: younger than its DMAs are step st-1's B stores and step st+1's DMAs
+      if (st + 1 < nst) {
+        if (st == 0)
+          wait_vmcnt<B * J>();
+        else
+          wait_vmcnt<B * (J + 1)>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      asm volatile("s_barrier" ::: "memory");  // every wave's share of step st has landed
+      const char* sb = reinterpret_cast<const char*>(ring + (st % 3) * (B * SF));
+      float acc[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const char* sl = sb + b * SF * 4;
+        float v[SR][SR][4];
 #pragma unroll
         for (int iy = 0; iy < SR; ++iy)
 #pragma unroll
           for (int ix = 0; ix < SR; ++ix) {
-            float val = ((wt[iy][ix][0] * w[woff[iy][ix][0]] + wt[iy][ix][1] * w[woff[iy][ix][1]]) +
-                         wt[iy][ix][2] * w[woff[iy][ix][2]]) +
-                        wt[iy][ix][3] * w[woff[iy][ix][3]];
-            acc = acc + (ok[iy][ix] ? val : 0.0f);
+            v[iy][ix][0] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][0]);
+            v[iy][ix][1] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][1]);
+            v[iy][ix][2] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][0]);
+            v[iy][ix][3] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][1]);
           }
-        o[(int64_t)(cc + chn) * nbins] = acc / g.count;
+        float a = 0.0f;
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix) {
+            float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                        wt[iy][ix][3] * v[iy][ix][3];
+            a = a + (ok[iy][ix] ? val : 0.0f);
+          }
+        acc[b] = a * 0.25f;
       }
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int ci = st * B + b;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[b]), orr, ci < nch ? ovoff : 0x40000000,
+                                              (c0 + ci) * ostep, 0);
+      }
+      // buffer (st + 2) % 3 was last read in step st - 1, which every wave finished before this step's barrier
+      if (st + 2 < nst) issue(st + 2);
     }
+  };
+  const int J = (Q + kGrp - 1) / kGrp;
+  auto with_b = [&](auto jj) {
+    if (3 * 4 * SF <= kRing)
+      run(jj, std::integral_constant<int, 4>{});
+    else if (3 * 2 * SF <= kRing)
+      run(jj, std::integral_constant<int, 2>{});
+    else
+      run(jj, std::integral_constant<int, 1>{});
+  };
+  if (J <= 1)
+    with_b(std::integral_constant<int, 1>{});
+  else if (J <= 2)
+    with_b(std::integral_constant<int, 2>{});
+  else if (J <= 3)
+    with_b(std::integral_constant<int, 3>{});
+  else  // only the 4-byte staging (kV = 1) gets here
+    run(std::integral_constant<int, 16>{}, std::integral_constant<int, 1>{});
+  if (kDiag) {
     __syncthreads();
+    stamp(2 + (3 * 4 * SF <= kRing ? 4 : 3 * 2 * SF <= kRing ? 2 : 1) * 16 + J * 4, U);
   }
 }
 
@@ -1101,6 +1215,7 @@ extern "C" int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float 
   return check_launch("frh_roi_level_map");
 }
 
+
 static int32_t roi_common_checks(int32_t batch, int32_t channels, int64_t num_rois, int32_t ph, int32_t pw,
                                  const float* rois) {
   FRH_REQUIRE(batch >= 1 && channels >= 1 && num_rois >= 0 && ph >= 1 && pw >= 1, "bad sizes");
@@ -1109,14 +1224,40 @@ static int32_t roi_common_checks(int32_t batch, int32_t channels, int64_t num_ro
   return FRH_OK;
 }
 
-// variant: 0 = direct gather, 1 = LDS-staged window, -1 = best available.
-// Exported for the kernel micro-benchmarks (tools/bench_roi_align.py).
+// shape classes of the forward kernels
+struct FwdCaps {
+  bool buf;    // 32-bit byte offsets within every (image, level) slice, sampling 2, ph*pw <= 256
+  bool lds;    // + ph*pw <= 64 and 2*ph, 2*pw <= 64
+  bool x4;     // + unit x stride, 16-B aligned rows / channel planes / bases (16-B LDS-DMA)
+};
+
+static FwdCaps fwd_caps(const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw, int32_t sr) {
+  FwdCaps f;
+  f.buf = sr == 2 && ph * pw <= kRoiThreads;
+  for (int l = 0; l < lv.L; ++l) {
+    const int64_t ext = ((int64_t)(channels - 1) * lv.sc[l] + (int64_t)(lv.h[l] - 1) * lv.sy[l] +
+                         (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
+    f.buf = f.buf && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
+  }
+  f.lds = f.buf && ph * pw <= 64 && 2 * ph <= 64 && 2 * pw <= 64;
+  f.x4 = f.lds;
+  for (int l = 0; l < lv.L; ++l)
+    f.x4 = f.x4 && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 && lv.sb[l] % 4 == 0 &&
+           (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
+  return f;
+}
+
+static int32_t group_bound(int64_t num_rois) { return (int32_t)((num_rois + kGrp - 1) / kGrp + 64); }
+
+// variant: 0 = direct gather, 10 = per-RoI LDS windows, 50 = grouped (needs the
+// workspace of frh_roi_align_workspace), -1 = best available.  Exported for
+// the kernel micro-benchmark (tools/bench_roi_align.py) and the parity tests.
 extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
                                              const int32_t* feat_hw, const int64_t* strides, const float* scales,
                                              int32_t batch, int32_t channels, const float* rois,
                                              const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
                                              int32_t pooled_w, int32_t sampling_ratio, int32_t aligned, float* out,
-                                             void* stream) {
+                                             void* workspace, size_t ws_bytes, void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
   FRH_REQUIRE((feats && out) || num_rois == 0, "null pointer argument");
@@ -1125,61 +1266,56 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   if (r) return r;
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
-  dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  const bool staged_ok = sampling_ratio > 0 && pooled_h * sampling_ratio <= kStageTaps &&
-                         pooled_w * sampling_ratio <= kStageTaps;
-  const bool regtap_ok = sampling_ratio == 2 && pooled_h * pooled_w <= kRoiThreads;
-  // the descriptor variant addresses one (image, level) slice with 32-bit byte offsets
-  bool buf_ok = regtap_ok;
-  for (int l = 0; l < lv.L; ++l) {
-    const int64_t ext = ((int64_t)(channels - 1) * lv.sc[l] + (int64_t)(lv.h[l] - 1) * lv.sy[l] +
-                         (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
-    buf_ok = buf_ok && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
-  }
-  const bool lds_ok = buf_ok && pooled_h * pooled_w <= 64 && 2 * pooled_h <= 64 && 2 * pooled_w <= 64;
-  if (variant < 0) variant = lds_ok ? 10 : buf_ok ? 8 : 0;
-  FRH_REQUIRE(variant == 0 || (variant == 1 && staged_ok) || (variant >= 2 && variant <= 6 && regtap_ok) ||
-                  (variant >= 7 && variant <= 8 && buf_ok) || (variant >= 9 && variant <= 16 && lds_ok),
+  const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+  const bool grp_ok = f.lds && num_rois <= kPlanMaxRois && workspace &&
+                      ws_bytes >= ((size_t)num_rois + group_bound(num_rois) + 2) * sizeof(int32_t);
+  // -1: the per-RoI LDS kernel (measured fastest on cfg2); -2: the
+  // grouped kernel when the workspace allows it (frh_roi_align_fwd_ws)
+  if (variant == -2) variant = grp_ok ? 50 : -1;
+  if (variant < 0) variant = f.lds ? 10 : 0;
+  FRH_REQUIRE(variant == 0 || (variant == 10 && f.lds) || ((variant == 50 || variant == 51) && grp_ok),
               "roi_align variant %d unsupported here", variant);
-  if (variant == 9)
-    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<kWinMax>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 10)
+  if (variant == 50 || variant == 51) {
+    int32_t* order = static_cast<int32_t*>(workspace);
+    int32_t* ngroups = order + num_rois;
+    int32_t* gstart = ngroups + 1;
+    hipLaunchKernelGGL(roi_group_plan_kernel, dim3(1), dim3(kPlanThreads), 0, as_stream(stream), rois, roi_levels,
+                       (int32_t)num_rois, order, gstart, ngroups);
+    r = check_launch("frh_roi_align_fwd (plan)");
+    if (r) return r;
+    const GroupPlan gp{order, gstart, ngroups};
+    const int64_t nchunk = (channels + kGrpChans - 1) / kGrpChans;
+    const dim3 grid((unsigned)(8 * ((group_bound(num_rois) + 7) / 8) * nchunk));
+    if (variant == 51)  // diagnostics: per-workgroup stamps past the results (tools/bench_roi_align.py)
+      hipLaunchKernelGGL((roi_align_fwd_group_kernel<4, 1>), grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp,
+                         out);
+    else if (f.x4)
+      hipLaunchKernelGGL(roi_align_fwd_group_kernel<4>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
+    else
+      hipLaunchKernelGGL(roi_align_fwd_group_kernel<1>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
+  } else if (variant == 10) {
+    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 11)
-    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<128>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 12)
-    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<64>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 13)
-    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 1>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 14)
-    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 2>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 15)
-    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 256>),
-                       dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0,
-                       as_stream(stream), lv, c, out);
-  else if (variant == 16)
-    hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 128>),
-                       dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0,
-                       as_stream(stream), lv, c, out);
-  else if (variant == 7)
-    hipLaunchKernelGGL(roi_align_fwd_buf_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 8)
-    hipLaunchKernelGGL(roi_align_fwd_buf_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 4)
-    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 5)
-    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 6)
-    hipLaunchKernelGGL(roi_align_fwd_vec4_kernel<4>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 3)
-    hipLaunchKernelGGL(roi_align_fwd_winreg_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 2)
-    hipLaunchKernelGGL(roi_align_fwd_regtap_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else if (variant == 1)
-    hipLaunchKernelGGL(roi_align_fwd_staged_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  else
+  } else {
+    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  }
   return check_launch("frh_roi_align_fwd");
+}
+
+extern "C" size_t frh_roi_align_workspace(int64_t num_rois) {
+  if (num_rois <= 0 || num_rois > kPlanMaxRois) return 0;
+  return ((size_t)num_rois + group_bound(num_rois) + 2) * sizeof(int32_t);
+}
+
+extern "C" int32_t frh_roi_align_fwd_ws(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                                        const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
+                                        const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                        int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                                        float* out, void* workspace, size_t ws_bytes, void* stream) {
+  return frh_roi_align_fwd_variant(-2, num_levels, feats, feat_hw, strides, scales, batch, channels, rois,
+                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, workspace,
+                                   ws_bytes, stream);
 }
 
 extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
@@ -1188,7 +1324,8 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
                                              int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
                                              int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
   return frh_roi_align_fwd_variant(-1, num_levels, feats, feat_hw, strides, scales, batch, channels, rois,
-                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, stream);
+                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, nullptr, 0,
+                                   stream);
 }
 
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,

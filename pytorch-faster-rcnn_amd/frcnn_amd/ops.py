@@ -399,6 +399,24 @@ def _feat_desc(feats):
 ROI_ALIGN_PROFILE = {'on': False, 'records': []}
 
 
+def roi_align_variant(variant, feats, rois, levels, scales, output_size, sampling_ratio):
+    """One named RoIAlign forward kernel (0 direct, 10 per-RoI LDS = default, 50 grouped);
+    parity tests and the micro-benchmark.  The grouped kernel's workspace comes from the
+    caching allocator like every other op's."""
+    _need_cuda(rois, *feats)
+    feats = [_f32(f) for f in feats]
+    rois = _f32(rois).contiguous()
+    K, C = rois.shape[0], feats[0].shape[1]
+    ph, pw = output_size
+    out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
+    hw, st = _feat_desc(feats)
+    ws = workspace(_lib.query('frh_roi_align_workspace', K), rois.device)
+    call('frh_roi_align_fwd_variant', int(variant), len(feats), ptr_array(feats), hw, st, f32_array(scales),
+         feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), 0, ptr(out), ptr(ws),
+         ws.numel(), stream_of(out))
+    return out
+
+
 class _RoIAlignMulti(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, levels, scales, output_size, sampling_ratio, aligned, *feats):

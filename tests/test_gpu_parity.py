@@ -337,6 +337,27 @@ def _rois(seed, n, batch):
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
+def test_roi_align_forward_kernels_identical(dev, layout):
+    """Every forward kernel (0 direct, 10 per-RoI LDS = default, 50 grouped union staging)
+    against the oracle and bit-identical to each other; P2-sized maps and 600 RoIs so the
+    grouped kernel takes both its union path and its per-RoI fallback (large windows)."""
+    from frcnn_amd import ops
+    grids = [(152, 256), (76, 128), (38, 64), (19, 32)]
+    feats = inputs.feature_maps(42, grids, 96, 2)
+    rois = _rois(43, 600, 2)
+    levels = oracle.roi_level_map(rois, 56.0, 4)
+    scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
+    ref = oracle.roi_align(feats, rois, levels, scales, (7, 7), 2)
+    ft = [T(f, dev) for f in feats]
+    if layout == 'nhwc':  # no 16-B staging: unit-stride rows are required
+        ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
+    outs = {v: ops.roi_align_variant(v, ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
+            for v in (0, 10, 50)}
+    np.testing.assert_allclose(outs[0], ref, rtol=1e-5, atol=1e-5)
+    assert np.array_equal(outs[10], outs[0]) and np.array_equal(outs[50], outs[0])
+
+
+@pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
 @pytest.mark.parametrize('sampling', [2, 0])
 def test_roi_align_multilevel_vs_oracle(dev, layout, sampling):
     from frcnn_amd import ops

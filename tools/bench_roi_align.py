@@ -21,7 +21,6 @@ def calibrate(variants, dev, small=False):
     takes its block-gather path.  Run under rocprofv3 --pmc FETCH_SIZE."""
     lib = _lib.load()
     fn = lib.frh_roi_align_fwd_variant
-    fn.restype = ctypes.c_int32
     C, S = (65536, 29) if small is False else (262144, 12)
     rois = torch.tensor([[0.0, 0.0, 0.0, S - 1.0, S - 1.0]], device=dev)
     levels = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -31,8 +30,9 @@ def calibrate(variants, dev, small=False):
         hw, st = ops._feat_desc(feats)
         out = torch.empty(1, C, 7, 7, device=dev)
         torch.cuda.synchronize()
+        ws = torch.empty(64, dtype=torch.uint8, device=dev)
         s = fn(v, 1, _lib.ptr_array(feats), hw, st, _lib.f32_array([1.0]), 1, C, _lib.ptr(rois), _lib.ptr(levels),
-               ctypes.c_int64(1), 7, 7, 2, 0, _lib.ptr(out), _lib.stream_of(out))
+               1, 7, 7, 2, 0, _lib.ptr(out), _lib.ptr(ws), 64, _lib.stream_of(out))
         assert s == 0, lib.frh_last_error()
         torch.cuda.synchronize()
         print('variant', v, 'done', flush=True)
@@ -41,7 +41,7 @@ def calibrate(variants, dev, small=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=50)
-    ap.add_argument('--variants', default='0,1')
+    ap.add_argument('--variants', default='0,10,50')
     ap.add_argument('--calib', action='store_true', help='known-byte FETCH_SIZE calibration launches only')
     ap.add_argument('--calib-small', action='store_true', help='calibration on the staged (small-window) path')
     ap.add_argument('--dump', help='save the RoIs / levels / level shapes of the recorded launch to this .npz')
@@ -66,17 +66,20 @@ def main():
     if args.dump:
         np.savez(args.dump, rois=r, levels=lv, shapes=np.array(shapes), scales=np.array(scales))
     lib = _lib.load()
-    fn = lib.frh_roi_align_fwd_variant
-    fn.restype = ctypes.c_int32
     K, C = rois.shape[0], shapes[0][1]
     hw, st = ops._feat_desc(feats)
     outs = {}
-    for v in [int(x) for x in args.variants.split(',')]:
-        out = torch.empty(K, C, ph, pw, device=dev)
+    wsb = int(lib.frh_roi_align_workspace(ctypes.c_int64(K)))
+    wsp = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
+    for spec in args.variants.split(','):
+        v = int(spec)
+        full = torch.zeros(K * C * ph * pw + (8 * 4096 * 8 if v == 51 else 0), device=dev)  # 51: stamps after
+        out = full[:K * C * ph * pw].view(K, C, ph, pw)
+
         def launch():
-            s = fn(v, len(feats), _lib.ptr_array(feats), hw, st, _lib.f32_array(scales), shapes[0][0], C,
-                   _lib.ptr(rois), _lib.ptr(levels), ctypes.c_int64(K), ph, pw, sr, 0, _lib.ptr(out),
-                   _lib.stream_of(out))
+            s = lib.frh_roi_align_fwd_variant(v, len(feats), _lib.ptr_array(feats), hw, st, _lib.f32_array(scales),
+                                              shapes[0][0], C, _lib.ptr(rois), _lib.ptr(levels), K, ph, pw, sr, 0,
+                                              _lib.ptr(full), _lib.ptr(wsp), wsb, _lib.stream_of(out))
             assert s == 0, lib.frh_last_error()
         for _ in range(5):
             launch()
@@ -88,10 +91,34 @@ def main():
             ts.append((e0, e1))
         torch.cuda.synchronize()
         ms = np.array([a.elapsed_time(b) for a, b in ts])
+        if v == 51:  # per-workgroup stamps [start, union, end, path | U << 8] (s_memrealtime, 100 MHz)
+            st = full[K * C * ph * pw:].view(torch.int64).view(-1, 4).cpu().numpy()
+            st = st[st[:, 0] > 0]
+            t0 = st[:, 0].min()
+            dur, pro = (st[:, 2] - st[:, 0]) / 100.0, (st[:, 1] - st[:, 0]) / 100.0
+            path = st[:, 3] & 255
+            print('  {} workgroups; span {:.1f} us; start p50/90/max {}'.format(
+                len(st), (st[:, 2].max() - t0) / 100.0, np.percentile((st[:, 0] - t0) / 100.0, [50, 90, 100]).round(1).tolist()))
+            for pth in sorted(set(path.tolist())):
+                m = path == pth
+                print('  path {:3d}: n {:4d} dur p50/90/max {} prologue p50 {:.2f} U p50 {}'.format(
+                    pth, m.sum(), np.percentile(dur[m], [50, 90, 100]).round(1).tolist(), np.median(pro[m]),
+                    int(np.median(st[m, 3] >> 8))), flush=True)
+        ref = outs[min(outs)] if outs else out
         outs[v] = out
-        d = float((out - outs[min(outs)]).abs().max())
-        print('variant {}: {:8.1f} us (min {:7.1f})  {:7.1f} GB/s algorithmic  max|diff| {:.3g}'.format(
-            v, ms.mean() * 1e3, ms.min() * 1e3, nbytes / (ms.mean() * 1e-3) / 1e9, d), flush=True)
+        d = float((out - ref).abs().max())
+        print('variant {:>4}: {:8.1f} us (min {:7.1f})  {:7.1f} GB/s algorithmic  max|diff| {:.3g}'.format(
+            spec, ms.mean() * 1e3, ms.min() * 1e3, nbytes / (ms.mean() * 1e-3) / 1e9, d), flush=True)
+        if d > 0:  # which RoIs differ: level, box, tap window of the scaled box
+            per = (out - ref).abs().flatten(1).max(1).values.cpu().numpy()
+            bad = np.nonzero(per > 0)[0]
+            print('  {} RoIs differ; first: '.format(len(bad)), flush=True)
+            for i in bad[:12]:
+                sc = scales[lv[i]]
+                bx = r[i, 1:] * sc
+                print('   roi {} lvl {} box {} win w {:.1f} h {:.1f} maxdiff {:.3g} ch-diff {}'.format(
+                    i, lv[i], r[i, 1:].round(1).tolist(), bx[2] - bx[0], bx[3] - bx[1], per[i],
+                    int(((out[i] - ref[i]).abs().flatten(1).max(1).values > 0).sum())), flush=True)
 
 
 if __name__ == '__main__':
