@@ -1031,10 +1031,12 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
   const int Q = (U + kPiece - 1) / kPiece;
   const int SF = Q * kPiece;
   float* junk = ring + kRing;
-  auto run = [&](auto jj, auto bb) {
-    constexpr int J = decltype(jj)::value;  // DMA rounds per wave per channel
-    constexpr int B = decltype(bb)::value;  // channels per step
-    static_assert(B * (J + 1) < 64, "vmcnt range");
+  auto run = [&](auto jj, auto bb, auto ddp) {
+    constexpr int J = decltype(jj)::value;   // DMA rounds per wave per channel
+    constexpr int B = decltype(bb)::value;   // channels per step
+    constexpr int D = decltype(ddp)::value;  // steps in flight ahead of the one being read
+    constexpr int NB = D + 1;                // step buffers
+    static_assert(B * (J + 1) * (D - 1) < 64 && B * J * D < 64, "vmcnt range");
     int goff[J], dst[J];
 #pragma unroll
     for (int q = 0; q < J; ++q) {
@@ -1047,8 +1049,8 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
       dst[q] = real ? piece * kPiece : -1;
     }
     const int nch = c1 - c0, nst = (nch + B - 1) / B;
-    auto issue = [&](int st) {  // step st: channels c0 + B*st + b (clamped) -> buffer st % 3
-      float* sb = ring + (st % 3) * (B * SF);
+    auto issue = [&](int st) {  // step st: channels c0 + B*st + b (clamped) -> buffer st % NB
+      float* sb = ring + (st % NB) * (B * SF);
 #pragma unroll
       for (int b = 0; b < B; ++b) {
         const int ch = c0 + min(st * B + b, nch - 1);
@@ -1056,20 +1058,20 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
         for (int q = 0; q < J; ++q) lds_dma<4 * kV>(fr, dst[q] >= 0 ? sb + b * SF + dst[q] : junk, goff[q], ch * cstep);
       }
     };
-    issue(0);
-    if (nst > 1) issue(1);
+    for (int st = 0; st < D && st < nst; ++st) issue(st);
     for (int st = 0; st < nst; ++st) {
-      // retire step st: younger than its DMAs are step st-1's B stores and step st+1's DMAs
-      if (st + 1 < nst) {
+      // retire step st: younger than its DMAs are, for each of the D-1 steps issued after
+      // it, B stores and B*J DMAs (the first step has no stores before; the tail waits all)
+      if (st + D - 1 < nst) {
         if (st == 0)
-          wait_vmcnt<B * J>();
+          wait_vmcnt<B * J * (D - 1)>();
         else
-          wait_vmcnt<B * (J + 1)>();
+          wait_vmcnt<B * (J + 1) * (D - 1)>();
       } else {
         wait_vmcnt<0>();
       }
       asm volatile("s_barrier" ::: "memory");  // every wave's share of step st has landed
-      const char* sb = reinterpret_cast<const char*>(ring + (st % 3) * (B * SF));
+      const char* sb = reinterpret_cast<const char*>(ring + (st % NB) * (B * SF));
       float acc[B];
 #pragma unroll
       for (int b = 0; b < B; ++b) {
@@ -1101,30 +1103,48 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[b]), orr, ci < nch ? ovoff : 0x40000000,
                                               (c0 + ci) * ostep, 0);
       }
-      // buffer (st + 2) % 3 was last read in step st - 1, which every wave finished before this step's barrier
-      if (st + 2 < nst) issue(st + 2);
+      // buffer (st + D) % NB was last read in step st - 1, which every wave finished before this step's barrier
+      if (st + D < nst) issue(st + D);
     }
   };
   const int J = (Q + kGrp - 1) / kGrp;
-  auto with_b = [&](auto jj) {
-    if (3 * 4 * SF <= kRing)
-      run(jj, std::integral_constant<int, 4>{});
-    else if (3 * 2 * SF <= kRing)
-      run(jj, std::integral_constant<int, 2>{});
+  // deepest pipeline the ring holds: B channels per step, D steps ahead
+  // B channels per step, D steps ahead: the deepest pipeline the ring holds within vmcnt range
+  const int n4 = kRing / (4 * SF), n2 = kRing / (2 * SF), n1 = kRing / SF;  // step buffers that fit
+  const int shape = n4 >= 7 ? 0 : n4 >= 5 ? 1 : n4 >= 3 ? 2 : n2 >= 5 ? 3 : n2 >= 3 ? 4 : n1 >= 5 ? 5 : 6;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  using I6 = std::integral_constant<int, 6>;
+  auto with_bd = [&](auto jj) {
+    constexpr int Jc = decltype(jj)::value;
+    constexpr bool f46 = 4 * (Jc + 1) * 5 < 64, f44 = 4 * (Jc + 1) * 3 < 64;
+    if (shape == 0 && f46)
+      run(jj, I4{}, std::conditional_t<f46, I6, I2>{});
+    else if (shape <= 1 && f44)
+      run(jj, I4{}, std::conditional_t<f44, I4, I2>{});
+    else if (shape <= 2)
+      run(jj, I4{}, I2{});
+    else if (shape == 3)
+      run(jj, I2{}, I4{});
+    else if (shape == 4)
+      run(jj, I2{}, I2{});
+    else if (shape == 5)
+      run(jj, I1{}, I4{});
     else
-      run(jj, std::integral_constant<int, 1>{});
+      run(jj, I1{}, I2{});
   };
   if (J <= 1)
-    with_b(std::integral_constant<int, 1>{});
+    with_bd(std::integral_constant<int, 1>{});
   else if (J <= 2)
-    with_b(std::integral_constant<int, 2>{});
+    with_bd(std::integral_constant<int, 2>{});
   else if (J <= 3)
-    with_b(std::integral_constant<int, 3>{});
+    with_bd(std::integral_constant<int, 3>{});
   else  // only the 4-byte staging (kV = 1) gets here
-    run(std::integral_constant<int, 16>{}, std::integral_constant<int, 1>{});
+    run(std::integral_constant<int, 16>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
   if (kDiag) {
     __syncthreads();
-    stamp(2 + (3 * 4 * SF <= kRing ? 4 : 3 * 2 * SF <= kRing ? 2 : 1) * 16 + J * 4, U);
+    stamp(2 + J * 4, U);
   }
 }
 
