@@ -11,6 +11,11 @@
 //        waves OR the kept rows' words into the LDS suppression bitmap with
 //        8 independent loads per lane in flight.
 #include <stdlib.h>
+#include <string.h>
+
+#include <math.h>
+
+#include <type_traits>
 
 #include "block_ops.h"
 
@@ -18,24 +23,70 @@ namespace frh {
 
 constexpr int kMaxNmsWords = 256;  // n <= 16384 boxes per segment
 
-__global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
-                                                      const int32_t* __restrict__ counts, int64_t n_max, int nbw,
-                                                      double thr, uint64_t* __restrict__ mask) {
-  __shared__ float4 cb_box[64];
-  __shared__ float cb_area[64];
-  const int s = blockIdx.z, rb = blockIdx.y, cb = blockIdx.x;
-  if (cb < rb) return;
+// The suppression test IoU > thr without the division.  v = RN(inter / union) is
+// a float, so v > thr (double) <=> v >= t_up, the smallest float above thr, <=>
+// inter / union > mid = (t_dn + t_up) / 2 (ties: round-half-even picks t_up iff its
+// significand is even).  mid has 25 significant bits and union 24, so mid * union
+// is exact in double and the comparison below decides exactly what the reference's
+// float division + double compare decides.  union <= 0 / NaN take the division.
+struct NmsThr {
+  double thr, mid;
+  int tie_up, fast;
+};
+
+static NmsThr nms_thr(double thr) {
+  NmsThr t{thr, 0.0, 0, 0};
+  if (!(thr > 0.0 && thr < 1.0)) return t;
+  float up = (float)thr;
+  if ((double)up <= thr) up = nextafterf(up, 2.0f);
+  const float dn = nextafterf(up, 0.0f);
+  t.mid = 0.5 * ((double)dn + (double)up);
+  uint32_t bits;
+  memcpy(&bits, &up, 4);
+  t.tie_up = (bits & 1u) == 0;
+  t.fast = 1;
+  return t;
+}
+
+// kFast (0 < thr < 1): IoU <= 0 or NaN whenever union <= 0 or NaN, never above thr
+template <bool kFast>
+__device__ __forceinline__ bool iou_above(float4 a, float area_a, float4 b, float area_b, const NmsThr& T) {
+  const float w = fmaxf(0.0f, fminf(a.z, b.z) - fmaxf(a.x, b.x));
+  const float h = fmaxf(0.0f, fminf(a.w, b.w) - fmaxf(a.y, b.y));
+  const float inter = w * h;
+  const float uni = (area_a + area_b) - inter;
+  if (kFast) {  // bitwise, not short-circuit: no branches in the unrolled column loop
+    const double lhs = (double)inter, rhs = T.mid * (double)uni;
+    return (uni > 0.0f) & ((lhs > rhs) | ((lhs == rhs) & (T.tie_up != 0)));
+  }
+  return (double)(inter / uni) > T.thr;
+}
+
+// one wave per (segment, 64-row block, 64-col block >= row block); four column
+// blocks per 256-thread workgroup, each wave staging its own column boxes
+template <int kMode = 0>  // timing diagnostics only (tools/bench_nms.py): 1 = no IoU loop, 2 = no store
+__global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
+                                                       const int32_t* __restrict__ counts, int64_t n_max, int nbw,
+                                                       NmsThr T, uint64_t* __restrict__ mask) {
+  __shared__ float4 cb_box_all[4][64];
+  __shared__ float cb_area_all[4][64];
+  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int s = blockIdx.z, rb = blockIdx.y, cb = blockIdx.x * 4 + wv;
+  if (cb < rb || cb >= nbw) return;
   const int n = counts[s];
   if (rb * 64 >= n || cb * 64 >= n) return;
+  float4* cb_box = cb_box_all[wv];
+  float* cb_area = cb_area_all[wv];
   const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
-  const int t = threadIdx.x;
   const int col = cb * 64 + t;
   if (col < n) {
     float4 c = bx[col];
     cb_box[t] = c;
     cb_area[t] = (c.z - c.x) * (c.w - c.y);
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int row = rb * 64 + t;
   if (row >= n) return;
   const float4 a = bx[row];
@@ -43,11 +94,35 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
   const int ncols = min(64, n - cb * 64);
   const int start = (cb == rb) ? t + 1 : 0;
   uint64_t bits = 0;
-  for (int j = start; j < ncols; ++j) {
-    float v = iou_tv(a, aa, cb_box[j], cb_area[j]);
-    if ((double)v > thr) bits |= 1ull << j;
+  // uniform trip count, unrolled: the LDS broadcast reads of 8 column boxes issue together
+  // (columns outside [start, ncols) are masked, their LDS slots may hold stale boxes)
+  if (kMode != 1) {
+    auto sweep = [&](auto fast) {
+      constexpr bool F = decltype(fast)::value;
+      for (int j0 = 0; j0 < 64; j0 += 8) {
+        float4 cbx[8];
+        float cba[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          cbx[u] = cb_box[j0 + u];
+          cba[u] = cb_area[j0 + u];
+        }
+        uint32_t hit = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hit |= (uint32_t)iou_above<F>(a, aa, cbx[u], cba[u], T) << u;
+        bits |= (uint64_t)hit << j0;
+      }
+    };
+    if (T.fast)
+      sweep(std::true_type{});
+    else
+      sweep(std::false_type{});
+    // columns outside [start, ncols) (stale LDS slots, the diagonal and below)
+    const uint64_t hi = ncols >= 64 ? ~0ull : ((1ull << ncols) - 1ull);
+    const uint64_t lo = start >= 64 ? ~0ull : ((1ull << start) - 1ull);
+    bits &= hi & ~lo;
   }
-  mask[((int64_t)s * n_max + row) * nbw + cb] = bits;
+  if (kMode != 2 || bits == 12345ull) mask[((int64_t)s * n_max + row) * nbw + cb] = bits;
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
@@ -321,14 +396,23 @@ __global__ void __launch_bounds__(256) nms_scan_pipe_kernel(const uint64_t* __re
 // tools/bench_nms.py hooks (not part of the public header): scan variant 0 = legacy
 // block-synchronous scan, 1 = pipelined; optional per-block resolver timestamps.
 static int g_nms_scan_variant = -1;
+static int g_nms_mask_mode = 0;
 static uint64_t* g_nms_dbg = nullptr;
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                           uint64_t* mask, hipStream_t st) {
   const int nbw = (n_max + 63) / 64;
-  dim3 g(nbw, nbw, S);
-  hipLaunchKernelGGL(nms_mask_kernel, g, dim3(64), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw, thr, mask);
+  dim3 g((nbw + 3) / 4, nbw, S);
+  if (g_nms_mask_mode == 1)
+    hipLaunchKernelGGL(nms_mask_kernel<1>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
+                       nms_thr(thr), mask);
+  else if (g_nms_mask_mode == 2)
+    hipLaunchKernelGGL(nms_mask_kernel<2>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
+                       nms_thr(thr), mask);
+  else
+    hipLaunchKernelGGL(nms_mask_kernel<0>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
+                       nms_thr(thr), mask);
   if (g_nms_scan_variant < 0) g_nms_scan_variant = getenv("FRH_NMS_SCAN_LEGACY") ? 0 : 1;
   if (g_nms_scan_variant == 0)
     hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw, max_keep, keep,
@@ -353,6 +437,8 @@ size_t nms_mask_bytes(int32_t S, int32_t n_max) {
 }  // namespace frh
 
 using namespace frh;
+
+extern "C" void frh_nms_mask_debug(int32_t mode) { g_nms_mask_mode = mode; }
 
 extern "C" void frh_nms_scan_debug(int32_t variant, void* timestamps) {
   g_nms_scan_variant = variant;

@@ -304,6 +304,29 @@ def test_nms_keep_bit_exact(dev, n, thr):
     np.testing.assert_array_equal(keep, oracle.nms(boxes, scores, thr))
 
 
+@pytest.mark.parametrize('thr', [0.7, 0.5, 0.3])
+def test_nms_threshold_boundary(dev, thr):
+    """Pairs of boxes whose IoU straddles the threshold by a few float ulps: the kernel's
+    division-free test (inter > mid * union in double) must decide exactly like the
+    reference's float division followed by the double comparison."""
+    from frcnn_amd import ops
+    rng = np.random.default_rng(int(thr * 100))
+    n = 1024
+    w = np.float32(100.0)
+    # IoU of [0, 0, w, w] and its x-shift by d: (w - d) / (w + d); the crossing at d* = w (1 - thr) / (1 + thr)
+    dstar = float(w) * (1 - thr) / (1 + thr)
+    d = (dstar + rng.integers(-40, 41, n // 2) * dstar * 2e-7).astype(np.float32)
+    base = (np.arange(n // 2) * 1000.0).astype(np.float32)  # pairs far apart: no cross-pair overlap
+    a = np.stack([base, np.zeros_like(base), base + w, np.full_like(base, w)], 1)
+    b = np.stack([base + d, np.zeros_like(base), base + d + w, np.full_like(base, w)], 1)
+    boxes = np.ascontiguousarray(np.stack([a, b], 1).reshape(n, 4))
+    scores = np.tile(np.array([0.9, 0.8], np.float32), n // 2)
+    keep = ops.nms(T(boxes, dev), T(scores, dev), thr).cpu().numpy()
+    ref = oracle.nms(boxes, scores, thr)
+    np.testing.assert_array_equal(keep, ref)
+    assert 0 < len(ref) - n // 2 < n // 2  # both outcomes occur
+
+
 def test_nms_empty_and_batched(dev):
     from frcnn_amd import ops, utils
     e = ops.nms(torch.zeros(0, 4, device=dev), torch.zeros(0, device=dev), 0.5)

@@ -56,6 +56,21 @@ def main():
         res[v] = (keep.clone(), kc.clone())
         print('scan variant {}: {:.1f} us per nms_sorted (mask + scan), kept {}'.format(
             v, e0.elapsed_time(e1) / a.iters * 1e3, kc.tolist()), flush=True)
+    # mask kernel alone, by diagnostic mode (0 full, 1 no IoU loop, 2 no store); scan skipped via max_keep
+    lib.frh_nms_mask_debug.argtypes = [ctypes.c_int32]
+    for mode in (0, 1, 2):
+        lib.frh_nms_mask_debug(mode)
+        for _ in range(3):
+            ops.nms_sorted(boxes, counts, a.n, a.thr)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            ops.nms_sorted(boxes, counts, a.n, a.thr)
+        e1.record()
+        torch.cuda.synchronize()
+        print('mask mode {}: {:.1f} us per nms_sorted'.format(mode, e0.elapsed_time(e1) / a.iters * 1e3), flush=True)
+    lib.frh_nms_mask_debug(0)
     for v in vs[1:]:
         ok = torch.equal(res[vs[0]][1], res[v][1])
         for sg in range(a.segs):
