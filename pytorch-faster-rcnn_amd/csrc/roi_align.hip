@@ -1070,7 +1070,9 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
       } else {
         wait_vmcnt<0>();
       }
+      const uint64_t t_w = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
       asm volatile("s_barrier" ::: "memory");  // every wave's share of step st has landed
+      const uint64_t t_b = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
       const char* sb = reinterpret_cast<const char*>(ring + (st % NB) * (B * SF));
       float acc[B];
 #pragma unroll
@@ -1105,6 +1107,14 @@ __global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLev
       }
       // buffer (st + D) % NB was last read in step st - 1, which every wave finished before this step's barrier
       if (st + D < nst) issue(st + D);
+      if (kDiag && lane == 0 && blockIdx.x < 64 && st < 20 && (wave == 0 || wave == 7)) {
+        int64_t* d = reinterpret_cast<int64_t*>(out + c.K * c.C * c.ph * c.pw) + 8192 +
+                     ((int64_t)(blockIdx.x * 2 + (wave ? 1 : 0)) * 20 + st) * 4;
+        d[0] = (int64_t)t_w;
+        d[1] = (int64_t)t_b;
+        d[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        d[3] = B * 100 + D;
+      }
     }
   };
   const int J = (Q + kGrp - 1) / kGrp;

@@ -92,13 +92,24 @@ def main():
         torch.cuda.synchronize()
         ms = np.array([a.elapsed_time(b) for a, b in ts])
         if v == 51:  # per-workgroup stamps [start, union, end, path | U << 8] (s_memrealtime, 100 MHz)
-            st = full[K * C * ph * pw:].view(torch.int64).view(-1, 4).cpu().numpy()
+            allst = full[K * C * ph * pw:].view(torch.int64)
+            steps = allst[8192:8192 + 128 * 20 * 4].view(64, 2, 20, 4).cpu().numpy()
+            st = allst[:8192].view(-1, 4).cpu().numpy()
             st = st[st[:, 0] > 0]
             t0 = st[:, 0].min()
             dur, pro = (st[:, 2] - st[:, 0]) / 100.0, (st[:, 1] - st[:, 0]) / 100.0
             path = st[:, 3] & 255
             print('  {} workgroups; span {:.1f} us; start p50/90/max {}'.format(
                 len(st), (st[:, 2].max() - t0) / 100.0, np.percentile((st[:, 0] - t0) / 100.0, [50, 90, 100]).round(1).tolist()))
+            for wg in range(3):  # per-step timeline of waves 0 and 7: wait->barrier->eval done (us from WG start)
+                for wv in (0, 1):
+                    sw = steps[wg, wv]
+                    sw = sw[sw[:, 0] > 0]
+                    if len(sw):
+                        b0 = st[wg, 0] if wg < len(st) else sw[0, 0]
+                        print('  wg {} wave {} (B,D)={}: '.format(wg, 7 * wv, sw[0, 3]) + ' '.join(
+                            '{:.1f}/{:.1f}/{:.1f}'.format((x[0] - b0) / 100, (x[1] - b0) / 100, (x[2] - b0) / 100)
+                            for x in sw[:10]), flush=True)
             for pth in sorted(set(path.tolist())):
                 m = path == pth
                 print('  path {:3d}: n {:4d} dur p50/90/max {} prologue p50 {:.2f} U p50 {}'.format(
