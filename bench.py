@@ -130,6 +130,10 @@ def main():
     ap.add_argument('--sampler', default='device', choices=['device', 'numpy'])
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--mode', default='fwd', choices=['fwd', 'train'],
+                    help='fwd: forward+loss (the BASELINE metric); train: forward+loss+backward with the '
+                         'DDP gradient all-reduce (RCCL) + grad clip + SGD step (frcnn_amd.train)')
+    ap.add_argument('--bucket-mb', type=float, default=None, help='DDP all-reduce bucket size (train mode)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -147,9 +151,18 @@ def main():
     model, cfg = make_model(dev, seed=0)
     batch = make_batch(dev, args.batch, seed=0, rank=rank)
 
-    def step():
-        losses = model.forward_train(*batch)
-        return sum(losses.values())
+    if args.mode == 'train':
+        from frcnn_amd.train import TrainStep, DEFAULT_BUCKET_MB
+        opt_cfg = cfg.get('optimizer_config', None) or {}
+        train_step = TrainStep(model, cfg.get('optimizer', None), opt_cfg.get('grad_clip', None), world, dev,
+                               args.bucket_mb or DEFAULT_BUCKET_MB)
+
+        def step():
+            return train_step(*batch)
+    else:
+        def step():
+            losses = model.forward_train(*batch)
+            return sum(losses.values())
 
     for _ in range(args.warmup):
         step()
@@ -199,7 +212,8 @@ def main():
     if rank == 0:
         imgs_total = world * args.batch * args.steps
         out = {
-            'metric': 'img/s FasterRCNN_R50_FPN 1000x600 fwd+loss',
+            'metric': 'img/s FasterRCNN_R50_FPN 1000x600 ' + ('fwd+loss' if args.mode == 'fwd' else
+                                                               'train step (fwd+loss+bwd+allreduce+SGD)'),
             'value': imgs_total / t_max,
             'unit': 'img/s',
             'n_gpus': world,
@@ -214,7 +228,7 @@ def main():
             'config': {'workload': 'configs/faster_rcnn_r50_fpn.py (BASELINE config 2) forward_train',
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
-                       'sampler': args.sampler},
+                       'sampler': args.sampler, 'mode': args.mode},
             'roofline': {'kernel': 'roi_align_fwd_lds_kernel<256, 0, 64>', 'bound': 'hbm',
                          'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': traffic,

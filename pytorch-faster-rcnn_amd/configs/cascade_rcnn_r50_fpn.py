@@ -1,6 +1,6 @@
 # Cascade R-CNN R50-FPN (BASELINE config 4), in the reference's config-file format.
 # Hyper-parameters follow the reference's configs/cascade_rcnn_r50_fpn.py (3 stages,
-# class-agnostic regression, stage IoU 0.5 / 0.6 / 0.7); pipeline / optimiser out of scope.
+# class-agnostic regression, stage IoU 0.5 / 0.6 / 0.7); data pipeline out of scope.
 
 _strides = [4, 8, 16, 32, 64]
 _stds = [[0.1, 0.1, 0.2, 0.2], [0.05, 0.05, 0.1, 0.1], [0.033, 0.033, 0.067, 0.067]]
@@ -46,3 +46,7 @@ test_cfg = dict(
 )
 
 data = dict(train=dict(imgs_per_gpu=2), test=dict(imgs_per_gpu=2))
+
+# optimiser of the reference config (lib/trainer: OptimizerHook clips, then SGD steps)
+optimizer = dict(type='SGD', lr=0.0025, momentum=0.9, weight_decay=0.0001)
+optimizer_config = dict(grad_clip=dict(max_norm=35, norm_type=2))

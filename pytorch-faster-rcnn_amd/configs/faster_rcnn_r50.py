@@ -1,6 +1,6 @@
 # Faster R-CNN R50-C4 (BASELINE config 1), in the reference's config-file format.
 # Hyper-parameters follow the reference's configs/faster_rcnn_r50.py (single stride-16
-# level, RoIPool); data pipeline / optimiser sections are out of this build's scope.
+# level, RoIPool); the data pipeline section is out of this build's scope.
 
 
 def _loss(kind, **kw):
@@ -42,3 +42,7 @@ test_cfg = dict(
 )
 
 data = dict(train=dict(imgs_per_gpu=2), test=dict(imgs_per_gpu=2))
+
+# optimiser of the reference config (lib/trainer: OptimizerHook clips, then SGD steps)
+optimizer = dict(type='SGD', lr=0.001, momentum=0.9, weight_decay=0.0005)
+optimizer_config = dict(grad_clip=None)

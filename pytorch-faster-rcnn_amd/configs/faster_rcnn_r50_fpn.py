@@ -1,7 +1,7 @@
 # Faster R-CNN R50-FPN (BASELINE config 2), in the reference's config-file
 # format (plain Python dicts read by frcnn_amd.config.Config.fromfile).
 # Hyper-parameters follow the reference's configs/faster_rcnn_r50_fpn.py;
-# data pipeline / optimiser sections are out of this build's scope.
+# the data pipeline section is out of this build's scope.
 
 _strides = [4, 8, 16, 32, 64]
 
@@ -46,3 +46,7 @@ test_cfg = dict(
 )
 
 data = dict(train=dict(imgs_per_gpu=2), test=dict(imgs_per_gpu=2))
+
+# optimiser of the reference config (lib/trainer: OptimizerHook clips, then SGD steps)
+optimizer = dict(type='SGD', lr=0.0025, momentum=0.9, weight_decay=0.0001)
+optimizer_config = dict(grad_clip=dict(max_norm=35, norm_type=2))

@@ -1,6 +1,6 @@
 # ATSS R50-FPN (BASELINE config 5), in the reference's config-file format.
 # Hyper-parameters follow the reference's configs/fcos_r50_fpn_atss.py;
-# data pipeline / optimiser sections are out of this build's scope.
+# the data pipeline section is out of this build's scope.
 
 model = dict(
     type='FCOS',
@@ -17,3 +17,7 @@ model = dict(
 train_cfg = dict(allowed_border=-1, total_epochs=24)
 
 test_cfg = dict(pre_nms=1000, min_bbox_size=0, min_score=0.05, nms_iou=0.6, nms_type='strict', max_per_img=100)
+
+# optimiser of the reference config (lib/trainer: OptimizerHook clips, then SGD steps)
+optimizer = dict(type='SGD', lr=0.00125, momentum=0.9, weight_decay=0.0001)
+optimizer_config = dict(grad_clip=None)

@@ -1,6 +1,6 @@
 # RetinaNet R50-FPN (BASELINE config 3), in the reference's config-file format.
-# Hyper-parameters follow the reference's configs/retinanet_r50_fpn.py; pipeline /
-# optimiser sections are out of this build's scope.
+# Hyper-parameters follow the reference's configs/retinanet_r50_fpn.py; the data
+# pipeline section is out of this build's scope.
 
 model = dict(
     type='RetinaNet',
@@ -19,3 +19,7 @@ train_cfg = dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.5, neg_iou=0.4, 
 test_cfg = dict(pre_nms=1000, min_bbox_size=0, min_score=0.05, nms_iou=0.5, nms_type='strict', max_per_img=100)
 
 data = dict(train=dict(imgs_per_gpu=8), test=dict(imgs_per_gpu=8))
+
+# optimiser of the reference config (lib/trainer: OptimizerHook clips, then SGD steps)
+optimizer = dict(type='SGD', lr=0.00125, momentum=0.9, weight_decay=0.0001)
+optimizer_config = dict(grad_clip=dict(max_norm=35, norm_type=2))

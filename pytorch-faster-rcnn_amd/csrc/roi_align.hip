@@ -1196,6 +1196,129 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv
   }
 }
 
+// Backward, window-accumulated (sampling 2, ph*pw <= 64): the default.  The
+// per-tap form above issues 16 scattered global float atomics per (bin, channel)
+// -- 205 M for a cfg2 batch, executed at the memory side at a small fraction of
+// the coalesced atomic rate (MI355X_MICROARCH.md, global float atomics): 7.7 ms
+// per train step.  Here each wave owns 16 channels of one RoI: per channel it
+// sums the 16 weighted taps of every bin into an LDS copy of the RoI's tap window
+// (ds_add_f32), then adds the window to the feature gradient with one global
+// atomic per non-zero cell, lanes along window rows.  Windows above kBwdSlab
+// floats keep the per-tap atomics.  Contributions are the reference's
+// grad * w / count; float atomics make the summation order (and the last bits)
+// run-dependent, as in torchvision's own CUDA backward.
+constexpr int kBwdSlab = 1024;  // floats per wave
+
+__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevels lv, RoiCfg c,
+                                                                        const float* __restrict__ gout) {
+  constexpr int SR = 2, kCh = kRoiChanChunk / (kRoiThreads / kWave);
+  __shared__ float slab_all[kRoiThreads / kWave][kBwdSlab];
+  const int64_t k = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
+  const int nch = min(kCh, c.C - cw0);
+  if (nch <= 0) return;
+  float* slab = slab_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {  // sampling 2: the "/ gh" of the sample position is an exact halving
+    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
+  }
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
+    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  if (y1 < y0 || x1 < x0) return;  // no valid tap: no gradient
+  const int WW = x1 - x0 + 1, n = (y1 - y0 + 1) * WW;
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const float* go = gout + (k * c.C + cw0) * nbins;
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = active && a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  if (n > kBwdSlab) {  // window larger than the slab: per-tap global atomics
+    for (int ch = 0; ch < nch; ++ch) {
+      const float gv = active ? go[ch * nbins + bin] : 0.0f;
+      float* f = gbase + (int64_t)ch * scs;
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          if (!ok[iy][ix]) continue;
+          const Tap a = ty[iy], b = tx[ix];
+          atomicAdd(&f[a.lo * sy + b.lo * sx], gv * wt[iy][ix][0] / g.count);
+          atomicAdd(&f[a.lo * sy + b.hi * sx], gv * wt[iy][ix][1] / g.count);
+          atomicAdd(&f[a.hi * sy + b.lo * sx], gv * wt[iy][ix][2] / g.count);
+          atomicAdd(&f[a.hi * sy + b.hi * sx], gv * wt[iy][ix][3] / g.count);
+        }
+    }
+    return;
+  }
+  int cell[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      const int rl = (a.lo - y0) * WW, rh = (a.hi - y0) * WW, cl = b.lo - x0, chh = b.hi - x0;
+      cell[iy][ix][0] = rl + cl;
+      cell[iy][ix][1] = rl + chh;
+      cell[iy][ix][2] = rh + cl;
+      cell[iy][ix][3] = rh + chh;
+    }
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  const int r0 = lane / WW, col0 = lane - r0 * WW, dr = kWave / WW, dc = kWave - dr * WW;
+  for (int ch = 0; ch < nch; ++ch) {
+    for (int e = lane; e < n; e += kWave) slab[e] = 0.0f;
+    wave_sync();
+    const float gv = active ? go[ch * nbins + bin] : 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix)
+        if (ok[iy][ix])
+#pragma unroll
+          for (int q = 0; q < 4; ++q) atomicAdd(&slab[cell[iy][ix][q]], gv * wt[iy][ix][q] / g.count);
+    wave_sync();
+    float* f = gbase + (int64_t)ch * scs;
+    int r = r0, col = col0;
+    for (int e = lane; e < n; e += kWave) {
+      const float v = slab[e];
+      if (v != 0.0f) atomicAdd(&f[(int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx], v);
+      r += dr;
+      col += dc;
+      if (col >= WW) col -= WW, ++r;
+    }
+    wave_sync();  // the window is re-zeroed for the next channel only after every lane read it
+  }
+}
+
 __global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int L, int64_t* levels) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
@@ -1373,7 +1496,10 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   FRH_REQUIRE(grad_feats && grad_out, "null pointer argument");
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  hipLaunchKernelGGL(roi_align_bwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
+  if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
+    hipLaunchKernelGGL(roi_align_bwd_lds_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
+  else
+    hipLaunchKernelGGL(roi_align_bwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   return check_launch("frh_roi_align_bwd");
 }
 

@@ -1,0 +1,73 @@
+"""One training iteration of the reference trainer, data-parallel over ranks.
+
+Reference: `BasicTrainer.train_one_iter` (`lib/trainer/trainer.py:100-127`):
+forward_train -> sum of the loss dict -> backward -> `OptimizerHook` gradient clipping
+(`lib/trainer/hooks.py:55-59`, `clip_grad_norm_(max_norm, norm_type)`) -> SGD step, with
+the optimizer of the config (`configs/faster_rcnn_r50_fpn.py:111-112`: SGD lr 0.0025,
+momentum 0.9, weight decay 1e-4, grad_clip max_norm 35).
+
+The reference is single-process (`README.md:8`, `train.py:117-120`).  Here each rank is
+one process per GPU holding its own image shard; the only exchange is the gradient
+all-reduce, done by DistributedDataParallel's bucketed all-reduce over RCCL (`nccl`
+backend on ROCm) while backward runs, averaged over ranks.  Losses stay normalised per
+rank (avg_factor of the local batch, `lib/heads/anchor_head.py:129`,
+`lib/heads/bbox_head.py:62`), which equals the reference's per-iteration semantics at
+imgs_per_gpu images per rank.  BN is frozen (eval-mode statistics, `lib/backbones.py:241-247`),
+so no SyncBN and no buffer broadcast.
+"""
+import torch
+from torch import nn
+
+# Gradient bucket size for the all-reduce.  cfg2 has 41 M trainable f32 parameters
+# (165 MB): 25 MB buckets give ~7 all-reduces that start while backward is still
+# producing the earlier layers' gradients, and each is large enough to keep RCCL's
+# channels over the 7 xGMI links busy.
+DEFAULT_BUCKET_MB = 25
+
+
+class DetectorLoss(nn.Module):
+    """forward(*batch) = sum of forward_train's loss dict (what DDP wraps)."""
+
+    def __init__(self, detector):
+        super().__init__()
+        self.detector = detector
+
+    def forward(self, img, gt_bboxes, gt_labels, img_metas):
+        losses = self.detector.forward_train(img, gt_bboxes, gt_labels, img_metas)
+        return sum(losses.values())
+
+
+def build_optimizer(params, cfg):
+    """The reference's optimizer dict (type SGD) -> torch optimizer."""
+    cfg = dict(cfg or dict(type='SGD', lr=0.0025, momentum=0.9, weight_decay=0.0001))
+    kind = cfg.pop('type')
+    if kind != 'SGD':
+        raise ValueError('unsupported optimizer type {}'.format(kind))
+    return torch.optim.SGD(params, **cfg)
+
+
+class TrainStep:
+    """Callable training iteration on this rank's batch; returns the (detached) local loss."""
+
+    def __init__(self, detector, optimizer_cfg=None, grad_clip=None, world_size=1, device=None,
+                 bucket_mb=DEFAULT_BUCKET_MB):
+        self.detector = detector
+        self.params = [p for p in detector.parameters() if p.requires_grad]
+        net = DetectorLoss(detector)
+        if world_size > 1:
+            ids = [device] if device is not None and device.type == 'cuda' else None
+            net = nn.parallel.DistributedDataParallel(net, device_ids=ids, bucket_cap_mb=bucket_mb,
+                                                      gradient_as_bucket_view=True, broadcast_buffers=False)
+        self.net = net
+        self.optimizer = build_optimizer(self.params, optimizer_cfg)
+        self.grad_clip = dict(grad_clip) if grad_clip else None
+
+    def __call__(self, img, gt_bboxes, gt_labels, img_metas):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss = self.net(img, gt_bboxes, gt_labels, img_metas)
+        loss.backward()
+        if self.grad_clip:
+            nn.utils.clip_grad_norm_(self.params, self.grad_clip['max_norm'],
+                                     self.grad_clip.get('norm_type', 2))
+        self.optimizer.step()
+        return loss.detach()
