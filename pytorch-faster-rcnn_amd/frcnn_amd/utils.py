@@ -32,6 +32,16 @@ def wh_from_xyxy(bbox):
     return bbox[2] - bbox[0] + 1, bbox[3] - bbox[1] + 1
 
 
+def xyxy2xywh(xyxy):
+    """utils.py:146-147: [4, n] inclusive-pixel xyxy -> xywh (w = x2 - x1 + 1)."""
+    return torch.stack([xyxy[0], xyxy[1], xyxy[2] - xyxy[0] + 1, xyxy[3] - xyxy[1] + 1])
+
+
+def xywh2xyxy(xywh):
+    """utils.py:148-149."""
+    return torch.stack([xywh[0], xywh[1], xywh[0] + xywh[2] - 1, xywh[1] + xywh[3] - 1])
+
+
 def center_of(bbox):
     return (bbox[2] + bbox[0]) / 2, (bbox[3] + bbox[1]) / 2
 
