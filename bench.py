@@ -23,6 +23,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -168,8 +169,23 @@ def main():
             losses = model.forward_train(*batch)
             return sum(losses.values())
 
-    for _ in range(args.warmup):
+    # Warmup (MIOpen's algorithm search runs here): a heartbeat on stderr keeps long
+    # searches visibly alive (train mode searches the backward convolutions too).
+    hb_stop = threading.Event()
+
+    def heartbeat(t_start=time.perf_counter()):
+        while not hb_stop.wait(30.0):
+            if rank == 0:
+                print('bench: warmup running, {:.0f} s'.format(time.perf_counter() - t_start), file=sys.stderr,
+                      flush=True)
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    for w in range(args.warmup):
         step()
+        if rank == 0:
+            print('bench: warmup step {}/{} done'.format(w + 1, args.warmup), file=sys.stderr, flush=True)
+    hb_stop.set()
 
     def barrier():
         if world > 1:

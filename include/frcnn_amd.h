@@ -317,6 +317,41 @@ int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gam
                    const float* beta, const float* mean, const float* var, float eps,
                    int64_t n, int32_t c, int64_t hw, int32_t relu, void* stream);
 
+/* ---------------------------------------------------------------- f1: fused losses
+ * Classification losses of lib/losses.py on the head outputs, summed (the reference's
+ * reductions): kind 0 = sigmoid_focal_loss (losses.py:33-61, one-hot[:, 1:] targets),
+ * 1 = CrossEntropyLoss(use_sigmoid=True) (losses.py:139-150; C == 1 takes the target
+ * value itself, int64 or, with target_is_float, f32), 2 = CrossEntropyLoss softmax
+ * (losses.py:151-153, labels in [0, C)).  Logit (i, k) is x[i*sr + k*sc] (any strides,
+ * so AnchorHead's [C, S] targets need no transpose copy); out is one f32 on the device.
+ * Backward writes grad_x (i, k) at grad_x[i*gsr + k*gsc] = grad_out[0] * dL/dx.
+ * Callers: AnchorHead.calc_loss (anchor_head.py:113-139), BBoxHead.calc_loss
+ * (bbox_head.py:56-87), FCOSHead losses (fcos_head.py:418-534). */
+size_t frh_loss_workspace(void);
+int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr,
+                         int64_t sc, const void* target, int32_t target_is_float, float alpha,
+                         float gamma, float* out, void* workspace, size_t ws_bytes, void* stream);
+int32_t frh_cls_loss_bwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr,
+                         int64_t sc, const void* target, int32_t target_is_float, float alpha,
+                         float gamma, const float* grad_out, float* grad_x, int64_t gsr,
+                         int64_t gsc, void* stream);
+/* smooth_l1_loss_v2 (losses.py:77-83) summed over rows i < n, columns j < m of
+ * x(i, j) = x[i*xs_i + j*xs_j + label[i]*xs_l] against y[i*ys_i + j*ys_j].  label (optional)
+ * masks rows with label <= 0 -- the reference's positive-row selection
+ * (anchor_head.py:126-128, bbox_head.py:71-76) -- and, with xs_l != 0, picks the labelled
+ * class's deltas (reg_out.view(-1, 4, C)[arange, :, label], bbox_head.py:70-72); labels
+ * >= n_sel make the sum NaN.  Backward writes only the selected unmasked elements of
+ * grad_x (zero-filled by the caller). */
+int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l,
+                          const float* y, int64_t ys_i, int64_t ys_j, const int64_t* label,
+                          int64_t n, int64_t m, int64_t n_sel, float beta, float* out,
+                          void* workspace, size_t ws_bytes, void* stream);
+int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l,
+                          const float* y, int64_t ys_i, int64_t ys_j, const int64_t* label,
+                          int64_t n, int64_t m, int64_t n_sel, float beta,
+                          const float* grad_out, float* grad_x, int64_t gs_i, int64_t gs_j,
+                          int64_t gs_l, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,15 @@ SIGNATURES = {
                                  c_vp]),
     'frh_atss_workspace': (c_size, [c_i32, c_i32, c_i32, c_i32, c_i64]),
     'frh_bn_act': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_i64, c_i32, c_vp]),
+    'frh_loss_workspace': (c_size, []),
+    'frh_cls_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,
+                                 c_size, c_vp]),
+    'frh_cls_loss_bwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,
+                                 c_i64, c_i64, c_vp]),
+    'frh_smooth_l1_fwd': (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
+                                  c_vp, c_vp, c_size, c_vp]),
+    'frh_smooth_l1_bwd': (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
+                                  c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     'frh_atss_assign': (c_i32, [c_i32, c_i32, P(c_i32), P(c_f32), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32,
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }

@@ -123,9 +123,13 @@ class AnchorHead(nn.Module):
         avg_factor = len(tar_labels) if sampling else pos.sum()
         if tar_labels.numel() != 0:
             cls_loss = self.loss_cls(tar_cls_out.t(), tar_labels) / avg_factor
-            m = pos.view(1, -1)
-            z = tar_reg_out.new_zeros(())
-            reg_loss = self.loss_bbox(torch.where(m, tar_reg_out, z), torch.where(m, tar_param, z)) / avg_factor
+            if isinstance(self.loss_bbox, losses.SmoothL1Loss):
+                # fused masked smooth-L1 over the positive columns of [4, S] (one kernel, no sync)
+                reg_loss = self.loss_bbox.masked(tar_reg_out, tar_param, tar_labels, rows_dim=1) / avg_factor
+            else:
+                m = pos.view(1, -1)
+                z = tar_reg_out.new_zeros(())
+                reg_loss = self.loss_bbox(torch.where(m, tar_reg_out, z), torch.where(m, tar_param, z)) / avg_factor
         else:
             logging.warning('%s recieved no samples to train, return dummy zero losses', type(self).__name__)
         return cls_loss, reg_loss

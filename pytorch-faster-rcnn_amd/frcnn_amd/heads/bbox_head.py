@@ -42,6 +42,13 @@ class BBoxHead(nn.Module):
             return cls_loss, reg_loss
         if tar_label.numel() != 0:
             cls_loss = self.loss_cls(cls_out, tar_label) / avg_factor
+            if isinstance(self.loss_bbox, losses.SmoothL1Loss):
+                # fused class selection + positive-row mask + smooth-L1 (one kernel each way)
+                if self.reg_class_agnostic:
+                    reg_loss = self.loss_bbox.masked(reg_out, tar_param.t(), tar_label, rows_dim=0)
+                else:
+                    reg_loss = self.loss_bbox.class_selected(reg_out, self.num_classes, tar_param.t(), tar_label)
+                return cls_loss, reg_loss / avg_factor
             if not self.reg_class_agnostic:
                 reg_out = reg_out.view(-1, 4, self.num_classes)
                 reg_out = reg_out[torch.arange(n, device=dev), :, tar_label]

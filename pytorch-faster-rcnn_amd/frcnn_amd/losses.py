@@ -1,15 +1,18 @@
-"""Detection losses (reference lib/losses.py), PyTorch autograd, sum reductions.
+"""Detection losses (reference lib/losses.py), sum reductions.
 
-These run after the HIP target kernels; fusing them into the gather kernels
-is SURVEY §8(f-1), the next row after the hot path.  Semantics follow the
-reference, including its quirk that FocalLoss ignores the configured
-alpha/gamma/loss_weight (losses.py:106-109).
+On HIP tensors FocalLoss, CrossEntropyLoss and SmoothL1Loss run the fused loss
+kernels (csrc/losses.hip): one streaming pass forward and one
+backward instead of a dozen elementwise torch passes.  The torch expressions
+below are the reference restatement; they serve CPU tensors and are the
+numerics reference of the GPU tests.  Semantics follow the reference, including
+its quirk that FocalLoss ignores the configured alpha/gamma/loss_weight
+(losses.py:106-109).
 """
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import utils
+from . import ops, utils
 
 
 def zero_loss(device):
@@ -60,6 +63,8 @@ class FocalLoss(nn.Module):
         self.alpha, self.gamma, self.loss_weight = 0.25, 2.0, 1.0  # reference ignores the cfg values
 
     def forward(self, pred, target):
+        if pred.is_cuda:
+            return self.loss_weight * ops.cls_loss(pred, target, ops.CLS_FOCAL, self.alpha, self.gamma)
         return self.loss_weight * sigmoid_focal_loss(pred, target, self.alpha, self.gamma)
 
 
@@ -69,7 +74,26 @@ class SmoothL1Loss(nn.Module):
         self.beta, self.loss_weight = beta, loss_weight
 
     def forward(self, x, y):
+        if x.is_cuda and x.dim() == 2:
+            return self.loss_weight * ops.smooth_l1_loss(x, y, self.beta)
         return self.loss_weight * smooth_l1_loss_v2(x, y, self.beta)
+
+    def masked(self, x, y, label, rows_dim=0):
+        """Sum over the rows with label > 0 only (the reference's positive-row selection,
+        anchor_head.py:126-128, without its boolean-index host sync)."""
+        if x.is_cuda:
+            return self.loss_weight * ops.smooth_l1_loss(x, y, self.beta, label, rows_dim)
+        m = (label > 0).view(-1, 1) if rows_dim == 0 else (label > 0).view(1, -1)
+        z = x.new_zeros(())
+        return self.loss_weight * smooth_l1_loss_v2(torch.where(m, x, z), torch.where(m, y, z), self.beta)
+
+    def class_selected(self, reg_out, num_classes, target, label):
+        """bbox_head.py:70-76: the labelled class's deltas of reg_out [n, 4*C] at the positive rows."""
+        if reg_out.is_cuda:
+            return self.loss_weight * ops.smooth_l1_class_select(reg_out, num_classes, target, label, self.beta)
+        n = len(label)
+        sel = reg_out.view(-1, 4, num_classes)[torch.arange(n), :, label]
+        return self.masked(sel, target, label, 0)
 
 
 class CrossEntropyLoss(nn.Module):
@@ -79,6 +103,13 @@ class CrossEntropyLoss(nn.Module):
 
     def forward(self, pred, label):
         c = pred.shape[1]
+        if pred.is_cuda:
+            if self.use_sigmoid:
+                kind = ops.CLS_SIGMOID_BCE
+                label = label.reshape(-1)  # C == 1: label.view(-1, 1).float() is the target itself
+            else:
+                kind = ops.CLS_SOFTMAX_CE
+            return ops.cls_loss(pred, label, kind) * self.loss_weight
         if self.use_sigmoid:
             if c == 1:
                 tgt = label.view(-1, 1).float()

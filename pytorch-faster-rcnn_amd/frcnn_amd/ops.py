@@ -617,3 +617,104 @@ def bn_act(x, bn, skip=None, relu=True):
             y = y + skip
         return torch.relu_(y) if relu else y
     return _FrozenBNAct.apply(x, skip, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu)
+
+
+# ---------------------------------------------------------------- f1: fused losses
+CLS_FOCAL, CLS_SIGMOID_BCE, CLS_SOFTMAX_CE = 0, 1, 2
+
+
+class _ClsLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target, kind, alpha, gamma):
+        n, c = x.shape
+        tfloat = int(target.dtype == torch.float32)
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = workspace(_lib.query('frh_loss_workspace'), x.device)
+        call('frh_cls_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
+             float(gamma), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+        ctx.save_for_backward(x, target)
+        ctx.cfg = (kind, tfloat, alpha, gamma)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, target = ctx.saved_tensors
+        kind, tfloat, alpha, gamma = ctx.cfg
+        n, c = x.shape
+        gx = torch.empty_like(x)
+        g = _f32(g).contiguous()
+        call('frh_cls_loss_bwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
+             float(gamma), ptr(g), ptr(gx), gx.stride(0), gx.stride(1), stream_of(x))
+        return gx, None, None, None, None
+
+
+def cls_loss(x, target, kind, alpha=0.25, gamma=2.0):
+    """Summed classification loss of logits x [n, C] (any strides) against target [n]
+    (frh_cls_loss_fwd/bwd; kinds CLS_FOCAL / CLS_SIGMOID_BCE / CLS_SOFTMAX_CE)."""
+    _need_cuda(x, target)
+    if x.dim() != 2 or target.dim() != 1 or target.shape[0] != x.shape[0]:
+        raise AssertionError('cls_loss: x [n, C] and target [n] expected')
+    if target.is_floating_point():
+        target = target.float()
+        if x.shape[1] != 1 or kind != CLS_SIGMOID_BCE:
+            raise AssertionError('cls_loss: float targets only for single-channel sigmoid BCE')
+    elif target.dtype != torch.int64:
+        target = target.long()
+    return _ClsLoss.apply(_f32(x), target.contiguous(), int(kind), alpha, gamma)
+
+
+class _SmoothL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, label, xs, ys, n, m, n_sel, beta):
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = workspace(_lib.query('frh_loss_workspace'), x.device)
+        call('frh_smooth_l1_fwd', ptr(x), xs[0], xs[1], xs[2], ptr(y), ys[0], ys[1], ptr(label), n, m, n_sel,
+             float(beta), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+        ctx.save_for_backward(x, y, label)
+        ctx.cfg = (xs, ys, n, m, n_sel, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, label = ctx.saved_tensors
+        xs, ys, n, m, n_sel, beta = ctx.cfg
+        gx = torch.zeros_like(x)
+        if gx.stride() != x.stride():
+            raise AssertionError('smooth_l1: gradient layout differs from the input')
+        g = _f32(g).contiguous()
+        call('frh_smooth_l1_bwd', ptr(x), xs[0], xs[1], xs[2], ptr(y), ys[0], ys[1], ptr(label), n, m, n_sel,
+             float(beta), ptr(g), ptr(gx), xs[0], xs[1], xs[2], stream_of(x))
+        return gx, None, None, None, None, None, None, None, None
+
+
+def smooth_l1_loss(x, y, beta, label=None, rows_dim=0):
+    """Summed smooth_l1_loss_v2 of x and y (same shape, 2-D, rows along `rows_dim`),
+    counting only rows whose label is > 0 when `label` is given (frh_smooth_l1_fwd/bwd)."""
+    _need_cuda(x, y, label)
+    if x.shape != y.shape or x.dim() != 2:
+        raise AssertionError('smooth_l1_loss: x and y must be equal 2-D shapes')
+    x, y = _f32(x), _f32(y)
+    if not (x.is_contiguous() or x.t().is_contiguous()):
+        x = x.contiguous()  # the zero-filled gradient must share x's strides
+    cd = 1 - rows_dim
+    n, m = x.shape[rows_dim], x.shape[cd]
+    if label is not None and label.numel() != n:
+        raise AssertionError('smooth_l1_loss: one label per row expected')
+    lab = label.contiguous().long() if label is not None else None
+    return _SmoothL1.apply(x, y, lab, (x.stride(rows_dim), x.stride(cd), 0), (y.stride(rows_dim), y.stride(cd)), n, m,
+                           1, beta)
+
+
+def smooth_l1_class_select(reg_out, num_classes, target, label, beta):
+    """BBoxHead's regression loss: reg_out [n, 4*C] viewed [n, 4, C], the labelled class's
+    deltas of the positive rows against target [n, 4] (any strides), summed."""
+    _need_cuda(reg_out, target, label)
+    n = reg_out.shape[0]
+    if reg_out.dim() != 2 or reg_out.shape[1] != 4 * num_classes or target.shape != (n, 4) or label.numel() != n:
+        raise AssertionError('smooth_l1_class_select: shape mismatch')
+    reg_out, target = _f32(reg_out), _f32(target)
+    if reg_out.stride(1) != 1:
+        reg_out = reg_out.contiguous()
+    xs = (reg_out.stride(0), num_classes, 1)
+    return _SmoothL1.apply(reg_out, target, label.contiguous().long(), xs, (target.stride(0), target.stride(1)), n, 4,
+                           num_classes, beta)

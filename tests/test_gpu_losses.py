@@ -1,0 +1,134 @@
+"""Fused loss kernels (csrc/losses.hip) against the torch fp32 restatement
+of lib/losses.py (frcnn_amd.losses' eager functions, the same expressions as the
+reference), forward sums and gradients.  Floating point: sums within rtol 2e-5 (reduction
+order differs), gradients within rtol 1e-4 / atol 1e-6."""
+import pytest
+import torch
+
+from frcnn_amd import losses, ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+
+
+def _labels(n, hi, pos_frac, gen):
+    lab = torch.randint(1, hi + 1, (n,), generator=gen)
+    lab[torch.rand(n, generator=gen) > pos_frac] = 0
+    return lab
+
+
+def _check(fused_fn, eager_fn, x0, scale=0.37):
+    xa = x0.clone().to(DEV).requires_grad_(True)
+    xb = x0.clone().to(DEV).requires_grad_(True)
+    la, lb = fused_fn(xa), eager_fn(xb)
+    torch.testing.assert_close(la, lb, rtol=2e-5, atol=1e-6)
+    (la * scale).backward()
+    (lb * scale).backward()
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('layout', ['rows', 'channel_major'])
+def test_focal_loss(layout):
+    g = torch.Generator().manual_seed(1)
+    n, c = 6000, 20
+    lab = _labels(n, c, 0.05, g).to(DEV)
+    x0 = torch.randn(n, c, generator=g) * 3
+    if layout == 'rows':
+        _check(lambda x: ops.cls_loss(x, lab, ops.CLS_FOCAL), lambda x: losses.sigmoid_focal_loss(x, lab), x0)
+    else:  # AnchorHead passes tar_cls_out.t(): a [C, S] tensor viewed [S, C]
+        xt = x0.t().contiguous()
+        _check(lambda x: ops.cls_loss(x.t(), lab, ops.CLS_FOCAL), lambda x: losses.sigmoid_focal_loss(x.t(), lab), xt)
+
+
+def test_focal_loss_module_dispatch():
+    g = torch.Generator().manual_seed(2)
+    x = (torch.randn(300, 20, generator=g) * 2).to(DEV)
+    lab = _labels(300, 20, 0.3, g).to(DEV)
+    torch.testing.assert_close(losses.FocalLoss()(x, lab), losses.sigmoid_focal_loss(x, lab), rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('c', [1, 20])
+def test_sigmoid_bce(c):
+    g = torch.Generator().manual_seed(3 + c)
+    n = 4096
+    lab = (torch.rand(n, generator=g) < 0.3).long() if c == 1 else _labels(n, c, 0.2, g)
+    lab = lab.to(DEV)
+    x0 = torch.randn(n, c, generator=g) * 4
+    eager = losses.CrossEntropyLoss(use_sigmoid=True)
+    cpu_ref = lambda x: eager(x.cpu(), lab.cpu()).to(DEV)  # the module's torch path runs for CPU tensors
+    _check(lambda x: losses.CrossEntropyLoss(use_sigmoid=True)(x, lab), cpu_ref, x0)
+
+
+def test_sigmoid_bce_float_targets():
+    # FCOS centerness: CrossEntropyLoss(use_sigmoid=True) on [n, 1] logits vs float targets
+    g = torch.Generator().manual_seed(5)
+    n = 777
+    t = torch.rand(n, generator=g).to(DEV)
+    x0 = torch.randn(n, 1, generator=g)
+    ref = lambda x: torch.nn.functional.binary_cross_entropy_with_logits(x, t.view(-1, 1), reduction='none').sum()
+    _check(lambda x: losses.CrossEntropyLoss(use_sigmoid=True)(x, t), ref, x0)
+
+
+def test_softmax_ce():
+    g = torch.Generator().manual_seed(6)
+    n, c = 1024, 21
+    lab = _labels(n, c - 1, 0.25, g).to(DEV)
+    x0 = torch.randn(n, c, generator=g) * 3
+    ref = lambda x: torch.nn.functional.cross_entropy(x, lab, reduction='none').sum()
+    _check(lambda x: losses.CrossEntropyLoss()(x, lab), ref, x0)
+
+
+def test_smooth_l1_masked_columns():
+    # AnchorHead: tar_reg_out / tar_param [4, S], positives by column
+    g = torch.Generator().manual_seed(7)
+    s = 512
+    lab = _labels(s, 1, 0.3, g).to(DEV)
+    y = (torch.randn(4, s, generator=g) * 0.2).to(DEV)
+    x0 = torch.randn(4, s, generator=g) * 0.2
+    m = (lab > 0).view(1, -1)
+    beta = 1.0 / 9.0
+    ref = lambda x: losses.smooth_l1_loss_v2(torch.where(m, x, x.new_zeros(())), torch.where(m, y, y.new_zeros(())),
+                                             beta)
+    _check(lambda x: losses.SmoothL1Loss(beta).masked(x, y, lab, rows_dim=1), ref, x0)
+
+
+def test_smooth_l1_unmasked():
+    g = torch.Generator().manual_seed(8)
+    y = torch.randn(300, 4, generator=g).to(DEV)
+    x0 = torch.randn(300, 4, generator=g)
+    _check(lambda x: losses.SmoothL1Loss(0.5)(x, y), lambda x: losses.smooth_l1_loss_v2(x, y, 0.5), x0)
+
+
+def test_smooth_l1_class_select():
+    # BBoxHead: reg_out [n, 4*C] viewed [n, 4, C], labelled class, positive rows, target tar_param.t()
+    g = torch.Generator().manual_seed(9)
+    n, c = 1024, 21
+    lab = _labels(n, c - 1, 0.25, g).to(DEV)
+    tp = (torch.randn(4, n, generator=g) * 0.5).to(DEV)
+    x0 = torch.randn(n, 4 * c, generator=g) * 0.5
+
+    def ref(x):
+        sel = x.view(-1, 4, c)[torch.arange(n, device=DEV), :, lab]
+        m = (lab > 0).view(-1, 1)
+        z = x.new_zeros(())
+        return losses.smooth_l1_loss_v2(torch.where(m, sel, z), torch.where(m, tp.t(), z), 1.0)
+
+    _check(lambda x: losses.SmoothL1Loss(1.0).class_selected(x, c, tp.t(), lab), ref, x0)
+
+
+def test_empty_inputs():
+    x = torch.zeros(0, 20, device=DEV, requires_grad=True)
+    lab = torch.zeros(0, dtype=torch.long, device=DEV)
+    loss = ops.cls_loss(x, lab, ops.CLS_FOCAL)
+    assert float(loss) == 0.0
+    loss.backward()
+    assert x.grad.shape == (0, 20)
+    y = torch.zeros(4, 0, device=DEV)
+    assert float(losses.SmoothL1Loss(1.0).masked(torch.zeros(4, 0, device=DEV), y, lab, rows_dim=1)) == 0.0
+
+
+def test_bad_label_gives_nan():
+    # a softmax label outside [0, C) poisons the sum instead of reading out of bounds
+    x = torch.randn(8, 5, device=DEV)
+    lab = torch.tensor([0, 1, 2, 3, 4, 5, 0, 1], device=DEV)
+    assert torch.isnan(ops.cls_loss(x, lab, ops.CLS_SOFTMAX_CE))
