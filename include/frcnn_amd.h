@@ -352,6 +352,22 @@ int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
                           const float* grad_out, float* grad_x, int64_t gs_i, int64_t gs_j,
                           int64_t gs_l, void* stream);
 
+/* ---------------------------------------------------------------- f4: image pipeline
+ * The train/test pipelines of configs/faster_rcnn_r50_fpn.py:120-139 (mmdet v1: Resize
+ * keep_ratio -> RandomFlip -> Normalize -> Pad(size_divisor) -> DefaultFormatBundle ->
+ * collate), fused: src holds uint8 HWC 3-channel images (image b at byte offset
+ * src_offsets[b], size src_hw[2b..2b+1] = h, w; host arrays); each is resized to
+ * dst_hw[b] with cv2.resize INTER_LINEAR's fixed-point arithmetic (exact 2x downscale:
+ * INTER_AREA), flipped horizontally when flip[b] (may be NULL), normalised
+ * (v - mean[c]) / std[c] in f32 (channels reversed first when to_rgb), and written to
+ * dst [batch][3][out_h][out_w] f32 with zeros outside [0, dst_h) x [0, dst_w).  The host
+ * side (lib-mirror frcnn_amd.datasets) computes the sizes, scale factors, box transforms
+ * and img_meta exactly as mmcv/mmdet do. */
+int32_t frh_image_preprocess(const uint8_t* src, int32_t batch, const int64_t* src_offsets,
+                             const int32_t* src_hw, const int32_t* dst_hw, const int32_t* flip,
+                             const float* mean, const float* std, int32_t to_rgb, float* dst,
+                             int32_t out_h, int32_t out_w, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

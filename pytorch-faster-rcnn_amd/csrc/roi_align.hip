@@ -1426,7 +1426,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   // grouped kernel when the workspace allows it (frh_roi_align_fwd_ws)
   if (variant == -2) variant = grp_ok ? 50 : -1;
   if (variant < 0) variant = f.lds ? 10 : 0;
-  FRH_REQUIRE(variant == 0 || (variant == 10 && f.lds) || ((variant == 50 || variant == 51) && grp_ok),
+  FRH_REQUIRE(variant == 0 || ((variant >= 10 && variant <= 12) && f.lds) || ((variant == 50 || variant == 51) && grp_ok),
               "roi_align variant %d unsupported here", variant);
   if (variant == 50 || variant == 51) {
     int32_t* order = static_cast<int32_t*>(workspace);
@@ -1446,9 +1446,15 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_group_kernel<4>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
     else
       hipLaunchKernelGGL(roi_align_fwd_group_kernel<1>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
-  } else if (variant == 10) {
+  } else if (variant >= 10 && variant <= 12) {
+    // 10: windows <= 256 floats staged (default); 11 / 12: stage up to 512 / 1024 (experiments)
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    if (variant == 10)
+      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 11)
+      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<512>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<1024>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   } else {
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
