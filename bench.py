@@ -34,7 +34,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-CONFIG = os.path.join(REPO, 'pytorch-faster-rcnn_amd', 'configs', 'faster_rcnn_r50_fpn.py')
+CONFIG_DIR = os.path.join(REPO, 'pytorch-faster-rcnn_amd', 'configs')
+CONFIG = os.path.join(CONFIG_DIR, 'faster_rcnn_r50_fpn.py')
+# --config choices (BASELINE configs 1-5) -> model name used in the metric string
+CONFIG_NAMES = {'faster_rcnn_r50_fpn': 'FasterRCNN_R50_FPN', 'faster_rcnn_r50': 'FasterRCNN_R50_C4',
+                'retinanet_r50_fpn': 'RetinaNet_R50_FPN', 'cascade_rcnn_r50_fpn': 'CascadeRCNN_R50_FPN',
+                'fcos_r50_fpn_atss': 'ATSS_R50_FPN'}
 IMG_SHAPE, PAD_SHAPE = (600, 1000), (608, 1024)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -134,10 +139,14 @@ def main():
     ap.add_argument('--mode', default='fwd', choices=['fwd', 'train'],
                     help='fwd: forward+loss (the BASELINE metric); train: forward+loss+backward with the '
                          'DDP gradient all-reduce (RCCL) + grad clip + SGD step (frcnn_amd.train)')
+    ap.add_argument('--config', default='faster_rcnn_r50_fpn', choices=sorted(CONFIG_NAMES),
+                    help='model config (the BASELINE metric is faster_rcnn_r50_fpn; others are extra lines)')
     ap.add_argument('--bucket-mb', type=float, default=None, help='DDP all-reduce bucket size (train mode)')
-    ap.add_argument('--no-conv-search', dest='conv_search', action='store_false',
-                    help='keep MIOpen\'s heuristic convolution algorithms instead of benchmarking them in the '
-                         'warmup (torch.backends.cudnn.benchmark; +5.8%% img/s on cfg2, ~1 min of search)')
+    ap.add_argument('--conv-search', default='auto', choices=['auto', 'on', 'off'],
+                    help='benchmark MIOpen convolution algorithms in the warmup (torch.backends.cudnn.benchmark; '
+                         '+5.8%% img/s on cfg2 fwd, ~1 min of search).  auto = on for fwd, off for train (the '
+                         'backward-convolution search takes several minutes)')
+    ap.add_argument('--no-conv-search', dest='conv_search', action='store_const', const='off')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -152,8 +161,11 @@ def main():
     frcnn_amd.set_sampler_mode(args.sampler, seed=1234 + rank)
     np.random.seed(rank)
 
-    torch.backends.cudnn.benchmark = bool(args.conv_search)
-    model, cfg = make_model(dev, seed=0)
+    if args.conv_search == 'auto':
+        args.conv_search = 'on' if args.mode == 'fwd' else 'off'
+    args.conv_search = args.conv_search == 'on'
+    torch.backends.cudnn.benchmark = args.conv_search
+    model, cfg = make_model(dev, seed=0, config=os.path.join(CONFIG_DIR, args.config + '.py'))
     batch = make_batch(dev, args.batch, seed=0, rank=rank)
 
     if args.mode == 'train':
@@ -232,7 +244,7 @@ def main():
     if rank == 0:
         imgs_total = world * args.batch * args.steps
         out = {
-            'metric': 'img/s FasterRCNN_R50_FPN 1000x600 ' + ('fwd+loss' if args.mode == 'fwd' else
+            'metric': 'img/s ' + CONFIG_NAMES[args.config] + ' 1000x600 ' + ('fwd+loss' if args.mode == 'fwd' else
                                                                'train step (fwd+loss+bwd+allreduce+SGD)'),
             'value': imgs_total / t_max,
             'unit': 'img/s',
@@ -245,7 +257,8 @@ def main():
             'vs_baseline': None,
             'dtype': 'f32',
             'data': 'synthetic images N(0,1) [B,3,608,1024], VOC07 trainval gt boxes, random-init weights',
-            'config': {'workload': 'configs/faster_rcnn_r50_fpn.py (BASELINE config 2) forward_train',
+            'config': {'workload': 'configs/{}.py{} forward_train'.format(
+                           args.config, ' (BASELINE config 2)' if args.config == 'faster_rcnn_r50_fpn' else ''),
                        'conv_algorithms': 'MIOpen benchmarked (warmup)' if args.conv_search else 'MIOpen heuristic',
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
@@ -259,7 +272,9 @@ def main():
                                    'pair on their stream; traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '
                                    'launch, profiles/roi_align_pmc.json'},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not recs:
+            out['roofline'] = None  # no RoIAlign on this model's path
+        if not args.no_cpu_baseline and world == 1 and args.config == 'faster_rcnn_r50_fpn':
             try:
                 out['cpu_baseline'] = cpu_baseline(0, args.cpu_baseline_seconds)
             except Exception as e:  # the baseline must never hide the GPU number
