@@ -361,7 +361,7 @@ def _rois(seed, n, batch):
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
 def test_roi_align_forward_kernels_identical(dev, layout):
-    """Every forward kernel (0 direct, 10 per-RoI LDS = default, 50 grouped union staging)
+    """Every forward kernel (0 direct, 10 per-RoI LDS, 20 channel-pair, 30 wide-staged, 50 grouped union staging)
     against the oracle and bit-identical to each other; P2-sized maps and 600 RoIs so the
     grouped kernel takes both its union path and its per-RoI fallback (large windows)."""
     from frcnn_amd import ops
@@ -375,9 +375,10 @@ def test_roi_align_forward_kernels_identical(dev, layout):
     if layout == 'nhwc':  # no 16-B staging: unit-stride rows are required
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
     outs = {v: ops.roi_align_variant(v, ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
-            for v in (0, 10, 50)}
+            for v in ((0, 10, 20, 30, 50) if layout == 'nchw' else (0, 10, 20, 50))}
     np.testing.assert_allclose(outs[0], ref, rtol=1e-5, atol=1e-5)
-    assert np.array_equal(outs[10], outs[0]) and np.array_equal(outs[50], outs[0])
+    for v in outs:
+        assert np.array_equal(outs[v], outs[0]), 'variant %d differs' % v
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])

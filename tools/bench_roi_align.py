@@ -44,6 +44,8 @@ def main():
     ap.add_argument('--variants', default='0,10,50')
     ap.add_argument('--calib', action='store_true', help='known-byte FETCH_SIZE calibration launches only')
     ap.add_argument('--calib-small', action='store_true', help='calibration on the staged (small-window) path')
+    ap.add_argument('--sort', action='store_true',
+                    help='order the RoIs by (image, level, 64-px tile) first (spatial locality experiment)')
     ap.add_argument('--dump', help='save the RoIs / levels / level shapes of the recorded launch to this .npz')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
@@ -58,6 +60,12 @@ def main():
     rec = ops.ROI_ALIGN_PROFILE['records'][-1]
     _, _, rois, levels, shapes, (ph, pw), feats, scales, sr = rec
     nbytes = bench.roi_align_bytes(rec)
+    if args.sort:
+        rr = rois.cpu().numpy()
+        cx, cy = (rr[:, 1] + rr[:, 3]) / 2, (rr[:, 2] + rr[:, 4]) / 2
+        key = ((rr[:, 0].astype(np.int64) * 8 + levels.cpu().numpy()) * 64 + (cy // 64).astype(np.int64)) * 64 + (cx // 64)
+        perm = torch.from_numpy(np.argsort(key, kind='stable')).to(dev)
+        rois, levels = rois[perm].contiguous(), levels[perm].contiguous()
     lv = levels.cpu().numpy()
     r = rois.cpu().numpy()
     side = np.sqrt((r[:, 3] - r[:, 1] + 1) * (r[:, 4] - r[:, 2] + 1))
@@ -73,7 +81,7 @@ def main():
     wsp = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
     for spec in args.variants.split(','):
         v = int(spec)
-        full = torch.zeros(K * C * ph * pw + (8 * 4096 * 8 if v == 51 else 0), device=dev)  # 51: stamps after
+        full = torch.zeros(K * C * ph * pw + (8 * 4096 * 8 if v in (24, 51) else 0), device=dev)  # stamps after
         out = full[:K * C * ph * pw].view(K, C, ph, pw)
 
         def launch():
@@ -91,6 +99,18 @@ def main():
             ts.append((e0, e1))
         torch.cuda.synchronize()
         ms = np.array([a.elapsed_time(b) for a, b in ts])
+        if v == 24:  # per-wave stamps [start, setup, ready0, done0, ready1, end, D, roi] (100 MHz)
+            st = full[K * C * ph * pw:].view(torch.int64)[:K * 8 * 8].view(-1, 8).cpu().numpy()
+            st = st[st[:, 0] > 0]
+            t0 = st[:, 0].min()
+            print('  {} waves; span {:.1f} us'.format(len(st), (st[:, 5].max() - t0) / 100.0))
+            for D in sorted(set(st[:, 6].tolist())):
+                m = st[:, 6] == D
+                x = st[m]
+                ph_ = lambda a, b: np.percentile((x[:, b] - x[:, a]) / 100.0, [50, 90]).round(2).tolist()
+                print('  D={} waves {:5d}: start p50/90 {} setup {} wait0 {} eval0 {} wait1 {} total {}'.format(
+                    D, m.sum(), np.percentile((x[:, 0] - t0) / 100.0, [50, 90]).round(1).tolist(), ph_(0, 1),
+                    ph_(1, 2), ph_(2, 3), ph_(3, 4), ph_(0, 5)), flush=True)
         if v == 51:  # per-workgroup stamps [start, union, end, path | U << 8] (s_memrealtime, 100 MHz)
             allst = full[K * C * ph * pw:].view(torch.int64)
             steps = allst[8192:8192 + 128 * 20 * 4].view(64, 2, 20, 4).cpu().numpy()
