@@ -93,6 +93,47 @@ def roi_align_bytes(rec):
     return 4 * C * (K * ph * pw + feat_elems) + 20 * K
 
 
+def nms_roofline(recs, dev):
+    """The timed steps' RPN NMS calls (all images x levels per call: mask + scan kernels)
+    replayed back to back between one HIP event pair on their stream, with preallocated
+    outputs; algorithmic bytes per ops.nms_bytes.  NMS at RPN sizes is
+    latency-bound (greedy scan), so the fraction is reported next to the microseconds."""
+    if not recs:
+        return None
+    from frcnn_amd import ops, _lib
+    outs = []
+    for ws, rows, cnt, P, thr, max_keep in recs:
+        S = rows.shape[0]
+        keep = torch.empty(S, P, dtype=torch.int32, device=dev)
+        kc = torch.empty(S, dtype=torch.int32, device=dev)
+        nws = _lib.workspace(_lib.query('frh_nms_workspace', S, P), dev)
+        outs.append((rows, cnt, P, thr, max_keep, keep, kc, nws))
+
+    def launch(o):
+        rows, cnt, P, thr, max_keep, keep, kc, nws = o
+        _lib.call('frh_nms_sorted', rows.shape[0], _lib.ptr(rows), rows.stride(0), _lib.ptr(cnt), P, thr, max_keep,
+                  _lib.ptr(keep), keep.stride(0), _lib.ptr(kc), _lib.ptr(nws), nws.numel(), _lib.stream_of(rows))
+    for o in outs[:2]:
+        launch(o)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for o in outs:
+        launch(o)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / len(outs)
+    nbytes = float(np.mean([ops.nms_bytes(o[1], o[6]) for o in outs]))
+    achieved = nbytes / (us * 1e-6) / 1e9
+    segs = outs[0][0].shape[0]
+    return {'kernel': 'nms_mask_kernel + nms_scan_pipe_kernel<1> (RPN, {} segments of <= {} boxes)'.format(
+                segs, outs[0][2]),
+            'bound': 'latency (greedy scan); hbm for the mask', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'avg_call_us': us,
+            'algorithmic_bytes_per_call': nbytes, 'calls': len(outs),
+            'timing': 'the timed steps\' RPN NMS calls replayed back to back between one HIP event pair'}
+
+
 def cpu_baseline(seed, max_s):
     """Same forward+loss on the host: torch CPU convs + the oracle's C hot path, 1 image."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -206,6 +247,8 @@ def main():
 
     ops.ROI_ALIGN_PROFILE['records'].clear()
     ops.ROI_ALIGN_PROFILE['on'] = True
+    ops.NMS_PROFILE['records'].clear()
+    ops.NMS_PROFILE['on'] = True
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -213,6 +256,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     ops.ROI_ALIGN_PROFILE['on'] = False
+    ops.NMS_PROFILE['on'] = False
     assert torch.isfinite(loss).all()
 
     t_max = max_over_ranks(elapsed, dev, world)
@@ -235,6 +279,9 @@ def main():
         avg_ms = r0.elapsed_time(r1) / len(recs)
     avg_bytes = float(np.mean(bytes_per)) if bytes_per else float('nan')
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if ms else None
+
+    nms_line = nms_roofline(ops.NMS_PROFILE['records'], dev)
+    ops.NMS_PROFILE['records'].clear()
 
     traffic = None
     pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json')
@@ -274,6 +321,8 @@ def main():
         }
         if not recs:
             out['roofline'] = None  # no RoIAlign on this model's path
+        if nms_line:
+            out['nms'] = nms_line
         if not args.no_cpu_baseline and world == 1 and args.config == 'faster_rcnn_r50_fpn':
             try:
                 out['cpu_baseline'] = cpu_baseline(0, args.cpu_baseline_seconds)

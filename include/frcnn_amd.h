@@ -207,6 +207,13 @@ int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* con
                           float* out_scores, int32_t* out_counts, void* workspace,
                           size_t ws_bytes, void* stream);
 
+/* Measurement hook: byte offsets in the frh_rpn_proposals workspace of its per-level
+ * NMS input (out[0] boxes [S, P, 4] in descending-score order, out[1] counts [S]
+ * int32), out[2] = P, out[3] = S = num_imgs * num_levels.  bench.py replays that
+ * NMS alone for its roofline line. */
+int32_t frh_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_levels, const int32_t* grid_hw,
+                                   int32_t num_anchors, int32_t pre_nms, int64_t* out);
+
 /* ---- a10: torchvision.ops.nms on pre-sorted segments --------------------------
  * boxes [S, n_max, 4] row-major xyxy, already in descending-score order
  * (stable); count[s] valid rows.  keep[s, :] = kept row positions (ascending

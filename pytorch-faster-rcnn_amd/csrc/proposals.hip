@@ -264,6 +264,20 @@ extern "C" size_t frh_rpn_proposals_workspace(int32_t num_imgs, int32_t num_leve
   return prop_layout(num_imgs, num_levels, grid_hw, num_anchors, pre_nms).total;
 }
 
+// Where frh_rpn_proposals leaves its per-level NMS input in the workspace (measurement:
+// bench.py replays that NMS alone).  out = {boxes byte offset ([S, P, 4] f32, rows in
+// descending-score order), counts byte offset ([S] int32), P, S}.
+extern "C" int32_t frh_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_levels, const int32_t* grid_hw,
+                                              int32_t num_anchors, int32_t pre_nms, int64_t* out) {
+  FRH_REQUIRE(num_imgs >= 1 && num_levels >= 1 && grid_hw && out, "bad arguments");
+  const PropLayout z = prop_layout(num_imgs, num_levels, grid_hw, num_anchors, pre_nms);
+  out[0] = (int64_t)z.boxes;
+  out[1] = (int64_t)z.cnt;
+  out[2] = z.P;
+  out[3] = (int64_t)num_imgs * num_levels;
+  return FRH_OK;
+}
+
 extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                      const float* const* reg_ptrs, const int32_t* grid_hw, int32_t num_anchors,
                                      int32_t cls_channels, const float* anchors, int64_t anchor_ld,

@@ -383,8 +383,10 @@ constexpr int kWinR = kWinMax / kWave;
 
 // kChunk: channels per workgroup (kChunk / 4 per wave).  kSkip (diagnostics only):
 // 1 = skip staged RoIs, 2 = skip gathered ones.
-template <int kStageMax, int kSkip = 0, int kChunk = kRoiChanChunk>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
+// kWpe: minimum waves per SIMD the register allocation must allow (0: compiler's choice).
+template <int kStageMax, int kSkip = 0, int kChunk = kRoiChanChunk, int kWpe = 0>
+__global__ void __launch_bounds__(kRoiThreads) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
+roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
                                                                         float* __restrict__ out) {
   constexpr int SR = 2;
   __shared__ float slab_all[kRoiThreads / kWave][kWinMax];
@@ -1031,8 +1033,9 @@ constexpr int kX4Slab = 2048;  // floats per wave: 8 quads per lane
 
 // kXcd: XCD x (= linear block id % 8) takes the x-th contiguous eighth of the
 // (RoI, chunk) items, so RoIs that are neighbours in the input order share an L2.
-template <int kSkip = 0, bool kXcd = false>
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_x4_kernel(RoiLevels lv, RoiCfg c,
+template <int kSkip = 0, bool kXcd = false, int kWpe = 0>
+__global__ void __launch_bounds__(kRoiThreads) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
+roi_align_fwd_x4_kernel(RoiLevels lv, RoiCfg c,
                                                                        float* __restrict__ out) {
   constexpr int SR = 2;
   constexpr int kWC = kRoiChanChunk / (kRoiThreads / kWave);  // 16 channels per wave
@@ -1857,8 +1860,8 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   const bool pair_ok = f.lds && channels % 2 == 0 && 4 * pooled_h <= kWave && 4 * pooled_w <= kWave &&
                        4 * pooled_h * (4 * pooled_w + 1) <= PairLayout<1>::kCells;
-  FRH_REQUIRE(variant == 0 || ((variant >= 10 && variant <= 14) && f.lds) || ((variant == 50 || variant == 51) && grp_ok) ||
-                  (variant >= 20 && variant <= 24 && pair_ok) || (variant >= 30 && variant <= 35 && x4_ok),
+  FRH_REQUIRE(variant == 0 || ((variant >= 10 && variant <= 16) && f.lds) || ((variant == 50 || variant == 51) && grp_ok) ||
+                  (variant >= 20 && variant <= 24 && pair_ok) || (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   if (variant == 50 || variant == 51) {
     int32_t* order = static_cast<int32_t*>(workspace);
@@ -1888,10 +1891,16 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_pair_kernel<1>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
     else
       hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, true>), grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
-  } else if (variant >= 30 && variant <= 35) {  // diagnostics: 31 / 32 skip large / small windows, 33 no stores, 34 no evaluation
+  } else if (variant >= 30 && variant <= 37) {  // diagnostics: 31 / 32 skip large / small windows, 33 no stores, 34 no evaluation
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     if (variant == 30)
       hipLaunchKernelGGL(roi_align_fwd_x4_kernel<0>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 36)  // occupancy: registers for 8 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, false, 8>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
+                         out);
+    else if (variant == 37)  // occupancy: registers for 6 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, false, 6>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
+                         out);
     else if (variant == 35)
       hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, true>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else if (variant == 33)
@@ -1902,11 +1911,17 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_x4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else
       hipLaunchKernelGGL(roi_align_fwd_x4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  } else if (variant >= 10 && variant <= 14) {
+  } else if (variant >= 10 && variant <= 16) {
     // 10: windows <= 256 floats staged (default); 11 / 12: stage up to 512 / 1024 (experiments)
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     if (variant == 10)
       hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 15)  // occupancy: registers for 8 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, kRoiChanChunk, 8>), grid, dim3(kRoiThreads), 0,
+                         as_stream(stream), lv, c, out);
+    else if (variant == 16)  // occupancy: registers for 6 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, kRoiChanChunk, 6>), grid, dim3(kRoiThreads), 0,
+                         as_stream(stream), lv, c, out);
     else if (variant == 13)  // diagnostics: gathered (large-window) RoIs only
       hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 1>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else if (variant == 14)  // diagnostics: staged (small-window) RoIs only

@@ -53,6 +53,7 @@ SIGNATURES = {
     'frh_param2bbox': (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, P(c_f32), P(c_f32), c_i32, c_f32, c_f32,
                                c_vp, c_i64, c_vp]),
     'frh_rpn_proposals_workspace': (c_size, [c_i32, c_i32, P(c_i32), c_i32, c_i32]),
+    'frh_rpn_proposals_nms_view': (c_i32, [c_i32, c_i32, P(c_i32), c_i32, c_i32, P(ctypes.c_int64)]),
     'frh_rpn_proposals': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i32), c_i32, c_i32, c_vp, c_i64,
                                   P(c_f32), P(c_f32), P(c_f32), P(c_f32), c_i32, c_i32, c_i32, c_f64, c_vp,
                                   c_vp, c_vp, c_vp, c_size, c_vp]),

@@ -6,6 +6,8 @@ The reference-API modules (anchor, region, bbox, utils, heads) are built on
 these.  The torchvision drop-ins the reference imports (`nms`, `roi_align`,
 `RoIAlign`, `RoIPool`) live here too.
 """
+import ctypes
+
 import numpy as np
 import torch
 from torch import nn
@@ -348,7 +350,24 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
          f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
          int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(),
          stream_of(boxes))
+    if NMS_PROFILE['on']:  # keep this call's per-level NMS input (in the workspace) for a replay
+        view = (ctypes.c_int64 * 4)()
+        call('frh_rpn_proposals_nms_view', B, L, grid_a, num_anchors, int(pre_nms), view)
+        o_box, o_cnt, P_, S_ = list(view)
+        rows = ws[o_box:o_box + S_ * P_ * 16].view(torch.float32).view(S_, P_, 4)
+        cnt = ws[o_cnt:o_cnt + 4 * S_].view(torch.int32)
+        NMS_PROFILE['records'].append((ws, rows, cnt, P_, float(nms_iou), int(post_nms) if post_nms > 0 else -1))
     return boxes, scores, counts
+
+
+NMS_PROFILE = {'on': False, 'records': []}
+
+
+def nms_bytes(counts, kept):
+    """Algorithmic bytes of one segmented NMS call: per segment of N boxes
+    20*N + 16*N*ceil(N/64) + 8*K_keep (boxes + scores read, 64-bit mask written and read once)."""
+    n = counts.long()
+    return int((20 * n + 16 * n * ((n + 63) // 64) + 8 * kept.long()).sum())
 
 
 # ---------------------------------------------------------------- NMS (a10)
