@@ -282,6 +282,20 @@ int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, const float* grad_out, void* stream);
 
+/* Tiled gather backward (sampling_ratio 2, pooled_h * pooled_w <= 64): the same
+ * gradient as frh_roi_align_bwd_strided without global atomics.  OVERWRITES every
+ * cell of grad_feats (no need to clear it first).  Workspace: caller-allocated,
+ * frh_roi_align_bwd_workspace bytes (tile lists over 16x16-cell tiles). */
+size_t frh_roi_align_bwd_workspace(int32_t num_levels, const int32_t* feat_hw, int32_t batch,
+                                   int64_t num_rois);
+int32_t frh_roi_align_bwd_tiled(int32_t num_levels, float* const* grad_feats,
+                                const int32_t* feat_hw, const int64_t* strides,
+                                const float* scales, int32_t batch, int32_t channels,
+                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                                int32_t aligned, const float* grad_out, void* workspace,
+                                size_t ws_bytes, void* stream);
+
 /* ---- RoIPool (torchvision.ops.RoIPool; C4 config configs/faster_rcnn_r50.py:26) --
  * feat [B, C, H, W] with element strides strides[0..3] = (b, c, y, x); rois
  * [K, 5]; out [K, C, ph, pw] + int32 argmax (flat y*W+x, -1 for empty bins). */

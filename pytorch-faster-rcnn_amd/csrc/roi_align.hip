@@ -19,6 +19,8 @@
 // P5[..., ::2, ::2]) all run.
 #include <math.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "common.h"
@@ -1632,7 +1634,8 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv
 // per train step.  Here each wave owns 16 channels of one RoI: per channel it
 // sums the 16 weighted taps of every bin into an LDS copy of the RoI's tap window
 // (ds_add_f32), then adds the window to the feature gradient with one global
-// atomic per non-zero cell, lanes along window rows.  Windows above kBwdSlab
+// atomic per non-zero cell, lanes along window rows (count = 4 at sampling 2:
+// (g * w) / 4 == (g * w) * 0.25 exactly, without the division sequence).  Windows above kBwdSlab
 // floats keep the per-tap atomics.  Contributions are the reference's
 // grad * w / count; float atomics make the summation order (and the last bits)
 // run-dependent, as in torchvision's own CUDA backward.
@@ -1733,7 +1736,7 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevel
       for (int ix = 0; ix < SR; ++ix)
         if (ok[iy][ix])
 #pragma unroll
-          for (int q = 0; q < 4; ++q) atomicAdd(&slab[cell[iy][ix][q]], gv * wt[iy][ix][q] / g.count);
+          for (int q = 0; q < 4; ++q) atomicAdd(&slab[cell[iy][ix][q]], gv * wt[iy][ix][q] * 0.25f);
     wave_sync();
     float* f = gbase + (int64_t)ch * scs;
     int r = r0, col = col0;
@@ -1745,6 +1748,323 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevel
       if (col >= WW) col -= WW, ++r;
     }
     wave_sync();  // the window is re-zeroed for the next channel only after every lane read it
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward into a channels-last gradient (sampling 2, ph*pw <= 64, C % 16 == 0):
+// the default.  Global float atomics execute at the memory side as 64-B
+// requests (MI355X_MICROARCH.md, global float atomics): the NCHW flush above
+// adds window rows of a few cells -- mostly partial 64-B requests -- and runs
+// at a fraction of the atomic byte rate.  Here the gradient is accumulated in
+// a [B, H, W, C] buffer (zeroed by the caller; the autograd wrapper returns it
+// as a channels_last view): each wave owns 16 channels of the RoI, sums its
+// taps into an LDS band of the tap window laid out [cell][16 channels] (row
+// stride 17: conflict-free both ways), and flushes each window cell's 16
+// channels as ONE full 64-B atomic request.  Windows taller than a band of
+// kClBandCells cells are done band by band.  Contributions are the reference's
+// grad * w / count (count = 4: an exact * 0.25); float atomics make the
+// summation order run-dependent, as in torchvision's own CUDA backward.
+// Measured (tools/bench_roi_bwd.py, cfg2 RoIs, incl. clearing): 1.38 ms vs 1.19 ms
+// for the NCHW kernel, so the NCHW kernel stays the default (ops.ROI_ALIGN_BWD);
+// this one runs whenever the caller hands a channels_last gradient.
+constexpr int kClChans = 16;      // channels per wave = floats per flushed 64-B segment
+constexpr int kClBandCells = 256;  // window cells per LDS band
+constexpr int kClStride = kClChans + 1;
+
+__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_cl_kernel(RoiLevels lv, RoiCfg c,
+                                                                       const float* __restrict__ gout) {
+  constexpr int SR = 2;
+  __shared__ float band_all[kRoiThreads / kWave][kClBandCells * kClStride];  // 68 KB
+  const int64_t k = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kClChans;
+  if (cw0 >= c.C) return;  // host: C % 16 == 0
+  float* band = band_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
+  }
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
+    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  if (y1 < y0 || x1 < x0) return;  // no valid tap: no gradient
+  const int WW = x1 - x0 + 1;      // host: every level's width <= kClBandCells
+  const int RB = kClBandCells / WW;  // window rows per band
+  const int64_t sy = lv.sy[l], sx = lv.sx[l];
+  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * lv.sc[l];
+  const float* go = gout + (k * c.C + cw0) * nbins;
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+  int row[SR][SR][4], col[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = active && a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+      row[iy][ix][0] = row[iy][ix][1] = a.lo - y0;
+      row[iy][ix][2] = row[iy][ix][3] = a.hi - y0;
+      col[iy][ix][0] = col[iy][ix][2] = b.lo - x0;
+      col[iy][ix][1] = col[iy][ix][3] = b.hi - x0;
+    }
+  float gq[kClChans];  // grad * 0.25 per channel: (g * w) / 4 == (g * 0.25) * w exactly
+#pragma unroll
+  for (int ch = 0; ch < kClChans; ++ch) gq[ch] = active ? go[ch * nbins + bin] * 0.25f : 0.0f;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  for (int r0 = 0; r0 <= y1 - y0; r0 += RB) {
+    const int nr = min(RB, y1 - y0 + 1 - r0), ncell = nr * WW;
+    for (int e = lane; e < ncell * kClStride; e += kWave) band[e] = 0.0f;
+    wave_sync();
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = row[iy][ix][q] - r0;
+          if (ok[iy][ix] && rr >= 0 && rr < nr) {
+            float* cell = band + (rr * WW + col[iy][ix][q]) * kClStride;
+            const float w = wt[iy][ix][q];
+#pragma unroll
+            for (int ch = 0; ch < kClChans; ++ch) atomicAdd(cell + ch, gq[ch] * w);
+          }
+        }
+    wave_sync();
+    // flush: lane = (cell, channel); the 16 channels of a cell are one 64-B segment
+    for (int e = lane; e < ncell * kClChans; e += kWave) {
+      const int ce = e / kClChans, ch = e - ce * kClChans;
+      const float v = band[ce * kClStride + ch];
+      const int y = y0 + r0 + ce / WW, x = x0 + ce % WW;
+      if (v != 0.0f) atomicAdd(gbase + (int64_t)ch * lv.sc[l] + (int64_t)y * sy + (int64_t)x * sx, v);
+    }
+    wave_sync();  // the band is re-zeroed only after every lane read it
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward, tiled gather (sampling 2, ph*pw <= 64): the default.  The
+// window-accumulated kernel above still ends in one global float atomic per
+// (RoI, channel, window cell) -- ~45 M for a cfg2 batch, bound by the L2
+// atomic rate (1.24 ms per train step).  Here the feature gradient is built
+// tile by tile with no global atomics:
+//   bin_count : per RoI, the tap window (as the forward) -> the 16x16-cell
+//               tiles of its level it overlaps; count per tile
+//   bin_scan  : one workgroup: tile list offsets
+//   bin_fill  : per RoI, append its id to each overlapped tile's list
+//   tile      : workgroup = (tile, 32 channels), wave = 8 channels; the wave
+//               zeroes an LDS copy of the tile for its channels, walks the
+//               tile's RoIs (lane = bin) adding grad * w / count of every tap
+//               that falls in the tile with ds_add_f32, then stores the tile --
+//               every cell of every level written once (zeros where no RoI
+//               reaches), so the caller need not clear the gradient.
+// Contributions are the reference's grad * w / count, as the kernels above;
+// the order of the RoIs within a tile follows the fill atomics, so the last
+// bits are run-dependent like torchvision's own CUDA backward.
+// Measured (tools/bench_roi_bwd.py, cfg2 RoIs): SLOWER than the atomic kernel --
+// a RoI overlaps 4.4 tiles on average and every (RoI, tile) pair evaluates all
+// 16 x 49 taps, and the positives around one ground truth pile up to 100 RoIs
+// on one tile (one workgroup's serial list).  Opt-in (ops.ROI_ALIGN_BWD).
+
+constexpr int kBwdTile = 16;                 // tile side in cells
+constexpr int kBwdTileCells = kBwdTile * kBwdTile;
+constexpr int kBwdTileChans = 32;            // channels per workgroup
+constexpr int kBwdWaveChans = kBwdTileChans / (kRoiThreads / kWave);  // 8
+
+struct TileMap {
+  int nty[FRH_MAX_LEVELS], ntx[FRH_MAX_LEVELS];
+  int64_t base[FRH_MAX_LEVELS + 1];  // first tile id of each level (images level-major inside)
+  int B;
+};
+
+struct TileLists {
+  uint32_t* count;  // [T]
+  uint32_t* off;    // [T + 1]
+  uint32_t* fill;   // [T]
+  int4* win;        // [K]: tile rows ty0..ty1, cols tx0..tx1 (ty0 > ty1: none)
+  int32_t* list;    // [cap]
+  int64_t cap;
+};
+
+// the RoI's tap window at its level (forward's make_tap over all 2*ph / 2*pw samples)
+__device__ __forceinline__ int4 roi_tap_window(const RoiCfg& c, const RoiLevels& lv, int64_t k, int* lvl, int* img) {
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int H = lv.h[g.lvl], W = lv.w[g.lvl];
+  int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
+  for (int p = 0; p < c.ph; ++p)
+    for (int i = 0; i < 2; ++i) {
+      const Tap t = make_tap(g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+      if (t.valid) y0 = min(y0, t.lo), y1 = max(y1, t.hi);
+    }
+  for (int p = 0; p < c.pw; ++p)
+    for (int i = 0; i < 2; ++i) {
+      const Tap t = make_tap(g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
+      if (t.valid) x0 = min(x0, t.lo), x1 = max(x1, t.hi);
+    }
+  *lvl = g.lvl;
+  *img = g.b;
+  if (y1 < y0 || x1 < x0) return make_int4(1, 0, 1, 0);
+  return make_int4(y0 / kBwdTile, y1 / kBwdTile, x0 / kBwdTile, x1 / kBwdTile);
+}
+
+__device__ __forceinline__ int64_t tile_id(const TileMap& tm, int l, int b, int ty, int tx) {
+  return tm.base[l] + ((int64_t)b * tm.nty[l] + ty) * tm.ntx[l] + tx;
+}
+
+__global__ void roi_bwd_bin_count_kernel(RoiLevels lv, RoiCfg c, TileMap tm, TileLists tl) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= c.K) return;
+  int l, b;
+  const int4 w = roi_tap_window(c, lv, k, &l, &b);
+  tl.win[k] = w;
+  for (int ty = w.x; ty <= w.y; ++ty)
+    for (int tx = w.z; tx <= w.w; ++tx) atomicAdd(&tl.count[tile_id(tm, l, b, ty, tx)], 1u);
+}
+
+__global__ void __launch_bounds__(1024) roi_bwd_bin_scan_kernel(TileLists tl, int64_t T) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (T + 1023) / 1024, s = t * per, e = min(T, s + per);
+  uint32_t sum = 0;
+  for (int64_t i = s; i < e; ++i) sum += tl.count[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int64_t i = s; i < e; ++i) {
+    tl.off[i] = run;
+    run += tl.count[i];
+  }
+  if (t == 1023) tl.off[T] = part[1023];
+}
+
+__global__ void roi_bwd_bin_fill_kernel(RoiLevels lv, RoiCfg c, TileMap tm, TileLists tl) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= c.K) return;
+  const int4 w = tl.win[k];
+  if (w.x > w.y) return;
+  const float* r = c.rois + k * 5;
+  const int b = (int)r[0], l = c.levels ? (int)c.levels[k] : 0;
+  for (int ty = w.x; ty <= w.y; ++ty)
+    for (int tx = w.z; tx <= w.w; ++tx) {
+      const int64_t t = tile_id(tm, l, b, ty, tx);
+      const uint32_t pos = tl.off[t] + atomicAdd(&tl.fill[t], 1u);
+      if (pos < tl.cap) tl.list[pos] = (int32_t)k;
+    }
+}
+
+__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_tile_kernel(RoiLevels lv, RoiCfg c, TileMap tm,
+                                                                         TileLists tl, const float* __restrict__ gout) {
+  constexpr int SR = 2;
+  __shared__ float tile_all[kRoiThreads / kWave][kBwdWaveChans * kBwdTileCells];  // 32 KB
+  const int64_t t = blockIdx.x;
+  int l = 0;
+  while (l + 1 < lv.L && t >= tm.base[l + 1]) ++l;
+  const int64_t lt = t - tm.base[l];
+  const int per_img = tm.nty[l] * tm.ntx[l];
+  const int b = (int)(lt / per_img), rem = (int)(lt - (int64_t)b * per_img);
+  const int tyi = rem / tm.ntx[l], txi = rem - tyi * tm.ntx[l];
+  const int H = lv.h[l], W = lv.w[l];
+  const int Y0 = tyi * kBwdTile, X0 = txi * kBwdTile;
+  const int th = min(kBwdTile, H - Y0), tw = min(kBwdTile, W - X0);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kBwdTileChans + wave * kBwdWaveChans;
+  const int nch = min(kBwdWaveChans, c.C - cw0);
+  if (nch <= 0) return;
+  float* tile = tile_all[wave];
+  for (int e = lane; e < kBwdWaveChans * kBwdTileCells; e += kWave) tile[e] = 0.0f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  const uint32_t i0 = tl.off[t], i1 = min((int64_t)tl.off[t + 1], tl.cap);
+  for (uint32_t i = i0; i < i1; ++i) {
+    const int64_t k = tl.list[i];
+    const RoiGeom g = roi_geom(c, lv, k);
+    Tap ty[SR], tx[SR];
+#pragma unroll
+    for (int s = 0; s < SR; ++s) {
+      ty[s] = make_tap(g.start_h + (float)py * g.bin_h + ((float)s + 0.5f) * g.bin_h * 0.5f, H);
+      tx[s] = make_tap(g.start_w + (float)px * g.bin_w + ((float)s + 0.5f) * g.bin_w * 0.5f, W);
+    }
+    // tile cells of this bin's 16 taps (-1: outside the tile or invalid sample) and weights
+    int cell[SR][SR][4];
+    float wt[SR][SR][4];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const Tap a = ty[iy], bb = tx[ix];
+        const bool ok = active && a.valid && bb.valid;
+        const int ylo = a.lo - Y0, yhi = a.hi - Y0, xlo = bb.lo - X0, xhi = bb.hi - X0;
+        const bool iyl = ylo >= 0 && ylo < th, iyh = yhi >= 0 && yhi < th;
+        const bool ixl = xlo >= 0 && xlo < tw, ixh = xhi >= 0 && xhi < tw;
+        cell[iy][ix][0] = ok && iyl && ixl ? ylo * kBwdTile + xlo : -1;
+        cell[iy][ix][1] = ok && iyl && ixh ? ylo * kBwdTile + xhi : -1;
+        cell[iy][ix][2] = ok && iyh && ixl ? yhi * kBwdTile + xlo : -1;
+        cell[iy][ix][3] = ok && iyh && ixh ? yhi * kBwdTile + xhi : -1;
+        wt[iy][ix][0] = a.h * bb.h;
+        wt[iy][ix][1] = a.h * bb.l;
+        wt[iy][ix][2] = a.l * bb.h;
+        wt[iy][ix][3] = a.l * bb.l;
+      }
+    const float* go = gout + (k * c.C + cw0) * nbins + bin;
+    float gv[kBwdWaveChans];
+#pragma unroll
+    for (int ch = 0; ch < kBwdWaveChans; ++ch) gv[ch] = (active && ch < nch) ? go[ch * nbins] : 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = cell[iy][ix][q];
+          if (e >= 0) {
+#pragma unroll
+            for (int ch = 0; ch < kBwdWaveChans; ++ch)
+              atomicAdd(&tile[ch * kBwdTileCells + e], gv[ch] * wt[iy][ix][q] * 0.25f);
+          }
+        }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float* gbase = lv.grad[l] + (int64_t)b * lv.sb[l] + (int64_t)cw0 * lv.sc[l];
+  for (int e = lane; e < nch * kBwdTileCells; e += kWave) {
+    const int ch = e / kBwdTileCells, cl = e - ch * kBwdTileCells;
+    const int y = cl / kBwdTile, x = cl - y * kBwdTile;
+    if (y < th && x < tw) gbase[(int64_t)ch * lv.sc[l] + (int64_t)(Y0 + y) * lv.sy[l] + (int64_t)(X0 + x) * lv.sx[l]] =
+        tile[e];
   }
 }
 
@@ -1977,11 +2297,98 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   FRH_REQUIRE(grad_feats && grad_out, "null pointer argument");
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
+  // channels-last gradient (channel stride 1): full 64-B atomic segments
+  bool cl = sampling_ratio == 2 && pooled_h * pooled_w <= 64 && channels % kClChans == 0;
+  for (int l = 0; l < lv.L; ++l) cl = cl && lv.sc[l] == 1 && lv.w[l] <= kClBandCells;
+  if (cl)
+    hipLaunchKernelGGL(roi_align_bwd_cl_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
+  else if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
     hipLaunchKernelGGL(roi_align_bwd_lds_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   else
     hipLaunchKernelGGL(roi_align_bwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   return check_launch("frh_roi_align_bwd");
+}
+
+static TileMap tile_map(int32_t L, const int32_t* feat_hw, int32_t batch, int64_t* max_tiles) {
+  TileMap tm{};
+  tm.B = batch;
+  tm.base[0] = 0;
+  *max_tiles = 1;
+  for (int l = 0; l < L; ++l) {
+    tm.nty[l] = (feat_hw[2 * l] + kBwdTile - 1) / kBwdTile;
+    tm.ntx[l] = (feat_hw[2 * l + 1] + kBwdTile - 1) / kBwdTile;
+    tm.base[l + 1] = tm.base[l] + (int64_t)batch * tm.nty[l] * tm.ntx[l];
+    *max_tiles = std::max<int64_t>(*max_tiles, (int64_t)tm.nty[l] * tm.ntx[l]);
+  }
+  return tm;
+}
+
+struct BwdLayout {
+  size_t count, off, fill, win, list, total;
+  int64_t cap;
+};
+
+static BwdLayout bwd_layout(int32_t L, const int32_t* feat_hw, int32_t batch, int64_t num_rois) {
+  int64_t mt;
+  const TileMap tm = tile_map(L, feat_hw, batch, &mt);
+  const int64_t T = tm.base[L];
+  auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  BwdLayout z;
+  z.cap = num_rois * mt;
+  z.count = 0;
+  z.off = z.count + al(T * 4);
+  z.fill = z.off + al((T + 1) * 4);
+  z.win = z.fill + al(T * 4);
+  z.list = z.win + al(num_rois * 16);
+  z.total = z.list + al(z.cap * 4);
+  return z;
+}
+
+extern "C" size_t frh_roi_align_bwd_workspace(int32_t num_levels, const int32_t* feat_hw, int32_t batch,
+                                              int64_t num_rois) {
+  if (num_levels < 1 || num_levels > FRH_MAX_LEVELS || !feat_hw || batch < 1 || num_rois < 0) return 0;
+  return bwd_layout(num_levels, feat_hw, batch, num_rois).total;
+}
+
+extern "C" int32_t frh_roi_align_bwd_tiled(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
+                                           const int64_t* strides, const float* scales, int32_t batch,
+                                           int32_t channels, const float* rois, const int64_t* roi_levels,
+                                           int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                                           int32_t sampling_ratio, int32_t aligned, const float* grad_out,
+                                           void* workspace, size_t ws_bytes, void* stream) {
+  int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
+  if (r) return r;
+  FRH_REQUIRE(sampling_ratio == 2 && pooled_h * pooled_w <= kWave, "tiled backward needs sampling_ratio 2 and "
+              "pooled_h * pooled_w <= 64 (got %d, %dx%d)", sampling_ratio, pooled_h, pooled_w);
+  RoiLevels lv;
+  r = make_levels(num_levels, nullptr, grad_feats, feat_hw, strides, scales, &lv);
+  if (r) return r;
+  FRH_REQUIRE(grad_feats && (grad_out || num_rois == 0), "null pointer argument");
+  const BwdLayout z = bwd_layout(num_levels, feat_hw, batch, num_rois);
+  FRH_REQUIRE(workspace && ws_bytes >= z.total, "workspace too small (%zu < %zu)", ws_bytes, z.total);
+  int64_t mt;
+  const TileMap tm = tile_map(num_levels, feat_hw, batch, &mt);
+  const int64_t T = tm.base[num_levels];
+  char* ws = static_cast<char*>(workspace);
+  TileLists tl{reinterpret_cast<uint32_t*>(ws + z.count), reinterpret_cast<uint32_t*>(ws + z.off),
+               reinterpret_cast<uint32_t*>(ws + z.fill), reinterpret_cast<int4*>(ws + z.win),
+               reinterpret_cast<int32_t*>(ws + z.list), z.cap};
+  hipStream_t st = as_stream(stream);
+  RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+  FRH_HIP(hipMemsetAsync(ws + z.count, 0, z.off - z.count, st));
+  FRH_HIP(hipMemsetAsync(ws + z.fill, 0, z.win - z.fill, st));
+  if (num_rois > 0) {
+    const unsigned nb = (unsigned)((num_rois + 255) / 256);
+    hipLaunchKernelGGL(roi_bwd_bin_count_kernel, dim3(nb), dim3(256), 0, st, lv, c, tm, tl);
+  }
+  hipLaunchKernelGGL(roi_bwd_bin_scan_kernel, dim3(1), dim3(1024), 0, st, tl, T);
+  if (num_rois > 0) {
+    const unsigned nb = (unsigned)((num_rois + 255) / 256);
+    hipLaunchKernelGGL(roi_bwd_bin_fill_kernel, dim3(nb), dim3(256), 0, st, lv, c, tm, tl);
+  }
+  dim3 grid((unsigned)T, (unsigned)((channels + kBwdTileChans - 1) / kBwdTileChans));
+  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, grid, dim3(kRoiThreads), 0, st, lv, c, tm, tl, grad_out);
+  return check_launch("frh_roi_align_bwd_tiled");
 }
 
 // dense-layout convenience entry points (header): layout 0 = NCHW, 1 = NHWC

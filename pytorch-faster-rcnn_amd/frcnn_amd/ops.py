@@ -465,13 +465,33 @@ class _RoIAlignMulti(torch.autograd.Function):
     def backward(ctx, grad):
         rois, levels = ctx.saved_tensors
         scales, (ph, pw), sr, aligned, shapes = ctx.cfg
-        grads = [torch.zeros(s, dtype=torch.float32, device=grad.device) for s in shapes]
         grad = grad.contiguous()
-        hw, st = _feat_desc(grads)
-        call('frh_roi_align_bwd_strided', len(grads), ptr_array(grads), hw, st, f32_array(scales),
-             shapes[0][0], shapes[0][1], ptr(rois), ptr(levels), rois.shape[0], ph, pw, int(sr),
-             int(bool(aligned)), ptr(grad), stream_of(grad))
+        K, B, C = rois.shape[0], shapes[0][0], shapes[0][1]
+        if ROI_ALIGN_BWD['mode'] == 'tiled' and sr == 2 and ph * pw <= 64:
+            # tiled gather: writes every gradient cell, no clearing, no global atomics
+            grads = [torch.empty(s, dtype=torch.float32, device=grad.device) for s in shapes]
+            hw, st = _feat_desc(grads)
+            ws = workspace(_lib.query('frh_roi_align_bwd_workspace', len(grads), hw, B, K), grad.device)
+            call('frh_roi_align_bwd_tiled', len(grads), ptr_array(grads), hw, st, f32_array(scales), B, C,
+                 ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), ptr(ws), ws.numel(),
+                 stream_of(grad))
+        else:
+            # 'channels_last': accumulate into [B, H, W, C] (returned as a channels_last view), so every
+            # window cell's 16-channel group is one full 64-B memory-side atomic; 'atomic': NCHW
+            fmt = torch.channels_last if ROI_ALIGN_BWD['mode'] == 'channels_last' else torch.contiguous_format
+            grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt).zero_()
+                     for s in shapes]
+            hw, st = _feat_desc(grads)
+            call('frh_roi_align_bwd_strided', len(grads), ptr_array(grads), hw, st, f32_array(scales), B, C,
+                 ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), stream_of(grad))
         return (None, None, None, None, None, None) + tuple(grads)
+
+
+# RoIAlign backward kernel: 'atomic' (default: per-RoI LDS window, one global atomic per cell and
+# channel into the NCHW gradient; measured fastest), 'channels_last' (LDS window bands, one 64-B
+# atomic per cell and 16 channels into a channels_last gradient) or 'tiled' (tile lists + LDS
+# gather, no global atomics).  Measurements: DESIGN.md §4.
+ROI_ALIGN_BWD = {'mode': 'atomic'}
 
 
 def roi_align_replay(rec, out=None):

@@ -408,12 +408,15 @@ def test_roi_align_module_and_strided_view(dev):
     np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize('mode', ['channels_last', 'tiled', 'atomic'])
 @pytest.mark.parametrize('case', ['small', 'p2', 'p2_nhwc', 'adaptive'])
-def test_roi_align_backward_vs_oracle(dev, case):
-    """Backward (window-accumulated LDS kernel for sampling 2; per-tap atomics for adaptive
-    sampling and windows over the slab) against the oracle: float atomics reorder the sums,
-    so the tolerance is f32-accumulation level."""
+def test_roi_align_backward_vs_oracle(dev, case, mode):
+    """Backward (the NCHW window kernel 'atomic' = the default; window bands + 64-B atomics
+    into a channels_last gradient; tiled gather; per-tap atomics for adaptive sampling)
+    against the oracle:
+    both reorder the float sums, so the tolerance is f32-accumulation level."""
     from frcnn_amd import ops
+    ops.ROI_ALIGN_BWD['mode'] = mode
     if case == 'small' or case == 'adaptive':
         grids, scales, C, K, L = [(38, 64), (19, 32)], [1 / 16, 1 / 32], 16, 120, 2
     else:
@@ -429,6 +432,7 @@ def test_roi_align_backward_vs_oracle(dev, case):
     ft = [f.requires_grad_(True) for f in ft]
     out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), sr)
     out.backward(T(g, dev))
+    ops.ROI_ALIGN_BWD['mode'] = 'atomic'
     ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, sr)
     for a, r in zip(ft, ref):
         np.testing.assert_allclose(a.grad.cpu().numpy(), r, rtol=1e-4, atol=2e-5)
