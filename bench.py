@@ -188,6 +188,9 @@ def main():
                          '+5.8%% img/s on cfg2 fwd, ~1 min of search).  auto = on for fwd, off for train (the '
                          'backward-convolution search takes several minutes)')
     ap.add_argument('--no-conv-search', dest='conv_search', action='store_const', const='off')
+    ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
+                    help='replay backbone + neck + RPN head convs as one captured hipGraph (frcnn_amd.graphs) '
+                         'after the warmup.  auto = on for fwd with a two-stage detector, off for train')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -239,6 +242,20 @@ def main():
         if rank == 0:
             print('bench: warmup step {}/{} done'.format(w + 1, args.warmup), file=sys.stderr, flush=True)
     hb_stop.set()
+
+    graphed = False
+    if args.graphs == 'auto':
+        args.graphs = 'on' if args.mode == 'fwd' and hasattr(model, 'graphed_trunk') else 'off'
+    if args.graphs == 'on':
+        from frcnn_amd.graphs import capture_trunk
+        if not hasattr(model, 'graphed_trunk'):
+            raise SystemExit('--graphs on: {} has no graphed trunk'.format(type(model).__name__))
+        capture_trunk(model, batch[0])
+        graphed = True
+        for _ in range(2):
+            step()
+        if rank == 0:
+            print('bench: trunk captured as a hipGraph', file=sys.stderr, flush=True)
 
     def barrier():
         if world > 1:
@@ -307,6 +324,7 @@ def main():
             'config': {'workload': 'configs/{}.py{} forward_train'.format(
                            args.config, ' (BASELINE config 2)' if args.config == 'faster_rcnn_r50_fpn' else ''),
                        'conv_algorithms': 'MIOpen benchmarked (warmup)' if args.conv_search else 'MIOpen heuristic',
+                       'trunk': 'hipGraph replay (backbone + neck + RPN head convs)' if graphed else 'eager',
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
                        'sampler': args.sampler, 'mode': args.mode},

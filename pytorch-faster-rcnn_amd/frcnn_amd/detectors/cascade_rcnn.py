@@ -39,6 +39,8 @@ class CascadeRCNN(nn.Module):
         self.rcnn_head = nn.ModuleList(heads)
         self.train_cfg = train_cfg
         self.test_cfg = test_cfg
+        # optional hipGraph of backbone + neck + RPN head convs (frcnn_amd.graphs.capture_trunk)
+        self.graphed_trunk = None
 
     def init_weights(self):
         self.backbone.init_weights()
@@ -58,10 +60,13 @@ class CascadeRCNN(nn.Module):
     def forward_train(self, img_data, gt_bboxes, gt_labels, img_metas):
         """cascade_rcnn.py:90-154."""
         losses = {}
-        feats = self.extract_feat(img_data)
+        if self.graphed_trunk is not None and self.graphed_trunk.matches(img_data):
+            feats, rpn_cls, rpn_reg = self.graphed_trunk(img_data)
+        else:
+            feats = self.extract_feat(img_data)
+            rpn_cls, rpn_reg = self.rpn_head(feats)
         cfg = self.train_cfg
         rpn_gt_labels = [torch.ones_like(g) for g in gt_labels]
-        rpn_cls, rpn_reg = self.rpn_head(feats)
         l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
         losses['rpn_cls_loss'] = l_cls
         losses['rpn_reg_loss'] = l_reg
