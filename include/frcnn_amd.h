@@ -252,6 +252,20 @@ int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, float* out, void* stream);
+/* Plane-sweep forward (the default for sampling_ratio 2, even C, unit x
+ * stride, W_l <= 256): one workgroup per (level, image, channel pair) streams
+ * that plane pair through an LDS row ring exactly once and evaluates every
+ * (RoI, bin row) as soon as its rows have landed; a small plan launch first
+ * writes each bin row's y taps and each (RoI, px)'s x taps into the workspace
+ * (frh_roi_align_sweep_workspace bytes).  Bit-identical to
+ * frh_roi_align_fwd_strided, which it falls back to for any other shape or a
+ * missing / short workspace. */
+size_t frh_roi_align_sweep_workspace(int64_t num_rois, int32_t pooled_h, int32_t pooled_w);
+int32_t frh_roi_align_fwd_sweep(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                                const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
+                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                                float* out, void* workspace, size_t ws_bytes, void* stream);
 /* The grouped forward (opt-in): a one-workgroup planning launch sorts the
  * RoIs into spatial groups of 8 (same image and level); the main launch
  * stages the union of each group's tap rows per channel into LDS by LDS-DMA

@@ -18,104 +18,19 @@
 // element strides: NCHW, channels_last and strided views (FPN P6 =
 // P5[..., ::2, ::2]) all run.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
 #include <type_traits>
 
-#include "common.h"
+#include "roi_common.h"
 
 namespace frh {
 
 constexpr int kRoiThreads = 256;
 constexpr int kRoiChanChunk = 64;
 constexpr int kMaxSamplesPerDim = 1024;
-
-struct RoiLevels {
-  const float* feat[FRH_MAX_LEVELS];
-  float* grad[FRH_MAX_LEVELS];
-  int32_t h[FRH_MAX_LEVELS], w[FRH_MAX_LEVELS];
-  int64_t sb[FRH_MAX_LEVELS], sc[FRH_MAX_LEVELS], sy[FRH_MAX_LEVELS], sx[FRH_MAX_LEVELS];
-  float scale[FRH_MAX_LEVELS];
-  int L;
-};
-
-struct RoiCfg {
-  const float* rois;         // [K, 5]
-  const int64_t* levels;     // [K] or nullptr
-  int64_t K;
-  int C, ph, pw, sampling, aligned;
-};
-
-struct Tap {
-  int lo, hi;
-  float l, h;  // fractional part and 1 - fractional part
-  int valid;
-};
-
-// One coordinate of torchvision's bilinear_interpolate / pre_calc.
-__device__ __forceinline__ Tap make_tap(float v, int size) {
-  Tap t;
-  if (v < -1.0f || v > (float)size) {
-    t.valid = 0;
-    t.lo = t.hi = 0;
-    t.l = t.h = 0.f;
-    return t;
-  }
-  t.valid = 1;
-  if (v <= 0.f) v = 0.f;
-  int lo = (int)v, hi;
-  if (lo >= size - 1) {
-    hi = lo = size - 1;
-    v = (float)lo;
-  } else {
-    hi = lo + 1;
-  }
-  t.lo = lo;
-  t.hi = hi;
-  t.l = v - (float)lo;
-  t.h = 1.0f - t.l;
-  return t;
-}
-
-struct RoiGeom {
-  int b, lvl, gh, gw;
-  float start_h, start_w, bin_h, bin_w;
-  float count;
-};
-
-__device__ __forceinline__ RoiGeom roi_geom(const RoiCfg& c, const RoiLevels& lv, int64_t k) {
-  RoiGeom g;
-  const float* r = c.rois + k * 5;
-  g.b = (int)r[0];
-  g.lvl = c.levels ? (int)c.levels[k] : 0;
-  const float sc = lv.scale[g.lvl];
-  const float off = c.aligned ? 0.5f : 0.0f;
-  float sw = r[1] * sc - off, sh = r[2] * sc - off;
-  float ew = r[3] * sc - off, eh = r[4] * sc - off;
-  float rw = ew - sw, rh = eh - sh;
-  if (!c.aligned) {
-    rw = fmaxf(rw, 1.0f);
-    rh = fmaxf(rh, 1.0f);
-  }
-  g.start_w = sw;
-  g.start_h = sh;
-  g.bin_h = rh / (float)c.ph;
-  g.bin_w = rw / (float)c.pw;
-  g.gh = c.sampling > 0 ? c.sampling : (int)ceilf(rh / (float)c.ph);
-  g.gw = c.sampling > 0 ? c.sampling : (int)ceilf(rw / (float)c.pw);
-  int cnt = g.gh * g.gw;
-  g.count = (float)(cnt > 1 ? cnt : 1);
-  return g;
-}
-
-// fill the separable sample tables: rows [ph*gh], cols [pw*gw]
-__device__ __forceinline__ float sample_y(const RoiGeom& g, int p, int i) {
-  return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h / (float)g.gh;
-}
-__device__ __forceinline__ float sample_x(const RoiGeom& g, int p, int i) {
-  return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w / (float)g.gw;
-}
 
 // true when the separable tables fit in LDS (always for fixed sampling ratios;
 // adaptive grids on huge RoIs fall back to computing taps per sample)
@@ -176,54 +91,6 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_kernel(RoiLevels lv
   }
 }
 
-
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
-  void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, 0, n, 0x00020000);
-}
-
-// Wave-wide min / max with DPP row ops (no LDS round trip); result in every lane.
-template <bool kMin>
-__device__ __forceinline__ int wave_minmax_i32(int v) {
-  const int id = kMin ? 0x7fffffff : (int)0x80000000;
-  auto op = [](int a, int b) { return kMin ? min(a, b) : max(a, b); };
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xf, 0xf, false));  // row_mirror
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast15
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast31
-  return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ int wave_min_i32(int v) { return wave_minmax_i32<true>(v); }
-__device__ __forceinline__ int wave_max_i32(int v) { return wave_minmax_i32<false>(v); }
-
-// buffer_load_dword{,x4} ... lds: kBytes per lane into LDS at lds + 4*kBytes/4 * lane.
-// The 16-byte form is a gfx950 instruction the host pass of hipcc cannot check,
-// hence the device-pass guard (the host never runs device code).
-template <int kBytes>
-__device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t r, float* lds, int voff, int soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  static_assert(kBytes == 4 || kBytes == 16, "LDS-DMA width");
-  if constexpr (kBytes == 16)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-  else
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, soff, 0, 0);
-#endif
-}
-
-// s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding).  The
-// compiler does not wait for LDS-DMA data before ds_reads: these are explicit.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
 // Buffer-descriptor variant (sampling ratio 2, ph*pw <= 256; the default).
 // Lane (bin, channel group cg) keeps its bin's 16 tap offsets in VGPRs as
@@ -826,7 +693,7 @@ struct PairLayout {
 // kSkip (diagnostics only): 1 = skip RoIs staged 8 pairs at a time, 2 = skip the others.
 // kDiag (diagnostics only): per-wave s_memrealtime stamps past the results:
 // [start, setup done, stage 0 ready, stage 0 done, stage 1 ready, end, D, RoI].
-template <int kSkip = 0, bool kDiag = false>
+template <int kSkip = 0, bool kDiag = false, int kPW = kPairWave>
 __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   constexpr int SR = 2;
   __shared__ __attribute__((aligned(16))) float slab[2 * kPairHalf];
@@ -834,8 +701,8 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   if (kDiag) stamp[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
   const int64_t k = blockIdx.x;
   const int lane = threadIdx.x;
-  const int cw0 = blockIdx.y * kPairChunk;
-  const int npairs = min(kPairWave, (c.C - cw0) / 2);  // host: C even
+  const int cw0 = blockIdx.y * 2 * kPW;
+  const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
@@ -2180,7 +2047,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   const bool pair_ok = f.lds && channels % 2 == 0 && 4 * pooled_h <= kWave && 4 * pooled_w <= kWave &&
                        4 * pooled_h * (4 * pooled_w + 1) <= PairLayout<1>::kCells;
-  FRH_REQUIRE(variant == 0 || ((variant >= 10 && variant <= 16) && f.lds) || ((variant == 50 || variant == 51) && grp_ok) ||
+  FRH_REQUIRE(variant == 0 || (((variant >= 9 && variant <= 19) && f.lds)) || ((variant == 50 || variant == 51) && grp_ok) ||
                   (variant >= 20 && variant <= 24 && pair_ok) || (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   if (variant == 50 || variant == 51) {
@@ -2203,7 +2070,13 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_group_kernel<1>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
   } else if (variant >= 20 && variant <= 24) {  // 21 / 22: diagnostics (skip large / small windows), 24: stamps
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kPairChunk - 1) / kPairChunk));
-    if (variant == 20 || variant == 23)
+    if (variant == 20 && getenv("FRH_PAIR_PW")) {
+      const int pw = atoi(getenv("FRH_PAIR_PW"));
+      const dim3 g2((unsigned)num_rois, (unsigned)((channels + 2 * pw - 1) / (2 * pw)));
+      if (pw == 32) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 32>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+      else if (pw == 16) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+      else hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    } else if (variant == 20 || variant == 23)
       hipLaunchKernelGGL(roi_align_fwd_pair_kernel<0>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
     else if (variant == 21)
       hipLaunchKernelGGL(roi_align_fwd_pair_kernel<2>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
@@ -2231,7 +2104,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_x4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else
       hipLaunchKernelGGL(roi_align_fwd_x4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  } else if (variant >= 10 && variant <= 16) {
+  } else if (variant >= 9 && variant <= 19) {
     // 10: windows <= 256 floats staged (default); 11 / 12: stage up to 512 / 1024 (experiments)
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     if (variant == 10)
@@ -2248,6 +2121,14 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 2>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else if (variant == 11)
       hipLaunchKernelGGL(roi_align_fwd_lds_kernel<512>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 17)
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 128>), dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 18)
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 256>), dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 19)
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<1024, 0, 256>), dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    else if (variant == 9)
+      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<1024, 0, 128>), dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
     else
       hipLaunchKernelGGL(roi_align_fwd_lds_kernel<1024>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   } else {
