@@ -266,6 +266,18 @@ int32_t frh_roi_align_fwd_sweep(int32_t num_levels, const float* const* feats, c
                                 const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                 int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
                                 float* out, void* workspace, size_t ws_bytes, void* stream);
+/* Plane-sweep backward: the same sweep accumulates each (image, channel pair)'s
+ * gradient rows in LDS and writes every element of grad_feats exactly once
+ * (no clearing, no global atomics).  Returns FRH_EUNSUPPORTED (nothing
+ * launched) outside the sweep's shapes or without the workspace
+ * (frh_roi_align_sweep_workspace bytes): the caller then clears the gradient
+ * and uses frh_roi_align_bwd_strided.  Float atomics in LDS: the summation
+ * order, and the last bits, vary from run to run (as torchvision's CUDA). */
+int32_t frh_roi_align_bwd_sweep(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
+                                const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
+                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                                const float* grad_out, void* workspace, size_t ws_bytes, void* stream);
 /* The grouped forward (opt-in): a one-workgroup planning launch sorts the
  * RoIs into spatial groups of 8 (same image and level); the main launch
  * stages the union of each group's tap rows per channel into LDS by LDS-DMA

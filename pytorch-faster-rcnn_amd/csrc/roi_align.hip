@@ -1619,6 +1619,158 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevel
 }
 
 // ---------------------------------------------------------------------------
+// Backward, separable tap sums (sampling 2, 4*ph and 4*pw <= 32): the default.
+// LDS float atomics (ds_add_f32) run several times slower than plain LDS
+// traffic on gfx950 (tools/probe/probe_bwd.py: the same accumulation took 7x
+// longer with ds_add_f32 than with a racy read-modify-write), and degenerate
+// RoIs (the random-init proposals clamped to the image border: half the cfg2
+// RoIs are < 1 px tall) pile all their taps on a few cells, which serialises
+// any per-cell scheme.  The taps are separable: cell (y, x) receives
+// (g[py][px] * (wy * wx)) * 0.25 for every y tap entry (py, iy, lo|hi) on row y
+// and every x tap entry (px, ix, lo|hi) on column x; wy * wx is exactly the
+// reference's w1..w4 (hy*hx, hy*lx, ly*hx, ly*lx), so every contribution is the
+// reference's grad * w / count.  A wave sorts its RoI's <= 4*ph y entries by
+// row and <= 4*pw x entries by column once.  Per channel pair, lane (half h,
+// j) owns x entry j of channel h and walks the y entries in row order (a
+// uniform loop): it accumulates its contributions, and at the end of each row
+// a segmented sum over the lanes of equal column leaves each (row, column)
+// cell's total in one lane, which adds it to the feature gradient with one
+// global atomic.  No LDS atomics, no divergence; the order of the float sums
+// differs from the reference's (float atomics already make it run-dependent,
+// as in torchvision's CUDA backward).
+constexpr int kSepEnt = 32;  // tap entries per axis and wave half: 4 * ph, 4 * pw <= 32
+
+__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
+                                                                        const float* __restrict__ gout) {
+  constexpr int kCh = kRoiChanChunk / (kRoiThreads / kWave);  // channels per wave (even)
+  __shared__ int yent_all[kRoiThreads / kWave][kSepEnt];      // row << 16 | py, sorted by (row, entry)
+  __shared__ float yw_all[kRoiThreads / kWave][kSepEnt];
+  __shared__ int xpos_all[kRoiThreads / kWave][kSepEnt];      // position of each x entry, unsorted
+  __shared__ float gv_all[kRoiThreads / kWave][2 * kWave];
+  const int64_t k = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
+  const int nch = min(kCh, c.C - cw0);
+  if (nch <= 0) return;
+  int* yent = yent_all[wave];
+  float* yw = yw_all[wave];
+  int* xpos = xpos_all[wave];
+  float* gv = gv_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int ph = c.ph, pw = c.pw, nbins = ph * pw;
+  const int nye = 4 * ph, nxe = 4 * pw;
+  const int h = lane >> 5, j = lane & 31;
+  // tap entry e of an axis: sample e / 2 (bin e / 4, sub-sample (e / 2) & 1), lo (e even) or hi
+  auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
+    const Tap t = make_tap(start + (float)(e >> 2) * bin + ((float)((e >> 1) & 1) + 0.5f) * bin * 0.5f, size);
+    *pos = t.valid ? ((e & 1) ? t.hi : t.lo) : -1;
+    *w = (e & 1) ? t.l : t.h;
+  };
+  int yp, xp;
+  float ywv, xwv;
+  entry(j, g.start_h, g.bin_h, H, &yp, &ywv);
+  entry(j, g.start_w, g.bin_w, W, &xp, &xwv);
+  if (j >= nye) yp = -1;
+  if (j >= nxe) xp = -1;
+  if (h == 0) xpos[j] = xp < 0 ? (1 << 20) : xp;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // x entries: rank by (col, entry); lane (h, j) takes the j-th in column order
+  int xrank = 0;
+  for (int e = 0; e < nxe; ++e) {
+    const int pe = xpos[e], pm = xpos[j];
+    xrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
+  }
+  // y entries: rank by (row, entry), written sorted
+  {
+    int yrank = 0;
+    const int pm = yp < 0 ? (1 << 20) : yp;
+    for (int e = 0; e < nye; ++e) {
+      const int pe = __shfl(yp < 0 ? (1 << 20) : yp, e, kWave);
+      yrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
+    }
+    if (h == 0 && j < nye && yp >= 0) {
+      yent[yrank] = (yp << 16) | (j >> 2);
+      yw[yrank] = ywv;
+    }
+  }
+  int nyv = 0, nxv = 0;  // valid entries (uniform)
+  {
+    const uint64_t my = __ballot(h == 0 && yp >= 0), mx = __ballot(h == 0 && xp >= 0);
+    nyv = __popcll(my);
+    nxv = __popcll(mx);
+  }
+  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  // this lane's x entry (column order) and the segment of lanes sharing its column
+  int my_col = -1, my_px = 0;
+  float my_wx = 0.0f;
+  // scatter the x entries into column order through LDS
+  __shared__ int xs_all[kRoiThreads / kWave][kSepEnt];
+  __shared__ float xw_all[kRoiThreads / kWave][kSepEnt];
+  int* xs = xs_all[wave];
+  float* xw = xw_all[wave];
+  if (h == 0 && xp >= 0) {
+    xs[xrank] = (xp << 16) | (j >> 2);
+    xw[xrank] = xwv;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool xv = j < nxv;
+  if (xv) {
+    my_col = xs[j] >> 16;
+    my_px = xs[j] & 0xffff;
+    my_wx = xw[j];
+  }
+  // segment of equal columns within the half: [j - lead, j + trail]
+  int trail = 0;
+  for (int d = 1; d < kSepEnt; ++d) {
+    const int jj = j + d;
+    if (jj < nxv && (xs[jj] >> 16) == my_col) trail = d;
+  }
+  const bool head = xv && (j == 0 || (xs[j - 1] >> 16) != my_col);
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const float* go = gout + (k * c.C + cw0) * nbins;
+  for (int ch = 0; ch < nch; ch += 2) {
+    // grad_out of channels ch, ch + 1 (a missing odd last channel reads 0 and is not written)
+    for (int e = lane; e < 2 * nbins; e += kWave) {
+      const int hh = e >= nbins ? 1 : 0;
+      gv[hh * kWave + (e - hh * nbins)] = (ch + hh < nch) ? go[(ch + hh) * nbins + (e - hh * nbins)] : 0.0f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* f = gbase + (int64_t)(ch + h) * scs;
+    const bool live = xv && ch + h < nch;
+    float acc = 0.0f;
+    for (int i = 0; i < nyv; ++i) {
+      const int ye = yent[i];
+      const int row = ye >> 16, py = ye & 0xffff;
+      const float wy = yw[i];
+      const float gvv = gv[h * kWave + py * pw + my_px];
+      acc = acc + (live ? gvv * (wy * my_wx) * 0.25f : 0.0f);  // (g * w) / count, count = 4
+      if (i + 1 == nyv || (yent[i + 1] >> 16) != row) {  // end of this row's entries (uniform)
+        float sum = acc;
+#pragma unroll
+        for (int d = 1; d < kSepEnt; d <<= 1) {
+          const float t = __shfl_down(sum, d, 32);
+          if (d <= trail) sum = sum + t;
+        }
+        if (head && live && sum != 0.0f) atomicAdd(&f[(int64_t)row * sy + (int64_t)my_col * sx], sum);
+        acc = 0.0f;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward into a channels-last gradient (sampling 2, ph*pw <= 64, C % 16 == 0):
 // the default.  Global float atomics execute at the memory side as 64-B
 // requests (MI355X_MICROARCH.md, global float atomics): the NCHW flush above
@@ -2183,6 +2335,8 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   for (int l = 0; l < lv.L; ++l) cl = cl && lv.sc[l] == 1 && lv.w[l] <= kClBandCells;
   if (cl)
     hipLaunchKernelGGL(roi_align_bwd_cl_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
+  else if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
+    hipLaunchKernelGGL(roi_align_bwd_sep_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   else if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
     hipLaunchKernelGGL(roi_align_bwd_lds_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   else

@@ -145,79 +145,93 @@ __device__ __forceinline__ SwLevel sweep_level(const RoiLevels& lv, int l, int b
   return q;
 }
 
-// Workgroup = (image b, channel pair cp): sweeps every level that has RoIs of
-// image b, finest first, as one continuous row stream through the ring.
-template <int NI>
-__global__ void __launch_bounds__(kSwThreads) roi_sweep_fwd_kernel(RoiLevels lv, RoiCfg c, SwArgs A, SwPlan P,
-                                                                   float* __restrict__ out, int64_t* dbg) {
-  // dbg (diagnostics only; nullptr in product runs): per workgroup 8 x int64 s_memrealtime stamps
-  const int64_t t_start = dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  constexpr int RS = (32 * NI + 1) * 8;  // ring row: 32 NI cells x 2 channels (+1 cell: bank spread)
-  // dynamic LDS only (no static __shared__ in front): the ring stays 16-B aligned
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int* sc = reinterpret_cast<int*>(smem);  // [0] total items, [1] passes, [2] global steps
-  int* lvi = sc + 4;                       // per level: hi, gbase (global step of its step 0), sbase
-  char* ring = smem + 128;
-  int2* pass = reinterpret_cast<int2*>(ring + kSwRing * RS);  // {i0, n | level << 16 | first << 31}
-  int* cnt = reinterpret_cast<int*>(pass + A.max_pass);     // [max_slots]: counts -> offsets
-  int* cur = cnt + A.max_slots;                             // [max_slots]: pass bases, then cursors
-  uint16_t* list = reinterpret_cast<uint16_t*>(cur + A.max_slots);
-  uint8_t* glev = reinterpret_cast<uint8_t*>(list + A.nitems);  // [max_slots]: level of global step g
+// LDS carve-up shared by the forward and backward sweeps (dynamic LDS only: no static
+// __shared__ in front, so the ring stays 16-B aligned).
+struct SwLds {
+  int* sc;         // [0] total items, [1] passes, [2] global steps
+  int* lvi;        // per level: last swept step, gbase (global step of its step 0), slot base
+  char* ring;      // kSwRing rows x RS bytes
+  int2* pass;      // [max_pass] {i0, n | level << 16 | first << 31}
+  int* cnt;        // [max_slots] counts -> item offsets
+  int* cur;        // [max_slots] pass bases, then scatter cursors
+  uint16_t* list;  // [nitems] item ids by (level, step)
+  uint8_t* glev;   // [max_slots] level of global step g
+};
 
+__device__ __forceinline__ SwLds sweep_lds(char* smem, const SwArgs& A, int RS) {
+  SwLds d;
+  d.sc = reinterpret_cast<int*>(smem);
+  d.lvi = d.sc + 4;
+  d.ring = smem + 128;
+  d.pass = reinterpret_cast<int2*>(d.ring + kSwRing * RS);
+  d.cnt = reinterpret_cast<int*>(d.pass + A.max_pass);
+  d.cur = d.cnt + A.max_slots;
+  d.list = reinterpret_cast<uint16_t*>(d.cur + A.max_slots);
+  d.glev = reinterpret_cast<uint8_t*>(d.list + A.nitems);
+  return d;
+}
+
+__device__ __forceinline__ int sweep_nst(const RoiLevels& lv, int l) { return (lv.h[l] + kSwStep - 1) / kSwStep; }
+__device__ __forceinline__ int sweep_sbase(const RoiLevels& lv, int l) {  // a level's steps, then its long-span slot
+  int s0 = 0;
+  for (int m = 0; m < l; ++m) s0 += sweep_nst(lv, m) + 1;
+  return s0;
+}
+
+// Buckets the items of image b by (level, step) in LDS and builds the pass table.
+// kAll: sweep every step of every level (backward: every gradient row is written);
+// else each level up to its last step with items (levels without items: skipped).
+template <bool kAll>
+__device__ void sweep_prologue(const RoiLevels& lv, const RoiCfg& c, const SwArgs& A, const SwPlan& P, const SwLds& d,
+                               int b) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int b = blockIdx.x / A.np, cp = blockIdx.x - b * A.np;
   const int L = lv.L;
-  auto nst_of = [&](int l) { return (lv.h[l] + kSwStep - 1) / kSwStep; };
-  auto sbase_of = [&](int l) {  // slot base of level l: its steps, then its long-span slot
-    int s0 = 0;
-    for (int m = 0; m < l; ++m) s0 += nst_of(m) + 1;
-    return s0;
-  };
-  const int nslots = sbase_of(L);
-
-  // ---- items of image b, bucketed by (level, step) in LDS; thread t takes a contiguous run of RoIs
-  for (int i = tid; i < nslots; i += kSwThreads) cnt[i] = 0;
+  const int nslots = sweep_sbase(lv, L);
+  for (int i = tid; i < nslots; i += kSwThreads) d.cnt[i] = 0;
   __syncthreads();
-  const int K = (int)c.K, ph = c.ph, pw = c.pw, nbins = ph * pw;
+  // thread t takes a contiguous run of RoIs: the lanes of a wave hit different steps (little LDS contention)
+  const int K = (int)c.K, ph = c.ph, pw = c.pw;
   const int per_t = (K + kSwThreads - 1) / kSwThreads;
   const int kb = tid * per_t, ke = min(K, kb + per_t);
   for (int k = kb; k < ke; ++k) {
     const uint32_t k0 = P.key[k * ph];
     const int bl = (int)(k0 >> 16), kbimg = bl / L;
     if (kbimg != b) continue;
-    const int l = bl - kbimg * L, s0 = sbase_of(l), big = s0 + nst_of(l);
+    const int l = bl - kbimg * L, s0 = sweep_sbase(lv, l), big = s0 + sweep_nst(lv, l);
     for (int py = 0; py < ph; ++py) {
       const uint32_t st = P.key[k * ph + py] & 0xffffu;
-      atomicAdd(&cnt[st == kSwBig ? big : s0 + (int)st], 1);
+      atomicAdd(&d.cnt[st == kSwBig ? big : s0 + (int)st], 1);
     }
   }
   __syncthreads();
   const int ipp = kSwLanes / pw;  // items per pass
   if (wave == 0) {
-    // per level: last step with items; global steps; exclusive scans of item offsets and pass bases
     int g = 0;
     for (int l = 0; l < L; ++l) {
-      const int s0 = sbase_of(l), n = nst_of(l);
-      int hi = -1;
-      for (int b0 = 0; b0 < n; b0 += kWave) {
-        const uint64_t m = __ballot(b0 + lane < n && cnt[s0 + b0 + lane] > 0);
-        if (m) hi = b0 + 63 - __clzll(m);
+      const int s0 = sweep_sbase(lv, l), n = sweep_nst(lv, l);
+      int hi = n - 1;
+      if (!kAll) {
+        hi = -1;
+        for (int b0 = 0; b0 < n; b0 += kWave) {
+          const uint64_t m = __ballot(b0 + lane < n && d.cnt[s0 + b0 + lane] > 0);
+          if (m) hi = b0 + 63 - __clzll(m);
+        }
       }
       if (lane == 0) {
-        lvi[3 * l] = hi;
-        lvi[3 * l + 1] = g;
-        lvi[3 * l + 2] = s0;
+        d.lvi[3 * l] = hi;
+        d.lvi[3 * l + 1] = g;
+        d.lvi[3 * l + 2] = s0;
       }
-      for (int j = lane; j <= hi; j += kWave) glev[g + j] = (uint8_t)l;
+      for (int j = lane; j <= hi; j += kWave) d.glev[g + j] = (uint8_t)l;
       g += hi + 1;
     }
     int run = 0, prun = 0;
     for (int l = 0; l < L; ++l) {
-      const int s0 = sbase_of(l), n = nst_of(l), hi = lvi[3 * l];
+      const int s0 = sweep_sbase(lv, l), n = sweep_nst(lv, l), hi = d.lvi[3 * l];
       for (int b0 = 0; b0 <= n; b0 += kWave) {  // steps 0 .. n - 1 and the long-span slot n
         const int j = b0 + lane;
-        const int v = j <= n ? cnt[s0 + j] : 0;
+        const int v = j <= n ? d.cnt[s0 + j] : 0;
         const int np = j <= hi ? max(1, (v + ipp - 1) / ipp) : 0;
         int inc = v, pinc = np;
 #pragma unroll
@@ -226,47 +240,90 @@ __global__ void __launch_bounds__(kSwThreads) roi_sweep_fwd_kernel(RoiLevels lv,
           if (lane >= o) inc += u, pinc += pu;
         }
         if (j <= n) {
-          cnt[s0 + j] = run + inc - v;
-          cur[s0 + j] = prun + pinc - np;
+          d.cnt[s0 + j] = run + inc - v;
+          d.cur[s0 + j] = prun + pinc - np;
         }
         run += __shfl(inc, kWave - 1, kWave);
         prun += __shfl(pinc, kWave - 1, kWave);
       }
     }
     if (lane == 0) {
-      sc[0] = run;
-      sc[1] = prun;
-      sc[2] = g;
+      d.sc[0] = run;
+      d.sc[1] = prun;
+      d.sc[2] = g;
     }
   }
   __syncthreads();
-  const int total = sc[0], npass = sc[1], G = sc[2];
-  if (total == 0) return;  // image without RoIs: uniform exit (nothing in flight yet)
-  // pass table; then the scatter cursors
+  // pass table (at least one pass per swept step), then the scatter cursors
   for (int f = tid; f < nslots; f += kSwThreads) {
     int l = 0;
-    while (l + 1 < L && sbase_of(l + 1) <= f) ++l;
-    const int s = f - sbase_of(l);
-    if (s > lvi[3 * l]) continue;  // past the level's last step, or its long-span slot
-    const int i0 = cnt[f], n = cnt[f + 1] - i0, pb = cur[f];
+    while (l + 1 < L && sweep_sbase(lv, l + 1) <= f) ++l;
+    const int s = f - sweep_sbase(lv, l);
+    if (s > d.lvi[3 * l]) continue;  // past the level's last swept step, or its long-span slot
+    const int i0 = d.cnt[f], n = d.cnt[f + 1] - i0, pb = d.cur[f];
     const int np = max(1, (n + ipp - 1) / ipp);
     for (int j = 0; j < np; ++j)
-      pass[pb + j] = make_int2(i0 + j * ipp, min(ipp, n - j * ipp) | (l << 16) | (j == 0 ? (int)0x80000000 : 0));
+      d.pass[pb + j] = make_int2(i0 + j * ipp, min(ipp, n - j * ipp) | (l << 16) | (j == 0 ? (int)0x80000000 : 0));
   }
   __syncthreads();
-  for (int f = tid; f < nslots; f += kSwThreads) cur[f] = cnt[f];
+  for (int f = tid; f < nslots; f += kSwThreads) d.cur[f] = d.cnt[f];
   __syncthreads();
   for (int k = kb; k < ke; ++k) {
     const uint32_t k0 = P.key[k * ph];
     const int bl = (int)(k0 >> 16), kbimg = bl / L;
     if (kbimg != b) continue;
-    const int l = bl - kbimg * L, s0 = sbase_of(l), big = s0 + nst_of(l);
+    const int l = bl - kbimg * L, s0 = sweep_sbase(lv, l), big = s0 + sweep_nst(lv, l);
     for (int py = 0; py < ph; ++py) {
       const uint32_t st = P.key[k * ph + py] & 0xffffu;
-      list[atomicAdd(&cur[st == kSwBig ? big : s0 + (int)st], 1)] = (uint16_t)(k * ph + py);
+      d.list[atomicAdd(&d.cur[st == kSwBig ? big : s0 + (int)st], 1)] = (uint16_t)(k * ph + py);
     }
   }
   __syncthreads();
+}
+
+// Unpacked taps of one bin (sampling ratio 2): rows / columns of the 2 x 2 samples.
+struct SwTaps {
+  int ylo[2], yhi[2], xlo[2], xhi[2];
+  float ly[2], lx[2];
+};
+
+__device__ __forceinline__ SwTaps sweep_taps(const int4& item, const int4& xtap) {
+  SwTaps t;
+  t.ylo[0] = (int)(short)(item.x & 0xffff), t.yhi[0] = item.x >> 16;
+  t.ylo[1] = (int)(short)(item.y & 0xffff), t.yhi[1] = item.y >> 16;
+  t.xlo[0] = (int)(short)(xtap.x & 0xffff), t.xhi[0] = xtap.x >> 16;
+  t.xlo[1] = (int)(short)(xtap.y & 0xffff), t.xhi[1] = xtap.y >> 16;
+  t.ly[0] = __int_as_float(item.z), t.ly[1] = __int_as_float(item.w);
+  t.lx[0] = __int_as_float(xtap.z), t.lx[1] = __int_as_float(xtap.w);
+  return t;
+}
+
+// Workgroup = (image b, channel pair cp): sweeps every level that has RoIs of
+// image b, finest first, as one continuous row stream through the ring.
+template <int NI>
+__global__ void __launch_bounds__(kSwThreads) roi_sweep_fwd_kernel(RoiLevels lv, RoiCfg c, SwArgs A, SwPlan P,
+                                                                   float* __restrict__ out, int64_t* dbg) {
+  // dbg (diagnostics only; nullptr in product runs): per workgroup 8 x int64 s_memrealtime stamps
+  const int64_t t_start = dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  constexpr int RS = (32 * NI + 1) * 8;  // ring row: 32 NI cells x 2 channels (+1 cell: bank spread)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SwLds D = sweep_lds(smem, A, RS);
+  char* ring = D.ring;
+  const int2* pass = D.pass;
+  const int* cnt = D.cnt;
+  const uint16_t* list = D.list;
+  const uint8_t* glev = D.glev;
+  const int* lvi = D.lvi;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int b = blockIdx.x / A.np, cp = blockIdx.x - b * A.np;
+  const int L = lv.L;
+  const int ph = c.ph, pw = c.pw, nbins = ph * pw;
+  const int nslots = sweep_sbase(lv, L);
+  auto nst_of = [&](int l) { return sweep_nst(lv, l); };
+  sweep_prologue<false>(lv, c, A, P, D, b);
+  const int total = D.sc[0], npass = D.sc[1], G = D.sc[2];
+  if (total == 0) return;  // image without RoIs: uniform exit (nothing in flight yet)
   const int64_t t_list = dbg ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
   if (wave < kSwLoad) {
@@ -421,6 +478,166 @@ __global__ void __launch_bounds__(kSwThreads) roi_sweep_fwd_kernel(RoiLevels lv,
   }
 }
 
+// Backward as the same sweep, run in reverse roles.  The ring holds the gradient
+// rows of this (image, channel pair) being accumulated: a step's rows enter the
+// ring zeroed, every item adds its bins' weighted grad_out into them with LDS
+// float atomics (the reference's grad * w / count per tap), and a row is written
+// to the gradient tensor with plain stores once no later item can touch it
+// (3 steps later: an item of step s reaches back kSwSpan - 1 rows).  Every
+// gradient element of every level is written exactly once (rows without
+// contributions as zeros), so the gradient needs no clearing and no global
+// atomics.  Long-span items add with global atomics after the sweep.  Like
+// torchvision's CUDA backward, the summation order (and the last bits) depends
+// on the order of the LDS atomics.
+template <int NI, int kMode = 0>  // kMode (diagnostics): 1 = plain LDS read-modify-write, 2 = no LDS update
+__global__ void __launch_bounds__(kSwThreads) roi_sweep_bwd_kernel(RoiLevels lv, RoiCfg c, SwArgs A, SwPlan P,
+                                                                   const float* __restrict__ gout) {
+  constexpr int RS = (32 * NI + 1) * 8;
+  static_assert(kSwSpan <= 2 * kSwStep + 1, "rows are flushed 3 steps after they enter the ring");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SwLds D = sweep_lds(smem, A, RS);
+  char* ring = D.ring;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int b = blockIdx.x / A.np, cp = blockIdx.x - b * A.np;
+  const int L = lv.L;
+  const int ph = c.ph, pw = c.pw, nbins = ph * pw;
+  sweep_prologue<true>(lv, c, A, P, D, b);
+  const int total = D.sc[0], npass = D.sc[1], G = D.sc[2];
+  const int* lvi = D.lvi;
+
+  if (wave < kSwLoad) {
+    // ---- flushers: row kSwStep s + wave of each step: zero it on entry, write it out 3 steps later
+    auto slot = [&](int g) { return ring + ((g * kSwStep + wave) & (kSwRing - 1)) * RS; };
+    auto zero = [&](int g) {
+      float4* r = reinterpret_cast<float4*>(slot(g));
+      for (int e = lane; e < 16 * NI; e += kWave) r[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto flush = [&](int g) {
+      if (g < 0 || g >= G) return;
+      const int l = D.glev[g];
+      const int y = (g - lvi[3 * l + 1]) * kSwStep + wave, H = lv.h[l], W = lv.w[l];
+      if (y >= H) return;
+      const f32x2* r = reinterpret_cast<const f32x2*>(slot(g));
+      float* g0 = lv.grad[l] + (int64_t)b * lv.sb[l] + (int64_t)(2 * cp) * lv.sc[l] + (int64_t)y * lv.sy[l];
+      float* g1 = g0 + lv.sc[l];
+      for (int x = lane; x < W; x += kWave) {
+        const f32x2 v = r[x];
+        g0[x] = v.x;
+        g1[x] = v.y;
+      }
+    };
+    zero(0);
+    for (int g = 0; g < G; ++g) {
+      __syncthreads();  // step g is being evaluated; steps <= g - 1 are done
+      flush(g - 3);
+      zero(g + 1);
+    }
+    __syncthreads();  // the last step is done
+    flush(G - 3);
+    flush(G - 2);
+    flush(G - 1);
+    __threadfence();  // the rows are visible before the long-span atomics add on top
+    __syncthreads();
+    return;
+  }
+
+  // ---- compute waves: lane = (item slot qi, px) of a pass, one bin per pass
+  const int q = (wave - kSwLoad) * kWave + lane;
+  const int qi = q / pw, qx = q - qi * pw;
+  struct SwGBin {
+    int id;
+    int4 item, xtap;
+    float g0, g1;
+  };
+  auto load_bin = [&](int id, int px) {
+    SwGBin r;
+    r.id = id;
+    const int i = id >= 0 ? id : 0;
+    const int k = i / ph, py = i - k * ph;
+    r.item = P.item[i];
+    r.xtap = P.xtap[(int64_t)k * pw + px];
+    const float* go = gout + ((int64_t)k * c.C + 2 * cp) * nbins + py * pw + px;
+    r.g0 = go[0];
+    r.g1 = go[nbins];
+    return r;
+  };
+  auto fetch = [&](int p) {
+    const int2 d = D.pass[p];
+    return load_bin(qi < (d.y & 0xffff) ? (int)D.list[d.x + qi] : -1, qx);
+  };
+  // kRing: add into the ring (level row y -> slot (row0 + y) & mask), else global atomics
+  auto scatter = [&](const SwGBin& r, int row0, float* g0, int64_t sy, int64_t sc, auto to_ring) {
+    constexpr bool kRing = decltype(to_ring)::value;
+    if (r.id < 0) return;
+    const SwTaps t = sweep_taps(r.item, r.xtap);
+#pragma unroll
+    for (int iy = 0; iy < 2; ++iy) {
+      if (t.ylo[iy] < 0) continue;
+      const float hy = 1.0f - t.ly[iy];
+#pragma unroll
+      for (int ix = 0; ix < 2; ++ix) {
+        if (t.xlo[ix] < 0) continue;
+        const float hx = 1.0f - t.lx[ix];
+        const float w[4] = {hy * hx, hy * t.lx[ix], t.ly[iy] * hx, t.ly[iy] * t.lx[ix]};
+        const int ys[4] = {t.ylo[iy], t.ylo[iy], t.yhi[iy], t.yhi[iy]};
+        const int xs[4] = {t.xlo[ix], t.xhi[ix], t.xlo[ix], t.xhi[ix]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a0 = r.g0 * w[e] * 0.25f, a1 = r.g1 * w[e] * 0.25f;  // (g * w) / count, count = 4
+          if constexpr (kRing) {
+            float* cell = reinterpret_cast<float*>(ring + ((row0 + ys[e]) & (kSwRing - 1)) * RS) + 2 * xs[e];
+            if (kMode == 0) {
+              atomicAdd(cell, a0);
+              atomicAdd(cell + 1, a1);
+            } else if (kMode == 1) {
+              cell[0] += a0;
+              cell[1] += a1;
+            } else if (a0 == 1234.5f) {
+              cell[0] = a1;
+            }
+          } else {
+            float* cell = g0 + ys[e] * sy + xs[e];
+            atomicAdd(cell, a0);
+            atomicAdd(cell + sc, a1);
+          }
+        }
+      }
+    }
+  };
+  SwGBin qb[kSwDepth];
+#pragma unroll
+  for (int u = 0; u < kSwDepth; ++u)
+    if (u < npass) qb[u] = fetch(u);
+  for (int p0 = 0; p0 < npass; p0 += kSwDepth) {
+#pragma unroll
+    for (int u = 0; u < kSwDepth; ++u) {
+      const int p = p0 + u;
+      if (p < npass) {
+        const int d = D.pass[p].y;
+        if (d < 0) __syncthreads();  // first pass of a step (uniform)
+        const int l = (d >> 16) & 0x7fff;
+        const SwGBin cu = qb[u];
+        if (p + kSwDepth < npass) qb[u] = fetch(p + kSwDepth);
+        scatter(cu, lvi[3 * l + 1] * kSwStep, nullptr, 0, 0, std::true_type{});
+      }
+    }
+  }
+  __syncthreads();  // the last step is done (the flushers write the last rows)
+  __syncthreads();  // ... and have written them
+  // ---- long-span items of every level: global atomics on top of the written rows (rare)
+  for (int l = 0; l < L; ++l) {
+    const int s0 = lvi[3 * l + 2], bs = s0 + sweep_nst(lv, l);
+    const int nb = (l + 1 < L ? D.cnt[bs + 1] : total) - D.cnt[bs];
+    if (nb <= 0) continue;
+    float* g0 = lv.grad[l] + (int64_t)b * lv.sb[l] + (int64_t)(2 * cp) * lv.sc[l];
+    for (int f = q; f < nb * pw; f += kSwLanes) {
+      const int fi = f / pw, px = f - fi * pw;
+      scatter(load_bin((int)D.list[D.cnt[bs] + fi], px), 0, g0, lv.sy[l], lv.sc[l], std::false_type{});
+    }
+  }
+}
+
 struct SwLayout {
   size_t key, item, xtap, total;
 };
@@ -529,4 +746,73 @@ extern "C" int32_t frh_roi_align_fwd_sweep(int32_t num_levels, const float* cons
   else
     hipLaunchKernelGGL(roi_sweep_fwd_kernel<8>, grid, dim3(kSwThreads), lds, st, lv, c, A, P, out, dbg);
   return check_launch("frh_roi_align_fwd_sweep");
+}
+
+extern "C" int32_t frh_roi_align_bwd_sweep(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
+                                           const int64_t* strides, const float* scales, int32_t batch,
+                                           int32_t channels, const float* rois, const int64_t* roi_levels,
+                                           int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                                           int32_t sampling_ratio, int32_t aligned, const float* grad_out,
+                                           void* workspace, size_t ws_bytes, void* stream) {
+  FRH_REQUIRE(batch >= 1 && channels >= 1 && num_rois >= 0 && pooled_h >= 1 && pooled_w >= 1, "bad sizes");
+  FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS && feat_hw && strides && scales, "bad levels");
+  FRH_REQUIRE(grad_feats, "null pointer argument");
+  RoiLevels lv;
+  lv.L = num_levels;
+  for (int l = 0; l < num_levels; ++l) {
+    lv.feat[l] = nullptr;
+    lv.grad[l] = grad_feats[l];
+    lv.h[l] = feat_hw[2 * l];
+    lv.w[l] = feat_hw[2 * l + 1];
+    FRH_REQUIRE(lv.h[l] > 0 && lv.w[l] > 0, "level %d has an empty feature map", l);
+    lv.sb[l] = strides[4 * l];
+    lv.sc[l] = strides[4 * l + 1];
+    lv.sy[l] = strides[4 * l + 2];
+    lv.sx[l] = strides[4 * l + 3];
+    lv.scale[l] = scales[l];
+  }
+  int ni = 0, max_slots = 0, max_pass = 0;
+  size_t lds = 0;
+  const SwLayout z = sweep_layout(num_rois, pooled_h, pooled_w);
+  hipStream_t st = as_stream(stream);
+  const bool ok = num_rois > 0 && rois && grad_out && workspace && ws_bytes >= z.total &&
+                  sweep_supported(lv, batch, channels, num_rois, pooled_h, pooled_w, sampling_ratio, &ni, &max_slots,
+                                  &max_pass, &lds);
+  if (!ok) {  // the caller clears the gradient and takes frh_roi_align_bwd_strided
+    set_error("frh_roi_align_bwd_sweep: shape / layout / workspace outside the sweep kernel");
+    return FRH_EUNSUPPORTED;
+  }
+  char* ws = static_cast<char*>(workspace);
+  SwPlan P{reinterpret_cast<uint32_t*>(ws + z.key), reinterpret_cast<int4*>(ws + z.item),
+           reinterpret_cast<int4*>(ws + z.xtap)};
+  RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+  const int64_t nplan = num_rois * std::max(pooled_h, pooled_w);
+  hipLaunchKernelGGL(roi_sweep_plan_kernel, dim3((unsigned)((nplan + 255) / 256)), dim3(256), 0, st, lv, c, batch, P);
+  SwArgs A{batch, channels / 2, max_slots, (int)(num_rois * pooled_h), max_pass};
+  const dim3 grid((unsigned)(batch * (channels / 2)));
+  static bool attr_done[4] = {false, false, false, false};
+  const void* fn = ni == 1 ? (const void*)roi_sweep_bwd_kernel<1, 0> : ni == 2 ? (const void*)roi_sweep_bwd_kernel<2, 0>
+                 : ni == 4 ? (const void*)roi_sweep_bwd_kernel<4, 0> : (const void*)roi_sweep_bwd_kernel<8, 0>;
+  const int ai = ni == 1 ? 0 : (ni == 2 ? 1 : (ni == 4 ? 2 : 3));
+  if (!attr_done[ai]) {
+    FRH_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_done[ai] = true;
+  }
+  static int bwd_mode = -1;
+  if (bwd_mode < 0) bwd_mode = getenv("FRH_SWEEP_BWD_MODE") ? atoi(getenv("FRH_SWEEP_BWD_MODE")) : 0;
+  if (ni == 8 && bwd_mode == 1) {
+    FRH_HIP(hipFuncSetAttribute((const void*)roi_sweep_bwd_kernel<8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipLaunchKernelGGL((roi_sweep_bwd_kernel<8, 1>), grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  } else if (ni == 8 && bwd_mode == 2) {
+    FRH_HIP(hipFuncSetAttribute((const void*)roi_sweep_bwd_kernel<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipLaunchKernelGGL((roi_sweep_bwd_kernel<8, 2>), grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  } else if (ni == 1)
+    hipLaunchKernelGGL(roi_sweep_bwd_kernel<1>, grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  else if (ni == 2)
+    hipLaunchKernelGGL(roi_sweep_bwd_kernel<2>, grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  else if (ni == 4)
+    hipLaunchKernelGGL(roi_sweep_bwd_kernel<4>, grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  else
+    hipLaunchKernelGGL(roi_sweep_bwd_kernel<8>, grid, dim3(kSwThreads), lds, st, lv, c, A, P, grad_out);
+  return check_launch("frh_roi_align_bwd_sweep");
 }
