@@ -395,3 +395,55 @@ def multiclass_nms(bbox, score, nms_channel, nms_iou, min_score=-1, max_num=None
     if max_num is not None and ks.size > max_num:
         kb, ks, kl = kb[:max_num], ks[:max_num], kl[:max_num]
     return kb, ks, kl
+
+
+# ------------------------------------------------------------------ losses (float64 restatements)
+def sigmoid_focal_loss(pred, target, alpha=0.25, gamma=2.0):
+    """lib/losses.py:33-61 summed, in float64: pred [n, C] logits, target [n] (0 = background,
+    k -> one-hot column k-1); BCE-with-logits * (alpha_t * (1 - p_t) ** gamma)."""
+    x = np.asarray(pred, np.float64)
+    t = np.zeros_like(x)
+    tg = np.asarray(target, np.int64)
+    fg = tg > 0
+    t[np.nonzero(fg)[0], tg[fg] - 1] = 1.0
+    p = 1.0 / (1.0 + np.exp(-x))
+    pt = p * t + (1 - p) * (1 - t)
+    w = (alpha * t + (1 - alpha) * (1 - t)) * (1 - pt) ** gamma
+    bce = np.maximum(x, 0) - x * t + np.log1p(np.exp(-np.abs(x)))
+    return float((bce * w).sum())
+
+
+def smooth_l1_v2(x, y, beta):
+    """lib/losses.py:77-83 summed, in float64."""
+    d = np.abs(np.asarray(x, np.float64) - np.asarray(y, np.float64))
+    return float(np.where(d < beta, d * d / (2 * beta), d - 0.5 * beta).sum())
+
+
+def anchor_head_loss(level_cls, level_reg, level_anchors, strides, gts, labels, img_shape, assign, allowed_border,
+                     beta, cls_channels, means=(0, 0, 0, 0), stds=(1, 1, 1, 1)):
+    """AnchorHead.loss for a sigmoid focal-loss head without sampler (lib/heads/anchor_head.py:152-199,
+    per-image targets :69-111, calc_loss :113-139, avg_factor = #positives).
+    level_cls / level_reg: per level [B, A*C, H, W] / [B, A*4, H, W]; level_anchors: per level
+    [4, A, H, W].  Returns (cls_loss, reg_loss, (tar_cls_out, tar_reg_out, tar_labels, tar_param))
+    with the targets concatenated in image order."""
+    A = level_anchors[0].shape[1]
+    anc = np.concatenate([a.reshape(4, -1) for a in level_anchors], 1)
+    ingrid = np.concatenate([inside_grid_mask(A, img_shape, a.shape[2:], s)
+                             for a, s in zip(level_anchors, strides)]).astype(bool)
+    mask = ingrid & inside_anchor_mask(anc, img_shape, allowed_border)
+    outs = [[] for _ in range(4)]
+    for b in range(len(gts)):
+        co = np.concatenate([c[b].reshape(cls_channels, -1) for c in level_cls], 1)
+        ro = np.concatenate([r[b].reshape(4, -1) for r in level_reg], 1)
+        t = anchor_target(co, ro, cls_channels, anc[:, mask], mask, gts[b], labels[b], assign, None, means, stds)
+        for k, v in enumerate((t[0], t[1], t[2], t[5])):
+            outs[k].append(v)
+    tc, tr = np.concatenate(outs[0], 1), np.concatenate(outs[1], 1)
+    tl, tp = np.concatenate(outs[2]), np.concatenate(outs[3], 1)
+    pos = tl > 0
+    npos = int(pos.sum())
+    if tl.size == 0:
+        return 0.0, 0.0, (tc, tr, tl, tp)
+    cls_loss = sigmoid_focal_loss(tc.T, tl) / npos if npos else float('inf')
+    reg_loss = smooth_l1_v2(tr[:, pos], tp[:, pos], beta) / npos if npos else 0.0
+    return cls_loss, reg_loss, (tc, tr, tl, tp)

@@ -615,6 +615,35 @@ def test_retina_loss_vs_reference(dev, golden):
         np.testing.assert_allclose([float(c), float(r)], g['loss_{}'.format(i)], rtol=1e-5)
 
 
+def test_retina_loss_batch8_equal_per_image_oracle(dev):
+    """cfg3 at its benchmark batch: RetinaHead.loss on 8 images in ONE batched target pass.
+    The batched targets (chosen outputs, labels exact; params 1e-5) equal the per-image oracle
+    results concatenated in image order, and the focal / smooth-L1 losses equal the oracle's
+    float64 sums over them (f32 device sums over ~1M terms -> rtol 2e-5)."""
+    from frcnn_amd.config import ConfigDict
+    gts = inputs.voc_gts()[4:12]
+    head = _retina_head(dev)
+    cfg = ConfigDict(dict(assigner=dict(type='MaxIoUAssigner', pos_iou=0.5, neg_iou=0.4, min_pos_iou=0.0),
+                          allowed_border=-1))
+    cls, reg = inputs.head_outputs(960, inputs.RETINA_GRIDS, 9, 20, batch=8, cls_scale=1.0, reg_scale=0.2)
+    args = ([T(x, dev) for x in cls], [T(x, dev) for x in reg], [T(x[0], dev) for x in gts],
+            [T(x[1], dev) for x in gts], [inputs.img_meta()] * 8, cfg)
+    tc, tr, tl, tp = head.targets_batched(*args)
+    c, r = head.loss(*args)
+    strides, grids = inputs.RETINA_STRIDES, inputs.RETINA_GRIDS
+    anc = [oracle.anchor_grid(s, [4 * 2 ** (i / 3) for i in range(3)], [0.5, 1.0, 2.0], s, g)
+           for s, g in zip(strides, grids)]
+    rc, rr, (oc, orr, ol, op) = oracle.anchor_head_loss(cls, reg, anc, strides, [x[0] for x in gts],
+                                                        [x[1] for x in gts], inputs.IMG_SHAPE, (0.5, 0.4, 0.0), -1,
+                                                        1.0 / 9.0, 20)
+    assert tl.numel() == ol.size and int((ol > 0).sum()) > 8
+    np.testing.assert_array_equal(tl.cpu().numpy(), ol)
+    np.testing.assert_array_equal(tc.detach().cpu().numpy(), oc)
+    np.testing.assert_array_equal(tr.detach().cpu().numpy(), orr)
+    np.testing.assert_allclose(tp.cpu().numpy(), op, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose([float(c), float(r)], [rc, rr], rtol=2e-5)
+
+
 def test_retina_predict_vs_reference(dev, golden):
     """cfg3 test path (anchor_head.py:207-262, strict multiclass NMS).  sigmoid / exp are
     device math (<= 1 ulp from torch CPU), so boxes/scores to 1e-4 and labels exact."""
@@ -658,18 +687,20 @@ def test_cascade_refine_vs_reference(dev, golden, agnostic):
 
 
 # ----------------------------------------------------------------- all BASELINE configs end to end
-@pytest.mark.parametrize('config', ['faster_rcnn_r50', 'faster_rcnn_r50_fpn', 'retinanet_r50_fpn',
-                                    'cascade_rcnn_r50_fpn', 'fcos_r50_fpn_atss'])
-def test_baseline_config_train_and_test(dev, config):
+@pytest.mark.parametrize('config,batch', [('faster_rcnn_r50', 2), ('faster_rcnn_r50_fpn', 2),
+                                          ('retinanet_r50_fpn', 2), ('retinanet_r50_fpn', 8),
+                                          ('cascade_rcnn_r50_fpn', 2), ('fcos_r50_fpn_atss', 2)])
+def test_baseline_config_train_and_test(dev, config, batch):
     """Every BASELINE.json config builds from its config file through the registry and runs
-    forward_train (+ backward) and forward_test on the HIP path (2 images, 600x1000)."""
+    forward_train (+ backward) and forward_test on the HIP path (600x1000 images; 2 per
+    batch, and cfg3 also at its benchmark batch of 8)."""
     import os
     import bench
     from frcnn_amd import set_sampler_mode
     set_sampler_mode('device', seed=3)
     path = os.path.join(bench.REPO, 'pytorch-faster-rcnn_amd', 'configs', config + '.py')
     model, _ = bench.make_model(dev, seed=0, config=path)
-    imgs, boxes, labels, metas = bench.make_batch(dev, 2, seed=1)
+    imgs, boxes, labels, metas = bench.make_batch(dev, batch, seed=1)
     losses = model.forward_train(imgs, boxes, labels, metas)
     assert len(losses) >= 2
     for k, v in losses.items():
@@ -678,7 +709,7 @@ def test_baseline_config_train_and_test(dev, config):
     model.eval()
     with torch.no_grad():
         preds = model.forward_test(imgs, metas)
-    assert len(preds) == 3 and len(preds[0]) == 2  # (boxes, scores, labels) per image
+    assert len(preds) == 3 and len(preds[0]) == batch  # (boxes, scores, labels) per image
     for b, s, l in zip(*preds):
         assert b.shape[0] == 4 and b.shape[1] == s.numel() == l.numel() <= 100
         if s.numel():

@@ -234,3 +234,22 @@ def test_multiclass_nms_vs_reference(golden, i):
     np.testing.assert_array_equal(kb, g['boxes_{}'.format(i)])
     np.testing.assert_array_equal(ks, g['scores_{}'.format(i)])
     np.testing.assert_array_equal(kl, g['labels_{}'.format(i)])
+
+
+def retina_level_anchors():
+    strides, grids, scales, ratios = CASES['retina']
+    return [oracle.anchor_grid(s, scales, ratios, s, g) for s, g in zip(strides, grids)]
+
+
+def test_retina_loss_oracle_vs_reference(golden):
+    """oracle.anchor_head_loss (sigmoid focal + smooth-L1 v2, MaxIoU 0.5/0.4/0.0, no sampler,
+    allowed_border -1) against the reference's AnchorHead.loss on two 2-image batches."""
+    g = golden('retina.npz')
+    gts = inputs.voc_gts()
+    anc = retina_level_anchors()
+    for i in range(2):
+        cls, reg = inputs.head_outputs(900 + i, inputs.RETINA_GRIDS, 9, 20, batch=2, cls_scale=1.0, reg_scale=0.2)
+        c, r, _ = oracle.anchor_head_loss(cls, reg, anc, inputs.RETINA_STRIDES,
+                                          [gts[2 * i + j][0] for j in range(2)], [gts[2 * i + j][1] for j in range(2)],
+                                          inputs.IMG_SHAPE, (0.5, 0.4, 0.0), -1, 1.0 / 9.0, 20)
+        np.testing.assert_allclose([c, r], g['loss_{}'.format(i)], rtol=1e-5)
