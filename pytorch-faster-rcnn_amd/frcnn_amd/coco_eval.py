@@ -10,8 +10,9 @@ not installed here, so this is a restatement of its published bbox algorithm
   scored as intersection / detection area;
 * per IoU threshold 0.50:0.05:0.95, greedy matching in score order to the best-IoU
   unmatched ground truth (crowd ground truths match repeatedly; a match to an ignored
-  ground truth ignores the detection); detections outside the area range unmatched and
-  ignored;
+  ground truth ignores the detection; a match is recorded as the ground truth's id, so
+  as in pycocotools a ground truth with id 0 never counts); detections outside the area
+  range unmatched and ignored;
 * accumulate: detections of all images merged by score (mergesort), cumulative TP/FP,
   precision made monotone from the right, sampled at 101 recall points
   (searchsorted 'left'; points past the last recall score 0);
@@ -98,7 +99,7 @@ class COCOEval:
                     if m == -1:
                         continue
                     dt_ig[ti, di] = g_ign[m]
-                    dtm[ti, di] = 1
+                    dtm[ti, di] = gts[m]['id']  # pycocotools keeps the gt id: a gt with id 0 never 'matches'
                     gtm[ti, m] = 1
         d_out = np.array([d['area'] < arng[0] or d['area'] > arng[1] for d in dts], bool).reshape(1, D)
         dt_ig = np.logical_or(dt_ig, np.logical_and(dtm == 0, np.repeat(d_out, T, 0)))

@@ -13,10 +13,20 @@ Replays use the convolution algorithms chosen before the capture, so graphed
 and eager trunks agree within MIOpen's f32 solver differences (a captured call
 may take another solver;
 ``tests/test_gpu_parity.py::test_graphed_trunk_matches_eager``).  Any batch whose
-shape, dtype or device differs from the captured one takes the eager path.
+shape, dtype or device differs from the captured one takes the eager path, and so
+does every batch after the trunk's parameters or buffers were moved, cast or
+replaced (the graph has their capture-time storage baked in).
+
+Output lifetime: every replay rewrites the same graph-owned output buffers.  Each
+replay bumps their autograd version counter, so a backward through outputs of an
+earlier replay raises instead of silently using the newer data, and
+``GraphedTrunk.replays`` / ``is_current(t)`` tell a caller whether a kept output
+is still the latest.  Callers that keep outputs across steps (gradient
+accumulation, profiling records) pass ``clone_outputs=True`` to get private copies.
 """
 import torch
 from torch import nn
+from torch.autograd.graph import increment_version
 
 
 class Trunk(nn.Module):
@@ -74,14 +84,17 @@ class GraphedTrunk:
     """The trunk's forward for one input shape captured as a hipGraph; ``matches(img)``
     says whether a batch can replay it."""
 
-    def __init__(self, trunk, sample_img, num_warmup_iters=3):
+    def __init__(self, trunk, sample_img, num_warmup_iters=3, clone_outputs=False):
         if not sample_img.is_cuda:
             raise RuntimeError('GraphedTrunk needs a HIP tensor (got {})'.format(sample_img.device))
         self.shape = tuple(sample_img.shape)
         self.dtype = sample_img.dtype
         self.device = sample_img.device
         self.trunk = trunk
+        self.clone_outputs = clone_outputs
+        self.replays = 0
         self.params = tuple(p for p in trunk.parameters() if p.requires_grad)
+        self._slots = self._state_slots()
         self.static_in = sample_img.detach().clone()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -93,14 +106,41 @@ class GraphedTrunk:
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.static_out = trunk(self.static_in)
 
+    def _state_slots(self):
+        """Every (owning dict, name, object, storage pointer) the capture baked in: the
+        trunk's submodules, parameters and buffers.  ``.to()``/``.half()``/``.cuda()``
+        give a tensor new storage; assigning a new Parameter, buffer or submodule
+        replaces the dict entry; either makes ``matches`` fail."""
+        slots = []
+        for mod in self.trunk.modules():
+            for d in (mod._modules, mod._parameters, mod._buffers):
+                for n, x in d.items():
+                    if x is not None:
+                        slots.append((d, n, x, x.data_ptr() if torch.is_tensor(x) else 0))
+        return slots
+
+    def state_unchanged(self):
+        for d, n, x, ptr in self._slots:  # ~0.2 us per entry: one dict lookup + pointer compare
+            if d.get(n) is not x or (ptr and x.data_ptr() != ptr):
+                return False
+        return True
+
     def matches(self, img):
         return (img.is_cuda and tuple(img.shape) == self.shape and img.dtype == self.dtype
-                and img.device == self.device)
+                and img.device == self.device and self.state_unchanged())
 
     def replay(self, img):
         if img.data_ptr() != self.static_in.data_ptr():
             self.static_in.copy_(img)
         self.graph.replay()
+        self.replays += 1
+        for o in self.static_out:
+            increment_version(o)
+
+    def is_current(self, t):
+        """True when ``t`` (an output of this trunk) still holds the data of the replay that
+        returned it, i.e. no later replay has overwritten it (cloned outputs always are)."""
+        return getattr(t, '_frh_replay', self.replays) == self.replays
 
     def __call__(self, img):
         if torch.is_grad_enabled():
@@ -108,17 +148,22 @@ class GraphedTrunk:
         else:
             self.replay(img)
             outs = tuple(o.detach() for o in self.static_out)
+        if self.clone_outputs:
+            outs = tuple(o.clone() for o in outs)
+        else:
+            for o in outs:
+                o._frh_replay = self.replays
         return split_trunk_outputs(outs)
 
 
-def capture_trunk(detector, sample_img, num_warmup_iters=3):
+def capture_trunk(detector, sample_img, num_warmup_iters=3, clone_outputs=False):
     """Capture ``detector``'s backbone + neck + RPN head convs for ``sample_img``'s shape and
     attach it (``detector.graphed_trunk``).  Call after any convolution-algorithm search
     (``torch.backends.cudnn.benchmark`` warmup): the capture freezes the chosen kernels."""
     neck = detector.neck if getattr(detector, 'with_neck', False) else None
     trunk = Trunk(detector.backbone, neck, detector.rpn_head)
     torch.cuda.synchronize(sample_img.device)
-    detector.graphed_trunk = GraphedTrunk(trunk, sample_img, num_warmup_iters)
+    detector.graphed_trunk = GraphedTrunk(trunk, sample_img, num_warmup_iters, clone_outputs)
     torch.cuda.synchronize(sample_img.device)
     return detector.graphed_trunk
 

@@ -414,7 +414,10 @@ def _feat_desc(feats):
 
 
 # Optional live timing of the RoIAlign forward launches (bench.py roofline):
-# HIP events recorded on the launch stream around each call.
+# HIP events recorded on the launch stream around each call.  A record keeps the
+# feature tensors only to replay the same launch shape for timing; with a graphed
+# trunk they alias the graph's output buffers, so a replay reads the newest step's
+# values -- never use a record's features for their contents.
 ROI_ALIGN_PROFILE = {'on': False, 'records': []}
 
 

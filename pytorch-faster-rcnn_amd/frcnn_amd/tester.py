@@ -52,11 +52,14 @@ class BasicTester:
 
 
 def image_result(bbox, score, category, img_meta):
-    """One image's entry of tester.py:38-52 (None when it has no predictions)."""
+    """One image's entry of tester.py:38-52.  The reference skips an image only when
+    ``len(bbox) == 0`` (tester.py:46); a detector's empty result is a [4, 0] tensor, whose
+    len is 4, so such an image is kept with empty bbox/score/category (it contributes no
+    COCO results).  None only for a bbox with no rows at all."""
     filename = osp.basename(img_meta['filename'])
     img_w, img_h = img_meta['ori_shape'][:2]  # tester.py:43 keeps the reference's (w, h) naming
     res = {'width': img_w, 'height': img_h, 'image_id': int(filename[:-4]), 'file_name': filename}
-    if bbox.numel() == 0:
+    if len(bbox) == 0:
         return None
     res['bbox'] = utils.xyxy2xywh(bbox).t() / img_meta['scale_factor']
     res['score'] = score

@@ -119,3 +119,43 @@ def refine_inputs(agnostic, n=512, ncls=21):
     reg_out = rng.normal(0, 1.0, (n, 4 if agnostic else 4 * ncls)).astype(np.float32)
     is_gt = (np.arange(n) < 9).astype(np.uint8)
     return props, label, reg_out, is_gt
+
+
+def eval_case():
+    """Fixed detections for the f3 evaluation fixture (tester.py:25-57 -> test.py:75-90):
+    per image (meta, boxes [4, n] f32 xyxy in the resized frame, scores [n] f32, labels [n]
+    i64); image 2 has no detections (the reference's warning/skip branch).  Plus a COCO
+    ground truth in the original frame: jittered copies of about half the detections
+    (some with another class, one crowd), and missed objects."""
+    rng = np.random.default_rng(1300)
+    names = ['000005.jpg', '000123.jpg', '001234.jpg', '009999.jpg']
+    counts = [37, 0, 12, 100]
+    images, anns, aid = [], [], 1
+    for name, n in zip(names, counts):
+        sf = float(rng.choice([1.6, 1.5, 2.0]))
+        meta = {'filename': '/data/VOC2007/JPEGImages/' + name, 'ori_shape': (375, 625, 3), 'scale_factor': sf,
+                'img_shape': IMG_SHAPE + (3,), 'pad_shape': PAD_SHAPE + (3,)}
+        b = random_boxes(int(rng.integers(1 << 30)), n, min_wh=4.0, max_wh=300.0)
+        s = np.sort(rng.uniform(0.05, 1.0, n)).astype(np.float32)[::-1].copy()
+        lab = rng.integers(1, 21, n).astype(np.int64)
+        images.append((meta, b, s, lab))
+        iid = int(name[:-4])
+        for j in range(n):
+            if rng.random() < 0.5:
+                x1, y1, x2, y2 = (b[:, j] / sf).tolist()
+                w, h = x2 - x1 + 1, y2 - y1 + 1
+                jit = rng.normal(0, 0.08, 4) * [w, h, w, h]
+                box = [round(float(v), 2) for v in np.add([x1, y1, w, h], jit).clip(1.0)]
+                cat = int(lab[j]) if rng.random() < 0.85 else int(rng.integers(1, 21))
+                anns.append({'id': aid, 'image_id': iid, 'category_id': cat, 'bbox': box,
+                             'iscrowd': int(aid == 7), 'area': box[2] * box[3]})
+                aid += 1
+        for _ in range(3):
+            box = [round(float(v), 2) for v in (rng.uniform(0, 500), rng.uniform(0, 300), rng.uniform(8, 120),
+                                                rng.uniform(8, 120))]
+            anns.append({'id': aid, 'image_id': iid, 'category_id': int(rng.integers(1, 21)), 'bbox': box,
+                         'iscrowd': 0, 'area': box[2] * box[3]})
+            aid += 1
+    gt = {'images': [{'id': int(n[:-4]), 'file_name': n} for n in names], 'annotations': anns,
+          'categories': [{'id': c} for c in range(1, 21)]}
+    return images, gt

@@ -120,7 +120,9 @@ def test_results_conversion_matches_reference_format():
                       'score': 0.912, 'category_id': 3}
     assert out[1]['bbox'] == [0.0, 0.0, 5.25, 10.12]   # 10.125 -> 10.12: Python round, half-even
     assert out[1]['id'] == 1
-    assert tester.image_result(torch.zeros(4, 0), torch.zeros(0), torch.zeros(0), meta) is None
+    empty = tester.image_result(torch.zeros(4, 0), torch.zeros(0), torch.zeros(0), meta)
+    assert empty['bbox'].shape == (0, 4) and tester.results_to_coco([empty]) == []  # kept, as tester.py:46
+    assert tester.image_result(torch.zeros(0, 4), torch.zeros(0), torch.zeros(0), meta) is None
     # converted results score themselves perfectly against the same boxes as ground truth
     gt = {'images': [{'id': 123}], 'categories': [{'id': 3}, {'id': 7}],
           'annotations': [{'id': i + 1, 'image_id': 123, 'category_id': o['category_id'], 'bbox': o['bbox'],
@@ -140,3 +142,109 @@ def test_tester_inference_loop():
     res = t.inference([{'img': torch.zeros(2, 3, 32, 32), 'img_meta': metas}])
     assert [r['image_id'] for r in res] == [1, 2]
     assert res[0]['bbox'].tolist() == [[0.0, 0.0, 10.0, 10.0]]
+
+
+# ---------------------------------------------------------------- product evaluator vs the oracle restatement
+import coco_oracle  # noqa: E402
+
+
+def _random_case(seed, n_img=6, n_cat=4, crowd_p=0.1):
+    rng = np.random.default_rng(seed)
+    anns, dts, aid = [], [], 1
+    for img in range(1, n_img + 1):
+        for _ in range(rng.integers(0, 12)):
+            w, h = rng.uniform(4, 200, 2)
+            box = [float(v) for v in (rng.uniform(0, 400), rng.uniform(0, 300), w, h)]
+            cat = int(rng.integers(1, n_cat + 1))
+            anns.append({'id': aid, 'image_id': img, 'category_id': cat, 'bbox': box,
+                         'iscrowd': int(rng.random() < crowd_p), 'area': box[2] * box[3]})
+            aid += 1
+            for _ in range(rng.integers(0, 3)):  # jittered detections of this gt, some with the wrong class
+                j = rng.normal(0, 0.15, 4) * [w, h, w, h]
+                dts.append({'image_id': img, 'category_id': cat if rng.random() < 0.8 else int(rng.integers(1, n_cat + 1)),
+                            'bbox': [round(float(v), 2) for v in np.add(box, j).clip(0.5)],
+                            'score': round(float(rng.random()), 3)})
+        for _ in range(rng.integers(0, 8)):  # background false positives
+            w, h = rng.uniform(4, 150, 2)
+            dts.append({'image_id': img, 'category_id': int(rng.integers(1, n_cat + 1)),
+                        'bbox': [round(float(v), 2) for v in (rng.uniform(0, 400), rng.uniform(0, 300), w, h)],
+                        'score': round(float(rng.random()), 3)})
+    gt = {'images': [{'id': i} for i in range(1, n_img + 1)], 'annotations': anns,
+          'categories': [{'id': c} for c in range(1, n_cat + 1)]}
+    return gt, dts
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_evaluator_matches_oracle_restatement(seed):
+    """frcnn_amd.coco_eval (numpy) == oracle/coco_oracle.py (scalar loops, written apart) on
+    random multi-image, multi-class cases with crowds, all area ranges, ties in score
+    (3-decimal rounding) and > 100 detections per image in one case."""
+    gt, dts = _random_case(seed, n_img=3 if seed == 5 else 6)
+    if seed == 5:
+        dts = dts * 12  # > maxDet 100 per image: the cut and the stable order matter
+    a, b = coco_eval.evaluate(gt, dts), coco_oracle.evaluate(gt, dts)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert a[k] == pytest.approx(b[k], abs=1e-12), k
+
+
+def test_evaluator_gt_id_zero_never_matches():
+    """pycocotools records a match as the gt's id: a gt annotated with id 0 is consumed by
+    its detection but the detection still counts as a false positive."""
+    gt = {'images': [{'id': 1}], 'categories': [{'id': 1}],
+          'annotations': [{'id': 0, 'image_id': 1, 'category_id': 1, 'bbox': [0, 0, 40, 40], 'iscrowd': 0,
+                           'area': 1600.0}]}
+    dt = [{'image_id': 1, 'category_id': 1, 'bbox': [0, 0, 40, 40], 'score': 0.9}]
+    assert coco_eval.evaluate(gt, dt)['AP'] == 0.0 == coco_oracle.evaluate(gt, dt)['AP']
+
+
+@pytest.mark.parametrize('case', ['perfect', 'interp', 'crowd', 'maxdet'])
+def test_hand_cases_on_oracle(case):
+    """The hand-worked cases above, on the oracle restatement too."""
+    if case == 'perfect':
+        g = [((10, 10, 50, 40), 1), ((100, 80, 120, 130), 2), ((5, 200, 20, 20), 1)]
+        s = coco_oracle.evaluate(_gt(g, cats=(1, 2), img_of=[1, 1, 2]), _dt([(b, c, 0.9) for b, c in g], [1, 1, 2]))
+        assert s['AP'] == pytest.approx(1.0) and s['APs'] == pytest.approx(1.0)
+    elif case == 'interp':
+        g = [((0, 0, 40, 40), 1), ((100, 100, 40, 40), 1)]
+        dt = _dt([((0, 0, 40, 40), 1, 0.9), ((300, 300, 40, 40), 1, 0.8), ((100, 100, 40, 40), 1, 0.7)])
+        assert coco_oracle.evaluate(_gt(g), dt)['AP'] == pytest.approx((51 + 50 * 2 / 3) / 101, abs=1e-12)
+    elif case == 'crowd':
+        g = [((0, 0, 200, 200), 1), ((300, 300, 40, 40), 1)]
+        dt = _dt([((10, 10, 50, 50), 1, 0.95), ((300, 300, 40, 40), 1, 0.5)])
+        assert coco_oracle.evaluate(_gt(g, crowd=[1, 0]), dt)['AP'] == pytest.approx(1.0)
+    else:
+        g = [((0, 0, 40, 40), 1), ((100, 0, 40, 40), 1), ((200, 0, 40, 40), 1)]
+        dt = _dt([((0, 0, 40, 40), 1, 0.9), ((100, 0, 40, 40), 1, 0.8), ((200, 0, 40, 40), 1, 0.7)])
+        s = coco_oracle.evaluate(_gt(g), dt)
+        assert s['AR1'] == pytest.approx(1 / 3) and s['AR10'] == pytest.approx(1.0)
+
+
+def test_eval_fixture_from_reference_conversion(golden_dir=None):
+    """f3 pinned on the reference: tests/golden/eval.json holds the COCO results the
+    reference's own BasicTester.inference (lib/tester.py:25-57) + test.py:75-90 produced for
+    the fixed detections of inputs.eval_case (gen_golden.gen_eval).  The product tester must
+    write the identical json, and the product evaluator must reproduce the fixture's summary
+    (computed by the oracle restatement of COCOeval)."""
+    import json
+    import os
+    import inputs
+    fx = json.load(open(os.path.join(os.path.dirname(inputs.__file__), 'eval.json')))
+    images, gt = inputs.eval_case()
+    assert gt == fx['gt']
+
+    class Model(torch.nn.Module):
+        def forward_test(self, img, metas):
+            b, s, l = images[int(img[0, 0, 0, 0])][1:]
+            return [torch.from_numpy(b)], [torch.from_numpy(s)], [torch.from_numpy(l)]
+
+    t = tester.BasicTester(Model(), {}, {}, torch.device('cpu'))
+    res = t.inference([{'img': torch.full((1, 3, 8, 8), float(i)), 'img_meta': [images[i][0]]}
+                       for i in range(len(images))])
+    assert [{k: r[k] for k in ('width', 'height', 'image_id', 'file_name')} for r in res] == fx['image_results']
+    out = tester.results_to_coco(res)
+    assert out == fx['results']
+    s = coco_eval.evaluate(gt, out)
+    for k, v in fx['summary'].items():
+        assert s[k] == pytest.approx(v, abs=1e-12), k
+    assert 0.2 < s['AP50'] < 0.8 and s['AP'] < s['AP50']

@@ -716,6 +716,67 @@ def test_baseline_config_train_and_test(dev, config, batch):
             assert (l >= 1).all() and (l <= 20).all()
 
 
+def test_eval_end_to_end_cfg2(dev):
+    """f3 on the GPU: cfg2 forward_test on a fixed synthetic batch -> BasicTester.inference
+    (tester.py:25-57) -> results_to_coco (test.py:75-90) -> coco_eval.evaluate.
+    The json equals the reference's conversion formula applied to the raw detections
+    (xyxy2xywh with +1, / scale_factor, bbox rounded to 2, score to 3), and the summary
+    equals the oracle restatement of COCOeval (oracle/coco_oracle.py) on a ground truth made
+    of the batch's boxes plus jittered copies of every other detection.  Random-init
+    weights give near-uniform class scores, so rcnn.min_score is lowered to 0.01."""
+    import bench
+    import coco_oracle
+    from frcnn_amd import tester, coco_eval, utils
+    model, _ = bench.make_model(dev, seed=0)
+    model.test_cfg.rcnn.min_score = 0.01
+    imgs, boxes, labels, metas = bench.make_batch(dev, 2, seed=4)
+    names = ['000017.jpg', '004321.jpg']
+    metas = [dict(m, filename='/voc/JPEGImages/' + n) for m, n in zip(metas, names)]
+    seen, fwd = [], model.forward_test
+
+    def forward_test(img, img_metas):  # keep the raw detections the tester converts
+        seen.append(fwd(img, img_metas))
+        return seen[-1]
+
+    model.forward_test = forward_test
+    t = tester.BasicTester(model, {}, model.test_cfg, dev)
+    res = t.inference([{'img': imgs, 'img_meta': metas}])
+    out = tester.results_to_coco(res)
+    raw = seen[0]
+    want, n = [], 0
+    for i, m in enumerate(metas):
+        # the reference's formula as the reference runs it on the GPU (tester.py:49 on device
+        # tensors: a tensor / python-float divide, which torch implements as a multiply by the
+        # reciprocal, so it is evaluated here on the device too)
+        b = raw[0][i]
+        xywh = (torch.stack([b[0], b[1], b[2] - b[0] + 1, b[3] - b[1] + 1]).t() / m['scale_factor']).cpu().numpy()
+        s, l = raw[1][i].cpu().numpy(), raw[2][i].cpu().numpy()
+        for j in range(b.shape[1]):
+            want.append({'id': n, 'image_id': int(names[i][:-4]), 'file_name': names[i],
+                         'bbox': [round(float(v), 2) for v in xywh[j]], 'score': round(float(s[j]), 3),
+                         'category_id': int(l[j])})
+            n += 1
+    assert len(out) > 20, 'expected detections from the lowered threshold'
+    assert out == want
+    rng = np.random.default_rng(0)
+    anns = []
+    for i, m in enumerate(metas):
+        g = (utils.xyxy2xywh(boxes[i]).t() / m['scale_factor']).cpu().numpy()
+        for j, (bb, lab) in enumerate(zip(g, labels[i].cpu().numpy())):
+            anns.append({'id': len(anns) + 1, 'image_id': int(names[i][:-4]), 'category_id': int(lab),
+                         'bbox': [float(v) for v in bb], 'iscrowd': 0, 'area': float(bb[2] * bb[3])})
+    for d in out[::2]:
+        bb = np.add(d['bbox'], rng.normal(0, 0.05, 4) * np.array(d['bbox'])[[2, 3, 2, 3]]).clip(1.0)
+        anns.append({'id': len(anns) + 1, 'image_id': d['image_id'], 'category_id': d['category_id'],
+                     'bbox': [float(v) for v in bb], 'iscrowd': 0, 'area': float(bb[2] * bb[3])})
+    gt = {'images': [{'id': int(nm[:-4])} for nm in names], 'annotations': anns,
+          'categories': [{'id': c} for c in range(1, 21)]}
+    s, r = coco_eval.evaluate(gt, out), coco_oracle.evaluate(gt, out)
+    for k in r:
+        assert s[k] == pytest.approx(r[k], abs=1e-12), k
+    assert 0.0 < s['AP50'] < 1.0
+
+
 def test_train_step_cfg2(dev):
     """frcnn_amd.train.TrainStep (the reference's train_one_iter: loss -> backward -> grad clip
     -> SGD, config optimizer) on cfg2 for two iterations: finite losses, trainable parameters
@@ -808,5 +869,39 @@ def test_graphed_trunk_matches_eager(dev):
         assert not g.matches(imgs[:1]) and g.matches(imgs)
         one = model.forward_train(imgs[:1], boxes[:1], labels[:1], metas[:1])  # eager fallback
         assert all(torch.isfinite(v).all() for v in one.values())
+
+        # outputs held across the next replay: flagged stale, and a backward through them raises
+        feats_n, _, _ = g(imgs)
+        loss_n = feats_n[0].float().square().mean()
+        n = g.replays
+        assert g.is_current(feats_n[0])
+        g(imgs * 0.5)
+        assert g.replays == n + 1 and not g.is_current(feats_n[0])
+        with pytest.raises(RuntimeError):
+            loss_n.backward()
+    finally:
+        release_trunk(model)
+
+    # clone_outputs: private copies survive the next replay unchanged
+    g = capture_trunk(model, imgs, clone_outputs=True)
+    try:
+        with torch.no_grad():
+            keep = g(imgs)[0][0]
+            kept = keep.clone()
+            g(imgs * 0.5)
+        assert torch.equal(keep, kept)
+        # parameters moved / replaced after capture: the graph no longer matches (eager path)
+        assert g.matches(imgs)
+        conv = model.rpn_head.conv if hasattr(model.rpn_head, 'conv') else None
+        if conv is not None:
+            old = conv.weight
+            conv.weight = torch.nn.Parameter(old.detach().clone())
+            assert not g.matches(imgs)
+            conv.weight = old
+            assert g.matches(imgs)
+        model.double()
+        assert not g.matches(imgs)
+        model.float()
+        assert not g.matches(imgs)
     finally:
         release_trunk(model)
