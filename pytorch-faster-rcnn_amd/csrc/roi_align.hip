@@ -650,7 +650,7 @@ __device__ __forceinline__ void roi_segment(const RoiLevels& lv, const RoiCfg& c
 // Invalid samples have zero weights and read cell 0 (finite features: +0, the
 // reference's own 0 * feature term).  Same operation order as torchvision:
 // bit-identical to the other kernels.
-constexpr int kPairWave = 64;                   // channel pairs per wave (= workgroup)
+constexpr int kPairWave = 8;                    // channel pairs per wave (= workgroup): 16 channels
 constexpr int kPairHalf = 1664;                 // dwords per buffer (13 KB per wave for both)
 constexpr int kPairChunk = 2 * kPairWave;       // channels per workgroup
 
@@ -682,9 +682,9 @@ __device__ __forceinline__ void lds_wait(f32x2 (&v)[8]) {
                : "memory");
 }
 
-template <int D>
+template <int D, int kHalf = kPairHalf>
 struct PairLayout {
-  static constexpr int RS = (kPairHalf / D) / kWave * kWave;  // dwords per pair region
+  static constexpr int RS = (kHalf / D) / kWave * kWave;  // dwords per pair region
   static constexpr int RP = RS / kWave;                       // DMA rounds per pair
   static constexpr int kCells = RS / 2;
   static_assert(D * RP + 2 * D < 64, "vmcnt is 6 bits");
@@ -693,15 +693,35 @@ struct PairLayout {
 // kSkip (diagnostics only): 1 = skip RoIs staged 8 pairs at a time, 2 = skip the others.
 // kDiag (diagnostics only): per-wave s_memrealtime stamps past the results:
 // [start, setup done, stage 0 ready, stage 0 done, stage 1 ready, end, D, RoI].
-template <int kSkip = 0, bool kDiag = false, int kPW = kPairWave>
-__global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+// kHalf: dwords per slab buffer.  kCls: 0 = every RoI; 1 = only RoIs whose slab has at
+// most kPairSplit cells (others skipped); 2 = only the others -- a small-slab launch
+// (more resident waves) for the common small windows plus a large-slab launch.
+constexpr int kPairSplit = 256;  // cells: PairLayout<1, 512>::kCells
+// kWPB: waves per workgroup; wave w of block b takes item (RoI, chunk) = b * kWPB + w
+// (RoI-major, ceil(C / (2 kPW)) chunks per RoI) -- fewer, larger workgroups than one per
+// (RoI, chunk): dispatching 16 K single-wave workgroups alone costs ~8.5 us.
+template <int kSkip = 0, bool kDiag = false, int kPW = kPairWave, int kHalf = kPairHalf, int kCls = 0, int kWPB = 1>
+__global__ void __launch_bounds__(kWave * kWPB) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c,
+                                                                          float* __restrict__ out) {
   constexpr int SR = 2;
-  __shared__ __attribute__((aligned(16))) float slab[2 * kPairHalf];
+  __shared__ __attribute__((aligned(16))) float slab_all[kWPB][2 * kHalf];
   int64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (kDiag) stamp[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  const int64_t k = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int cw0 = blockIdx.y * 2 * kPW;
+  const int wave = kWPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
+  // this wave's slab as an LDS byte address (integer: no generic-pointer casts)
+  const uint32_t sbase =
+      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)&slab_all[0][0]) +
+      (uint32_t)wave * 8u * kHalf;
+  int64_t k = blockIdx.x;
+  int cw0 = blockIdx.y * 2 * kPW;
+  if (kWPB > 1) {
+    const int G = (c.C + 2 * kPW - 1) / (2 * kPW);
+    const int64_t item = (int64_t)blockIdx.x * kWPB + wave;
+    k = item / G;
+    if (k >= c.K) return;
+    cw0 = (int)(item - k * G) * 2 * kPW;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl;
@@ -730,7 +750,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
   const int ostep = nbins * 4;
   if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: all bins 0
-    if (kSkip) return;
+    if (kSkip || kCls == 2) return;
     for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
     return;
   }
@@ -738,15 +758,23 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int R = dy ? y1 - y0 + 1 : nly, Cs = dx ? x1 - x0 + 1 : nlx;
   const int Cs2 = Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
   const int ncell = R * Cs2;
-  const bool small = ncell <= PairLayout<8>::kCells;
+  const bool small = ncell <= PairLayout<8, kHalf>::kCells;
   if (kSkip && (kSkip == 1) == small) return;
+  if (kCls == 3) return;  // diagnostics: setup only
+  if (kCls == 4) {        // diagnostics: setup + one DMA round + wait
+    lds_dma_at<4>(uniform_rsrc(lv.feat[l] + (int64_t)g.b * lv.sb[l], 4 * (int64_t)H * W), sbase, lane * 4, 0);
+    wait_vmcnt<0>();
+    return;
+  }
+  if (kCls == 1 && ncell > kPairSplit) return;
+  if (kCls == 2 && ncell <= kPairSplit) return;
   // feature byte offsets of slab row / column `lane`
   const int rsrc = (dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
   const int csrc = (dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
   // this lane's bin: weights (zero for invalid samples) and LDS addresses of its 16 taps
   const int bin = active ? lane : 0;
   const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const uint32_t lbase = sbase;
   float wt[SR][SR][4];
   uint32_t ta[SR][SR][4];
 #pragma unroll
@@ -774,7 +802,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const uint32_t inv = (65536u + (uint32_t)Cs2 - 1u) / (uint32_t)Cs2;  // e / Cs2 == (e * inv) >> 16 for e < 1024
 
   auto run = [&](auto dd) {
-    constexpr int D = decltype(dd)::value, RS = PairLayout<D>::RS, RP = PairLayout<D>::RP;
+    constexpr int D = decltype(dd)::value, RS = PairLayout<D, kHalf>::RS, RP = PairLayout<D, kHalf>::RP;
     const int nst = (npairs + D - 1) / D;
     // region dword j * 64 + lane of every pair  <-  channel (lane & 1) of cell (j * 64 + lane) / 2
     int goff[RP];
@@ -787,12 +815,12 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
     }
     if (kDiag) stamp[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
     auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
-      float* buf = slab + (s & 1) * kPairHalf;
+      const uint32_t buf = sbase + 4u * (uint32_t)((s & 1) * kHalf);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
 #pragma unroll
-        for (int j = 0; j < RP; ++j) lds_dma<4>(fr, buf + d * RS + j * kWave, goff[j], soff);
+        for (int j = 0; j < RP; ++j) lds_dma_at<4>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
       }
     };
     auto eval = [&](auto bb, int s) {
@@ -801,7 +829,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
       f32x2 v[2][8];
       f32x2 acc = {0.0f, 0.0f};
       auto load = [&](auto hh) {
-        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kPairHalf + d * RS);
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix)
 #pragma unroll
@@ -874,12 +902,316 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   };
   if (small)
     run(std::integral_constant<int, 8>{});
-  else if (ncell <= PairLayout<4>::kCells)
+  else if (ncell <= PairLayout<4, kHalf>::kCells)
     run(std::integral_constant<int, 4>{});
-  else if (ncell <= PairLayout<2>::kCells)
+  else if (ncell <= PairLayout<2, kHalf>::kCells)
     run(std::integral_constant<int, 2>{});
   else
     run(std::integral_constant<int, 1>{});
+}
+
+__global__ void roi_empty_kernel(float* out) {
+  if (threadIdx.x == 64) out[0] = 0.0f;  // never true: keeps the launch from being elided
+}
+
+// ---------------------------------------------------------------------------
+// Persistent channel-pair forward (variant 25).  The staging and evaluation of
+// the channel-pair kernel above, but a grid of resident single-wave workgroups
+// walks the items (RoI, kStrPairs channel pairs): wave w takes items w, w + G,
+// w + 2G, ...  The two-buffer LDS ring never drains between items: before the
+// last stage of item i is evaluated, item i+1's RoI / level / descriptor loads,
+// its tap window and DMA offsets are set up and its first stage is issued, so
+// the per-item setup and first-load latency (about half of a channel-pair
+// wave's life) overlap the previous item's evaluation.  Stage
+// shapes (D pairs per stage) may change from item to item; the vmcnt waits
+// count the DMAs and stores issued after the stage being retired (in-order
+// completion) and round down to a supported immediate (waiting for fewer
+// outstanding operations is always safe).  Bit-identical to the other kernels.
+constexpr int kStrPairs = 8;         // channel pairs per item
+constexpr int kStrGoff = PairLayout<1>::RP;
+
+struct StrItem {
+  int64_t k;
+  int ok, D, nst, npairs, cw0, scs4;
+  int H, W, y0, x0, dy, dx, Cs2;
+  float sh, sw, bh, bw;
+  __amdgpu_buffer_rsrc_t fr, orr;
+  int goff[kStrGoff];
+};
+
+__device__ __forceinline__ int str_dma_count(int D) { return D >= 4 ? 24 : 26; }
+
+// s_waitcnt vmcnt(N') for the largest supported N' <= n
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  if (n >= 42) wait_vmcnt<42>();
+  else if (n >= 40) wait_vmcnt<40>();
+  else if (n >= 34) wait_vmcnt<34>();
+  else if (n >= 32) wait_vmcnt<32>();
+  else if (n >= 30) wait_vmcnt<30>();
+  else if (n >= 28) wait_vmcnt<28>();
+  else if (n >= 26) wait_vmcnt<26>();
+  else if (n >= 24) wait_vmcnt<24>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else if (n >= 8) wait_vmcnt<8>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else wait_vmcnt<0>();
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// DMA-side setup of item t (uniform over the wave except goff)
+__device__ __forceinline__ void str_setup(StrItem& it, const RoiLevels& lv, const RoiCfg& c, float* out, int64_t t,
+                                          int G) {
+  constexpr int SR = 2;
+  const int lane = threadIdx.x;
+  it.k = t / G;
+  it.cw0 = (int)(t - it.k * G) * 2 * kStrPairs;
+  it.npairs = min(kStrPairs, (c.C - it.cw0) / 2);
+  const RoiGeom g = roi_geom(c, lv, it.k);
+  const int l = g.lvl;
+  it.H = lv.h[l];
+  it.W = lv.w[l];
+  it.sh = g.start_h;
+  it.sw = g.start_w;
+  it.bh = g.bin_h;
+  it.bw = g.bin_w;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  it.scs4 = scs * 4;
+  const int nbins = c.ph * c.pw;
+  it.orr = uniform_rsrc(out + (it.k * c.C + it.cw0) * nbins, (int64_t)2 * it.npairs * nbins * 4);
+  auto pos_y = [&](int p, int i) { return it.sh + (float)p * it.bh + ((float)i + 0.5f) * it.bh * 0.5f; };
+  auto pos_x = [&](int p, int i) { return it.sw + (float)p * it.bw + ((float)i + 0.5f) * it.bw * 0.5f; };
+  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
+  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  if (lane < nly) {
+    const int s = lane >> 1;
+    const Tap tp = make_tap(pos_y(s >> 1, s & 1), it.H);
+    if (tp.valid) yrow = (lane & 1) ? tp.hi : tp.lo, ylo = tp.lo, yhi = tp.hi;
+  }
+  if (lane < nlx) {
+    const int s = lane >> 1;
+    const Tap tp = make_tap(pos_x(s >> 1, s & 1), it.W);
+    if (tp.valid) xcol = (lane & 1) ? tp.hi : tp.lo, xlo = tp.lo, xhi = tp.hi;
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  it.ok = y1 >= y0 && x1 >= x0;
+  it.y0 = y0;
+  it.x0 = x0;
+  it.dy = y1 - y0 + 1 <= nly;
+  it.dx = x1 - x0 + 1 <= nlx;
+  const int R = it.dy ? y1 - y0 + 1 : nly, Cs = it.dx ? x1 - x0 + 1 : nlx;
+  it.Cs2 = Cs | 1;
+  const int ncell = R * it.Cs2;
+  it.D = ncell <= PairLayout<8>::kCells ? 8 : ncell <= PairLayout<4>::kCells ? 4 : ncell <= PairLayout<2>::kCells ? 2 : 1;
+  it.nst = (it.npairs + it.D - 1) / it.D;
+  if (!it.ok) return;
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(it.H - 1) * sy + (int64_t)(it.W - 1) * sx + 1) * 4;
+  it.fr = uniform_rsrc(base, extent);
+  const int rsrc = (it.dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
+  const int csrc = (it.dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
+  const uint32_t inv = (65536u + (uint32_t)it.Cs2 - 1u) / (uint32_t)it.Cs2;
+  const int RS = it.D == 8 ? PairLayout<8>::RS : it.D == 4 ? PairLayout<4>::RS : it.D == 2 ? PairLayout<2>::RS
+                                                                                               : PairLayout<1>::RS;
+  const int RP = RS / kWave;
+#pragma unroll
+  for (int j = 0; j < kStrGoff; ++j) {
+    int e = (j * kWave + lane) >> 1;
+    e = e < ncell ? e : 0;
+    const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * it.Cs2, Cs - 1);
+    const int v = __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * it.scs4;
+    it.goff[j] = j < RP ? v : 0;
+  }
+}
+
+// eval-side setup: this lane's bin weights (zero for invalid samples) and LDS tap addresses
+__device__ __forceinline__ void str_taps(const StrItem& it, const RoiCfg& c, uint32_t lbase, uint32_t (&ta)[2][2][4],
+                                         float (&wt)[2][2][4]) {
+  constexpr int SR = 2;
+  const int lane = threadIdx.x;
+  const int nbins = c.ph * c.pw;
+  const int bin = lane < nbins ? lane : 0;
+  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
+  auto pos_y = [&](int p, int i) { return it.sh + (float)p * it.bh + ((float)i + 0.5f) * it.bh * 0.5f; };
+  auto pos_x = [&](int p, int i) { return it.sw + (float)p * it.bw + ((float)i + 0.5f) * it.bw * 0.5f; };
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy) {
+    const Tap a = make_tap(pos_y(py, iy), it.H);
+    const int r0 = it.dy ? a.lo - it.y0 : 2 * (py * SR + iy), r1 = it.dy ? a.hi - it.y0 : 2 * (py * SR + iy) + 1;
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap b = make_tap(pos_x(px, ix), it.W);
+      const int q0 = it.dx ? b.lo - it.x0 : 2 * (px * SR + ix), q1 = it.dx ? b.hi - it.x0 : 2 * (px * SR + ix) + 1;
+      const bool ok = a.valid && b.valid;
+      wt[iy][ix][0] = ok ? a.h * b.h : 0.f;
+      wt[iy][ix][1] = ok ? a.h * b.l : 0.f;
+      wt[iy][ix][2] = ok ? a.l * b.h : 0.f;
+      wt[iy][ix][3] = ok ? a.l * b.l : 0.f;
+      ta[iy][ix][0] = lbase + (ok ? 8u * (uint32_t)(r0 * it.Cs2 + q0) : 0u);
+      ta[iy][ix][1] = lbase + (ok ? 8u * (uint32_t)(r0 * it.Cs2 + q1) : 0u);
+      ta[iy][ix][2] = lbase + (ok ? 8u * (uint32_t)(r1 * it.Cs2 + q0) : 0u);
+      ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * it.Cs2 + q1) : 0u);
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void str_issue(const StrItem& it, float* slab, int b, int s) {
+  constexpr int RS = PairLayout<D>::RS, RP = PairLayout<D>::RP;
+  float* buf = slab + b * kPairHalf;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {  // pairs past the last re-read it (their stores are dropped)
+    const int soff = (it.cw0 + 2 * min(s * D + d, it.npairs - 1)) * it.scs4;
+#pragma unroll
+    for (int j = 0; j < RP; ++j) lds_dma<4>(it.fr, buf + d * RS + j * kWave, it.goff[j], soff);
+  }
+}
+
+__device__ __forceinline__ void str_issue_dyn(const StrItem& it, float* slab, int b, int s) {
+  switch (it.D) {
+    case 8: str_issue<8>(it, slab, b, s); break;
+    case 4: str_issue<4>(it, slab, b, s); break;
+    case 2: str_issue<2>(it, slab, b, s); break;
+    default: str_issue<1>(it, slab, b, s); break;
+  }
+}
+
+template <int D, int kBuf>
+__device__ __forceinline__ void str_eval(const StrItem& it, int s, int ovoff, int ostep, const uint32_t (&ta)[2][2][4],
+                                         const float (&wt)[2][2][4]) {
+  constexpr int SR = 2, RS = PairLayout<D>::RS;
+  f32x2 v[2][8];
+  f32x2 acc = {0.0f, 0.0f};
+  auto load = [&](auto hh) {
+    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kPairHalf + d * RS);
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
+  };
+  load(std::integral_constant<int, 0>{});
+  static_for<0, 2 * D>([&](auto hh) {
+    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
+    if constexpr (h + 1 < 2 * D) {
+      load(std::integral_constant<int, h + 1>{});
+      lds_wait<8>(v[h & 1]);
+    } else {
+      lds_wait<0>(v[h & 1]);
+    }
+    if (iy == 0) acc = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const float* w = wt[iy][ix];
+      const f32x2* x = &v[h & 1][ix * 4];
+      const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
+      acc = acc + val;
+    }
+    if (iy == 1) {
+      const f32x2 r = acc * 0.25f;
+      const int p = s * D + d;
+      const int vo = p < it.npairs ? ovoff : 0x40000000;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), it.orr, vo, 2 * p * ostep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), it.orr, vo, (2 * p + 1) * ostep, 0);
+    }
+  });
+}
+
+__device__ __forceinline__ void str_eval_dyn(const StrItem& it, int b, int s, int ovoff, int ostep,
+                                             const uint32_t (&ta)[2][2][4], const float (&wt)[2][2][4]) {
+  if (b == 0) {
+    switch (it.D) {
+      case 8: str_eval<8, 0>(it, s, ovoff, ostep, ta, wt); break;
+      case 4: str_eval<4, 0>(it, s, ovoff, ostep, ta, wt); break;
+      case 2: str_eval<2, 0>(it, s, ovoff, ostep, ta, wt); break;
+      default: str_eval<1, 0>(it, s, ovoff, ostep, ta, wt); break;
+    }
+  } else {
+    switch (it.D) {
+      case 8: str_eval<8, 1>(it, s, ovoff, ostep, ta, wt); break;
+      case 4: str_eval<4, 1>(it, s, ovoff, ostep, ta, wt); break;
+      case 2: str_eval<2, 1>(it, s, ovoff, ostep, ta, wt); break;
+      default: str_eval<1, 1>(it, s, ovoff, ostep, ta, wt); break;
+    }
+  }
+}
+
+// an item with no valid sample: every bin of its channels is 0
+__device__ __forceinline__ void str_zero(const StrItem& it, int ovoff, int ostep) {
+  for (int ch = 0; ch < 2 * it.npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, it.orr, ovoff, ch * ostep, 0);
+}
+
+template <int kWpe = 0>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1))) roi_align_fwd_stream_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out,
+                                                                      int64_t nitems, int G) {
+  __shared__ __attribute__((aligned(16))) float slab[2 * kPairHalf];
+  const int lane = threadIdx.x;
+  const int nbins = c.ph * c.pw;
+  const int ovoff = lane < nbins ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  const int ostep = nbins * 4;
+  const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  int64_t t = blockIdx.x;
+  if (t >= nitems) return;
+  StrItem cur;
+  for (;;) {  // first item with a valid sample
+    str_setup(cur, lv, c, out, t, G);
+    if (cur.ok) break;
+    str_zero(cur, ovoff, ostep);
+    t += gridDim.x;
+    if (t >= nitems) return;
+  }
+  str_issue_dyn(cur, slab, 0, 0);
+  int bt = 0, prev_st = 0;
+  uint32_t ta[2][2][4];
+  float wt[2][2][4];
+  str_taps(cur, c, lbase, ta, wt);
+  for (;;) {
+    for (int s = 0; s + 1 < cur.nst; ++s) {
+      str_issue_dyn(cur, slab, bt ^ 1, s + 1);
+      wait_vmcnt_le(str_dma_count(cur.D) + prev_st);
+      wave_sync();
+      str_eval_dyn(cur, bt, s, ovoff, ostep, ta, wt);
+      prev_st = 2 * cur.D;
+      wave_sync();
+      bt ^= 1;
+    }
+    // last stage of this item: first set up and issue the next item's stage 0
+    StrItem nxt;
+    bool have = false;
+    int extra = 0;
+    int64_t t2 = t;
+    for (;;) {
+      t2 += gridDim.x;
+      if (t2 >= nitems) break;
+      str_setup(nxt, lv, c, out, t2, G);
+      if (nxt.ok) {
+        have = true;
+        break;
+      }
+      str_zero(nxt, ovoff, ostep);
+      extra += 2 * nxt.npairs;
+    }
+    int dn = 0;
+    if (have) {
+      str_issue_dyn(nxt, slab, bt ^ 1, 0);
+      dn = str_dma_count(nxt.D);
+    }
+    wait_vmcnt_le(dn + prev_st + extra);
+    wave_sync();
+    str_eval_dyn(cur, bt, cur.nst - 1, ovoff, ostep, ta, wt);
+    prev_st = 2 * cur.D;
+    wave_sync();
+    bt ^= 1;
+    if (!have) break;
+    cur = nxt;
+    t = t2;
+    str_taps(cur, c, lbase, ta, wt);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2168,6 +2500,26 @@ static FwdCaps fwd_caps(const RoiLevels& lv, int32_t channels, int32_t ph, int32
   return f;
 }
 
+// resident single-wave workgroups of the persistent forward: CUs x the occupancy the
+// kernel's LDS and registers allow (FRH_STR_WAVES overrides the per-CU count)
+template <int kWpe>
+static int64_t stream_grid_waves() {
+  static int64_t cached[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (!cached[dev]) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, roi_align_fwd_stream_kernel<kWpe>, kWave, 0) !=
+            hipSuccess ||
+        per <= 0)
+      per = 8;
+    if (const char* e = getenv("FRH_STR_WAVES")) per = std::max(1, atoi(e));
+    cached[dev] = (int64_t)cus * per;
+  }
+  return cached[dev];
+}
+
 static int32_t group_bound(int64_t num_rois) { return (int32_t)((num_rois + kGrp - 1) / kGrp + 64); }
 
 // variant: 0 = direct gather, 10 = per-RoI LDS windows, 50 = grouped (needs the
@@ -2193,14 +2545,16 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   // -1: the per-RoI LDS kernel (measured fastest on cfg2); -2: the
   // grouped kernel when the workspace allows it (frh_roi_align_fwd_ws)
   if (variant == -2) variant = grp_ok ? 50 : -1;
-  if (variant < 0) variant = f.lds ? 10 : 0;
   bool x4_ok = f.lds && 4 * pooled_h <= kWave;
   for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   const bool pair_ok = f.lds && channels % 2 == 0 && 4 * pooled_h <= kWave && 4 * pooled_w <= kWave &&
                        4 * pooled_h * (4 * pooled_w + 1) <= PairLayout<1>::kCells;
+  // default: the channel-pair kernel (46 us on the cfg2 RoIs vs 56 us for the per-RoI LDS
+  // kernel), else the per-RoI LDS kernel, else the direct gather
+  if (variant < 0) variant = pair_ok ? 20 : (f.lds ? 10 : 0);
   FRH_REQUIRE(variant == 0 || (((variant >= 9 && variant <= 19) && f.lds)) || ((variant == 50 || variant == 51) && grp_ok) ||
-                  (variant >= 20 && variant <= 24 && pair_ok) || (variant >= 30 && variant <= 37 && x4_ok),
+                  (((variant >= 20 && variant <= 29) || (variant >= 38 && variant <= 44)) && pair_ok) || (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   if (variant == 50 || variant == 51) {
     int32_t* order = static_cast<int32_t*>(workspace);
@@ -2220,6 +2574,54 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL(roi_align_fwd_group_kernel<4>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
     else
       hipLaunchKernelGGL(roi_align_fwd_group_kernel<1>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
+  } else if (variant == 27) {  // two launches: small windows with a 4 KB slab, then large windows
+    const int pw = getenv("FRH_PAIR_PW") ? atoi(getenv("FRH_PAIR_PW")) : 8;
+    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 2 * pw - 1) / (2 * pw)));
+    if (pw == 4) {
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 4, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 4, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    } else if (pw == 16) {
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    } else {
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    }
+  } else if (variant >= 41 && variant <= 44) {  // multi-wave workgroups: 41: 2 x pw8, 42: 4 x pw8, 43: 4 x pw4, 44: 2 x pw16
+    auto launch = [&](auto kern, int wpb, int pw) {
+      const int64_t items = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+      hipLaunchKernelGGL(kern, dim3((unsigned)((items + wpb - 1) / wpb)), dim3(kWave * wpb), 0, as_stream(stream), lv,
+                         c, out);
+    };
+    if (variant == 41) launch(roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 0, 2>, 2, 8);
+    else if (variant == 42) launch(roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 0, 4>, 4, 8);
+    else if (variant == 43) launch(roi_align_fwd_pair_kernel<0, false, 4, kPairHalf, 0, 4>, 4, 4);
+    else launch(roi_align_fwd_pair_kernel<0, false, 16, kPairHalf, 0, 2>, 2, 16);
+  } else if (variant >= 38 && variant <= 40) {  // diagnostics: 38 setup only, 39 setup + one DMA, 40 empty waves
+    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 15) / 16));
+    if (variant == 38)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 3>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else if (variant == 39)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 4>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL(roi_empty_kernel, g2, dim3(kWave), 0, as_stream(stream), out);
+  } else if (variant == 28 || variant == 29) {  // diagnostics: only the small (28) / large (29) launch of 27
+    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 15) / 16));
+    if (variant == 28)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 25 || variant == 26) {  // 26: registers for 3 waves per SIMD (spills)
+    const int G = (channels + 2 * kStrPairs - 1) / (2 * kStrPairs);
+    const int64_t nitems = num_rois * G;
+    if (variant == 25)
+      hipLaunchKernelGGL(roi_align_fwd_stream_kernel<0>,
+                         dim3((unsigned)std::min<int64_t>(nitems, stream_grid_waves<0>())), dim3(kWave), 0,
+                         as_stream(stream), lv, c, out, nitems, G);
+    else
+      hipLaunchKernelGGL(roi_align_fwd_stream_kernel<3>,
+                         dim3((unsigned)std::min<int64_t>(nitems, stream_grid_waves<3>())), dim3(kWave), 0,
+                         as_stream(stream), lv, c, out, nitems, G);
   } else if (variant >= 20 && variant <= 24) {  // 21 / 22: diagnostics (skip large / small windows), 24: stamps
     dim3 grid((unsigned)num_rois, (unsigned)((channels + kPairChunk - 1) / kPairChunk));
     if (variant == 20 && getenv("FRH_PAIR_PW")) {

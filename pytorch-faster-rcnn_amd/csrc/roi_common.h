@@ -133,6 +133,19 @@ __device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t r, float* lds, in
 #endif
 }
 
+// the same with the destination given as a wave-uniform LDS byte address
+template <int kBytes>
+__device__ __forceinline__ void lds_dma_at(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(kBytes == 4 || kBytes == 16, "LDS-DMA width");
+  auto* p = (__attribute__((address_space(3))) void*)(uintptr_t)lds_addr;
+  if constexpr (kBytes == 16)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 16, voff, soff, 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 4, voff, soff, 0, 0);
+#endif
+}
+
 // s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding).  The
 // compiler does not wait for LDS-DMA data before ds_reads: these are explicit.
 template <int N>

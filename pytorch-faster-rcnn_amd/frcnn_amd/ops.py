@@ -422,7 +422,7 @@ ROI_ALIGN_PROFILE = {'on': False, 'records': []}
 
 
 def roi_align_variant(variant, feats, rois, levels, scales, output_size, sampling_ratio):
-    """One named RoIAlign forward kernel (0 direct, 10 per-RoI LDS = default, 50 grouped);
+    """One named RoIAlign forward kernel (0 direct, 10 per-RoI LDS, 20 channel pairs = default, 50 grouped);
     parity tests and the micro-benchmark.  The grouped kernel's workspace comes from the
     caching allocator like every other op's."""
     _need_cuda(rois, *feats)
