@@ -252,75 +252,16 @@ int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, float* out, void* stream);
-/* Plane-sweep forward (the default for sampling_ratio 2, even C, unit x
- * stride, W_l <= 256): one workgroup per (level, image, channel pair) streams
- * that plane pair through an LDS row ring exactly once and evaluates every
- * (RoI, bin row) as soon as its rows have landed; a small plan launch first
- * writes each bin row's y taps and each (RoI, px)'s x taps into the workspace
- * (frh_roi_align_sweep_workspace bytes).  Bit-identical to
- * frh_roi_align_fwd_strided, which it falls back to for any other shape or a
- * missing / short workspace. */
-size_t frh_roi_align_sweep_workspace(int64_t num_rois, int32_t pooled_h, int32_t pooled_w);
-int32_t frh_roi_align_fwd_sweep(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                                const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
-                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
-                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                                float* out, void* workspace, size_t ws_bytes, void* stream);
-/* Plane-sweep backward: the same sweep accumulates each (image, channel pair)'s
- * gradient rows in LDS and writes every element of grad_feats exactly once
- * (no clearing, no global atomics).  Returns FRH_EUNSUPPORTED (nothing
- * launched) outside the sweep's shapes or without the workspace
- * (frh_roi_align_sweep_workspace bytes): the caller then clears the gradient
- * and uses frh_roi_align_bwd_strided.  Float atomics in LDS: the summation
- * order, and the last bits, vary from run to run (as torchvision's CUDA). */
-int32_t frh_roi_align_bwd_sweep(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
-                                const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
-                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
-                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                                const float* grad_out, void* workspace, size_t ws_bytes, void* stream);
-/* The grouped forward (opt-in): a one-workgroup planning launch sorts the
- * RoIs into spatial groups of 8 (same image and level); the main launch
- * stages the union of each group's tap rows per channel into LDS by LDS-DMA
- * and evaluates every RoI of the group from it, so a line shared by several
- * RoIs is fetched once.  Bit-identical to frh_roi_align_fwd_strided, which it
- * falls back to when the workspace is absent / short, K > 8192, or the shape
- * is outside (sampling 2, ph*pw <= 64).  workspace: frh_roi_align_workspace(K)
- * bytes.  Currently slower than the default on cfg2. */
-size_t frh_roi_align_workspace(int64_t num_rois);
-int32_t frh_roi_align_fwd_ws(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                             const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
-                             const float* rois, const int64_t* roi_levels, int64_t num_rois,
-                             int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                             float* out, void* workspace, size_t ws_bytes, void* stream);
-/* Diagnostics / micro-benchmark: a named forward kernel (0 direct gather, 10
- * per-RoI LDS windows = the default, 50 grouped, 51 grouped with timing stamps
- * written past the results; -1 = default, -2 = grouped if possible). */
-int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
-                                  const int32_t* feat_hw, const int64_t* strides, const float* scales,
-                                  int32_t batch, int32_t channels, const float* rois,
-                                  const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
-                                  int32_t pooled_w, int32_t sampling_ratio, int32_t aligned, float* out,
-                                  void* workspace, size_t ws_bytes, void* stream);
+/* Backward of the strided forward: grad_feats (same strides) must be cleared by the
+ * caller; contributions are added with float atomics (sampling 2, up to 8x8 bins:
+ * one atomic per row run of a RoI's taps), so the summation order -- and the last
+ * bits -- vary from run to run, as in torchvision's CUDA backward. */
 int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
                                   const int32_t* feat_hw, const int64_t* strides,
                                   const float* scales, int32_t batch, int32_t channels,
                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, const float* grad_out, void* stream);
-
-/* Tiled gather backward (sampling_ratio 2, pooled_h * pooled_w <= 64): the same
- * gradient as frh_roi_align_bwd_strided without global atomics.  OVERWRITES every
- * cell of grad_feats (no need to clear it first).  Workspace: caller-allocated,
- * frh_roi_align_bwd_workspace bytes (tile lists over 16x16-cell tiles). */
-size_t frh_roi_align_bwd_workspace(int32_t num_levels, const int32_t* feat_hw, int32_t batch,
-                                   int64_t num_rois);
-int32_t frh_roi_align_bwd_tiled(int32_t num_levels, float* const* grad_feats,
-                                const int32_t* feat_hw, const int64_t* strides,
-                                const float* scales, int32_t batch, int32_t channels,
-                                const float* rois, const int64_t* roi_levels, int64_t num_rois,
-                                int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
-                                int32_t aligned, const float* grad_out, void* workspace,
-                                size_t ws_bytes, void* stream);
 
 /* ---- RoIPool (torchvision.ops.RoIPool; C4 config configs/faster_rcnn_r50.py:26) --
  * feat [B, C, H, W] with element strides strides[0..3] = (b, c, y, x); rois

@@ -2,22 +2,28 @@
 // (call sites lib/heads/rpn_head.py:103, lib/utils.py:220).
 //
 // Two launches:
-//  mask: one wave per (segment, 64-row block, 64-col block >= row block);
-//        lane i sets bit j when IoU(row i, col j) > thr (j after i), the
-//        64 column boxes staged in LDS.  Rows are 64-bit words per col block.
-//  scan: one workgroup per segment walks the row blocks in score order.
-//        Wave 0 resolves the block's 64 candidates sequentially with
-//        readlane'd diagonal words (pure register/SALU work), then all
-//        waves OR the kept rows' words into the LDS suppression bitmap with
-//        8 independent loads per lane in flight.
+//  mask: one wave per (segment, 64-row block rb, 64-col block cb >= rb) -- the
+//        grid covers the upper triangle only.  The suppression relation is
+//        stored as COLUMN words: for column j of the tile, the 64-bit set of
+//        rows of block rb whose box suppresses box j (row < column, IoU > thr),
+//        Layout [segment][cb][rb][64 columns]: the tiles of one column block
+//        are contiguous.
+//  scan: one workgroup per segment walks the blocks in score order (the
+//        resolve chain of a segment is inherently sequential).  For block b the
+//        column span of tiles (0..b, b) is staged in LDS by LDS-DMA ahead of
+//        time; the suppression of b's candidates by all earlier kept rows is
+//        one per-lane AND/OR pass over the span plus one ballot, and the
+//        bit-parallel greedy over the 64 candidates is two ballots per round.
 #include <stdlib.h>
 #include <string.h>
 
 #include <math.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "block_ops.h"
+#include "cdna.h"
 
 namespace frh {
 
@@ -29,6 +35,9 @@ constexpr int kMaxNmsWords = 256;  // n <= 16384 boxes per segment
 // significand is even).  mid has 25 significant bits and union 24, so mid * union
 // is exact in double and the comparison below decides exactly what the reference's
 // float division + double compare decides.  union <= 0 / NaN take the division.
+// (This is torchvision's CPU rule; its CUDA kernel compares against float(thr) and
+// differs exactly at IoU == float(thr) when float(thr) > thr, e.g. thr = 0.3:
+// DESIGN.md §5, tests/test_hand_derived.py.)
 struct NmsThr {
   double thr, mid;
   int tie_up, fast;
@@ -62,73 +71,85 @@ __device__ __forceinline__ bool iou_above(float4 a, float area_a, float4 b, floa
   return (double)(inter / uni) > T.thr;
 }
 
-// one wave per (segment, 64-row block, 64-col block >= row block); four column
-// blocks per 256-thread workgroup, each wave staging its own column boxes
-template <int kMode = 0>  // timing diagnostics only (tools/bench_nms.py): 1 = no IoU loop, 2 = no store
+// tile t of a segment's upper triangle, row-major: rows before rb hold
+// T(rb) = rb * nbw - rb * (rb - 1) / 2 tiles; rb = max{r : T(r) <= t}
+__device__ __forceinline__ void tri_tile(int t, int nbw, int* rb, int* cb) {
+  const float b = 2.0f * (float)nbw + 1.0f;
+  int r = (int)((b - sqrtf(fmaxf(b * b - 8.0f * (float)t, 0.0f))) * 0.5f);
+  r = max(0, min(r, nbw - 1));
+  while (r > 0 && r * nbw - r * (r - 1) / 2 > t) --r;
+  while (r + 1 < nbw && (r + 1) * nbw - (r + 1) * r / 2 <= t) ++r;
+  *rb = r;
+  *cb = r + (t - (r * nbw - r * (r - 1) / 2));
+}
+
+__device__ __forceinline__ int64_t tile_word(int s, int nbw, int rb, int cb) {
+  return (((int64_t)s * nbw + cb) * nbw + rb) * 64;
+}
+
+// Four tiles per 256-thread workgroup, each wave staging its tile's 64 ROW boxes in
+// LDS; lane = column.  Lane j sweeps the rows and sets bit i of its column word when
+// row i suppresses box j.  IoU is symmetric bit for bit (min / max and the area sum
+// (area_i + area_j) - inter commute exactly), so this is the reference's test of the
+// kept box i against candidate j.
 __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
-                                                       const int32_t* __restrict__ counts, int64_t n_max, int nbw,
-                                                       NmsThr T, uint64_t* __restrict__ mask) {
-  __shared__ float4 cb_box_all[4][64];
-  __shared__ float cb_area_all[4][64];
+                                                       const int32_t* __restrict__ counts, int nbw, NmsThr T,
+                                                       uint64_t* __restrict__ mask) {
+  __shared__ float4 rb_box_all[4][64];
+  __shared__ float rb_area_all[4][64];
   const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const int s = blockIdx.z, rb = blockIdx.y, cb = blockIdx.x * 4 + wv;
-  if (cb < rb || cb >= nbw) return;
+  const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
+  if (tile >= nbw * (nbw + 1) / 2) return;
+  int rb, cb;
+  tri_tile(__builtin_amdgcn_readfirstlane(tile), nbw, &rb, &cb);
+  rb = __builtin_amdgcn_readfirstlane(rb);
+  cb = __builtin_amdgcn_readfirstlane(cb);
   const int n = counts[s];
   if (rb * 64 >= n || cb * 64 >= n) return;
-  float4* cb_box = cb_box_all[wv];
-  float* cb_area = cb_area_all[wv];
+  float4* rb_box = rb_box_all[wv];
+  float* rb_area = rb_area_all[wv];
   const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
-  const int col = cb * 64 + t;
-  if (col < n) {
-    float4 c = bx[col];
-    cb_box[t] = c;
-    cb_area[t] = (c.z - c.x) * (c.w - c.y);
+  const int row = rb * 64 + t;
+  if (row < n) {
+    const float4 r = bx[row];
+    rb_box[t] = r;
+    rb_area[t] = (r.z - r.x) * (r.w - r.y);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int row = rb * 64 + t;
-  if (row >= n) return;
-  const float4 a = bx[row];
+  const int col = cb * 64 + t;
+  const bool cvalid = col < n;
+  const float4 a = bx[cvalid ? col : 0];
   const float aa = (a.z - a.x) * (a.w - a.y);
-  const int ncols = min(64, n - cb * 64);
-  const int start = (cb == rb) ? t + 1 : 0;
-  uint64_t bits = 0;
-  // uniform trip count, unrolled: the LDS broadcast reads of 8 column boxes issue together
-  // (columns outside [start, ncols) are masked, their LDS slots may hold stale boxes)
-  if (kMode != 1) {
-    auto sweep = [&](auto fast) {
-      constexpr bool F = decltype(fast)::value;
-      for (int j0 = 0; j0 < 64; j0 += 8) {
-        float4 cbx[8];
-        float cba[8];
+  uint64_t colw = 0;
+  // uniform trip count, unrolled: the LDS broadcast reads of 8 row boxes issue together
+  // (rows past n are masked below, their LDS slots may hold stale boxes)
+  auto sweep = [&](auto fast) {
+    constexpr bool F = decltype(fast)::value;
+#pragma nounroll
+    for (int i0 = 0; i0 < 64; i0 += 8) {
+      float4 rbx[8];
+      float rba[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          cbx[u] = cb_box[j0 + u];
-          cba[u] = cb_area[j0 + u];
-        }
-        uint32_t hit = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) hit |= (uint32_t)iou_above<F>(a, aa, cbx[u], cba[u], T) << u;
-        bits |= (uint64_t)hit << j0;
+      for (int u = 0; u < 8; ++u) {
+        rbx[u] = rb_box[i0 + u];
+        rba[u] = rb_area[i0 + u];
       }
-    };
-    if (T.fast)
-      sweep(std::true_type{});
-    else
-      sweep(std::false_type{});
-    // columns outside [start, ncols) (stale LDS slots, the diagonal and below)
-    const uint64_t hi = ncols >= 64 ? ~0ull : ((1ull << ncols) - 1ull);
-    const uint64_t lo = start >= 64 ? ~0ull : ((1ull << start) - 1ull);
-    bits &= hi & ~lo;
-  }
-  if (kMode != 2 || bits == 12345ull) mask[((int64_t)s * n_max + row) * nbw + cb] = bits;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
-  uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-  uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
-  return ((uint64_t)hi << 32) | lo;
+      uint32_t hit = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hit |= (uint32_t)iou_above<F>(rbx[u], rba[u], a, aa, T) << u;
+      colw |= (uint64_t)hit << i0;
+    }
+  };
+  if (T.fast)
+    sweep(std::true_type{});
+  else
+    sweep(std::false_type{});
+  const int nrows = min(64, n - rb * 64);
+  if (nrows < 64) colw &= (1ull << nrows) - 1ull;
+  if (cb == rb) colw &= t == 0 ? 0ull : (~0ull >> (64 - t));  // rows before the column only
+  mask[tile_word(s, nbw, rb, cb) + t] = cvalid ? colw : 0ull;
 }
 
 __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
@@ -137,104 +158,10 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restrict__ mask,
-                                                       const int32_t* __restrict__ counts, int64_t n_max, int nbw,
-                                                       int max_keep, int32_t* __restrict__ keep, int64_t kstride,
-                                                       int32_t* __restrict__ kcounts) {
-  __shared__ uint64_t remv[kMaxNmsWords];
-  __shared__ uint64_t s_kb;
-  __shared__ int s_nkeep;
-  const int s = blockIdx.x, tid = threadIdx.x;
-  const int n = counts[s];
-  const int nb = (n + 63) >> 6;
-  for (int w = tid; w < nb; w += blockDim.x) remv[w] = 0;
-  if (tid == 0) s_nkeep = 0;
-  __syncthreads();
-  const uint64_t* M = mask + (int64_t)s * n_max * nbw;
-  int32_t* K = keep + (int64_t)s * kstride;
-  const int q = tid & 31, rg = tid >> 5;  // word offset / row group of 8 for the OR phase
-  for (int b = 0; b < nb; ++b) {
-    const int nk = s_nkeep;
-    if (max_keep >= 0 && nk >= max_keep) break;
-    if (tid < 64) {
-      const int row = b * 64 + tid;
-      const uint64_t diag = row < n ? M[(int64_t)row * nbw + b] : 0ull;
-      uint64_t r = remv[b];
-      const int valid = n - b * 64;
-      if (valid < 64) r |= (~0ull) << valid;
-      uint64_t kb = 0;
-      for (int i = 0; i < 64; ++i) {
-        uint64_t di = readlane64(diag, i);
-        if (!((r >> i) & 1ull)) {
-          kb |= 1ull << i;
-          r |= di;
-        }
-      }
-      if (max_keep >= 0) {
-        int room = max_keep - nk;
-        while (__popcll(kb) > room) kb &= ~(1ull << (63 - __clzll(kb)));  // drop lowest-score extras
-      }
-      if ((kb >> tid) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = row;
-      if (tid == 0) {
-        s_kb = kb;
-        s_nkeep = nk + __popcll(kb);
-      }
-    }
-    __syncthreads();
-    const uint64_t kb = s_kb;
-    if (kb) {
-      for (int w0 = b + 1; w0 < nb; w0 += 32) {
-        const int w = w0 + q;
-        if (w < nb) {
-          uint64_t v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            int row = b * 64 + rg * 8 + j;
-            row = row < n ? row : n - 1;
-            v[j] = M[(int64_t)row * nbw + w];
-          }
-          uint64_t acc = 0;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc |= ((kb >> (rg * 8 + j)) & 1ull) ? v[j] : 0ull;
-          if (acc) atomicOr((unsigned long long*)&remv[w], (unsigned long long)acc);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (tid == 0) kcounts[s] = s_nkeep;
-}
-
-// Pipelined scan: the resolve chain of one segment never waits on memory.
-//  wave 0 (resolver), per 64-row block b: suppression word remv[b] | own,
-//    resolve the 64 candidates by visiting only unsuppressed ones (lowest set
-//    bit of the complement, readlane of the diagonal word), publish the kept
-//    bits, and OR the kept rows' word b+1 itself (wave-wide OR) -> `own` for
-//    the next block.  Its diagonal / next-word tiles come from an LDS ring.
-//  wave 1 (loader): stages the diagonal and next-word tiles of blocks ahead
-//    of the resolver into a kNmsRing-deep LDS ring.
-//  waves 2..3 (helpers), per block j: prefetch rows of block j for words
-//    >= j+2 BEFORE its kept bits exist, then OR the kept rows into remv with
-//    LDS atomics and publish their own progress (one counter per wave).  The resolver needs block j's
-//    helpers only at block j+2: one block of slack.
-// Wave hand-off is through LDS counters (release/acquire, workgroup scope).
-constexpr int kNmsHelpers = 2;
-constexpr int kNmsRing = 8;
-constexpr int kNmsRowGroups = kNmsHelpers * kWave / 32;  // 4 row groups x 32 word lanes
-constexpr int kNmsRowsPer = 64 / kNmsRowGroups;
-
-// OR over the 64 lanes with DPP row ops (no LDS round trip); uniform result.
-__device__ __forceinline__ uint32_t wave_or_u32_dpp(uint32_t v) {
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);  // row_mirror
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast15
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ uint64_t wave_or_u64_dpp(uint64_t v) {
-  return ((uint64_t)wave_or_u32_dpp((uint32_t)(v >> 32)) << 32) | wave_or_u32_dpp((uint32_t)v);
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ int lds_acquire(int* p) {
@@ -244,85 +171,94 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t w = ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), o, kWave) << 32) |
-                       (uint32_t)__shfl_xor((int)(uint32_t)v, o, kWave);
-    v |= w;
-  }
-  return v;
+// s_waitcnt vmcnt(N') for the largest supported N' <= n (waiting for fewer
+// outstanding operations than needed is always safe)
+__device__ __forceinline__ void wait_vmcnt_atmost(int n) {
+  if (n >= 32) wait_vmcnt<32>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else if (n >= 8) wait_vmcnt<8>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else if (n >= 1) wait_vmcnt<1>();
+  else wait_vmcnt<0>();
 }
 
-template <int kParallel>
-__global__ void __launch_bounds__(256) nms_scan_pipe_kernel(const uint64_t* __restrict__ mask,
-                                                            const int32_t* __restrict__ counts, int64_t n_max,
-                                                            int nbw, int max_keep, int32_t* __restrict__ keep,
-                                                            int64_t kstride, int32_t* __restrict__ kcounts,
-                                                            uint64_t* __restrict__ dbg) {
-  __shared__ uint64_t remv[kMaxNmsWords];
-  __shared__ uint64_t kbs[kMaxNmsWords];
-  __shared__ uint64_t ring_diag[kNmsRing][kWave], ring_next[kNmsRing][kWave];
-  __shared__ int s_resolved, s_tiles, s_stop;
-  __shared__ int s_applied[kNmsHelpers];  // per helper wave: blocks applied (a shared count could hide a laggard)
+// Scan, one 256-thread workgroup per segment: wave 0 resolves, waves 1..3 stage.
+//
+//  Staging (wave 1 + (b % 3) stages block b): the span of tiles (j, b), j in
+//  [j0, b], j0 = max(0, b - kNmsSpan + 1), contiguous in the mask, is copied by
+//  16-B LDS-DMA into ring slot b % kNmsRing.  A loader first waits until the
+//  resolver has finished block b - kNmsRing (the slot's previous user), issues
+//  the copies, and keeps up to two of its blocks in flight: when a third is
+//  issued, a counted vmcnt wait retires the oldest, which is then published
+//  (ready[slot] = block + 1).  Three loaders, each with its own vmcnt counter,
+//  keep up to six blocks in flight.
+//  Resolver, block b: waits ready[b % kNmsRing] == b + 1 (acquire), then
+//    acc = OR_j (tile(j, b)[lane] & kept[j]) over j < b  (LDS; global for j < j0)
+//    suppressed = ballot(acc != 0) | past-the-end columns,
+//  resolves the 64 candidates with the diagonal tile (b, b) in bit-parallel
+//  rounds (an undecided candidate with no undecided suppressor before it is kept,
+//  its victims dropped; same keep set as the one-by-one greedy, rounds =
+//  suppression-chain depth), stores the kept indices, kept[b] = kb (LDS, read by
+//  itself only) and s_resolved = b + 1 (release).
+//  No wave waits on a counter that its waiter must advance first: loaders wait
+//  on the resolver (slot reuse), the resolver on the loaders (ready flags), and
+//  a slot is reused only kNmsRing blocks later.  A max_keep stop sets s_stop and
+//  advances s_resolved past the end so every loader exits.
+constexpr int kNmsRing = 8;
+constexpr int kNmsSpan = 32;     // tiles per staged span (segments up to 2048 boxes fully staged)
+constexpr int kNmsLoaders = 3;
+
+__global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restrict__ mask,
+                                                       const int32_t* __restrict__ counts, int nbw, int span,
+                                                       int max_keep, int32_t* __restrict__ keep, int64_t kstride,
+                                                       int32_t* __restrict__ kcounts) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t nms_lds[];
+  __shared__ uint64_t kept[kMaxNmsWords];
+  __shared__ int ready[kNmsRing];
+  __shared__ int s_resolved, s_stop;
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
   const int n = counts[s];
   const int nb = (n + 63) >> 6;
-  for (int w = tid; w < nb; w += blockDim.x) remv[w] = 0;
-  if (tid < kNmsHelpers) s_applied[tid] = 0;
+  if (tid < kNmsRing) ready[tid] = 0;
   if (tid == 0) {
     s_resolved = 0;
-    s_tiles = 0;
     s_stop = nb;
   }
   __syncthreads();
-  const uint64_t* M = mask + (int64_t)s * n_max * nbw;
+  const int slot_words = ((span + 1) & ~1) * 64;  // whole 1 KB copies: an even number of tiles
   if (wave == 0) {
     int32_t* K = keep + (int64_t)s * kstride;
     int nk = 0;
-    uint64_t own = 0;
+    uint64_t keptv = 0;  // lane j: kept set of block j (j < 64); later blocks in kept[]
+    auto kept_at = [&](int j) { return j < 64 ? readlane64(keptv, j) : kept[j]; };
     for (int b = 0; b < nb; ++b) {
-      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b] = wall_clock64();
-      while (lds_acquire(&s_tiles) < b + 1) __builtin_amdgcn_s_sleep(1);
-      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 1] = wall_clock64();
-      if (b >= 2)
-        for (int hw = 0; hw < kNmsHelpers; ++hw)
-          while (lds_acquire(&s_applied[hw]) < b - 1) __builtin_amdgcn_s_sleep(1);
-      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 2] = wall_clock64();
-      const uint64_t diag = ring_diag[b % kNmsRing][lane], nxt = ring_next[b % kNmsRing][lane];
-      // r / kb / todo are wave-uniform: readfirstlane makes that provable, so the
-      // visit loop runs on the scalar unit (s_ff1, s_or) with one readlane pair each
-      uint64_t r = readfirstlane64(remv[b] | own);
+      while (lds_acquire(&ready[b % kNmsRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
+      const uint64_t* slot = nms_lds + (b % kNmsRing) * slot_words;
+      const int j0 = max(0, b - span + 1);
+      uint64_t acc = 0;
+      for (int j = 0; j < j0; ++j) acc |= mask[tile_word(s, nbw, j, b) + lane] & kept_at(j);
+      // eight staged words per batch: their LDS reads overlap
+      int j = j0;
+      for (; j + 8 <= b; j += 8) {
+        uint64_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = slot[(j + u - j0) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc |= t[u] & kept_at(j + u);
+      }
+      for (; j < b; ++j) acc |= slot[(j - j0) * 64 + lane] & kept_at(j);
+      const uint64_t d = slot[(b - j0) * 64 + lane];
+      uint64_t r = __ballot(acc != 0ull);
       const int valid = n - b * 64;
       if (valid < 64) r |= (~0ull) << valid;
-      // Bit-parallel greedy: an undecided candidate with no undecided suppressor
-      // before it is kept; the victims of the newly kept are dropped; repeat.
-      // Same keep set as the one-by-one greedy (the lowest undecided index is
-      // always decided, so it terminates), in rounds = suppression-chain depth.
       uint64_t kb = 0, und = ~r;
-      if (kParallel == 1) {
-        while (und) {
-          const uint64_t sup = wave_or_u64_dpp(((und >> lane) & 1ull) ? diag : 0ull);
-          const uint64_t nk = und & ~sup;
-          kb |= nk;
-          const uint64_t vic = wave_or_u64_dpp(((nk >> lane) & 1ull) ? diag : 0ull);
-          und &= ~(nk | vic);
-        }
-      } else if (kParallel == 2) {
-        while (und) {
-          const uint64_t sup = readfirstlane64(wave_or_u64(((und >> lane) & 1ull) ? diag : 0ull));
-          const uint64_t nk = und & ~sup;
-          kb |= nk;
-          const uint64_t vic = readfirstlane64(wave_or_u64(((nk >> lane) & 1ull) ? diag : 0ull));
-          und &= ~(nk | vic);
-        }
-      } else {
-        while (und) {
-          const int i = __builtin_ctzll(und);
-          kb |= 1ull << i;
-          r |= readlane64(diag, i);
-          und = ~r & ((i == 63) ? 0ull : (~0ull << (i + 1)));
-        }
+      while (und) {
+        const uint64_t sup = __ballot((d & und) != 0ull);
+        const uint64_t nkp = und & ~sup;
+        kb |= nkp;
+        const uint64_t vic = __ballot((d & nkp) != 0ull);
+        und &= ~(nkp | vic);
       }
       bool stop = false;
       if (max_keep >= 0) {
@@ -332,118 +268,87 @@ __global__ void __launch_bounds__(256) nms_scan_pipe_kernel(const uint64_t* __re
       }
       if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
       nk += __popcll(kb);
-      own = wave_or_u64_dpp(((kb >> lane) & 1ull) ? nxt : 0ull);
-      if (dbg && lane == 0) dbg[(int64_t)s * 4 * kMaxNmsWords + 4 * b + 3] = wall_clock64();
+      if (b < 64) keptv = lane == b ? kb : keptv;
       if (lane == 0) {
-        kbs[b] = kb;
+        kept[b] = kb;
         if (stop) s_stop = b;
-        lds_release(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1);
+        // the loaders only need this wave's LDS reads of the slot done, not the keep-list
+        // stores to global memory that a release fence would also wait for
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __hip_atomic_store(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (stop) break;
     }
     if (lane == 0) kcounts[s] = nk;
-  } else if (wave == 1) {
-    for (int j = 0; j < nb; ++j) {
-      const int row = j * 64 + lane, rc = row < n ? row : n - 1;
-      const uint64_t d = M[(int64_t)rc * nbw + j];
-      const uint64_t x = M[(int64_t)rc * nbw + (j + 1 < nbw ? j + 1 : j)];
-      while (lds_acquire(&s_resolved) < j - kNmsRing + 1) __builtin_amdgcn_s_sleep(1);
-      if (s_stop < j) break;
-      ring_diag[j % kNmsRing][lane] = row < n ? d : 0ull;
-      ring_next[j % kNmsRing][lane] = (row < n && j + 1 < nb) ? x : 0ull;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) lds_release(&s_tiles, j + 1);
-    }
   } else {
-    const int h = tid - 2 * kWave;   // 0 .. 127
-    const int q = h & 31, rg = h >> 5;  // word lane, row group
-    // rows of block j, first word chunk (word j + 2 + q), loaded one block ahead
-    auto load = [&](int j, uint64_t (&v)[kNmsRowsPer]) {
-      const int wq = j + 2 + q, wc = wq < nbw ? wq : nbw - 1;
-#pragma unroll
-      for (int t = 0; t < kNmsRowsPer; ++t) {
-        const int rowj = j * 64 + rg + kNmsRowGroups * t;
-        v[t] = M[(int64_t)(rowj < n ? rowj : n - 1) * nbw + wc];
-      }
+    // descriptor over this segment's tiles (32-bit byte range)
+    const int64_t seg_words = (int64_t)nbw * nbw * 64;
+    const __amdgpu_buffer_rsrc_t mr = uniform_rsrc(mask + s * seg_words, seg_words * 8);
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint64_t*)nms_lds);
+    // up to two blocks of this loader in flight; a block is published once a counted
+    // vmcnt wait shows its copies landed (LDS-DMA writes are complete in LDS then, and
+    // the flag store goes through the same LDS after them: no fence, which would also
+    // wait for the younger copies)
+    int q0 = -1, q1 = -1, n1 = 0;
+    auto publish = [&](int blk) {  // after a vmcnt wait that covers blk's copies
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&ready[blk % kNmsRing], blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    uint64_t v[kNmsRowsPer], vn[kNmsRowsPer];
-    load(0, v);
-    for (int j = 0; j < nb; ++j) {
-      const int wq = j + 2 + q;
-      load(j + 1 < nb ? j + 1 : j, vn);  // unconditional: keeps the vmcnt accounting exact
-      while (lds_acquire(&s_resolved) < j + 1) __builtin_amdgcn_s_sleep(1);
-      if (s_stop < j) break;
-      const uint64_t kb = kbs[j];
-      for (int w = wq; w < nb; w += 32) {
-        uint64_t acc = 0;
-#pragma unroll
-        for (int t = 0; t < kNmsRowsPer; ++t) {
-          const int rr = rg + kNmsRowGroups * t, rowj = j * 64 + rr;
-          if (((kb >> rr) & 1ull) && rowj < n) acc |= (w == wq) ? v[t] : M[(int64_t)rowj * nbw + w];
-        }
-        if (acc) atomicOr((unsigned long long*)&remv[w], (unsigned long long)acc);
+    for (int b = wave - 1; b < nb; b += kNmsLoaders) {
+      while (lds_acquire(&s_resolved) < b - kNmsRing + 1) __builtin_amdgcn_s_sleep(1);
+      if (s_stop < b) break;
+      const int j0 = max(0, b - span + 1);
+      const int ninst = (b - j0 + 2) >> 1;  // 1 KB (two tiles) per wave-instruction
+      const uint32_t dst = lds0 + (uint32_t)((b % kNmsRing) * slot_words * 8);
+      const int src = (int)((tile_word(s, nbw, j0, b) - s * seg_words) * 8);
+      for (int k = 0; k < ninst; ++k) lds_dma_at<16>(mr, dst + (uint32_t)k * 1024u, lane * 16, src + k * 1024);
+      if (q1 >= 0) {  // three in flight: retire the oldest
+        wait_vmcnt_atmost(n1 + ninst);
+        publish(q0);
+        q0 = q1;
+        q1 = b;
+        n1 = ninst;
+      } else if (q0 >= 0) {
+        q1 = b;
+        n1 = ninst;
+      } else {
+        q0 = b;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) lds_release(&s_applied[wave - 2], j + 1);
-#pragma unroll
-      for (int t = 0; t < kNmsRowsPer; ++t) v[t] = vn[t];
     }
+    wait_vmcnt<0>();
+    if (q0 >= 0) publish(q0);
+    if (q1 >= 0) publish(q1);
   }
 }
-
-// tools/bench_nms.py hooks (not part of the public header): scan variant 0 = legacy
-// block-synchronous scan, 1 = pipelined; optional per-block resolver timestamps.
-static int g_nms_scan_variant = -1;
-static int g_nms_mask_mode = 0;
-static uint64_t* g_nms_dbg = nullptr;
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                           uint64_t* mask, hipStream_t st) {
   const int nbw = (n_max + 63) / 64;
-  dim3 g((nbw + 3) / 4, nbw, S);
-  if (g_nms_mask_mode == 1)
-    hipLaunchKernelGGL(nms_mask_kernel<1>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
-                       nms_thr(thr), mask);
-  else if (g_nms_mask_mode == 2)
-    hipLaunchKernelGGL(nms_mask_kernel<2>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
-                       nms_thr(thr), mask);
-  else
-    hipLaunchKernelGGL(nms_mask_kernel<0>, g, dim3(256), 0, st, boxes, seg_stride, counts, (int64_t)n_max, nbw,
-                       nms_thr(thr), mask);
-  if (g_nms_scan_variant < 0) g_nms_scan_variant = getenv("FRH_NMS_SCAN_LEGACY") ? 0 : 1;
-  if (g_nms_scan_variant == 0)
-    hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw, max_keep, keep,
-                       kstride, kcounts);
-  else if (g_nms_scan_variant == 3)
-    hipLaunchKernelGGL(nms_scan_pipe_kernel<2>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
-                       max_keep, keep, kstride, kcounts, g_nms_dbg);
-  else if (g_nms_scan_variant == 2)
-    hipLaunchKernelGGL(nms_scan_pipe_kernel<0>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
-                       max_keep, keep, kstride, kcounts, g_nms_dbg);
-  else
-    hipLaunchKernelGGL(nms_scan_pipe_kernel<1>, dim3(S), dim3(256), 0, st, mask, counts, (int64_t)n_max, nbw,
-                       max_keep, keep, kstride, kcounts, g_nms_dbg);
+  dim3 g((nbw * (nbw + 1) / 2 + 3) / 4, S);
+  hipLaunchKernelGGL(nms_mask_kernel, g, dim3(256), 0, st, boxes, seg_stride, counts, nbw, nms_thr(thr), mask);
+  const int span = std::min(nbw, kNmsSpan);
+  const size_t lds = (size_t)kNmsRing * ((span + 1) & ~1) * 64 * sizeof(uint64_t);
+  static bool attr = false;
+  if (!attr) {
+    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kNmsRing * kNmsSpan * 64 * 8));
+    attr = true;
+  }
+  hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep, kstride,
+                     kcounts);
   return check_launch("nms");
 }
 
-size_t nms_mask_bytes(int32_t S, int32_t n_max) {
+size_t nms_mask_bytes(int32_t S, int32_t n_max) {  // [S][cb][rb][64] column words
   const size_t nbw = (size_t)((n_max + 63) / 64);
-  return (size_t)S * (size_t)n_max * nbw * sizeof(uint64_t);
+  return (size_t)S * nbw * nbw * 64 * sizeof(uint64_t);
 }
 
 }  // namespace frh
 
 using namespace frh;
-
-extern "C" void frh_nms_mask_debug(int32_t mode) { g_nms_mask_mode = mode; }
-
-extern "C" void frh_nms_scan_debug(int32_t variant, void* timestamps) {
-  g_nms_scan_variant = variant;
-  g_nms_dbg = reinterpret_cast<uint64_t*>(timestamps);
-}
 
 extern "C" size_t frh_nms_workspace(int32_t num_segs, int32_t n_max) {
   return nms_mask_bytes(num_segs, n_max > 0 ? n_max : 1);

@@ -4,2420 +4,24 @@
 // per-level torchvision RoIAlign(output_size, 1/stride, sampling_ratio=2)),
 // torchvision legacy (aligned=False) RoIAlign semantics.
 //
-// Forward kernels (all bit-identical: -ffp-contract=off, reference op order):
-//  * roi_align_fwd_lds_kernel -- the default: per (RoI, 64 channels) workgroup,
-//    each wave copies its RoI's tap window of 16 channels into LDS (windows
-//    <= 256 floats) or gathers per bin (larger windows).
-//  * roi_align_fwd_group_kernel -- opt-in (frh_roi_align_fwd_ws): a
-//    planning launch sorts the RoIs into spatial groups of 8; a workgroup
-//    stages the UNION of its group's tap rows for one channel at a time into
-//    LDS with 16-B LDS-DMA (three-slot ring, one barrier per channel) and its
-//    8 waves evaluate one RoI each.  Overlapping RoIs share each staged line.
+// Forward (all bit-identical: -ffp-contract=off, reference op order; kernels in
+// roi_kernels.h):
+//  * roi_align_fwd_pair_kernel -- the default (sampling 2, up to 8x8 bins, even C):
+//    one wave per (RoI, 16 channels); the RoI's tap window staged by LDS-DMA with
+//    channel pairs interleaved, packed-f32 bilinear sums.
+//  * roi_align_fwd_lds_kernel -- odd channel counts: per-(RoI, 64 channels)
+//    workgroup, windows <= 256 floats staged in LDS, larger ones gathered.
 //  * roi_align_fwd_kernel -- direct gather, any pooled size / sampling ratio.
-// Feature tensors are addressed through explicit (batch, channel, y, x)
-// element strides: NCHW, channels_last and strided views (FPN P6 =
-// P5[..., ::2, ::2]) all run.
-#include <math.h>
-#include <stdlib.h>
-
-#include <algorithm>
-
-#include <type_traits>
-
-#include "roi_common.h"
+// Backward: roi_align_bwd_sep_kernel (sampling 2, up to 8x8 bins: separable
+// row-run sums, one atomic per run) / roi_align_bwd_lds_kernel (up to 64 bins) /
+// roi_align_bwd_kernel (per-tap atomics, any shape).
+// Feature tensors are addressed through explicit (batch, channel, y, x) element
+// strides: NCHW, channels_last and strided views (FPN P6 = P5[..., ::2, ::2]) all
+// run.  The losing / diagnostic variants measured along the way live in the
+// tools-only library (tools/csrc/roi_variants.hip).
+#include "roi_kernels.h"
 
 namespace frh {
-
-constexpr int kRoiThreads = 256;
-constexpr int kRoiChanChunk = 64;
-constexpr int kMaxSamplesPerDim = 1024;
-
-// true when the separable tables fit in LDS (always for fixed sampling ratios;
-// adaptive grids on huge RoIs fall back to computing taps per sample)
-__device__ __forceinline__ bool taps_fit(const RoiGeom& g, const RoiCfg& c) {
-  return c.ph * g.gh <= kMaxSamplesPerDim && c.pw * g.gw <= kMaxSamplesPerDim;
-}
-
-__device__ __forceinline__ void fill_taps(const RoiGeom& g, const RoiCfg& c, int H, int W, Tap* ty, Tap* tx) {
-  if (!taps_fit(g, c)) return;
-  const int ny = c.ph * g.gh, nx = c.pw * g.gw;
-  for (int e = threadIdx.x; e < ny + nx; e += blockDim.x) {
-    if (e < ny) {
-      int p = e / g.gh, i = e - p * g.gh;
-      ty[e] = make_tap(sample_y(g, p, i), H);
-    } else {
-      int q = e - ny;
-      int p = q / g.gw, i = q - p * g.gw;
-      tx[q] = make_tap(sample_x(g, p, i), W);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  fill_taps(g, c, H, W, ty, tx);
-  __syncthreads();
-  const int nbins = c.ph * c.pw;
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const bool tab = taps_fit(g, c);
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  float* o = out + (k * c.C + c0) * nbins;
-  for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
-    const int cl = item / nbins, bin = item - cl * nbins;
-    const int py = bin / c.pw, px = bin - py * c.pw;
-    const float* f = base + (int64_t)(c0 + cl) * scs;
-    float acc = 0.0f;
-    for (int iy = 0; iy < g.gh; ++iy) {
-      const Tap a = tab ? ty[py * g.gh + iy] : make_tap(sample_y(g, py, iy), H);
-      for (int ix = 0; ix < g.gw; ++ix) {
-        const Tap bx = tab ? tx[px * g.gw + ix] : make_tap(sample_x(g, px, ix), W);
-        float val = 0.0f;
-        if (a.valid && bx.valid) {
-          float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
-          float v1 = f[a.lo * sy + bx.lo * sx], v2 = f[a.lo * sy + bx.hi * sx];
-          float v3 = f[a.hi * sy + bx.lo * sx], v4 = f[a.hi * sy + bx.hi * sx];
-          val = ((w1 * v1 + w2 * v2) + w3 * v3) + w4 * v4;
-        }
-        acc = acc + val;
-      }
-    }
-    o[item] = acc / g.count;
-  }
-}
-
-
-// Buffer-descriptor variant (sampling ratio 2, ph*pw <= 256; the default).
-// Lane (bin, channel group cg) keeps its bin's 16 tap offsets in VGPRs as
-// 32-bit byte offsets into a descriptor over this (image, level, channel
-// chunk) slice; the channel walk moves only the wave-uniform soffset, so the
-// loop carries no per-lane address arithmetic.  When every x-sample of the
-// wave has x_hi = x_lo + 1 (all but right-border clamped samples) the taps of
-// a sample row are one 8-byte load: 8 loads per (bin, channel) instead of 16.
-// The 1/count of SR=2 is an exact power of two, so acc * 0.25 == acc / 4.
-// Results identical to the direct kernel.
-template <int U>
-__device__ __forceinline__ void fwd_buf_block(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out,
-                                              int64_t k, int c0, const RoiGeom& g) {
-  constexpr int SR = 2;
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int groups = kRoiThreads / nbins;
-  const int t = threadIdx.x;
-  if (t >= groups * nbins) return;
-  const int bin = t % nbins, cg = t / nbins;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(sample_y(g, py, i), H);
-    tx[i] = make_tap(sample_x(g, px, i), W);
-  }
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
-  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + c0) * nbins, (int64_t)nch * nbins * 4);
-  const int cstep = groups * scs * 4, ostep = groups * nbins * 4;
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-  int row[SR][2], col[SR][2];
-  bool pair = sx == 1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    row[i][0] = (cg * scs + (ty[i].valid ? ty[i].lo * sy : 0)) * 4;
-    row[i][1] = (cg * scs + (ty[i].valid ? ty[i].hi * sy : 0)) * 4;
-    col[i][0] = tx[i].valid ? tx[i].lo * sx * 4 : 0;
-    col[i][1] = tx[i].valid ? tx[i].hi * sx * 4 : 0;
-    pair = pair && (!tx[i].valid || tx[i].hi == tx[i].lo + 1);
-  }
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  auto bin_value = [&](const float (&v)[SR][SR][4]) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
-                    wt[iy][ix][3] * v[iy][ix][3];
-        acc = acc + (ok[iy][ix] ? val : 0.0f);
-      }
-    return acc * 0.25f;
-  };
-  // wave-uniform trip counts (soffset must stay scalar): every lane has a
-  // channel in the first nch / groups steps, the tail step is lane-guarded
-  const int full = nch / groups, iters = (nch + groups - 1) / groups;
-  const bool tail_ok = cg + full * groups < nch;
-  if (__all(pair)) {
-    int off[SR][2][SR];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) off[iy][r][ix] = row[iy][r] + col[ix][0];
-    int it = 0;
-    for (; it + U <= full; it += U) {
-      u32x2 rv[U][SR][2][SR];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int ix = 0; ix < SR; ++ix)
-              rv[u][iy][r][ix] = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][r][ix], (it + u) * cstep, 0);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float v[SR][SR][4];
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-          for (int ix = 0; ix < SR; ++ix) {
-            v[iy][ix][0] = __uint_as_float(rv[u][iy][0][ix].x);
-            v[iy][ix][1] = __uint_as_float(rv[u][iy][0][ix].y);
-            v[iy][ix][2] = __uint_as_float(rv[u][iy][1][ix].x);
-            v[iy][ix][3] = __uint_as_float(rv[u][iy][1][ix].y);
-          }
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, (it + u) * ostep, 0);
-      }
-    }
-    for (; it < iters; ++it) {
-      if (it == full && !tail_ok) break;
-      float v[SR][SR][4];
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][0][ix], it * cstep, 0);
-          const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][1][ix], it * cstep, 0);
-          v[iy][ix][0] = __uint_as_float(a.x);
-          v[iy][ix][1] = __uint_as_float(a.y);
-          v[iy][ix][2] = __uint_as_float(b.x);
-          v[iy][ix][3] = __uint_as_float(b.y);
-        }
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
-    }
-  } else {
-    for (int it = 0; it < iters; ++it) {
-      if (it == full && !tail_ok) break;
-      float v[SR][SR][4];
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v[iy][ix][q] = __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(fr, row[iy][q >> 1] + col[ix][q & 1], it * cstep, 0));
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
-    }
-  }
-}
-
-
-// Wave-staged variant (sampling ratio 2, ph*pw <= 64, 2*ph and 2*pw <= 64).
-// Every tap of a RoI lies in the window [y0, y1] x [x0, x1] of its level;
-// after FPN level mapping that window is a few to ~30 cells per side.  Each
-// wave owns 16 channels of the RoI and, per channel, copies the window into
-// its own LDS slab with lane-contiguous loads (every feature line fetched
-// once per RoI-channel, instead of 8 gathers per bin hitting the same lines),
-// then lane = bin reads its 16 taps from LDS.  The loads of channel i+1 are
-// in flight while channel i is evaluated.  The slab row has one extra column
-// holding a copy of the window's last feature column, so a right-border
-// clamped tap (x_lo = x_hi = W-1) reads (x_lo, x_lo + 1) like every other
-// sample.  No block barriers: waves are independent.  Windows above
-// kWinMax floats take the per-wave gather path.  Results identical to the
-// direct kernel.
-constexpr int kWinMax = 1024;
-constexpr int kWinR = kWinMax / kWave;
-
-// kChunk: channels per workgroup (kChunk / 4 per wave).  kSkip (diagnostics only):
-// 1 = skip staged RoIs, 2 = skip gathered ones.
-// kWpe: minimum waves per SIMD the register allocation must allow (0: compiler's choice).
-template <int kStageMax, int kSkip = 0, int kChunk = kRoiChanChunk, int kWpe = 0>
-__global__ void __launch_bounds__(kRoiThreads) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
-roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
-                                                                        float* __restrict__ out) {
-  constexpr int SR = 2;
-  __shared__ float slab_all[kRoiThreads / kWave][kWinMax];
-  const int64_t k = blockIdx.x;
-  // readfirstlane: the wave index is uniform, and the compiler must know it (soffset operands)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  constexpr int kWC = kChunk / (kRoiThreads / kWave);
-  const int cw0 = blockIdx.y * kChunk + wave * kWC;
-  const int nch = min(kWC, c.C - cw0);
-  float* slab = slab_all[wave];
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  // window of the valid taps: lane i evaluates y sample i and x sample i
-  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-  if (lane < c.ph * SR) {
-    const Tap t = make_tap(sample_y(g, lane / SR, lane % SR), H);
-    if (t.valid) ylo = t.lo, yhi = t.hi;
-  }
-  if (lane < c.pw * SR) {
-    const Tap t = make_tap(sample_x(g, lane / SR, lane % SR), W);
-    if (t.valid) xlo = t.lo, xhi = t.hi;
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  const bool any = y1 >= y0 && x1 >= x0;
-  // odd slab row stride: the 4 tap rows of a wave's bins spread over the LDS banks
-  const int ws = (x1 - x0 + 2) | 1, n = any ? (y1 - y0 + 1) * ws : 0;
-  if (n > kStageMax) {  // uniform over the block (one RoI): large windows take the block gather path
-    if (kSkip != 2)
-      for (int cc = 0; cc < kChunk && blockIdx.y * kChunk + cc < c.C; cc += kRoiChanChunk)
-        fwd_buf_block<2>(lv, c, out, k, blockIdx.y * kChunk + cc, g);
-    return;
-  }
-  if (kSkip == 1) return;
-  if (nch <= 0) return;
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
-  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)nch * nbins * 4);
-  const int cstep = scs * 4, ostep = nbins * 4;
-  // this lane's bin: taps, weights, validity
-  const int bin = lane < nbins ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(sample_y(g, py, i), H);
-    tx[i] = make_tap(sample_x(g, px, i), W);
-  }
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  auto bin_value = [&](const float (&v)[SR][SR][4]) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
-                    wt[iy][ix][3] * v[iy][ix][3];
-        acc = acc + (ok[iy][ix] ? val : 0.0f);
-      }
-    return acc * 0.25f;
-  };
-  const bool active = lane < nbins;
-  if (n <= kStageMax) {
-    // slab addresses of this bin's sample rows (x_lo, x_lo + 1 pairs)
-    int sa[SR][2][SR];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        const bool v = ok[iy][ix];
-        sa[iy][0][ix] = v ? (ty[iy].lo - y0) * ws + (tx[ix].lo - x0) : 0;
-        sa[iy][1][ix] = v ? (ty[iy].hi - y0) * ws + (tx[ix].lo - x0) : 0;
-      }
-    // staging: slab element e = lane + 64 j  <-  feature (y0 + e / ws, min(x0 + e % ws, W - 1));
-    // the j loop is specialised on RB = 64-element rounds (1, 2, 4, 8, 16) so it unrolls branch-free
-    auto run = [&](auto rb) {
-      constexpr int RB = decltype(rb)::value, D = kWinR / RB;  // D channel windows per round, 16 loads/lane
-      int goff[RB];
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        const int e = lane + j * kWave;
-        const int r = e / ws, cc = e - r * ws;
-        // lanes past the window re-read its first element: no extra cache line per round
-        goff[j] = e < n ? ((y0 + r) * sy + min(x0 + cc, W - 1) * sx) * 4 : (y0 * sy + x0 * sx) * 4;
-      }
-      float st[D][RB];
-      auto issue = [&](int c0r) {
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-#pragma unroll
-          for (int j = 0; j < RB; ++j)
-            st[d][j] = __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(fr, goff[j], min(c0r + d, nch - 1) * cstep, 0));
-      };
-      issue(0);
-      for (int i = 0; i < nch; i += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-#pragma unroll
-          for (int j = 0; j < RB; ++j) slab[(d * RB + j) * kWave + lane] = st[d][j];  // [n, 64 RB) junk, unread
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (i + D < nch) issue(i + D);
-        if (active) {
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            if (i + d < nch) {
-              const float* sl = slab + d * RB * kWave;
-              float v[SR][SR][4];
-#pragma unroll
-              for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-                for (int ix = 0; ix < SR; ++ix) {
-                  v[iy][ix][0] = sl[sa[iy][0][ix]];
-                  v[iy][ix][1] = sl[sa[iy][0][ix] + 1];
-                  v[iy][ix][2] = sl[sa[iy][1][ix]];
-                  v[iy][ix][3] = sl[sa[iy][1][ix] + 1];
-                }
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, lane * 4, (i + d) * ostep, 0);
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    };
-    const int R = (n + kWave - 1) / kWave;
-    if (R <= 1)
-      run(std::integral_constant<int, 1>{});
-    else if (R <= 2 || kStageMax <= 2 * kWave)
-      run(std::integral_constant<int, 2>{});
-    else if (R <= 4 || kStageMax <= 4 * kWave)
-      run(std::integral_constant<int, 4>{});
-    else if (R <= 8 || kStageMax <= 8 * kWave)
-      run(std::integral_constant<int, 8>{});
-    else
-      run(std::integral_constant<int, kWinR>{});
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// One wave, one RoI, channels [c0, c1): the RoI's tap rows (dense window
-// [y0, y1] when it has <= 4*ph rows, else the (y_lo, y_hi) list of its 2*ph
-// y-samples) x columns [x0 & ~(kV-1), x1] are staged channel by channel into
-// the wave's slab by LDS-DMA (kV floats per lane), two batches in flight with
-// counted vmcnt waits; lane = bin evaluates from LDS.  Slabs beyond kSlab /
-// 2 are gathered per bin.  Used where a group's union does not fit.
-template <int kSlab, int kV>
-__device__ __forceinline__ void roi_segment(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, float* slab,
-                                            int64_t k, int c0, int c1, int lane) {
-  constexpr int SR = 2;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw, nsy = c.ph * SR;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  const bool active = lane < nbins;
-  const int bin = active ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {  // sampling 2: the "/ gh" of the sample position is an exact halving
-    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
-    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
-  }
-  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
-    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  const bool any = y1 >= y0 && x1 >= x0;
-  const int xs0 = x0 & ~(kV - 1);
-  const int ws = kV == 1 ? ((x1 - x0 + 1) | 1) : ((x1 - xs0 + kV) & ~(kV - 1));
-  const bool dense = any && y1 - y0 + 1 <= 2 * nsy;
-  const int nrows = !any ? 0 : dense ? y1 - y0 + 1 : 2 * nsy;
-  const int R = (nrows * ws + kV * kWave - 1) / (kV * kWave);
-  const int Rr = R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 16;
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + k * c.C * nbins, (int64_t)c.C * nbins * 4);
-  const int cstep = scs * 4, ostep = nbins * 4;
-  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  if (!any) {
-    for (int ch = c0; ch < c1; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
-    return;
-  }
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  auto combine = [&](const float (&v)[SR][SR][4]) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
-                    wt[iy][ix][3] * v[iy][ix][3];
-        acc = acc + (ok[iy][ix] ? val : 0.0f);
-      }
-    return acc * 0.25f;
-  };
-  if (Rr * kV * kWave * 2 > kSlab) {
-    // window larger than half the slab: per-bin gather, two channels in flight
-    int off[SR][SR][4];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        const bool v = ok[iy][ix];
-        const int r0 = v ? ty[iy].lo * sy : 0, r1 = v ? ty[iy].hi * sy : 0;
-        const int q0 = v ? tx[ix].lo * sx : 0, q1 = v ? tx[ix].hi * sx : 0;
-        off[iy][ix][0] = (r0 + q0) * 4;
-        off[iy][ix][1] = (r0 + q1) * 4;
-        off[iy][ix][2] = (r1 + q0) * 4;
-        off[iy][ix][3] = (r1 + q1) * 4;
-      }
-    for (int ch = c0; ch < c1; ch += 2) {
-      const int chb = min(ch + 1, c1 - 1);
-      float va[SR][SR][4], vb[SR][SR][4];
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            va[iy][ix][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fr, off[iy][ix][q], ch * cstep, 0));
-            vb[iy][ix][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fr, off[iy][ix][q], chb * cstep, 0));
-          }
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(combine(va)), orr, ovoff, ch * ostep, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(combine(vb)), orr, ch + 1 < c1 ? ovoff : 0x40000000,
-                                            (ch + 1) * ostep, 0);
-    }
-    return;
-  }
-  // slab byte offsets of this bin's taps: [iy][row lo/hi][ix][col lo/hi]
-  int sa[SR][2][SR][2];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      const bool v = ok[iy][ix];
-      const int rlo = dense ? a.lo - y0 : 2 * (py * SR + iy), rhi = dense ? a.hi - y0 : 2 * (py * SR + iy) + 1;
-      sa[iy][0][ix][0] = v ? (rlo * ws + (b.lo - xs0)) * 4 : 0;
-      sa[iy][0][ix][1] = v ? (rlo * ws + (b.hi - xs0)) * 4 : 0;
-      sa[iy][1][ix][0] = v ? (rhi * ws + (b.lo - xs0)) * 4 : 0;
-      sa[iy][1][ix][1] = v ? (rhi * ws + (b.hi - xs0)) * 4 : 0;
-    }
-  auto bin_value = [&](const char* sl) {
-    float v[SR][SR][4];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        v[iy][ix][0] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][0]);
-        v[iy][ix][1] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][1]);
-        v[iy][ix][2] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][0]);
-        v[iy][ix][3] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][1]);
-      }
-    return combine(v);
-  };
-  // sparse rows: entry 2i / 2i+1 = y_lo / y_hi of y-sample i = ty[i % 2] of lane (i / 2) * pw
-  const int tyl0 = ty[0].valid ? ty[0].lo : y0, tyh0 = ty[0].valid ? ty[0].hi : y0;
-  const int tyl1 = ty[1].valid ? ty[1].lo : y0, tyh1 = ty[1].valid ? ty[1].hi : y0;
-  const int n = nrows * ws;
-  auto run = [&](auto rb) {
-    constexpr int RB = decltype(rb)::value;
-    constexpr int kB0 = kSlab / (2 * RB * kV * kWave);
-    constexpr int kB = kB0 < 1 ? 1 : (kB0 < 16 ? kB0 : 16);  // channels per batch
-    constexpr int F = RB * kV * kWave * 4;                     // slab bytes per channel
-    static_assert(kB * (RB + 1) < 64, "batch too large for vmcnt");
-    if (kB0 < 1) return;  // excluded by the gather test above
-    int goff[RB];
-    {
-      const int step = kV * kWave, dr = step / ws, dc = step - dr * ws;
-      int r = (kV * lane) / ws, col = kV * lane - r * ws;
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        const int e = kV * lane + j * step;
-        const int rs = min(r, 2 * nsy - 1), src = (rs >> 2) * c.pw;
-        const int a0 = __shfl(tyl0, src, kWave), a1 = __shfl(tyh0, src, kWave);
-        const int b0 = __shfl(tyl1, src, kWave), b1 = __shfl(tyh1, src, kWave);
-        const int srow = (rs & 2) ? ((rs & 1) ? b1 : b0) : ((rs & 1) ? a1 : a0);
-        const int fy = dense ? y0 + r : srow;
-        // columns past the row end only fill slab cells no tap reads; lanes past the slab
-        // re-read its first element (no extra line)
-        const int fx = kV == 1 ? min(xs0 + col, W - 1) : xs0 + col;
-        goff[j] = e < n ? (fy * sy + fx * sx) * 4 : (y0 * sy + xs0 * sx) * 4;
-        r += dr;
-        col += dc;
-        if (col >= ws) col -= ws, ++r;
-      }
-    }
-    const int nb = (c1 - c0 + kB - 1) / kB;
-    auto issue = [&](int b) {  // batch b -> slot b & 1; channels past c1 re-read the last one
-      const int slot = (b & 1) * kB;
-#pragma unroll
-      for (int s = 0; s < kB; ++s) {
-        const int ch = min(c0 + b * kB + s, c1 - 1);
-#pragma unroll
-        for (int j = 0; j < RB; ++j)
-          lds_dma<4 * kV>(fr, slab + (slot + s) * (F / 4) + j * kV * kWave, goff[j], ch * cstep);
-      }
-    };
-    issue(0);
-    if (nb > 1) issue(1);
-    for (int b = 0; b < nb; ++b) {
-      // retire batch b: younger than it are batch b-1's kB stores and batch b+1's DMAs
-      if (b + 1 < nb) {
-        if (b == 0)
-          wait_vmcnt<kB * RB>();
-        else
-          wait_vmcnt<kB * RB + kB>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      const char* sl = reinterpret_cast<const char*>(slab + (b & 1) * kB * (F / 4));
-#pragma unroll
-      for (int s = 0; s < kB; ++s) {
-        const int ch = c0 + b * kB + s;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(sl + s * F)), orr,
-                                              ch < c1 ? ovoff : 0x40000000, ch * ostep, 0);
-      }
-      if (b + 2 < nb) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot b & 1 fully read before it is refilled
-        issue(b + 2);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  if (Rr == 1)
-    run(std::integral_constant<int, 1>{});
-  else if (Rr == 2)
-    run(std::integral_constant<int, 2>{});
-  else if (Rr == 4)
-    run(std::integral_constant<int, 4>{});
-  else if (Rr == 8)
-    run(std::integral_constant<int, 8>{});
-  else
-    run(std::integral_constant<int, 16>{});
-}
-
-// ---------------------------------------------------------------------------
-// Channel-pair forward (variant 20).  One wave per (RoI, 128 channels), lane =
-// bin.  The RoI's tap grid is staged into the wave's LDS slab by 4-B LDS-DMA
-// with the two channels of a pair interleaved ([cell][2]), so every tap of a
-// bin is ONE aligned ds_read_b64 (2 LDS cycles per wave-instruction, twice the
-// bytes of ds_read_b32) and the bilinear sums run as packed f32 (v_pk_mul_f32
-// / v_pk_add_f32) on both channels at once -- halving the two per-output
-// costs (LDS tap reads, VALU) that bound the per-RoI kernels.  Each slab
-// dimension is either the dense tap window [y0, y1] (at most 4*ph rows) or the
-// list of the 2*ph samples' (lo, hi) taps, so every RoI fits (<= 28 x 29 cells
-// at 7x7) and large RoIs need no per-bin gather.  A DMA round moves 32
-// consecutive cells of one pair (two feature planes, one or two lines each).
-// The slab is two buffers; a stage is the D pairs (D = 8, 4, 2, 1, as the cell
-// count allows) one buffer holds, and stage s+1 is in flight while stage s is
-// evaluated (counted vmcnt waits); the tap reads of half-sample-row h+1 are in
-// flight while h is summed.  The RoI geometry is set up once per 64 pairs.
-// Invalid samples have zero weights and read cell 0 (finite features: +0, the
-// reference's own 0 * feature term).  Same operation order as torchvision:
-// bit-identical to the other kernels.
-constexpr int kPairWave = 8;                    // channel pairs per wave (= workgroup): 16 channels
-constexpr int kPairHalf = 1664;                 // dwords per buffer (13 KB per wave for both)
-constexpr int kPairChunk = 2 * kPairWave;       // channels per workgroup
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// ds_read_b64 by hand: the compiler would pair two of them into ds_read2_b64,
-// which runs at half the rate (8 LDS cycles instead of 2 x 2, MI355X_MICROARCH
-// §LDS).  The caller waits with lds_wait<N>, which also orders the values.
-template <int OFF>
-__device__ __forceinline__ f32x2 lds_read_b64(uint32_t addr) {
-  f32x2 v;
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
-  return v;
-}
-template <int N>
-__device__ __forceinline__ void lds_wait(f32x2 (&v)[8]) {
-  asm volatile("s_waitcnt lgkmcnt(%8)"
-               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-               : "i"(N)
-               : "memory");
-}
-
-template <int D, int kHalf = kPairHalf>
-struct PairLayout {
-  static constexpr int RS = (kHalf / D) / kWave * kWave;  // dwords per pair region
-  static constexpr int RP = RS / kWave;                       // DMA rounds per pair
-  static constexpr int kCells = RS / 2;
-  static_assert(D * RP + 2 * D < 64, "vmcnt is 6 bits");
-};
-
-// kSkip (diagnostics only): 1 = skip RoIs staged 8 pairs at a time, 2 = skip the others.
-// kDiag (diagnostics only): per-wave s_memrealtime stamps past the results:
-// [start, setup done, stage 0 ready, stage 0 done, stage 1 ready, end, D, RoI].
-// kHalf: dwords per slab buffer.  kCls: 0 = every RoI; 1 = only RoIs whose slab has at
-// most kPairSplit cells (others skipped); 2 = only the others -- a small-slab launch
-// (more resident waves) for the common small windows plus a large-slab launch.
-constexpr int kPairSplit = 256;  // cells: PairLayout<1, 512>::kCells
-// kWPB: waves per workgroup; wave w of block b takes item (RoI, chunk) = b * kWPB + w
-// (RoI-major, ceil(C / (2 kPW)) chunks per RoI) -- fewer, larger workgroups than one per
-// (RoI, chunk): dispatching 16 K single-wave workgroups alone costs ~8.5 us.
-template <int kSkip = 0, bool kDiag = false, int kPW = kPairWave, int kHalf = kPairHalf, int kCls = 0, int kWPB = 1>
-__global__ void __launch_bounds__(kWave * kWPB) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c,
-                                                                          float* __restrict__ out) {
-  constexpr int SR = 2;
-  __shared__ __attribute__((aligned(16))) float slab_all[kWPB][2 * kHalf];
-  int64_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (kDiag) stamp[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  const int wave = kWPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
-  // this wave's slab as an LDS byte address (integer: no generic-pointer casts)
-  const uint32_t sbase =
-      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)&slab_all[0][0]) +
-      (uint32_t)wave * 8u * kHalf;
-  int64_t k = blockIdx.x;
-  int cw0 = blockIdx.y * 2 * kPW;
-  if (kWPB > 1) {
-    const int G = (c.C + 2 * kPW - 1) / (2 * kPW);
-    const int64_t item = (int64_t)blockIdx.x * kWPB + wave;
-    k = item / G;
-    if (k >= c.K) return;
-    cw0 = (int)(item - k * G) * 2 * kPW;
-  }
-  const int lane = threadIdx.x & (kWave - 1);
-  const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  // sample positions (sampling ratio 2: the reference's "/ 2" is an exact halving)
-  auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
-  auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
-  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;  // tap lists: entry i = tap (i & 1 ? hi : lo) of sample i / 2
-  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-  if (lane < nly) {
-    const int s = lane >> 1;
-    const Tap t = make_tap(pos_y(s >> 1, s & 1), H);
-    if (t.valid) yrow = (lane & 1) ? t.hi : t.lo, ylo = t.lo, yhi = t.hi;
-  }
-  if (lane < nlx) {
-    const int s = lane >> 1;
-    const Tap t = make_tap(pos_x(s >> 1, s & 1), W);
-    if (t.valid) xcol = (lane & 1) ? t.hi : t.lo, xlo = t.lo, xhi = t.hi;
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  const bool active = lane < nbins;
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)2 * npairs * nbins * 4);
-  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  const int ostep = nbins * 4;
-  if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: all bins 0
-    if (kSkip || kCls == 2) return;
-    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
-    return;
-  }
-  const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;
-  const int R = dy ? y1 - y0 + 1 : nly, Cs = dx ? x1 - x0 + 1 : nlx;
-  const int Cs2 = Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
-  const int ncell = R * Cs2;
-  const bool small = ncell <= PairLayout<8, kHalf>::kCells;
-  if (kSkip && (kSkip == 1) == small) return;
-  if (kCls == 3) return;  // diagnostics: setup only
-  if (kCls == 4) {        // diagnostics: setup + one DMA round + wait
-    lds_dma_at<4>(uniform_rsrc(lv.feat[l] + (int64_t)g.b * lv.sb[l], 4 * (int64_t)H * W), sbase, lane * 4, 0);
-    wait_vmcnt<0>();
-    return;
-  }
-  if (kCls == 1 && ncell > kPairSplit) return;
-  if (kCls == 2 && ncell <= kPairSplit) return;
-  // feature byte offsets of slab row / column `lane`
-  const int rsrc = (dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
-  const int csrc = (dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
-  // this lane's bin: weights (zero for invalid samples) and LDS addresses of its 16 taps
-  const int bin = active ? lane : 0;
-  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  const uint32_t lbase = sbase;
-  float wt[SR][SR][4];
-  uint32_t ta[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy) {
-    const Tap a = make_tap(pos_y(py, iy), H);
-    const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap b = make_tap(pos_x(px, ix), W);
-      const int q0 = dx ? b.lo - x0 : 2 * (px * SR + ix), q1 = dx ? b.hi - x0 : 2 * (px * SR + ix) + 1;
-      const bool ok = a.valid && b.valid;
-      wt[iy][ix][0] = ok ? a.h * b.h : 0.f;
-      wt[iy][ix][1] = ok ? a.h * b.l : 0.f;
-      wt[iy][ix][2] = ok ? a.l * b.h : 0.f;
-      wt[iy][ix][3] = ok ? a.l * b.l : 0.f;
-      ta[iy][ix][0] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q0) : 0u);
-      ta[iy][ix][1] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q1) : 0u);
-      ta[iy][ix][2] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q0) : 0u);
-      ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q1) : 0u);
-    }
-  }
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const uint32_t inv = (65536u + (uint32_t)Cs2 - 1u) / (uint32_t)Cs2;  // e / Cs2 == (e * inv) >> 16 for e < 1024
-
-  auto run = [&](auto dd) {
-    constexpr int D = decltype(dd)::value, RS = PairLayout<D, kHalf>::RS, RP = PairLayout<D, kHalf>::RP;
-    const int nst = (npairs + D - 1) / D;
-    // region dword j * 64 + lane of every pair  <-  channel (lane & 1) of cell (j * 64 + lane) / 2
-    int goff[RP];
-#pragma unroll
-    for (int j = 0; j < RP; ++j) {
-      int e = (j * kWave + lane) >> 1;
-      e = e < ncell ? e : 0;
-      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
-      goff[j] = __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
-    }
-    if (kDiag) stamp[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
-      const uint32_t buf = sbase + 4u * (uint32_t)((s & 1) * kHalf);
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
-#pragma unroll
-        for (int j = 0; j < RP; ++j) lds_dma_at<4>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
-      }
-    };
-    auto eval = [&](auto bb, int s) {
-      constexpr int kBuf = decltype(bb)::value;
-      // half-rows h = 2 d + iy: 8 tap reads each; reads of h + 1 in flight while h is summed
-      f32x2 v[2][8];
-      f32x2 acc = {0.0f, 0.0f};
-      auto load = [&](auto hh) {
-        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
-      };
-      load(std::integral_constant<int, 0>{});
-      static_for<0, 2 * D>([&](auto hh) {
-        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
-        if constexpr (h + 1 < 2 * D) {
-          load(std::integral_constant<int, h + 1>{});
-          lds_wait<8>(v[h & 1]);
-        } else {
-          lds_wait<0>(v[h & 1]);
-        }
-        if (iy == 0) acc = f32x2{0.0f, 0.0f};
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          const float* w = wt[iy][ix];
-          const f32x2* x = &v[h & 1][ix * 4];
-          const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
-          acc = acc + val;
-        }
-        if (iy == 1) {
-          const f32x2 r = acc * 0.25f;
-          const int p = s * D + d;
-          const int vo = p < npairs ? ovoff : 0x40000000;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, 0);
-        }
-      });
-    };
-    auto step = [&](auto bb, int s) {
-      if (s >= nst) return;
-      // retire stage s: younger than its DMAs are stage s-1's 2D stores and stage s+1's DMAs
-      if (s + 1 < nst) {
-        issue(s + 1);
-        if (s == 0)
-          wait_vmcnt<D * RP>();
-        else
-          wait_vmcnt<D * RP + 2 * D>();
-      } else if (s == 0) {
-        wait_vmcnt<0>();
-      } else {
-        wait_vmcnt<2 * D>();
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (kDiag && s < 2) stamp[2 + 2 * s] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      eval(bb, s);
-      if (kDiag && s < 1) stamp[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    issue(0);
-    for (int s = 0; s < nst; s += 2) {
-      step(std::integral_constant<int, 0>{}, s);
-      step(std::integral_constant<int, 1>{}, s + 1);
-    }
-    if (kDiag) {
-      wait_vmcnt<0>();
-      stamp[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      stamp[6] = D;
-      stamp[7] = k;
-      const int64_t wid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-      int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + wid * 8;
-      if (lane < 8) st[lane] = stamp[lane];
-    }
-  };
-  if (small)
-    run(std::integral_constant<int, 8>{});
-  else if (ncell <= PairLayout<4, kHalf>::kCells)
-    run(std::integral_constant<int, 4>{});
-  else if (ncell <= PairLayout<2, kHalf>::kCells)
-    run(std::integral_constant<int, 2>{});
-  else
-    run(std::integral_constant<int, 1>{});
-}
-
-__global__ void roi_empty_kernel(float* out) {
-  if (threadIdx.x == 64) out[0] = 0.0f;  // never true: keeps the launch from being elided
-}
-
-// ---------------------------------------------------------------------------
-// Persistent channel-pair forward (variant 25).  The staging and evaluation of
-// the channel-pair kernel above, but a grid of resident single-wave workgroups
-// walks the items (RoI, kStrPairs channel pairs): wave w takes items w, w + G,
-// w + 2G, ...  The two-buffer LDS ring never drains between items: before the
-// last stage of item i is evaluated, item i+1's RoI / level / descriptor loads,
-// its tap window and DMA offsets are set up and its first stage is issued, so
-// the per-item setup and first-load latency (about half of a channel-pair
-// wave's life) overlap the previous item's evaluation.  Stage
-// shapes (D pairs per stage) may change from item to item; the vmcnt waits
-// count the DMAs and stores issued after the stage being retired (in-order
-// completion) and round down to a supported immediate (waiting for fewer
-// outstanding operations is always safe).  Bit-identical to the other kernels.
-constexpr int kStrPairs = 8;         // channel pairs per item
-constexpr int kStrGoff = PairLayout<1>::RP;
-
-struct StrItem {
-  int64_t k;
-  int ok, D, nst, npairs, cw0, scs4;
-  int H, W, y0, x0, dy, dx, Cs2;
-  float sh, sw, bh, bw;
-  __amdgpu_buffer_rsrc_t fr, orr;
-  int goff[kStrGoff];
-};
-
-__device__ __forceinline__ int str_dma_count(int D) { return D >= 4 ? 24 : 26; }
-
-// s_waitcnt vmcnt(N') for the largest supported N' <= n
-__device__ __forceinline__ void wait_vmcnt_le(int n) {
-  if (n >= 42) wait_vmcnt<42>();
-  else if (n >= 40) wait_vmcnt<40>();
-  else if (n >= 34) wait_vmcnt<34>();
-  else if (n >= 32) wait_vmcnt<32>();
-  else if (n >= 30) wait_vmcnt<30>();
-  else if (n >= 28) wait_vmcnt<28>();
-  else if (n >= 26) wait_vmcnt<26>();
-  else if (n >= 24) wait_vmcnt<24>();
-  else if (n >= 16) wait_vmcnt<16>();
-  else if (n >= 8) wait_vmcnt<8>();
-  else if (n >= 4) wait_vmcnt<4>();
-  else if (n >= 2) wait_vmcnt<2>();
-  else wait_vmcnt<0>();
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// DMA-side setup of item t (uniform over the wave except goff)
-__device__ __forceinline__ void str_setup(StrItem& it, const RoiLevels& lv, const RoiCfg& c, float* out, int64_t t,
-                                          int G) {
-  constexpr int SR = 2;
-  const int lane = threadIdx.x;
-  it.k = t / G;
-  it.cw0 = (int)(t - it.k * G) * 2 * kStrPairs;
-  it.npairs = min(kStrPairs, (c.C - it.cw0) / 2);
-  const RoiGeom g = roi_geom(c, lv, it.k);
-  const int l = g.lvl;
-  it.H = lv.h[l];
-  it.W = lv.w[l];
-  it.sh = g.start_h;
-  it.sw = g.start_w;
-  it.bh = g.bin_h;
-  it.bw = g.bin_w;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  it.scs4 = scs * 4;
-  const int nbins = c.ph * c.pw;
-  it.orr = uniform_rsrc(out + (it.k * c.C + it.cw0) * nbins, (int64_t)2 * it.npairs * nbins * 4);
-  auto pos_y = [&](int p, int i) { return it.sh + (float)p * it.bh + ((float)i + 0.5f) * it.bh * 0.5f; };
-  auto pos_x = [&](int p, int i) { return it.sw + (float)p * it.bw + ((float)i + 0.5f) * it.bw * 0.5f; };
-  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
-  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-  if (lane < nly) {
-    const int s = lane >> 1;
-    const Tap tp = make_tap(pos_y(s >> 1, s & 1), it.H);
-    if (tp.valid) yrow = (lane & 1) ? tp.hi : tp.lo, ylo = tp.lo, yhi = tp.hi;
-  }
-  if (lane < nlx) {
-    const int s = lane >> 1;
-    const Tap tp = make_tap(pos_x(s >> 1, s & 1), it.W);
-    if (tp.valid) xcol = (lane & 1) ? tp.hi : tp.lo, xlo = tp.lo, xhi = tp.hi;
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  it.ok = y1 >= y0 && x1 >= x0;
-  it.y0 = y0;
-  it.x0 = x0;
-  it.dy = y1 - y0 + 1 <= nly;
-  it.dx = x1 - x0 + 1 <= nlx;
-  const int R = it.dy ? y1 - y0 + 1 : nly, Cs = it.dx ? x1 - x0 + 1 : nlx;
-  it.Cs2 = Cs | 1;
-  const int ncell = R * it.Cs2;
-  it.D = ncell <= PairLayout<8>::kCells ? 8 : ncell <= PairLayout<4>::kCells ? 4 : ncell <= PairLayout<2>::kCells ? 2 : 1;
-  it.nst = (it.npairs + it.D - 1) / it.D;
-  if (!it.ok) return;
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(it.H - 1) * sy + (int64_t)(it.W - 1) * sx + 1) * 4;
-  it.fr = uniform_rsrc(base, extent);
-  const int rsrc = (it.dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
-  const int csrc = (it.dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
-  const uint32_t inv = (65536u + (uint32_t)it.Cs2 - 1u) / (uint32_t)it.Cs2;
-  const int RS = it.D == 8 ? PairLayout<8>::RS : it.D == 4 ? PairLayout<4>::RS : it.D == 2 ? PairLayout<2>::RS
-                                                                                               : PairLayout<1>::RS;
-  const int RP = RS / kWave;
-#pragma unroll
-  for (int j = 0; j < kStrGoff; ++j) {
-    int e = (j * kWave + lane) >> 1;
-    e = e < ncell ? e : 0;
-    const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * it.Cs2, Cs - 1);
-    const int v = __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * it.scs4;
-    it.goff[j] = j < RP ? v : 0;
-  }
-}
-
-// eval-side setup: this lane's bin weights (zero for invalid samples) and LDS tap addresses
-__device__ __forceinline__ void str_taps(const StrItem& it, const RoiCfg& c, uint32_t lbase, uint32_t (&ta)[2][2][4],
-                                         float (&wt)[2][2][4]) {
-  constexpr int SR = 2;
-  const int lane = threadIdx.x;
-  const int nbins = c.ph * c.pw;
-  const int bin = lane < nbins ? lane : 0;
-  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  auto pos_y = [&](int p, int i) { return it.sh + (float)p * it.bh + ((float)i + 0.5f) * it.bh * 0.5f; };
-  auto pos_x = [&](int p, int i) { return it.sw + (float)p * it.bw + ((float)i + 0.5f) * it.bw * 0.5f; };
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy) {
-    const Tap a = make_tap(pos_y(py, iy), it.H);
-    const int r0 = it.dy ? a.lo - it.y0 : 2 * (py * SR + iy), r1 = it.dy ? a.hi - it.y0 : 2 * (py * SR + iy) + 1;
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap b = make_tap(pos_x(px, ix), it.W);
-      const int q0 = it.dx ? b.lo - it.x0 : 2 * (px * SR + ix), q1 = it.dx ? b.hi - it.x0 : 2 * (px * SR + ix) + 1;
-      const bool ok = a.valid && b.valid;
-      wt[iy][ix][0] = ok ? a.h * b.h : 0.f;
-      wt[iy][ix][1] = ok ? a.h * b.l : 0.f;
-      wt[iy][ix][2] = ok ? a.l * b.h : 0.f;
-      wt[iy][ix][3] = ok ? a.l * b.l : 0.f;
-      ta[iy][ix][0] = lbase + (ok ? 8u * (uint32_t)(r0 * it.Cs2 + q0) : 0u);
-      ta[iy][ix][1] = lbase + (ok ? 8u * (uint32_t)(r0 * it.Cs2 + q1) : 0u);
-      ta[iy][ix][2] = lbase + (ok ? 8u * (uint32_t)(r1 * it.Cs2 + q0) : 0u);
-      ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * it.Cs2 + q1) : 0u);
-    }
-  }
-}
-
-template <int D>
-__device__ __forceinline__ void str_issue(const StrItem& it, float* slab, int b, int s) {
-  constexpr int RS = PairLayout<D>::RS, RP = PairLayout<D>::RP;
-  float* buf = slab + b * kPairHalf;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {  // pairs past the last re-read it (their stores are dropped)
-    const int soff = (it.cw0 + 2 * min(s * D + d, it.npairs - 1)) * it.scs4;
-#pragma unroll
-    for (int j = 0; j < RP; ++j) lds_dma<4>(it.fr, buf + d * RS + j * kWave, it.goff[j], soff);
-  }
-}
-
-__device__ __forceinline__ void str_issue_dyn(const StrItem& it, float* slab, int b, int s) {
-  switch (it.D) {
-    case 8: str_issue<8>(it, slab, b, s); break;
-    case 4: str_issue<4>(it, slab, b, s); break;
-    case 2: str_issue<2>(it, slab, b, s); break;
-    default: str_issue<1>(it, slab, b, s); break;
-  }
-}
-
-template <int D, int kBuf>
-__device__ __forceinline__ void str_eval(const StrItem& it, int s, int ovoff, int ostep, const uint32_t (&ta)[2][2][4],
-                                         const float (&wt)[2][2][4]) {
-  constexpr int SR = 2, RS = PairLayout<D>::RS;
-  f32x2 v[2][8];
-  f32x2 acc = {0.0f, 0.0f};
-  auto load = [&](auto hh) {
-    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kPairHalf + d * RS);
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
-  };
-  load(std::integral_constant<int, 0>{});
-  static_for<0, 2 * D>([&](auto hh) {
-    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
-    if constexpr (h + 1 < 2 * D) {
-      load(std::integral_constant<int, h + 1>{});
-      lds_wait<8>(v[h & 1]);
-    } else {
-      lds_wait<0>(v[h & 1]);
-    }
-    if (iy == 0) acc = f32x2{0.0f, 0.0f};
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const float* w = wt[iy][ix];
-      const f32x2* x = &v[h & 1][ix * 4];
-      const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
-      acc = acc + val;
-    }
-    if (iy == 1) {
-      const f32x2 r = acc * 0.25f;
-      const int p = s * D + d;
-      const int vo = p < it.npairs ? ovoff : 0x40000000;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), it.orr, vo, 2 * p * ostep, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), it.orr, vo, (2 * p + 1) * ostep, 0);
-    }
-  });
-}
-
-__device__ __forceinline__ void str_eval_dyn(const StrItem& it, int b, int s, int ovoff, int ostep,
-                                             const uint32_t (&ta)[2][2][4], const float (&wt)[2][2][4]) {
-  if (b == 0) {
-    switch (it.D) {
-      case 8: str_eval<8, 0>(it, s, ovoff, ostep, ta, wt); break;
-      case 4: str_eval<4, 0>(it, s, ovoff, ostep, ta, wt); break;
-      case 2: str_eval<2, 0>(it, s, ovoff, ostep, ta, wt); break;
-      default: str_eval<1, 0>(it, s, ovoff, ostep, ta, wt); break;
-    }
-  } else {
-    switch (it.D) {
-      case 8: str_eval<8, 1>(it, s, ovoff, ostep, ta, wt); break;
-      case 4: str_eval<4, 1>(it, s, ovoff, ostep, ta, wt); break;
-      case 2: str_eval<2, 1>(it, s, ovoff, ostep, ta, wt); break;
-      default: str_eval<1, 1>(it, s, ovoff, ostep, ta, wt); break;
-    }
-  }
-}
-
-// an item with no valid sample: every bin of its channels is 0
-__device__ __forceinline__ void str_zero(const StrItem& it, int ovoff, int ostep) {
-  for (int ch = 0; ch < 2 * it.npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, it.orr, ovoff, ch * ostep, 0);
-}
-
-template <int kWpe = 0>
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1))) roi_align_fwd_stream_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out,
-                                                                      int64_t nitems, int G) {
-  __shared__ __attribute__((aligned(16))) float slab[2 * kPairHalf];
-  const int lane = threadIdx.x;
-  const int nbins = c.ph * c.pw;
-  const int ovoff = lane < nbins ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  const int ostep = nbins * 4;
-  const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
-  int64_t t = blockIdx.x;
-  if (t >= nitems) return;
-  StrItem cur;
-  for (;;) {  // first item with a valid sample
-    str_setup(cur, lv, c, out, t, G);
-    if (cur.ok) break;
-    str_zero(cur, ovoff, ostep);
-    t += gridDim.x;
-    if (t >= nitems) return;
-  }
-  str_issue_dyn(cur, slab, 0, 0);
-  int bt = 0, prev_st = 0;
-  uint32_t ta[2][2][4];
-  float wt[2][2][4];
-  str_taps(cur, c, lbase, ta, wt);
-  for (;;) {
-    for (int s = 0; s + 1 < cur.nst; ++s) {
-      str_issue_dyn(cur, slab, bt ^ 1, s + 1);
-      wait_vmcnt_le(str_dma_count(cur.D) + prev_st);
-      wave_sync();
-      str_eval_dyn(cur, bt, s, ovoff, ostep, ta, wt);
-      prev_st = 2 * cur.D;
-      wave_sync();
-      bt ^= 1;
-    }
-    // last stage of this item: first set up and issue the next item's stage 0
-    StrItem nxt;
-    bool have = false;
-    int extra = 0;
-    int64_t t2 = t;
-    for (;;) {
-      t2 += gridDim.x;
-      if (t2 >= nitems) break;
-      str_setup(nxt, lv, c, out, t2, G);
-      if (nxt.ok) {
-        have = true;
-        break;
-      }
-      str_zero(nxt, ovoff, ostep);
-      extra += 2 * nxt.npairs;
-    }
-    int dn = 0;
-    if (have) {
-      str_issue_dyn(nxt, slab, bt ^ 1, 0);
-      dn = str_dma_count(nxt.D);
-    }
-    wait_vmcnt_le(dn + prev_st + extra);
-    wave_sync();
-    str_eval_dyn(cur, bt, cur.nst - 1, ovoff, ostep, ta, wt);
-    prev_st = 2 * cur.D;
-    wave_sync();
-    bt ^= 1;
-    if (!have) break;
-    cur = nxt;
-    t = t2;
-    str_taps(cur, c, lbase, ta, wt);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Wide-staged forward (variant 30).  Workgroup = (RoI, 64 channels), wave = 16
-// channels, lane = bin, as the per-RoI LDS kernel -- but every RoI is staged:
-// the slab is the RoI's tap rows (the dense window [y0, y1] when it has at most
-// 4*ph rows, else the list of the 2*ph samples' (lo, hi) rows) x the columns
-// [x0 & ~3, x1 + 1] rounded up to whole 16-B quads, copied with 16-B loads
-// (one buffer_load_dwordx4 per lane per 64 quads: a quarter of the load
-// instructions of 4-B staging, which is what bound staging large windows) and
-// ds_write_b128.  The x-pair (x_lo, x_lo + 1) of a sample row is one
-// ds_read2_b32 into a register pair, and both products of the pair run as one
-// v_pk_mul_f32 (the sum keeps the reference order, so results stay
-// bit-identical).  A round stages 8 / RB channel windows (RB = 16-B loads per
-// lane per window); the next round's loads are in flight while this round is
-// evaluated.  Invalid samples have zero weights and read cell 0.  Windows
-// beyond kX4Slab floats (none at 7x7 sampling 2 below 28 x 36) take the block
-// gather.
-constexpr int kX4Slab = 2048;  // floats per wave: 8 quads per lane
-
-// kXcd: XCD x (= linear block id % 8) takes the x-th contiguous eighth of the
-// (RoI, chunk) items, so RoIs that are neighbours in the input order share an L2.
-template <int kSkip = 0, bool kXcd = false, int kWpe = 0>
-__global__ void __launch_bounds__(kRoiThreads) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
-roi_align_fwd_x4_kernel(RoiLevels lv, RoiCfg c,
-                                                                       float* __restrict__ out) {
-  constexpr int SR = 2;
-  constexpr int kWC = kRoiChanChunk / (kRoiThreads / kWave);  // 16 channels per wave
-  __shared__ __attribute__((aligned(16))) float slab_all[kRoiThreads / kWave][kX4Slab];
-  int64_t k = blockIdx.x;
-  int chunk = blockIdx.y;
-  if (kXcd) {
-    const int64_t total = (int64_t)gridDim.x * gridDim.y, per = (total + 7) / 8;
-    const int64_t lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-    const int64_t w = (lin % 8) * per + lin / 8;
-    if (w >= total) return;
-    k = w / gridDim.y;
-    chunk = (int)(w - k * gridDim.y);
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  const int cw0 = chunk * kRoiChanChunk + wave * kWC;
-  const int nch = min(kWC, c.C - cw0);
-  float* slab = slab_all[wave];
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int sy = (int)lv.sy[l], scs = (int)lv.sc[l];  // sx == 1 (host check)
-  auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
-  auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
-  const int nly = 2 * SR * c.ph;  // row list: entry i = row (i & 1 ? hi : lo) of y-sample i / 2
-  int yrow = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-  if (lane < nly) {
-    const int s = lane >> 1;
-    const Tap t = make_tap(pos_y(s >> 1, s & 1), H);
-    if (t.valid) yrow = (lane & 1) ? t.hi : t.lo, ylo = t.lo, yhi = t.hi;
-  }
-  if (lane < SR * c.pw) {
-    const Tap t = make_tap(pos_x(lane >> 1, lane & 1), W);
-    if (t.valid) xlo = t.lo, xhi = t.hi;
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  const bool any = y1 >= y0 && x1 >= x0;
-  const bool dy = y1 - y0 + 1 <= nly;
-  const int R = !any ? 0 : dy ? y1 - y0 + 1 : nly;
-  const int xs0 = x0 & ~3, wq = any ? (x1 + 2 - xs0 + 3) >> 2 : 0;  // quads per slab row (covers x1 + 1)
-  const int Wr = 4 * wq, nq = R * wq;
-  if (4 * nq > kX4Slab) {  // uniform over the block (one RoI)
-    if (kSkip != 2 && kSkip != 3) fwd_buf_block<2>(lv, c, out, k, chunk * kRoiChanChunk, g);
-    return;
-  }
-  const int RB = (nq + kWave - 1) / kWave;
-  if ((kSkip == 1 || kSkip == 2) && (kSkip == 1) == (RB <= 1)) return;
-  if (nch <= 0) return;
-  const bool active = lane < nbins;
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)nch * nbins * 4);
-  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  const int ostep = nbins * 4;
-  if (!any) {
-    for (int ch = 0; ch < nch; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
-    return;
-  }
-  // one descriptor per channel plane: quads past the plane's last element read 0
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
-  const int64_t plane = ((int64_t)(H - 1) * sy + W) * 4;
-  // this lane's bin: weights (zero for invalid samples) and slab offsets of its x-pairs
-  const int bin = active ? lane : 0;
-  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  f32x2 wlo[SR][SR], whi[SR][SR];  // (w_ll, w_lh), (w_hl, w_hh)
-  int sa[SR][SR][2];               // slab floats of the (x_lo, x_lo + 1) pair in rows lo / hi
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy) {
-    const Tap a = make_tap(pos_y(py, iy), H);
-    const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap b = make_tap(pos_x(px, ix), W);
-      const bool ok = a.valid && b.valid;
-      wlo[iy][ix] = ok ? f32x2{a.h * b.h, a.h * b.l} : f32x2{0.f, 0.f};
-      whi[iy][ix] = ok ? f32x2{a.l * b.h, a.l * b.l} : f32x2{0.f, 0.f};
-      sa[iy][ix][0] = ok ? r0 * Wr + (b.lo - xs0) : 0;
-      sa[iy][ix][1] = ok ? r1 * Wr + (b.lo - xs0) : 0;
-    }
-  }
-  auto bin_value = [&](const float* sl) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        const f32x2 lo = {sl[sa[iy][ix][0]], sl[sa[iy][ix][0] + 1]};
-        const f32x2 hi = {sl[sa[iy][ix][1]], sl[sa[iy][ix][1] + 1]};
-        const f32x2 p = wlo[iy][ix] * lo, q = whi[iy][ix] * hi;
-        acc = acc + (((p.x + p.y) + q.x) + q.y);
-      }
-    return acc * 0.25f;
-  };
-  // quad e = lane + 64 j of a window  <-  feature row (dense: y0 + e / wq; list: row e / wq), columns xs0 + 4 (e % wq)
-  const uint32_t invq = (65536u + (uint32_t)wq - 1u) / (uint32_t)wq;
-  auto run = [&](auto rb) {
-    constexpr int RBc = decltype(rb)::value, D = 8 / RBc;  // D channel windows per round, 8 loads per lane
-    int goff[RBc];
-#pragma unroll
-    for (int j = 0; j < RBc; ++j) {
-      int e = lane + j * kWave;
-      e = e < nq ? e : 0;  // lanes past the window re-read its first quad
-      const int r = (int)(((uint32_t)e * invq) >> 16), m = e - r * wq;
-      const int fy = dy ? y0 + r : __shfl(yrow >= 0 ? yrow : y0, r, kWave);
-      goff[j] = (fy * sy + xs0 + 4 * m) * 4;
-    }
-    u32x4 st[D][RBc];
-    auto issue = [&](int c0r) {
-#pragma unroll
-      for (int d = 0; d < D; ++d)
-#pragma unroll
-        for (int j = 0; j < RBc; ++j)
-          st[d][j] = __builtin_amdgcn_raw_buffer_load_b128(
-              uniform_rsrc(base + (int64_t)min(c0r + d, nch - 1) * scs, plane), goff[j], 0, 0);
-    };
-    issue(0);
-    for (int i = 0; i < nch; i += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d)
-#pragma unroll
-        for (int j = 0; j < RBc; ++j)
-          *reinterpret_cast<u32x4*>(slab + ((d * RBc + j) * kWave + lane) * 4) = st[d][j];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (i + D < nch) issue(i + D);
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        if (i + d < nch) {
-          if (kSkip == 3) {  // diagnostics: evaluate, do not store
-            const float v = bin_value(slab + d * RBc * kWave * 4);
-            asm volatile("" ::"v"(v));
-          } else {
-            const float v = kSkip == 4 ? 0.0f : bin_value(slab + d * RBc * kWave * 4);  // 4: store, do not evaluate
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orr, ovoff, (i + d) * ostep, 0);
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  };
-  if (RB <= 1)
-    run(std::integral_constant<int, 1>{});
-  else if (RB <= 2)
-    run(std::integral_constant<int, 2>{});
-  else if (RB <= 4)
-    run(std::integral_constant<int, 4>{});
-  else
-    run(std::integral_constant<int, 8>{});
-}
-
-// ---------------------------------------------------------------------------
-// Grouped forward (opt-in: frh_roi_align_fwd_ws).  Measured on cfg2 (1024 RoIs):
-// 76-85 us vs 55 us for the per-RoI kernel -- each workgroup is a serial chain
-// of a ~6 us dependent-load prologue plus ~2 us per 4-channel step (DESIGN.md
-// §4); it moves half the L2 lines but does not yet hide the latency.
-//
-// roi_group_plan_kernel (one workgroup, K <= 8192): counting sort of the RoIs
-// by (image, level, 128-px tile of the RoI centre), then the sorted sequence is
-// cut into groups of kGrp consecutive RoIs of one (image, level).  Output:
-// order [K], gstart [ngroups + 1], ngroups.
-//
-// roi_align_fwd_group_kernel: workgroup = (group, 64 channels), wave w = the
-// group's RoI w.  The union of the group's tap rows (a bitmask over feature
-// rows) x the union of their columns is staged per channel into a three-slot
-// LDS ring by LDS-DMA (all 512 threads, fixed per-thread offsets), one barrier
-// per channel; wave w evaluates RoI w's 49 bins from the slot.  A feature line
-// shared by several RoIs of the group is fetched once, not once per RoI (the
-// RoI-by-RoI kernels are bound by the L1-miss line rate: ~3.1M mostly partial
-// lines for cfg2 vs ~1.6M here).  Groups whose union exceeds a slot fall back
-// to roi_segment per wave.  XCD x (= block % 8) takes the x-th eighth of the
-// groups, so neighbouring groups share an L2.
-constexpr int kGrp = 8;                    // RoIs per group = waves per workgroup
-constexpr int kGrpThreads = kGrp * kWave;  // 512
-constexpr int kGrpChans = 64;              // channels per workgroup
-constexpr int kGrpRing = 18432;            // LDS ring floats (72 KB: two workgroups per CU)
-constexpr int kRowWords = 32;              // union row bitmask: feature maps up to 1024 rows
-constexpr int kMaxURows = 512;
-constexpr int kPlanThreads = 1024, kPlanMaxRois = 8192, kPlanBuckets = 4096;
-
-struct GroupPlan {
-  const int32_t* order;    // [K] RoI ids, grouped
-  const int32_t* gstart;   // [maxg + 1]; gstart[ngroups] = K
-  const int32_t* ngroups;  // [1]
-};
-
-// block-wide exclusive scan (sum or max) of one value per thread
-template <bool kMax>
-__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* wsum, uint32_t* total) {
-  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-  auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : a + b; };
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t u = __shfl_up(inc, o, kWave);
-    if (lane >= o) inc = op(inc, u);
-  }
-  if (lane == kWave - 1) wsum[w] = inc;
-  __syncthreads();
-  uint32_t base = 0, all = 0;
-  for (int i = 0; i < (int)(blockDim.x / kWave); ++i) {
-    if (i < w) base = op(base, wsum[i]);
-    all = op(all, wsum[i]);
-  }
-  *total = all;
-  __syncthreads();
-  // exclusive: the inclusive value of the previous lane, folded into the earlier waves' total
-  const uint32_t prev = __shfl_up(inc, 1, kWave);
-  return lane == 0 ? base : op(base, prev);
-}
-
-__global__ void __launch_bounds__(kPlanThreads) roi_group_plan_kernel(const float* rois, const int64_t* levels,
-                                                                      int32_t K, int32_t* order, int32_t* gstart,
-                                                                      int32_t* ngroups) {
-  __shared__ uint32_t cnt[kPlanBuckets];
-  __shared__ uint16_t keys[kPlanMaxRois];
-  __shared__ uint16_t pkey[kPlanMaxRois];
-  __shared__ uint32_t wsum[kPlanThreads / kWave];
-  const int t = threadIdx.x;
-  for (int b = t; b < kPlanBuckets; b += kPlanThreads) cnt[b] = 0;
-  __syncthreads();
-  for (int k = t; k < K; k += kPlanThreads) {
-    const float* r = rois + (int64_t)k * 5;
-    const int lvl = levels ? (int)levels[k] : 0;
-    const float xc = 0.5f * (r[1] + r[3]), yc = 0.5f * (r[2] + r[4]);
-    const int ty = yc < 0.0f ? 0 : (yc >= 896.0f ? 7 : (int)(yc * (1.0f / 128.0f)));
-    const int tx = xc < 0.0f ? 0 : (xc >= 896.0f ? 7 : (int)(xc * (1.0f / 128.0f)));
-    const uint16_t key = (uint16_t)((((int)r[0] & 15) << 8) | ((lvl & 3) << 6) | (ty << 3) | tx);
-    keys[k] = key;
-    atomicAdd(&cnt[key], 1u);
-  }
-  __syncthreads();
-  constexpr int P = kPlanBuckets / kPlanThreads;
-  uint32_t loc[P], s = 0, tot;
-#pragma unroll
-  for (int i = 0; i < P; ++i) {
-    loc[i] = s;
-    s += cnt[t * P + i];
-  }
-  const uint32_t base = block_exscan<false>(s, wsum, &tot);
-#pragma unroll
-  for (int i = 0; i < P; ++i) cnt[t * P + i] = base + loc[i];
-  __syncthreads();
-  for (int k = t; k < K; k += kPlanThreads) {
-    const uint32_t pos = atomicAdd(&cnt[keys[k]], 1u);  // order inside a bucket: arbitrary
-    order[pos] = k;
-    pkey[pos] = keys[k];
-  }
-  __syncthreads();
-  // groups: runs of equal (image, level) = pkey >> 6, cut every kGrp positions
-  constexpr int Q = kPlanMaxRois / kPlanThreads;
-  uint32_t segs[Q], lastseg = 0;
-#pragma unroll
-  for (int i = 0; i < Q; ++i) {
-    const int p = t * Q + i;
-    const bool head = p < K && (p == 0 || (pkey[p] >> 6) != (pkey[p - 1] >> 6));
-    if (head) lastseg = (uint32_t)p;
-    segs[i] = lastseg;  // running segment start inside this thread's span (0 = none yet)
-  }
-  const uint32_t carry = block_exscan<true>(lastseg, wsum, &tot);  // latest head before this span
-  uint32_t nhead = 0;
-  bool gflag[Q];
-#pragma unroll
-  for (int i = 0; i < Q; ++i) {
-    const int p = t * Q + i;
-    const uint32_t ss = segs[i] > carry ? segs[i] : carry;
-    gflag[i] = p < K && ((uint32_t)p - ss) % kGrp == 0;
-    nhead += gflag[i];
-  }
-  const uint32_t gbase = block_exscan<false>(nhead, wsum, &tot);
-  uint32_t gid = gbase;
-#pragma unroll
-  for (int i = 0; i < Q; ++i)
-    if (gflag[i]) gstart[gid++] = t * Q + i;
-  if (t == 0) {
-    gstart[tot] = K;
-    ngroups[0] = (int32_t)tot;
-  }
-}
-
-// kDiag (timing diagnostics only, variant 51): thread 0 of every workgroup writes
-// int64 [start, union ready, end, path | U << 8] past the K*C*ph*pw results.
-template <int kV, int kDiag = 0>
-__global__ void __launch_bounds__(kGrpThreads) roi_align_fwd_group_kernel(RoiLevels lv, RoiCfg c, GroupPlan gp,
-                                                                          float* __restrict__ out) {
-  const uint64_t t_start = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
-  constexpr int SR = 2;
-  __shared__ float ring[kGrpRing];
-  __shared__ uint32_t umask[kRowWords], upre[kRowWords + 1];
-  __shared__ uint16_t urows[kMaxURows];
-  __shared__ int ux[2];
-  const int t = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(t / kWave), lane = t & (kWave - 1);
-  const int ng = __builtin_amdgcn_readfirstlane(gp.ngroups[0]);
-  const int gq = (ng + 7) >> 3;  // groups per XCD slice
-  const int nchunk = (c.C + kGrpChans - 1) / kGrpChans;
-  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
-  const int chunk = gq ? j / gq : 0, gi = j - chunk * gq;
-  const int grp = xcd * gq + gi;
-  if (gq == 0 || chunk >= nchunk || grp >= ng) return;  // uniform over the block
-  const int gs = __builtin_amdgcn_readfirstlane(gp.gstart[grp]);
-  const int gn = __builtin_amdgcn_readfirstlane(gp.gstart[grp + 1]) - gs;
-  const bool has = wave < gn;  // waves past the group mirror its first RoI and store nothing
-  const int64_t k = __builtin_amdgcn_readfirstlane(gp.order[gs + (has ? wave : 0)]);
-  const int c0 = chunk * kGrpChans, c1 = min(c.C, c0 + kGrpChans);
-  if (t < kRowWords) umask[t] = 0;
-  if (t == 0) ux[0] = 1 << 30, ux[1] = -1;
-  __syncthreads();
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
-  const bool active = lane < nbins;
-  const int bin = active ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
-    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
-  }
-  // the union: every row a tap reads, and the column span
-  int xlo = 1 << 30, xhi = -1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    if (active && ty[i].valid && ty[i].hi < kRowWords * 32) {
-      atomicOr(&umask[ty[i].lo >> 5], 1u << (ty[i].lo & 31));
-      atomicOr(&umask[ty[i].hi >> 5], 1u << (ty[i].hi & 31));
-    }
-    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
-  }
-  const int wx0 = wave_min_i32(xlo), wx1 = wave_max_i32(xhi);
-  if (lane == 0 && wx1 >= 0) {
-    atomicMin(&ux[0], wx0);
-    atomicMax(&ux[1], wx1);
-  }
-  __syncthreads();
-  if (wave == 0) {  // prefix counts of the row mask, and the union's row list
-    const uint32_t w = lane < kRowWords ? umask[lane] : 0u;
-    uint32_t inc = __popc(w);
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, kWave);
-      if (lane >= o) inc += u;
-    }
-    const uint32_t ex = inc - __popc(w);
-    if (lane < kRowWords) upre[lane] = ex;
-    if (lane == kRowWords - 1) upre[kRowWords] = inc;
-    uint32_t m = w, r = ex;
-    while (m) {
-      const int b = __ffs(m) - 1;
-      if (r < (uint32_t)kMaxURows) urows[r] = (uint16_t)(lane * 32 + b);
-      ++r;
-      m &= m - 1;
-    }
-  }
-  __syncthreads();
-  const uint64_t t_union = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
-  auto stamp = [&](int path, int U) {
-    if (kDiag && t == 0) {
-      int64_t* d = reinterpret_cast<int64_t*>(out + c.K * c.C * c.ph * c.pw) + (int64_t)blockIdx.x * 4;
-      d[0] = (int64_t)t_start;
-      d[1] = (int64_t)t_union;
-      d[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      d[3] = path | ((int64_t)U << 8);
-    }
-  };
-  const int nr = (int)upre[kRowWords];
-  const int ux0 = ux[0], ux1 = ux[1];
-  const int xs0 = ux0 & ~(kV - 1);
-  const int uw = kV == 1 ? ((ux1 - ux0 + 1) | 1) : ((ux1 - xs0 + kV) & ~(kV - 1));
-  const int U = nr * uw;
-  bool rows_ok = H <= kRowWords * 32;
-  const int nbig = __builtin_amdgcn_readfirstlane((int)(ux1 < 0 ? 0 : 1));
-  if (nbig == 0 || !rows_ok || nr > kMaxURows || 3 * U > kGrpRing - 2 * kV * kWave * kGrp) {
-    // no valid tap anywhere, or a union too large for three slots: each wave on its own RoI
-    if (has) roi_segment<kGrpRing / kGrp, kV>(lv, c, out, ring + wave * (kGrpRing / kGrp), k, c0, c1, lane);
-    if (kDiag) {
-      __syncthreads();
-      stamp(1, U);
-    }
-    return;
-  }
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-  int sa[SR][2][SR][2];
-  auto ridx = [&](int y) { return (int)upre[y >> 5] + __popc(umask[y >> 5] & ((1u << (y & 31)) - 1u)); };
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy) {
-    const int rl = ty[iy].valid ? ridx(ty[iy].lo) : 0, rh = ty[iy].valid ? ridx(ty[iy].hi) : 0;
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      const bool v = a.valid && b.valid;
-      ok[iy][ix] = v;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-      sa[iy][0][ix][0] = v ? (rl * uw + (b.lo - xs0)) * 4 : 0;
-      sa[iy][0][ix][1] = v ? (rl * uw + (b.hi - xs0)) * 4 : 0;
-      sa[iy][1][ix][0] = v ? (rh * uw + (b.lo - xs0)) * 4 : 0;
-      sa[iy][1][ix][1] = v ? (rh * uw + (b.hi - xs0)) * 4 : 0;
-    }
-  }
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + k * c.C * nbins, (int64_t)c.C * nbins * 4);
-  const int cstep = scs * 4, ostep = nbins * 4;
-  const int ovoff = (has && active) ? lane * 4 : 0x40000000;  // dropped by the range check
-  // Staging: a channel's union is Q wave-instructions of kV*64 floats; instruction q is
-  // issued by wave q % 8 (round q / 8).  Every wave issues the same J rounds per
-  // channel (rounds past Q load a dummy into a junk block), so one counted vmcnt fits
-  // all waves.  A step is B channels (B slots of Q*kV*64 floats); three step buffers,
-  // two steps in flight ahead of the one being read, one barrier per step.
-  constexpr int kPiece = kV * kWave;  // floats per DMA wave-instruction
-  constexpr int kRing = kGrpRing - kPiece;
-  const int Q = (U + kPiece - 1) / kPiece;
-  const int SF = Q * kPiece;
-  float* junk = ring + kRing;
-  auto run = [&](auto jj, auto bb, auto ddp) {
-    constexpr int J = decltype(jj)::value;   // DMA rounds per wave per channel
-    constexpr int B = decltype(bb)::value;   // channels per step
-    constexpr int D = decltype(ddp)::value;  // steps in flight ahead of the one being read
-    constexpr int NB = D + 1;                // step buffers
-    static_assert(B * (J + 1) * (D - 1) < 64 && B * J * D < 64, "vmcnt range");
-    int goff[J], dst[J];
-#pragma unroll
-    for (int q = 0; q < J; ++q) {
-      const int piece = wave + q * kGrp;
-      const int e = kV * lane + piece * kPiece;
-      const int r = e / uw, col = e - r * uw;
-      const int fx = kV == 1 ? min(xs0 + col, W - 1) : xs0 + col;
-      const bool real = piece < Q;
-      goff[q] = real && e < U ? ((int)urows[r] * sy + fx * sx) * 4 : ((int)urows[0] * sy + xs0 * sx) * 4;
-      dst[q] = real ? piece * kPiece : -1;
-    }
-    const int nch = c1 - c0, nst = (nch + B - 1) / B;
-    auto issue = [&](int st) {  // step st: channels c0 + B*st + b (clamped) -> buffer st % NB
-      float* sb = ring + (st % NB) * (B * SF);
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const int ch = c0 + min(st * B + b, nch - 1);
-#pragma unroll
-        for (int q = 0; q < J; ++q) lds_dma<4 * kV>(fr, dst[q] >= 0 ? sb + b * SF + dst[q] : junk, goff[q], ch * cstep);
-      }
-    };
-    for (int st = 0; st < D && st < nst; ++st) issue(st);
-    for (int st = 0; st < nst; ++st) {
-      // retire step st: younger than its DMAs are, for each of the D-1 steps issued after
-      // it, B stores and B*J DMAs (the first step has no stores before; the tail waits all)
-      if (st + D - 1 < nst) {
-        if (st == 0)
-          wait_vmcnt<B * J * (D - 1)>();
-        else
-          wait_vmcnt<B * (J + 1) * (D - 1)>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      const uint64_t t_w = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
-      asm volatile("s_barrier" ::: "memory");  // every wave's share of step st has landed
-      const uint64_t t_b = kDiag ? __builtin_amdgcn_s_memrealtime() : 0;
-      const char* sb = reinterpret_cast<const char*>(ring + (st % NB) * (B * SF));
-      float acc[B];
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const char* sl = sb + b * SF * 4;
-        float v[SR][SR][4];
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-          for (int ix = 0; ix < SR; ++ix) {
-            v[iy][ix][0] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][0]);
-            v[iy][ix][1] = *reinterpret_cast<const float*>(sl + sa[iy][0][ix][1]);
-            v[iy][ix][2] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][0]);
-            v[iy][ix][3] = *reinterpret_cast<const float*>(sl + sa[iy][1][ix][1]);
-          }
-        float a = 0.0f;
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-          for (int ix = 0; ix < SR; ++ix) {
-            float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
-                        wt[iy][ix][3] * v[iy][ix][3];
-            a = a + (ok[iy][ix] ? val : 0.0f);
-          }
-        acc[b] = a * 0.25f;
-      }
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const int ci = st * B + b;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[b]), orr, ci < nch ? ovoff : 0x40000000,
-                                              (c0 + ci) * ostep, 0);
-      }
-      // buffer (st + D) % NB was last read in step st - 1, which every wave finished before this step's barrier
-      if (st + D < nst) issue(st + D);
-      if (kDiag && lane == 0 && blockIdx.x < 64 && st < 20 && (wave == 0 || wave == 7)) {
-        int64_t* d = reinterpret_cast<int64_t*>(out + c.K * c.C * c.ph * c.pw) + 8192 +
-                     ((int64_t)(blockIdx.x * 2 + (wave ? 1 : 0)) * 20 + st) * 4;
-        d[0] = (int64_t)t_w;
-        d[1] = (int64_t)t_b;
-        d[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        d[3] = B * 100 + D;
-      }
-    }
-  };
-  const int J = (Q + kGrp - 1) / kGrp;
-  // deepest pipeline the ring holds: B channels per step, D steps ahead
-  // B channels per step, D steps ahead: the deepest pipeline the ring holds within vmcnt range
-  const int n4 = kRing / (4 * SF), n2 = kRing / (2 * SF), n1 = kRing / SF;  // step buffers that fit
-  const int shape = n4 >= 7 ? 0 : n4 >= 5 ? 1 : n4 >= 3 ? 2 : n2 >= 5 ? 3 : n2 >= 3 ? 4 : n1 >= 5 ? 5 : 6;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I4 = std::integral_constant<int, 4>;
-  using I6 = std::integral_constant<int, 6>;
-  auto with_bd = [&](auto jj) {
-    constexpr int Jc = decltype(jj)::value;
-    constexpr bool f46 = 4 * (Jc + 1) * 5 < 64, f44 = 4 * (Jc + 1) * 3 < 64;
-    if (shape == 0 && f46)
-      run(jj, I4{}, std::conditional_t<f46, I6, I2>{});
-    else if (shape <= 1 && f44)
-      run(jj, I4{}, std::conditional_t<f44, I4, I2>{});
-    else if (shape <= 2)
-      run(jj, I4{}, I2{});
-    else if (shape == 3)
-      run(jj, I2{}, I4{});
-    else if (shape == 4)
-      run(jj, I2{}, I2{});
-    else if (shape == 5)
-      run(jj, I1{}, I4{});
-    else
-      run(jj, I1{}, I2{});
-  };
-  if (J <= 1)
-    with_bd(std::integral_constant<int, 1>{});
-  else if (J <= 2)
-    with_bd(std::integral_constant<int, 2>{});
-  else if (J <= 3)
-    with_bd(std::integral_constant<int, 3>{});
-  else  // only the 4-byte staging (kV = 1) gets here
-    run(std::integral_constant<int, 16>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-  if (kDiag) {
-    __syncthreads();
-    stamp(2 + J * 4, U);
-  }
-}
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
-                                                                    const float* __restrict__ gout) {
-  __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];
-  const int64_t k = blockIdx.x;
-  const int c0 = blockIdx.y * kRoiChanChunk;
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  fill_taps(g, c, H, W, ty, tx);
-  __syncthreads();
-  const int nbins = c.ph * c.pw;
-  const int nch = min(kRoiChanChunk, c.C - c0);
-  const bool tab = taps_fit(g, c);
-  float* base = lv.grad[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  const float* go = gout + (k * c.C + c0) * nbins;
-  for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
-    const int cl = item / nbins, bin = item - cl * nbins;
-    const int py = bin / c.pw, px = bin - py * c.pw;
-    float* f = base + (int64_t)(c0 + cl) * scs;
-    const float gv = go[item];
-    for (int iy = 0; iy < g.gh; ++iy) {
-      const Tap a = tab ? ty[py * g.gh + iy] : make_tap(sample_y(g, py, iy), H);
-      if (!a.valid) continue;
-      for (int ix = 0; ix < g.gw; ++ix) {
-        const Tap bx = tab ? tx[px * g.gw + ix] : make_tap(sample_x(g, px, ix), W);
-        if (!bx.valid) continue;
-        float g1 = gv * (a.h * bx.h) / g.count, g2 = gv * (a.h * bx.l) / g.count;
-        float g3 = gv * (a.l * bx.h) / g.count, g4 = gv * (a.l * bx.l) / g.count;
-        atomicAdd(&f[a.lo * sy + bx.lo * sx], g1);
-        atomicAdd(&f[a.lo * sy + bx.hi * sx], g2);
-        atomicAdd(&f[a.hi * sy + bx.lo * sx], g3);
-        atomicAdd(&f[a.hi * sy + bx.hi * sx], g4);
-      }
-    }
-  }
-}
-
-// Backward, window-accumulated (sampling 2, ph*pw <= 64): the default.  The
-// per-tap form above issues 16 scattered global float atomics per (bin, channel)
-// -- 205 M for a cfg2 batch, executed at the memory side at a small fraction of
-// the coalesced atomic rate (MI355X_MICROARCH.md, global float atomics): 7.7 ms
-// per train step.  Here each wave owns 16 channels of one RoI: per channel it
-// sums the 16 weighted taps of every bin into an LDS copy of the RoI's tap window
-// (ds_add_f32), then adds the window to the feature gradient with one global
-// atomic per non-zero cell, lanes along window rows (count = 4 at sampling 2:
-// (g * w) / 4 == (g * w) * 0.25 exactly, without the division sequence).  Windows above kBwdSlab
-// floats keep the per-tap atomics.  Contributions are the reference's
-// grad * w / count; float atomics make the summation order (and the last bits)
-// run-dependent, as in torchvision's own CUDA backward.
-constexpr int kBwdSlab = 1024;  // floats per wave
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevels lv, RoiCfg c,
-                                                                        const float* __restrict__ gout) {
-  constexpr int SR = 2, kCh = kRoiChanChunk / (kRoiThreads / kWave);
-  __shared__ float slab_all[kRoiThreads / kWave][kBwdSlab];
-  const int64_t k = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
-  const int nch = min(kCh, c.C - cw0);
-  if (nch <= 0) return;
-  float* slab = slab_all[wave];
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const bool active = lane < nbins;
-  const int bin = active ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {  // sampling 2: the "/ gh" of the sample position is an exact halving
-    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
-    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
-  }
-  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
-    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  if (y1 < y0 || x1 < x0) return;  // no valid tap: no gradient
-  const int WW = x1 - x0 + 1, n = (y1 - y0 + 1) * WW;
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
-  const float* go = gout + (k * c.C + cw0) * nbins;
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = active && a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-    }
-  if (n > kBwdSlab) {  // window larger than the slab: per-tap global atomics
-    for (int ch = 0; ch < nch; ++ch) {
-      const float gv = active ? go[ch * nbins + bin] : 0.0f;
-      float* f = gbase + (int64_t)ch * scs;
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          if (!ok[iy][ix]) continue;
-          const Tap a = ty[iy], b = tx[ix];
-          atomicAdd(&f[a.lo * sy + b.lo * sx], gv * wt[iy][ix][0] / g.count);
-          atomicAdd(&f[a.lo * sy + b.hi * sx], gv * wt[iy][ix][1] / g.count);
-          atomicAdd(&f[a.hi * sy + b.lo * sx], gv * wt[iy][ix][2] / g.count);
-          atomicAdd(&f[a.hi * sy + b.hi * sx], gv * wt[iy][ix][3] / g.count);
-        }
-    }
-    return;
-  }
-  int cell[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      const int rl = (a.lo - y0) * WW, rh = (a.hi - y0) * WW, cl = b.lo - x0, chh = b.hi - x0;
-      cell[iy][ix][0] = rl + cl;
-      cell[iy][ix][1] = rl + chh;
-      cell[iy][ix][2] = rh + cl;
-      cell[iy][ix][3] = rh + chh;
-    }
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  const int r0 = lane / WW, col0 = lane - r0 * WW, dr = kWave / WW, dc = kWave - dr * WW;
-  for (int ch = 0; ch < nch; ++ch) {
-    for (int e = lane; e < n; e += kWave) slab[e] = 0.0f;
-    wave_sync();
-    const float gv = active ? go[ch * nbins + bin] : 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix)
-        if (ok[iy][ix])
-#pragma unroll
-          for (int q = 0; q < 4; ++q) atomicAdd(&slab[cell[iy][ix][q]], gv * wt[iy][ix][q] * 0.25f);
-    wave_sync();
-    float* f = gbase + (int64_t)ch * scs;
-    int r = r0, col = col0;
-    for (int e = lane; e < n; e += kWave) {
-      const float v = slab[e];
-      if (v != 0.0f) atomicAdd(&f[(int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx], v);
-      r += dr;
-      col += dc;
-      if (col >= WW) col -= WW, ++r;
-    }
-    wave_sync();  // the window is re-zeroed for the next channel only after every lane read it
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward, separable tap sums (sampling 2, 4*ph and 4*pw <= 32): the default.
-// LDS float atomics (ds_add_f32) run several times slower than plain LDS
-// traffic on gfx950 (tools/probe/probe_bwd.py: the same accumulation took 7x
-// longer with ds_add_f32 than with a racy read-modify-write), and degenerate
-// RoIs (the random-init proposals clamped to the image border: half the cfg2
-// RoIs are < 1 px tall) pile all their taps on a few cells, which serialises
-// any per-cell scheme.  The taps are separable: cell (y, x) receives
-// (g[py][px] * (wy * wx)) * 0.25 for every y tap entry (py, iy, lo|hi) on row y
-// and every x tap entry (px, ix, lo|hi) on column x; wy * wx is exactly the
-// reference's w1..w4 (hy*hx, hy*lx, ly*hx, ly*lx), so every contribution is the
-// reference's grad * w / count.  A wave sorts its RoI's <= 4*ph y entries by
-// row and <= 4*pw x entries by column once.  Per channel pair, lane (half h,
-// j) owns x entry j of channel h and walks the y entries in row order (a
-// uniform loop): it accumulates its contributions, and at the end of each row
-// a segmented sum over the lanes of equal column leaves each (row, column)
-// cell's total in one lane, which adds it to the feature gradient with one
-// global atomic.  No LDS atomics, no divergence; the order of the float sums
-// differs from the reference's (float atomics already make it run-dependent,
-// as in torchvision's CUDA backward).
-constexpr int kSepEnt = 32;  // tap entries per axis and wave half: 4 * ph, 4 * pw <= 32
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
-                                                                        const float* __restrict__ gout) {
-  constexpr int kCh = kRoiChanChunk / (kRoiThreads / kWave);  // channels per wave (even)
-  __shared__ int yent_all[kRoiThreads / kWave][kSepEnt];      // row << 16 | py, sorted by (row, entry)
-  __shared__ float yw_all[kRoiThreads / kWave][kSepEnt];
-  __shared__ int xpos_all[kRoiThreads / kWave][kSepEnt];      // position of each x entry, unsorted
-  __shared__ float gv_all[kRoiThreads / kWave][2 * kWave];
-  const int64_t k = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
-  const int nch = min(kCh, c.C - cw0);
-  if (nch <= 0) return;
-  int* yent = yent_all[wave];
-  float* yw = yw_all[wave];
-  int* xpos = xpos_all[wave];
-  float* gv = gv_all[wave];
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int ph = c.ph, pw = c.pw, nbins = ph * pw;
-  const int nye = 4 * ph, nxe = 4 * pw;
-  const int h = lane >> 5, j = lane & 31;
-  // tap entry e of an axis: sample e / 2 (bin e / 4, sub-sample (e / 2) & 1), lo (e even) or hi
-  auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
-    const Tap t = make_tap(start + (float)(e >> 2) * bin + ((float)((e >> 1) & 1) + 0.5f) * bin * 0.5f, size);
-    *pos = t.valid ? ((e & 1) ? t.hi : t.lo) : -1;
-    *w = (e & 1) ? t.l : t.h;
-  };
-  int yp, xp;
-  float ywv, xwv;
-  entry(j, g.start_h, g.bin_h, H, &yp, &ywv);
-  entry(j, g.start_w, g.bin_w, W, &xp, &xwv);
-  if (j >= nye) yp = -1;
-  if (j >= nxe) xp = -1;
-  if (h == 0) xpos[j] = xp < 0 ? (1 << 20) : xp;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // x entries: rank by (col, entry); lane (h, j) takes the j-th in column order
-  int xrank = 0;
-  for (int e = 0; e < nxe; ++e) {
-    const int pe = xpos[e], pm = xpos[j];
-    xrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
-  }
-  // y entries: rank by (row, entry), written sorted
-  {
-    int yrank = 0;
-    const int pm = yp < 0 ? (1 << 20) : yp;
-    for (int e = 0; e < nye; ++e) {
-      const int pe = __shfl(yp < 0 ? (1 << 20) : yp, e, kWave);
-      yrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
-    }
-    if (h == 0 && j < nye && yp >= 0) {
-      yent[yrank] = (yp << 16) | (j >> 2);
-      yw[yrank] = ywv;
-    }
-  }
-  int nyv = 0, nxv = 0;  // valid entries (uniform)
-  {
-    const uint64_t my = __ballot(h == 0 && yp >= 0), mx = __ballot(h == 0 && xp >= 0);
-    nyv = __popcll(my);
-    nxv = __popcll(mx);
-  }
-  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
-  // this lane's x entry (column order) and the segment of lanes sharing its column
-  int my_col = -1, my_px = 0;
-  float my_wx = 0.0f;
-  // scatter the x entries into column order through LDS
-  __shared__ int xs_all[kRoiThreads / kWave][kSepEnt];
-  __shared__ float xw_all[kRoiThreads / kWave][kSepEnt];
-  int* xs = xs_all[wave];
-  float* xw = xw_all[wave];
-  if (h == 0 && xp >= 0) {
-    xs[xrank] = (xp << 16) | (j >> 2);
-    xw[xrank] = xwv;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const bool xv = j < nxv;
-  if (xv) {
-    my_col = xs[j] >> 16;
-    my_px = xs[j] & 0xffff;
-    my_wx = xw[j];
-  }
-  // segment of equal columns within the half: [j - lead, j + trail]
-  int trail = 0;
-  for (int d = 1; d < kSepEnt; ++d) {
-    const int jj = j + d;
-    if (jj < nxv && (xs[jj] >> 16) == my_col) trail = d;
-  }
-  const bool head = xv && (j == 0 || (xs[j - 1] >> 16) != my_col);
-  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
-  const float* go = gout + (k * c.C + cw0) * nbins;
-  for (int ch = 0; ch < nch; ch += 2) {
-    // grad_out of channels ch, ch + 1 (a missing odd last channel reads 0 and is not written)
-    for (int e = lane; e < 2 * nbins; e += kWave) {
-      const int hh = e >= nbins ? 1 : 0;
-      gv[hh * kWave + (e - hh * nbins)] = (ch + hh < nch) ? go[(ch + hh) * nbins + (e - hh * nbins)] : 0.0f;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float* f = gbase + (int64_t)(ch + h) * scs;
-    const bool live = xv && ch + h < nch;
-    float acc = 0.0f;
-    for (int i = 0; i < nyv; ++i) {
-      const int ye = yent[i];
-      const int row = ye >> 16, py = ye & 0xffff;
-      const float wy = yw[i];
-      const float gvv = gv[h * kWave + py * pw + my_px];
-      acc = acc + (live ? gvv * (wy * my_wx) * 0.25f : 0.0f);  // (g * w) / count, count = 4
-      if (i + 1 == nyv || (yent[i + 1] >> 16) != row) {  // end of this row's entries (uniform)
-        float sum = acc;
-#pragma unroll
-        for (int d = 1; d < kSepEnt; d <<= 1) {
-          const float t = __shfl_down(sum, d, 32);
-          if (d <= trail) sum = sum + t;
-        }
-        if (head && live && sum != 0.0f) atomicAdd(&f[(int64_t)row * sy + (int64_t)my_col * sx], sum);
-        acc = 0.0f;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward into a channels-last gradient (sampling 2, ph*pw <= 64, C % 16 == 0):
-// the default.  Global float atomics execute at the memory side as 64-B
-// requests (MI355X_MICROARCH.md, global float atomics): the NCHW flush above
-// adds window rows of a few cells -- mostly partial 64-B requests -- and runs
-// at a fraction of the atomic byte rate.  Here the gradient is accumulated in
-// a [B, H, W, C] buffer (zeroed by the caller; the autograd wrapper returns it
-// as a channels_last view): each wave owns 16 channels of the RoI, sums its
-// taps into an LDS band of the tap window laid out [cell][16 channels] (row
-// stride 17: conflict-free both ways), and flushes each window cell's 16
-// channels as ONE full 64-B atomic request.  Windows taller than a band of
-// kClBandCells cells are done band by band.  Contributions are the reference's
-// grad * w / count (count = 4: an exact * 0.25); float atomics make the
-// summation order run-dependent, as in torchvision's own CUDA backward.
-// Measured (tools/bench_roi_bwd.py, cfg2 RoIs, incl. clearing): 1.38 ms vs 1.19 ms
-// for the NCHW kernel, so the NCHW kernel stays the default (ops.ROI_ALIGN_BWD);
-// this one runs whenever the caller hands a channels_last gradient.
-constexpr int kClChans = 16;      // channels per wave = floats per flushed 64-B segment
-constexpr int kClBandCells = 256;  // window cells per LDS band
-constexpr int kClStride = kClChans + 1;
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_cl_kernel(RoiLevels lv, RoiCfg c,
-                                                                       const float* __restrict__ gout) {
-  constexpr int SR = 2;
-  __shared__ float band_all[kRoiThreads / kWave][kClBandCells * kClStride];  // 68 KB
-  const int64_t k = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kClChans;
-  if (cw0 >= c.C) return;  // host: C % 16 == 0
-  float* band = band_all[wave];
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int nbins = c.ph * c.pw;
-  const bool active = lane < nbins;
-  const int bin = active ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  Tap ty[SR], tx[SR];
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
-    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
-  }
-  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-#pragma unroll
-  for (int i = 0; i < SR; ++i) {
-    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
-    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  if (y1 < y0 || x1 < x0) return;  // no valid tap: no gradient
-  const int WW = x1 - x0 + 1;      // host: every level's width <= kClBandCells
-  const int RB = kClBandCells / WW;  // window rows per band
-  const int64_t sy = lv.sy[l], sx = lv.sx[l];
-  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * lv.sc[l];
-  const float* go = gout + (k * c.C + cw0) * nbins;
-  bool ok[SR][SR];
-  float wt[SR][SR][4];
-  int row[SR][SR][4], col[SR][SR][4];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap a = ty[iy], b = tx[ix];
-      ok[iy][ix] = active && a.valid && b.valid;
-      wt[iy][ix][0] = a.h * b.h;
-      wt[iy][ix][1] = a.h * b.l;
-      wt[iy][ix][2] = a.l * b.h;
-      wt[iy][ix][3] = a.l * b.l;
-      row[iy][ix][0] = row[iy][ix][1] = a.lo - y0;
-      row[iy][ix][2] = row[iy][ix][3] = a.hi - y0;
-      col[iy][ix][0] = col[iy][ix][2] = b.lo - x0;
-      col[iy][ix][1] = col[iy][ix][3] = b.hi - x0;
-    }
-  float gq[kClChans];  // grad * 0.25 per channel: (g * w) / 4 == (g * 0.25) * w exactly
-#pragma unroll
-  for (int ch = 0; ch < kClChans; ++ch) gq[ch] = active ? go[ch * nbins + bin] * 0.25f : 0.0f;
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  for (int r0 = 0; r0 <= y1 - y0; r0 += RB) {
-    const int nr = min(RB, y1 - y0 + 1 - r0), ncell = nr * WW;
-    for (int e = lane; e < ncell * kClStride; e += kWave) band[e] = 0.0f;
-    wave_sync();
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rr = row[iy][ix][q] - r0;
-          if (ok[iy][ix] && rr >= 0 && rr < nr) {
-            float* cell = band + (rr * WW + col[iy][ix][q]) * kClStride;
-            const float w = wt[iy][ix][q];
-#pragma unroll
-            for (int ch = 0; ch < kClChans; ++ch) atomicAdd(cell + ch, gq[ch] * w);
-          }
-        }
-    wave_sync();
-    // flush: lane = (cell, channel); the 16 channels of a cell are one 64-B segment
-    for (int e = lane; e < ncell * kClChans; e += kWave) {
-      const int ce = e / kClChans, ch = e - ce * kClChans;
-      const float v = band[ce * kClStride + ch];
-      const int y = y0 + r0 + ce / WW, x = x0 + ce % WW;
-      if (v != 0.0f) atomicAdd(gbase + (int64_t)ch * lv.sc[l] + (int64_t)y * sy + (int64_t)x * sx, v);
-    }
-    wave_sync();  // the band is re-zeroed only after every lane read it
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward, tiled gather (sampling 2, ph*pw <= 64): the default.  The
-// window-accumulated kernel above still ends in one global float atomic per
-// (RoI, channel, window cell) -- ~45 M for a cfg2 batch, bound by the L2
-// atomic rate (1.24 ms per train step).  Here the feature gradient is built
-// tile by tile with no global atomics:
-//   bin_count : per RoI, the tap window (as the forward) -> the 16x16-cell
-//               tiles of its level it overlaps; count per tile
-//   bin_scan  : one workgroup: tile list offsets
-//   bin_fill  : per RoI, append its id to each overlapped tile's list
-//   tile      : workgroup = (tile, 32 channels), wave = 8 channels; the wave
-//               zeroes an LDS copy of the tile for its channels, walks the
-//               tile's RoIs (lane = bin) adding grad * w / count of every tap
-//               that falls in the tile with ds_add_f32, then stores the tile --
-//               every cell of every level written once (zeros where no RoI
-//               reaches), so the caller need not clear the gradient.
-// Contributions are the reference's grad * w / count, as the kernels above;
-// the order of the RoIs within a tile follows the fill atomics, so the last
-// bits are run-dependent like torchvision's own CUDA backward.
-// Measured (tools/bench_roi_bwd.py, cfg2 RoIs): SLOWER than the atomic kernel --
-// a RoI overlaps 4.4 tiles on average and every (RoI, tile) pair evaluates all
-// 16 x 49 taps, and the positives around one ground truth pile up to 100 RoIs
-// on one tile (one workgroup's serial list).  Opt-in (ops.ROI_ALIGN_BWD).
-
-constexpr int kBwdTile = 16;                 // tile side in cells
-constexpr int kBwdTileCells = kBwdTile * kBwdTile;
-constexpr int kBwdTileChans = 32;            // channels per workgroup
-constexpr int kBwdWaveChans = kBwdTileChans / (kRoiThreads / kWave);  // 8
-
-struct TileMap {
-  int nty[FRH_MAX_LEVELS], ntx[FRH_MAX_LEVELS];
-  int64_t base[FRH_MAX_LEVELS + 1];  // first tile id of each level (images level-major inside)
-  int B;
-};
-
-struct TileLists {
-  uint32_t* count;  // [T]
-  uint32_t* off;    // [T + 1]
-  uint32_t* fill;   // [T]
-  int4* win;        // [K]: tile rows ty0..ty1, cols tx0..tx1 (ty0 > ty1: none)
-  int32_t* list;    // [cap]
-  int64_t cap;
-};
-
-// the RoI's tap window at its level (forward's make_tap over all 2*ph / 2*pw samples)
-__device__ __forceinline__ int4 roi_tap_window(const RoiCfg& c, const RoiLevels& lv, int64_t k, int* lvl, int* img) {
-  const RoiGeom g = roi_geom(c, lv, k);
-  const int H = lv.h[g.lvl], W = lv.w[g.lvl];
-  int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
-  for (int p = 0; p < c.ph; ++p)
-    for (int i = 0; i < 2; ++i) {
-      const Tap t = make_tap(g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
-      if (t.valid) y0 = min(y0, t.lo), y1 = max(y1, t.hi);
-    }
-  for (int p = 0; p < c.pw; ++p)
-    for (int i = 0; i < 2; ++i) {
-      const Tap t = make_tap(g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
-      if (t.valid) x0 = min(x0, t.lo), x1 = max(x1, t.hi);
-    }
-  *lvl = g.lvl;
-  *img = g.b;
-  if (y1 < y0 || x1 < x0) return make_int4(1, 0, 1, 0);
-  return make_int4(y0 / kBwdTile, y1 / kBwdTile, x0 / kBwdTile, x1 / kBwdTile);
-}
-
-__device__ __forceinline__ int64_t tile_id(const TileMap& tm, int l, int b, int ty, int tx) {
-  return tm.base[l] + ((int64_t)b * tm.nty[l] + ty) * tm.ntx[l] + tx;
-}
-
-__global__ void roi_bwd_bin_count_kernel(RoiLevels lv, RoiCfg c, TileMap tm, TileLists tl) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= c.K) return;
-  int l, b;
-  const int4 w = roi_tap_window(c, lv, k, &l, &b);
-  tl.win[k] = w;
-  for (int ty = w.x; ty <= w.y; ++ty)
-    for (int tx = w.z; tx <= w.w; ++tx) atomicAdd(&tl.count[tile_id(tm, l, b, ty, tx)], 1u);
-}
-
-__global__ void __launch_bounds__(1024) roi_bwd_bin_scan_kernel(TileLists tl, int64_t T) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int64_t per = (T + 1023) / 1024, s = t * per, e = min(T, s + per);
-  uint32_t sum = 0;
-  for (int64_t i = s; i < e; ++i) sum += tl.count[i];
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t v = t >= d ? part[t - d] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - sum;
-  for (int64_t i = s; i < e; ++i) {
-    tl.off[i] = run;
-    run += tl.count[i];
-  }
-  if (t == 1023) tl.off[T] = part[1023];
-}
-
-__global__ void roi_bwd_bin_fill_kernel(RoiLevels lv, RoiCfg c, TileMap tm, TileLists tl) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= c.K) return;
-  const int4 w = tl.win[k];
-  if (w.x > w.y) return;
-  const float* r = c.rois + k * 5;
-  const int b = (int)r[0], l = c.levels ? (int)c.levels[k] : 0;
-  for (int ty = w.x; ty <= w.y; ++ty)
-    for (int tx = w.z; tx <= w.w; ++tx) {
-      const int64_t t = tile_id(tm, l, b, ty, tx);
-      const uint32_t pos = tl.off[t] + atomicAdd(&tl.fill[t], 1u);
-      if (pos < tl.cap) tl.list[pos] = (int32_t)k;
-    }
-}
-
-__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_tile_kernel(RoiLevels lv, RoiCfg c, TileMap tm,
-                                                                         TileLists tl, const float* __restrict__ gout) {
-  constexpr int SR = 2;
-  __shared__ float tile_all[kRoiThreads / kWave][kBwdWaveChans * kBwdTileCells];  // 32 KB
-  const int64_t t = blockIdx.x;
-  int l = 0;
-  while (l + 1 < lv.L && t >= tm.base[l + 1]) ++l;
-  const int64_t lt = t - tm.base[l];
-  const int per_img = tm.nty[l] * tm.ntx[l];
-  const int b = (int)(lt / per_img), rem = (int)(lt - (int64_t)b * per_img);
-  const int tyi = rem / tm.ntx[l], txi = rem - tyi * tm.ntx[l];
-  const int H = lv.h[l], W = lv.w[l];
-  const int Y0 = tyi * kBwdTile, X0 = txi * kBwdTile;
-  const int th = min(kBwdTile, H - Y0), tw = min(kBwdTile, W - X0);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  const int cw0 = blockIdx.y * kBwdTileChans + wave * kBwdWaveChans;
-  const int nch = min(kBwdWaveChans, c.C - cw0);
-  if (nch <= 0) return;
-  float* tile = tile_all[wave];
-  for (int e = lane; e < kBwdWaveChans * kBwdTileCells; e += kWave) tile[e] = 0.0f;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int nbins = c.ph * c.pw;
-  const bool active = lane < nbins;
-  const int bin = active ? lane : 0;
-  const int py = bin / c.pw, px = bin - py * c.pw;
-  const uint32_t i0 = tl.off[t], i1 = min((int64_t)tl.off[t + 1], tl.cap);
-  for (uint32_t i = i0; i < i1; ++i) {
-    const int64_t k = tl.list[i];
-    const RoiGeom g = roi_geom(c, lv, k);
-    Tap ty[SR], tx[SR];
-#pragma unroll
-    for (int s = 0; s < SR; ++s) {
-      ty[s] = make_tap(g.start_h + (float)py * g.bin_h + ((float)s + 0.5f) * g.bin_h * 0.5f, H);
-      tx[s] = make_tap(g.start_w + (float)px * g.bin_w + ((float)s + 0.5f) * g.bin_w * 0.5f, W);
-    }
-    // tile cells of this bin's 16 taps (-1: outside the tile or invalid sample) and weights
-    int cell[SR][SR][4];
-    float wt[SR][SR][4];
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        const Tap a = ty[iy], bb = tx[ix];
-        const bool ok = active && a.valid && bb.valid;
-        const int ylo = a.lo - Y0, yhi = a.hi - Y0, xlo = bb.lo - X0, xhi = bb.hi - X0;
-        const bool iyl = ylo >= 0 && ylo < th, iyh = yhi >= 0 && yhi < th;
-        const bool ixl = xlo >= 0 && xlo < tw, ixh = xhi >= 0 && xhi < tw;
-        cell[iy][ix][0] = ok && iyl && ixl ? ylo * kBwdTile + xlo : -1;
-        cell[iy][ix][1] = ok && iyl && ixh ? ylo * kBwdTile + xhi : -1;
-        cell[iy][ix][2] = ok && iyh && ixl ? yhi * kBwdTile + xlo : -1;
-        cell[iy][ix][3] = ok && iyh && ixh ? yhi * kBwdTile + xhi : -1;
-        wt[iy][ix][0] = a.h * bb.h;
-        wt[iy][ix][1] = a.h * bb.l;
-        wt[iy][ix][2] = a.l * bb.h;
-        wt[iy][ix][3] = a.l * bb.l;
-      }
-    const float* go = gout + (k * c.C + cw0) * nbins + bin;
-    float gv[kBwdWaveChans];
-#pragma unroll
-    for (int ch = 0; ch < kBwdWaveChans; ++ch) gv[ch] = (active && ch < nch) ? go[ch * nbins] : 0.0f;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = cell[iy][ix][q];
-          if (e >= 0) {
-#pragma unroll
-            for (int ch = 0; ch < kBwdWaveChans; ++ch)
-              atomicAdd(&tile[ch * kBwdTileCells + e], gv[ch] * wt[iy][ix][q] * 0.25f);
-          }
-        }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  float* gbase = lv.grad[l] + (int64_t)b * lv.sb[l] + (int64_t)cw0 * lv.sc[l];
-  for (int e = lane; e < nch * kBwdTileCells; e += kWave) {
-    const int ch = e / kBwdTileCells, cl = e - ch * kBwdTileCells;
-    const int y = cl / kBwdTile, x = cl - y * kBwdTile;
-    if (y < th && x < tw) gbase[(int64_t)ch * lv.sc[l] + (int64_t)(Y0 + y) * lv.sy[l] + (int64_t)(X0 + x) * lv.sx[l]] =
-        tile[e];
-  }
-}
 
 __global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int L, int64_t* levels) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2432,26 +36,6 @@ __global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int
   float hi = (float)(L - 1);
   fl = fl < 0.0f ? 0.0f : (fl > hi ? hi : fl);
   levels[k] = (int64_t)fl;
-}
-
-static int32_t make_levels(int32_t L, const float* const* feats, float* const* grads, const int32_t* feat_hw,
-                           const int64_t* strides, const float* scales, RoiLevels* lv) {
-  FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "num_levels %d out of range", L);
-  FRH_REQUIRE(feat_hw && scales && strides, "null pointer argument");
-  lv->L = L;
-  for (int l = 0; l < L; ++l) {
-    lv->feat[l] = feats ? feats[l] : nullptr;
-    lv->grad[l] = grads ? grads[l] : nullptr;
-    lv->h[l] = feat_hw[2 * l];
-    lv->w[l] = feat_hw[2 * l + 1];
-    FRH_REQUIRE(lv->h[l] > 0 && lv->w[l] > 0, "level %d has an empty feature map", l);
-    lv->sb[l] = strides[4 * l];
-    lv->sc[l] = strides[4 * l + 1];
-    lv->sy[l] = strides[4 * l + 2];
-    lv->sx[l] = strides[4 * l + 3];
-    lv->scale[l] = scales[l];
-  }
-  return FRH_OK;
 }
 
 }  // namespace frh
@@ -2469,68 +53,11 @@ extern "C" int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float 
 }
 
 
-static int32_t roi_common_checks(int32_t batch, int32_t channels, int64_t num_rois, int32_t ph, int32_t pw,
-                                 const float* rois) {
-  FRH_REQUIRE(batch >= 1 && channels >= 1 && num_rois >= 0 && ph >= 1 && pw >= 1, "bad sizes");
-  FRH_REQUIRE(num_rois == 0 || rois, "null rois");
-  FRH_REQUIRE(num_rois < (int64_t)0x7fffffff, "too many rois");
-  return FRH_OK;
-}
-
-// shape classes of the forward kernels
-struct FwdCaps {
-  bool buf;    // 32-bit byte offsets within every (image, level) slice, sampling 2, ph*pw <= 256
-  bool lds;    // + ph*pw <= 64 and 2*ph, 2*pw <= 64
-  bool x4;     // + unit x stride, 16-B aligned rows / channel planes / bases (16-B LDS-DMA)
-};
-
-static FwdCaps fwd_caps(const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw, int32_t sr) {
-  FwdCaps f;
-  f.buf = sr == 2 && ph * pw <= kRoiThreads;
-  for (int l = 0; l < lv.L; ++l) {
-    const int64_t ext = ((int64_t)(channels - 1) * lv.sc[l] + (int64_t)(lv.h[l] - 1) * lv.sy[l] +
-                         (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
-    f.buf = f.buf && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
-  }
-  f.lds = f.buf && ph * pw <= 64 && 2 * ph <= 64 && 2 * pw <= 64;
-  f.x4 = f.lds;
-  for (int l = 0; l < lv.L; ++l)
-    f.x4 = f.x4 && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 && lv.sb[l] % 4 == 0 &&
-           (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
-  return f;
-}
-
-// resident single-wave workgroups of the persistent forward: CUs x the occupancy the
-// kernel's LDS and registers allow (FRH_STR_WAVES overrides the per-CU count)
-template <int kWpe>
-static int64_t stream_grid_waves() {
-  static int64_t cached[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-  if (!cached[dev]) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, roi_align_fwd_stream_kernel<kWpe>, kWave, 0) !=
-            hipSuccess ||
-        per <= 0)
-      per = 8;
-    if (const char* e = getenv("FRH_STR_WAVES")) per = std::max(1, atoi(e));
-    cached[dev] = (int64_t)cus * per;
-  }
-  return cached[dev];
-}
-
-static int32_t group_bound(int64_t num_rois) { return (int32_t)((num_rois + kGrp - 1) / kGrp + 64); }
-
-// variant: 0 = direct gather, 10 = per-RoI LDS windows, 50 = grouped (needs the
-// workspace of frh_roi_align_workspace), -1 = best available.  Exported for
-// the kernel micro-benchmark (tools/bench_roi_align.py) and the parity tests.
-extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
-                                             const int32_t* feat_hw, const int64_t* strides, const float* scales,
-                                             int32_t batch, int32_t channels, const float* rois,
-                                             const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
-                                             int32_t pooled_w, int32_t sampling_ratio, int32_t aligned, float* out,
-                                             void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                                             const int64_t* strides, const float* scales, int32_t batch,
+                                             int32_t channels, const float* rois, const int64_t* roi_levels,
+                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
   FRH_REQUIRE((feats && out) || num_rois == 0, "null pointer argument");
@@ -2540,181 +67,17 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
-  const bool grp_ok = f.lds && num_rois <= kPlanMaxRois && workspace &&
-                      ws_bytes >= ((size_t)num_rois + group_bound(num_rois) + 2) * sizeof(int32_t);
-  // -1: the per-RoI LDS kernel (measured fastest on cfg2); -2: the
-  // grouped kernel when the workspace allows it (frh_roi_align_fwd_ws)
-  if (variant == -2) variant = grp_ok ? 50 : -1;
-  bool x4_ok = f.lds && 4 * pooled_h <= kWave;
-  for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
-                                         lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
-  const bool pair_ok = f.lds && channels % 2 == 0 && 4 * pooled_h <= kWave && 4 * pooled_w <= kWave &&
-                       4 * pooled_h * (4 * pooled_w + 1) <= PairLayout<1>::kCells;
-  // default: the channel-pair kernel (46 us on the cfg2 RoIs vs 56 us for the per-RoI LDS
-  // kernel), else the per-RoI LDS kernel, else the direct gather
-  if (variant < 0) variant = pair_ok ? 20 : (f.lds ? 10 : 0);
-  FRH_REQUIRE(variant == 0 || (((variant >= 9 && variant <= 19) && f.lds)) || ((variant == 50 || variant == 51) && grp_ok) ||
-                  (((variant >= 20 && variant <= 29) || (variant >= 38 && variant <= 44)) && pair_ok) || (variant >= 30 && variant <= 37 && x4_ok),
-              "roi_align variant %d unsupported here", variant);
-  if (variant == 50 || variant == 51) {
-    int32_t* order = static_cast<int32_t*>(workspace);
-    int32_t* ngroups = order + num_rois;
-    int32_t* gstart = ngroups + 1;
-    hipLaunchKernelGGL(roi_group_plan_kernel, dim3(1), dim3(kPlanThreads), 0, as_stream(stream), rois, roi_levels,
-                       (int32_t)num_rois, order, gstart, ngroups);
-    r = check_launch("frh_roi_align_fwd (plan)");
-    if (r) return r;
-    const GroupPlan gp{order, gstart, ngroups};
-    const int64_t nchunk = (channels + kGrpChans - 1) / kGrpChans;
-    const dim3 grid((unsigned)(8 * ((group_bound(num_rois) + 7) / 8) * nchunk));
-    if (variant == 51)  // diagnostics: per-workgroup stamps past the results (tools/bench_roi_align.py)
-      hipLaunchKernelGGL((roi_align_fwd_group_kernel<4, 1>), grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp,
-                         out);
-    else if (f.x4)
-      hipLaunchKernelGGL(roi_align_fwd_group_kernel<4>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
-    else
-      hipLaunchKernelGGL(roi_align_fwd_group_kernel<1>, grid, dim3(kGrpThreads), 0, as_stream(stream), lv, c, gp, out);
-  } else if (variant == 27) {  // two launches: small windows with a 4 KB slab, then large windows
-    const int pw = getenv("FRH_PAIR_PW") ? atoi(getenv("FRH_PAIR_PW")) : 8;
-    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 2 * pw - 1) / (2 * pw)));
-    if (pw == 4) {
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 4, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 4, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    } else if (pw == 16) {
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    } else {
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    }
-  } else if (variant >= 41 && variant <= 44) {  // multi-wave workgroups: 41: 2 x pw8, 42: 4 x pw8, 43: 4 x pw4, 44: 2 x pw16
-    auto launch = [&](auto kern, int wpb, int pw) {
-      const int64_t items = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
-      hipLaunchKernelGGL(kern, dim3((unsigned)((items + wpb - 1) / wpb)), dim3(kWave * wpb), 0, as_stream(stream), lv,
-                         c, out);
-    };
-    if (variant == 41) launch(roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 0, 2>, 2, 8);
-    else if (variant == 42) launch(roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 0, 4>, 4, 8);
-    else if (variant == 43) launch(roi_align_fwd_pair_kernel<0, false, 4, kPairHalf, 0, 4>, 4, 4);
-    else launch(roi_align_fwd_pair_kernel<0, false, 16, kPairHalf, 0, 2>, 2, 16);
-  } else if (variant >= 38 && variant <= 40) {  // diagnostics: 38 setup only, 39 setup + one DMA, 40 empty waves
-    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 15) / 16));
-    if (variant == 38)
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 3>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else if (variant == 39)
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 4>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else
-      hipLaunchKernelGGL(roi_empty_kernel, g2, dim3(kWave), 0, as_stream(stream), out);
-  } else if (variant == 28 || variant == 29) {  // diagnostics: only the small (28) / large (29) launch of 27
-    const dim3 g2((unsigned)num_rois, (unsigned)((channels + 15) / 16));
-    if (variant == 28)
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, 512, 1>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8, kPairHalf, 2>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-  } else if (variant == 25 || variant == 26) {  // 26: registers for 3 waves per SIMD (spills)
-    const int G = (channels + 2 * kStrPairs - 1) / (2 * kStrPairs);
-    const int64_t nitems = num_rois * G;
-    if (variant == 25)
-      hipLaunchKernelGGL(roi_align_fwd_stream_kernel<0>,
-                         dim3((unsigned)std::min<int64_t>(nitems, stream_grid_waves<0>())), dim3(kWave), 0,
-                         as_stream(stream), lv, c, out, nitems, G);
-    else
-      hipLaunchKernelGGL(roi_align_fwd_stream_kernel<3>,
-                         dim3((unsigned)std::min<int64_t>(nitems, stream_grid_waves<3>())), dim3(kWave), 0,
-                         as_stream(stream), lv, c, out, nitems, G);
-  } else if (variant >= 20 && variant <= 24) {  // 21 / 22: diagnostics (skip large / small windows), 24: stamps
-    dim3 grid((unsigned)num_rois, (unsigned)((channels + kPairChunk - 1) / kPairChunk));
-    if (variant == 20 && getenv("FRH_PAIR_PW")) {
-      const int pw = atoi(getenv("FRH_PAIR_PW"));
-      const dim3 g2((unsigned)num_rois, (unsigned)((channels + 2 * pw - 1) / (2 * pw)));
-      if (pw == 32) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 32>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-      else if (pw == 16) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 16>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-      else hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, false, 8>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    } else if (variant == 20 || variant == 23)
-      hipLaunchKernelGGL(roi_align_fwd_pair_kernel<0>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else if (variant == 21)
-      hipLaunchKernelGGL(roi_align_fwd_pair_kernel<2>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else if (variant == 22)
-      hipLaunchKernelGGL(roi_align_fwd_pair_kernel<1>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
-    else
-      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<0, true>), grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
-  } else if (variant >= 30 && variant <= 37) {  // diagnostics: 31 / 32 skip large / small windows, 33 no stores, 34 no evaluation
-    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    if (variant == 30)
-      hipLaunchKernelGGL(roi_align_fwd_x4_kernel<0>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 36)  // occupancy: registers for 8 waves per SIMD
-      hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, false, 8>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
-                         out);
-    else if (variant == 37)  // occupancy: registers for 6 waves per SIMD
-      hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, false, 6>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
-                         out);
-    else if (variant == 35)
-      hipLaunchKernelGGL((roi_align_fwd_x4_kernel<0, true>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 33)
-      hipLaunchKernelGGL(roi_align_fwd_x4_kernel<3>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 34)
-      hipLaunchKernelGGL(roi_align_fwd_x4_kernel<4>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 31)
-      hipLaunchKernelGGL(roi_align_fwd_x4_kernel<2>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else
-      hipLaunchKernelGGL(roi_align_fwd_x4_kernel<1>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-  } else if (variant >= 9 && variant <= 19) {
-    // 10: windows <= 256 floats staged (default); 11 / 12: stage up to 512 / 1024 (experiments)
-    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    if (variant == 10)
-      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 15)  // occupancy: registers for 8 waves per SIMD
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, kRoiChanChunk, 8>), grid, dim3(kRoiThreads), 0,
-                         as_stream(stream), lv, c, out);
-    else if (variant == 16)  // occupancy: registers for 6 waves per SIMD
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, kRoiChanChunk, 6>), grid, dim3(kRoiThreads), 0,
-                         as_stream(stream), lv, c, out);
-    else if (variant == 13)  // diagnostics: gathered (large-window) RoIs only
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 1>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 14)  // diagnostics: staged (small-window) RoIs only
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 2>), grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 11)
-      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<512>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 17)
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 128>), dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 18)
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<256, 0, 256>), dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 19)
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<1024, 0, 256>), dim3((unsigned)num_rois, (unsigned)((channels + 255) / 256)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else if (variant == 9)
-      hipLaunchKernelGGL((roi_align_fwd_lds_kernel<1024, 0, 128>), dim3((unsigned)num_rois, (unsigned)((channels + 127) / 128)), dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
-    else
-      hipLaunchKernelGGL(roi_align_fwd_lds_kernel<1024>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+  if (pair_ok(f, channels, pooled_h, pooled_w)) {
+    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kPairChunk - 1) / kPairChunk));
+    hipLaunchKernelGGL(roi_align_fwd_pair_kernel<>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (f.lds) {
+    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
+    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   } else {
-    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
+    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
   }
   return check_launch("frh_roi_align_fwd");
-}
-
-extern "C" size_t frh_roi_align_workspace(int64_t num_rois) {
-  if (num_rois <= 0 || num_rois > kPlanMaxRois) return 0;
-  return ((size_t)num_rois + group_bound(num_rois) + 2) * sizeof(int32_t);
-}
-
-extern "C" int32_t frh_roi_align_fwd_ws(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                                        const int64_t* strides, const float* scales, int32_t batch, int32_t channels,
-                                        const float* rois, const int64_t* roi_levels, int64_t num_rois,
-                                        int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                                        float* out, void* workspace, size_t ws_bytes, void* stream) {
-  return frh_roi_align_fwd_variant(-2, num_levels, feats, feat_hw, strides, scales, batch, channels, rois,
-                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, workspace,
-                                   ws_bytes, stream);
-}
-
-extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                                             const int64_t* strides, const float* scales, int32_t batch,
-                                             int32_t channels, const float* rois, const int64_t* roi_levels,
-                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
-                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
-  return frh_roi_align_fwd_variant(-1, num_levels, feats, feat_hw, strides, scales, batch, channels, rois,
-                                   roi_levels, num_rois, pooled_h, pooled_w, sampling_ratio, aligned, out, nullptr, 0,
-                                   stream);
 }
 
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
@@ -2732,12 +95,7 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   FRH_REQUIRE(grad_feats && grad_out, "null pointer argument");
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  // channels-last gradient (channel stride 1): full 64-B atomic segments
-  bool cl = sampling_ratio == 2 && pooled_h * pooled_w <= 64 && channels % kClChans == 0;
-  for (int l = 0; l < lv.L; ++l) cl = cl && lv.sc[l] == 1 && lv.w[l] <= kClBandCells;
-  if (cl)
-    hipLaunchKernelGGL(roi_align_bwd_cl_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
-  else if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
+  if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
     hipLaunchKernelGGL(roi_align_bwd_sep_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   else if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
     hipLaunchKernelGGL(roi_align_bwd_lds_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
@@ -2746,89 +104,6 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   return check_launch("frh_roi_align_bwd");
 }
 
-static TileMap tile_map(int32_t L, const int32_t* feat_hw, int32_t batch, int64_t* max_tiles) {
-  TileMap tm{};
-  tm.B = batch;
-  tm.base[0] = 0;
-  *max_tiles = 1;
-  for (int l = 0; l < L; ++l) {
-    tm.nty[l] = (feat_hw[2 * l] + kBwdTile - 1) / kBwdTile;
-    tm.ntx[l] = (feat_hw[2 * l + 1] + kBwdTile - 1) / kBwdTile;
-    tm.base[l + 1] = tm.base[l] + (int64_t)batch * tm.nty[l] * tm.ntx[l];
-    *max_tiles = std::max<int64_t>(*max_tiles, (int64_t)tm.nty[l] * tm.ntx[l]);
-  }
-  return tm;
-}
-
-struct BwdLayout {
-  size_t count, off, fill, win, list, total;
-  int64_t cap;
-};
-
-static BwdLayout bwd_layout(int32_t L, const int32_t* feat_hw, int32_t batch, int64_t num_rois) {
-  int64_t mt;
-  const TileMap tm = tile_map(L, feat_hw, batch, &mt);
-  const int64_t T = tm.base[L];
-  auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-  BwdLayout z;
-  z.cap = num_rois * mt;
-  z.count = 0;
-  z.off = z.count + al(T * 4);
-  z.fill = z.off + al((T + 1) * 4);
-  z.win = z.fill + al(T * 4);
-  z.list = z.win + al(num_rois * 16);
-  z.total = z.list + al(z.cap * 4);
-  return z;
-}
-
-extern "C" size_t frh_roi_align_bwd_workspace(int32_t num_levels, const int32_t* feat_hw, int32_t batch,
-                                              int64_t num_rois) {
-  if (num_levels < 1 || num_levels > FRH_MAX_LEVELS || !feat_hw || batch < 1 || num_rois < 0) return 0;
-  return bwd_layout(num_levels, feat_hw, batch, num_rois).total;
-}
-
-extern "C" int32_t frh_roi_align_bwd_tiled(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
-                                           const int64_t* strides, const float* scales, int32_t batch,
-                                           int32_t channels, const float* rois, const int64_t* roi_levels,
-                                           int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
-                                           int32_t sampling_ratio, int32_t aligned, const float* grad_out,
-                                           void* workspace, size_t ws_bytes, void* stream) {
-  int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
-  if (r) return r;
-  FRH_REQUIRE(sampling_ratio == 2 && pooled_h * pooled_w <= kWave, "tiled backward needs sampling_ratio 2 and "
-              "pooled_h * pooled_w <= 64 (got %d, %dx%d)", sampling_ratio, pooled_h, pooled_w);
-  RoiLevels lv;
-  r = make_levels(num_levels, nullptr, grad_feats, feat_hw, strides, scales, &lv);
-  if (r) return r;
-  FRH_REQUIRE(grad_feats && (grad_out || num_rois == 0), "null pointer argument");
-  const BwdLayout z = bwd_layout(num_levels, feat_hw, batch, num_rois);
-  FRH_REQUIRE(workspace && ws_bytes >= z.total, "workspace too small (%zu < %zu)", ws_bytes, z.total);
-  int64_t mt;
-  const TileMap tm = tile_map(num_levels, feat_hw, batch, &mt);
-  const int64_t T = tm.base[num_levels];
-  char* ws = static_cast<char*>(workspace);
-  TileLists tl{reinterpret_cast<uint32_t*>(ws + z.count), reinterpret_cast<uint32_t*>(ws + z.off),
-               reinterpret_cast<uint32_t*>(ws + z.fill), reinterpret_cast<int4*>(ws + z.win),
-               reinterpret_cast<int32_t*>(ws + z.list), z.cap};
-  hipStream_t st = as_stream(stream);
-  RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
-  FRH_HIP(hipMemsetAsync(ws + z.count, 0, z.off - z.count, st));
-  FRH_HIP(hipMemsetAsync(ws + z.fill, 0, z.win - z.fill, st));
-  if (num_rois > 0) {
-    const unsigned nb = (unsigned)((num_rois + 255) / 256);
-    hipLaunchKernelGGL(roi_bwd_bin_count_kernel, dim3(nb), dim3(256), 0, st, lv, c, tm, tl);
-  }
-  hipLaunchKernelGGL(roi_bwd_bin_scan_kernel, dim3(1), dim3(1024), 0, st, tl, T);
-  if (num_rois > 0) {
-    const unsigned nb = (unsigned)((num_rois + 255) / 256);
-    hipLaunchKernelGGL(roi_bwd_bin_fill_kernel, dim3(nb), dim3(256), 0, st, lv, c, tm, tl);
-  }
-  dim3 grid((unsigned)T, (unsigned)((channels + kBwdTileChans - 1) / kBwdTileChans));
-  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, grid, dim3(kRoiThreads), 0, st, lv, c, tm, tl, grad_out);
-  return check_launch("frh_roi_align_bwd_tiled");
-}
-
-// dense-layout convenience entry points (header): layout 0 = NCHW, 1 = NHWC
 static void dense_strides(int32_t L, const int32_t* hw, int32_t C, int32_t layout, int64_t* st) {
   for (int l = 0; l < L; ++l) {
     int64_t H = hw[2 * l], W = hw[2 * l + 1];

@@ -1,0 +1,1008 @@
+// RoIAlign kernels shared by the product library (csrc/roi_align.hip) and the
+// tools-only variant library (tools/csrc/roi_variants.hip).  See roi_align.hip.
+#pragma once
+#include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include <type_traits>
+
+#include "roi_common.h"
+
+namespace frh {
+
+constexpr int kRoiThreads = 256;
+constexpr int kRoiChanChunk = 64;
+constexpr int kMaxSamplesPerDim = 1024;
+
+// true when the separable tables fit in LDS (always for fixed sampling ratios;
+// adaptive grids on huge RoIs fall back to computing taps per sample)
+__device__ __forceinline__ bool taps_fit(const RoiGeom& g, const RoiCfg& c) {
+  return c.ph * g.gh <= kMaxSamplesPerDim && c.pw * g.gw <= kMaxSamplesPerDim;
+}
+
+__device__ __forceinline__ void fill_taps(const RoiGeom& g, const RoiCfg& c, int H, int W, Tap* ty, Tap* tx) {
+  if (!taps_fit(g, c)) return;
+  const int ny = c.ph * g.gh, nx = c.pw * g.gw;
+  for (int e = threadIdx.x; e < ny + nx; e += blockDim.x) {
+    if (e < ny) {
+      int p = e / g.gh, i = e - p * g.gh;
+      ty[e] = make_tap(sample_y(g, p, i), H);
+    } else {
+      int q = e - ny;
+      int p = q / g.gw, i = q - p * g.gw;
+      tx[q] = make_tap(sample_x(g, p, i), W);
+    }
+  }
+}
+
+static __global__ void __launch_bounds__(kRoiThreads) roi_align_fwd_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  fill_taps(g, c, H, W, ty, tx);
+  __syncthreads();
+  const int nbins = c.ph * c.pw;
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const bool tab = taps_fit(g, c);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* o = out + (k * c.C + c0) * nbins;
+  for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
+    const int cl = item / nbins, bin = item - cl * nbins;
+    const int py = bin / c.pw, px = bin - py * c.pw;
+    const float* f = base + (int64_t)(c0 + cl) * scs;
+    float acc = 0.0f;
+    for (int iy = 0; iy < g.gh; ++iy) {
+      const Tap a = tab ? ty[py * g.gh + iy] : make_tap(sample_y(g, py, iy), H);
+      for (int ix = 0; ix < g.gw; ++ix) {
+        const Tap bx = tab ? tx[px * g.gw + ix] : make_tap(sample_x(g, px, ix), W);
+        float val = 0.0f;
+        if (a.valid && bx.valid) {
+          float w1 = a.h * bx.h, w2 = a.h * bx.l, w3 = a.l * bx.h, w4 = a.l * bx.l;
+          float v1 = f[a.lo * sy + bx.lo * sx], v2 = f[a.lo * sy + bx.hi * sx];
+          float v3 = f[a.hi * sy + bx.lo * sx], v4 = f[a.hi * sy + bx.hi * sx];
+          val = ((w1 * v1 + w2 * v2) + w3 * v3) + w4 * v4;
+        }
+        acc = acc + val;
+      }
+    }
+    o[item] = acc / g.count;
+  }
+}
+
+
+// Buffer-descriptor variant (sampling ratio 2, ph*pw <= 256; the default).
+// Lane (bin, channel group cg) keeps its bin's 16 tap offsets in VGPRs as
+// 32-bit byte offsets into a descriptor over this (image, level, channel
+// chunk) slice; the channel walk moves only the wave-uniform soffset, so the
+// loop carries no per-lane address arithmetic.  When every x-sample of the
+// wave has x_hi = x_lo + 1 (all but right-border clamped samples) the taps of
+// a sample row are one 8-byte load: 8 loads per (bin, channel) instead of 16.
+// The 1/count of SR=2 is an exact power of two, so acc * 0.25 == acc / 4.
+// Results identical to the direct kernel.
+template <int U>
+__device__ __forceinline__ void fwd_buf_block(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out,
+                                              int64_t k, int c0, const RoiGeom& g) {
+  constexpr int SR = 2;
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int groups = kRoiThreads / nbins;
+  const int t = threadIdx.x;
+  if (t >= groups * nbins) return;
+  const int bin = t % nbins, cg = t / nbins;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)c0 * scs;
+  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + c0) * nbins, (int64_t)nch * nbins * 4);
+  const int cstep = groups * scs * 4, ostep = groups * nbins * 4;
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+  int row[SR][2], col[SR][2];
+  bool pair = sx == 1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    row[i][0] = (cg * scs + (ty[i].valid ? ty[i].lo * sy : 0)) * 4;
+    row[i][1] = (cg * scs + (ty[i].valid ? ty[i].hi * sy : 0)) * 4;
+    col[i][0] = tx[i].valid ? tx[i].lo * sx * 4 : 0;
+    col[i][1] = tx[i].valid ? tx[i].hi * sx * 4 : 0;
+    pair = pair && (!tx[i].valid || tx[i].hi == tx[i].lo + 1);
+  }
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  auto bin_value = [&](const float (&v)[SR][SR][4]) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    return acc * 0.25f;
+  };
+  // wave-uniform trip counts (soffset must stay scalar): every lane has a
+  // channel in the first nch / groups steps, the tail step is lane-guarded
+  const int full = nch / groups, iters = (nch + groups - 1) / groups;
+  const bool tail_ok = cg + full * groups < nch;
+  if (__all(pair)) {
+    int off[SR][2][SR];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) off[iy][r][ix] = row[iy][r] + col[ix][0];
+    int it = 0;
+    for (; it + U <= full; it += U) {
+      u32x2 rv[U][SR][2][SR];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int ix = 0; ix < SR; ++ix)
+              rv[u][iy][r][ix] = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][r][ix], (it + u) * cstep, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float v[SR][SR][4];
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix) {
+            v[iy][ix][0] = __uint_as_float(rv[u][iy][0][ix].x);
+            v[iy][ix][1] = __uint_as_float(rv[u][iy][0][ix].y);
+            v[iy][ix][2] = __uint_as_float(rv[u][iy][1][ix].x);
+            v[iy][ix][3] = __uint_as_float(rv[u][iy][1][ix].y);
+          }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, (it + u) * ostep, 0);
+      }
+    }
+    for (; it < iters; ++it) {
+      if (it == full && !tail_ok) break;
+      float v[SR][SR][4];
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][0][ix], it * cstep, 0);
+          const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(fr, off[iy][1][ix], it * cstep, 0);
+          v[iy][ix][0] = __uint_as_float(a.x);
+          v[iy][ix][1] = __uint_as_float(a.y);
+          v[iy][ix][2] = __uint_as_float(b.x);
+          v[iy][ix][3] = __uint_as_float(b.y);
+        }
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
+    }
+  } else {
+    for (int it = 0; it < iters; ++it) {
+      if (it == full && !tail_ok) break;
+      float v[SR][SR][4];
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[iy][ix][q] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(fr, row[iy][q >> 1] + col[ix][q & 1], it * cstep, 0));
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, t * 4, it * ostep, 0);
+    }
+  }
+}
+
+
+// Wave-staged variant (sampling ratio 2, ph*pw <= 64, 2*ph and 2*pw <= 64).
+// Every tap of a RoI lies in the window [y0, y1] x [x0, x1] of its level;
+// after FPN level mapping that window is a few to ~30 cells per side.  Each
+// wave owns 16 channels of the RoI and, per channel, copies the window into
+// its own LDS slab with lane-contiguous loads (every feature line fetched
+// once per RoI-channel, instead of 8 gathers per bin hitting the same lines),
+// then lane = bin reads its 16 taps from LDS.  The loads of channel i+1 are
+// in flight while channel i is evaluated.  The slab row has one extra column
+// holding a copy of the window's last feature column, so a right-border
+// clamped tap (x_lo = x_hi = W-1) reads (x_lo, x_lo + 1) like every other
+// sample.  No block barriers: waves are independent.  Windows above
+// kWinMax floats take the per-wave gather path.  Results identical to the
+// direct kernel.
+constexpr int kWinMax = 1024;
+constexpr int kWinR = kWinMax / kWave;
+
+// kChunk: channels per workgroup (kChunk / 4 per wave).
+// kWpe: minimum waves per SIMD the register allocation must allow (0: compiler's choice).
+template <int kStageMax, int kChunk = kRoiChanChunk, int kWpe = 0>
+__global__ void __launch_bounds__(kRoiThreads) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
+roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
+                                                                        float* __restrict__ out) {
+  constexpr int SR = 2;
+  __shared__ float slab_all[kRoiThreads / kWave][kWinMax];
+  const int64_t k = blockIdx.x;
+  // readfirstlane: the wave index is uniform, and the compiler must know it (soffset operands)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  constexpr int kWC = kChunk / (kRoiThreads / kWave);
+  const int cw0 = blockIdx.y * kChunk + wave * kWC;
+  const int nch = min(kWC, c.C - cw0);
+  float* slab = slab_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  // window of the valid taps: lane i evaluates y sample i and x sample i
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  if (lane < c.ph * SR) {
+    const Tap t = make_tap(sample_y(g, lane / SR, lane % SR), H);
+    if (t.valid) ylo = t.lo, yhi = t.hi;
+  }
+  if (lane < c.pw * SR) {
+    const Tap t = make_tap(sample_x(g, lane / SR, lane % SR), W);
+    if (t.valid) xlo = t.lo, xhi = t.hi;
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  const bool any = y1 >= y0 && x1 >= x0;
+  // odd slab row stride: the 4 tap rows of a wave's bins spread over the LDS banks
+  const int ws = (x1 - x0 + 2) | 1, n = any ? (y1 - y0 + 1) * ws : 0;
+  if (n > kStageMax) {  // uniform over the block (one RoI): large windows take the block gather path
+    for (int cc = 0; cc < kChunk && blockIdx.y * kChunk + cc < c.C; cc += kRoiChanChunk)
+      fwd_buf_block<2>(lv, c, out, k, blockIdx.y * kChunk + cc, g);
+    return;
+  }
+  if (nch <= 0) return;
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const int64_t extent = ((int64_t)(nch - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)nch * nbins * 4);
+  const int cstep = scs * 4, ostep = nbins * 4;
+  // this lane's bin: taps, weights, validity
+  const int bin = lane < nbins ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    ty[i] = make_tap(sample_y(g, py, i), H);
+    tx[i] = make_tap(sample_x(g, px, i), W);
+  }
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  auto bin_value = [&](const float (&v)[SR][SR][4]) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        float val = ((wt[iy][ix][0] * v[iy][ix][0] + wt[iy][ix][1] * v[iy][ix][1]) + wt[iy][ix][2] * v[iy][ix][2]) +
+                    wt[iy][ix][3] * v[iy][ix][3];
+        acc = acc + (ok[iy][ix] ? val : 0.0f);
+      }
+    return acc * 0.25f;
+  };
+  const bool active = lane < nbins;
+  if (n <= kStageMax) {
+    // slab addresses of this bin's sample rows (x_lo, x_lo + 1 pairs)
+    int sa[SR][2][SR];
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const bool v = ok[iy][ix];
+        sa[iy][0][ix] = v ? (ty[iy].lo - y0) * ws + (tx[ix].lo - x0) : 0;
+        sa[iy][1][ix] = v ? (ty[iy].hi - y0) * ws + (tx[ix].lo - x0) : 0;
+      }
+    // staging: slab element e = lane + 64 j  <-  feature (y0 + e / ws, min(x0 + e % ws, W - 1));
+    // the j loop is specialised on RB = 64-element rounds (1, 2, 4, 8, 16) so it unrolls branch-free
+    auto run = [&](auto rb) {
+      constexpr int RB = decltype(rb)::value, D = kWinR / RB;  // D channel windows per round, 16 loads/lane
+      int goff[RB];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int e = lane + j * kWave;
+        const int r = e / ws, cc = e - r * ws;
+        // lanes past the window re-read its first element: no extra cache line per round
+        goff[j] = e < n ? ((y0 + r) * sy + min(x0 + cc, W - 1) * sx) * 4 : (y0 * sy + x0 * sx) * 4;
+      }
+      float st[D][RB];
+      auto issue = [&](int c0r) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+          for (int j = 0; j < RB; ++j)
+            st[d][j] = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(fr, goff[j], min(c0r + d, nch - 1) * cstep, 0));
+      };
+      issue(0);
+      for (int i = 0; i < nch; i += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+          for (int j = 0; j < RB; ++j) slab[(d * RB + j) * kWave + lane] = st[d][j];  // [n, 64 RB) junk, unread
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (i + D < nch) issue(i + D);
+        if (active) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            if (i + d < nch) {
+              const float* sl = slab + d * RB * kWave;
+              float v[SR][SR][4];
+#pragma unroll
+              for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+                for (int ix = 0; ix < SR; ++ix) {
+                  v[iy][ix][0] = sl[sa[iy][0][ix]];
+                  v[iy][ix][1] = sl[sa[iy][0][ix] + 1];
+                  v[iy][ix][2] = sl[sa[iy][1][ix]];
+                  v[iy][ix][3] = sl[sa[iy][1][ix] + 1];
+                }
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bin_value(v)), orr, lane * 4, (i + d) * ostep, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    };
+    const int R = (n + kWave - 1) / kWave;
+    if (R <= 1)
+      run(std::integral_constant<int, 1>{});
+    else if (R <= 2 || kStageMax <= 2 * kWave)
+      run(std::integral_constant<int, 2>{});
+    else if (R <= 4 || kStageMax <= 4 * kWave)
+      run(std::integral_constant<int, 4>{});
+    else if (R <= 8 || kStageMax <= 8 * kWave)
+      run(std::integral_constant<int, 8>{});
+    else
+      run(std::integral_constant<int, kWinR>{});
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Channel-pair forward (the default).  One wave per (RoI, 2 * kPW channels), lane =
+// bin.  The RoI's tap grid is staged into the wave's LDS slab by 4-B LDS-DMA
+// with the two channels of a pair interleaved ([cell][2]), so every tap of a
+// bin is ONE aligned ds_read_b64 (2 LDS cycles per wave-instruction, twice the
+// bytes of ds_read_b32) and the bilinear sums run as packed f32 (v_pk_mul_f32
+// / v_pk_add_f32) on both channels at once -- halving the two per-output
+// costs (LDS tap reads, VALU) that bound the per-RoI kernels.  Each slab
+// dimension is either the dense tap window [y0, y1] (at most 4*ph rows) or the
+// list of the 2*ph samples' (lo, hi) taps, so every RoI fits (<= 28 x 29 cells
+// at 7x7) and large RoIs need no per-bin gather.  A DMA round moves 32
+// consecutive cells of one pair (two feature planes, one or two lines each).
+// The slab is two buffers; a stage is the D pairs (D = 8, 4, 2, 1, as the cell
+// count allows) one buffer holds, and stage s+1 is in flight while stage s is
+// evaluated (counted vmcnt waits); the tap reads of half-sample-row h+1 are in
+// flight while h is summed.  The RoI geometry is set up once per kPW pairs
+// (kPW = 8 measured fastest on the cfg2 RoIs: 45 us vs 62 us at 64 pairs).
+// Invalid samples have zero weights and read cell 0 (finite features: +0, the
+// reference's own 0 * feature term).  Same operation order as torchvision:
+// bit-identical to the other kernels.
+constexpr int kPairWave = 8;                    // channel pairs per wave (= workgroup): 16 channels
+constexpr int kPairHalf = 1664;                 // dwords per buffer (13 KB per wave for both)
+constexpr int kPairChunk = 2 * kPairWave;       // channels per workgroup
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// ds_read_b64 by hand: the compiler would pair two of them into ds_read2_b64,
+// which runs at half the rate (8 LDS cycles instead of 2 x 2, MI355X_MICROARCH
+// §LDS).  The caller waits with lds_wait<N>, which also orders the values.
+template <int OFF>
+__device__ __forceinline__ f32x2 lds_read_b64(uint32_t addr) {
+  f32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(f32x2 (&v)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+               : "i"(N)
+               : "memory");
+}
+
+template <int D, int kHalf = kPairHalf>
+struct PairLayout {
+  static constexpr int RS = (kHalf / D) / kWave * kWave;  // dwords per pair region
+  static constexpr int RP = RS / kWave;                       // DMA rounds per pair
+  static constexpr int kCells = RS / 2;
+  static_assert(D * RP + 2 * D < 64, "vmcnt is 6 bits");
+};
+
+// kPW: channel pairs per wave; kHalf: dwords per slab buffer.
+template <int kPW = kPairWave, int kHalf = kPairHalf>
+__global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  constexpr int SR = 2;
+  __shared__ __attribute__((aligned(16))) float slab[2 * kHalf];
+  // the slab as an LDS byte address (integer: no generic-pointer casts)
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const int64_t k = blockIdx.x;
+  const int cw0 = blockIdx.y * 2 * kPW;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  // sample positions (sampling ratio 2: the reference's "/ 2" is an exact halving)
+  auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
+  auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
+  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;  // tap lists: entry i = tap (i & 1 ? hi : lo) of sample i / 2
+  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  if (lane < nly) {
+    const int s = lane >> 1;
+    const Tap t = make_tap(pos_y(s >> 1, s & 1), H);
+    if (t.valid) yrow = (lane & 1) ? t.hi : t.lo, ylo = t.lo, yhi = t.hi;
+  }
+  if (lane < nlx) {
+    const int s = lane >> 1;
+    const Tap t = make_tap(pos_x(s >> 1, s & 1), W);
+    if (t.valid) xcol = (lane & 1) ? t.hi : t.lo, xlo = t.lo, xhi = t.hi;
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)2 * npairs * nbins * 4);
+  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  const int ostep = nbins * 4;
+  if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: all bins 0
+    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
+    return;
+  }
+  const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;
+  const int R = dy ? y1 - y0 + 1 : nly, Cs = dx ? x1 - x0 + 1 : nlx;
+  const int Cs2 = Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
+  const int ncell = R * Cs2;
+  const bool small = ncell <= PairLayout<8, kHalf>::kCells;
+  // feature byte offsets of slab row / column `lane`
+  const int rsrc = (dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
+  const int csrc = (dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
+  // this lane's bin: weights (zero for invalid samples) and LDS addresses of its 16 taps
+  const int bin = active ? lane : 0;
+  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
+  const uint32_t lbase = sbase;
+  float wt[SR][SR][4];
+  uint32_t ta[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy) {
+    const Tap a = make_tap(pos_y(py, iy), H);
+    const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap b = make_tap(pos_x(px, ix), W);
+      const int q0 = dx ? b.lo - x0 : 2 * (px * SR + ix), q1 = dx ? b.hi - x0 : 2 * (px * SR + ix) + 1;
+      const bool ok = a.valid && b.valid;
+      wt[iy][ix][0] = ok ? a.h * b.h : 0.f;
+      wt[iy][ix][1] = ok ? a.h * b.l : 0.f;
+      wt[iy][ix][2] = ok ? a.l * b.h : 0.f;
+      wt[iy][ix][3] = ok ? a.l * b.l : 0.f;
+      ta[iy][ix][0] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q0) : 0u);
+      ta[iy][ix][1] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q1) : 0u);
+      ta[iy][ix][2] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q0) : 0u);
+      ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q1) : 0u);
+    }
+  }
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  const uint32_t inv = (65536u + (uint32_t)Cs2 - 1u) / (uint32_t)Cs2;  // e / Cs2 == (e * inv) >> 16 for e < 1024
+
+  auto run = [&](auto dd) {
+    constexpr int D = decltype(dd)::value, RS = PairLayout<D, kHalf>::RS, RP = PairLayout<D, kHalf>::RP;
+    const int nst = (npairs + D - 1) / D;
+    // region dword j * 64 + lane of every pair  <-  channel (lane & 1) of cell (j * 64 + lane) / 2
+    int goff[RP];
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      int e = (j * kWave + lane) >> 1;
+      e = e < ncell ? e : 0;
+      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
+      goff[j] = __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
+    }
+    auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
+      const uint32_t buf = sbase + 4u * (uint32_t)((s & 1) * kHalf);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
+#pragma unroll
+        for (int j = 0; j < RP; ++j) lds_dma_at<4>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
+      }
+    };
+    auto eval = [&](auto bb, int s) {
+      constexpr int kBuf = decltype(bb)::value;
+      // half-rows h = 2 d + iy: 8 tap reads each; reads of h + 1 in flight while h is summed
+      f32x2 v[2][8];
+      f32x2 acc = {0.0f, 0.0f};
+      auto load = [&](auto hh) {
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
+      };
+      load(std::integral_constant<int, 0>{});
+      static_for<0, 2 * D>([&](auto hh) {
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
+        if constexpr (h + 1 < 2 * D) {
+          load(std::integral_constant<int, h + 1>{});
+          lds_wait<8>(v[h & 1]);
+        } else {
+          lds_wait<0>(v[h & 1]);
+        }
+        if (iy == 0) acc = f32x2{0.0f, 0.0f};
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const float* w = wt[iy][ix];
+          const f32x2* x = &v[h & 1][ix * 4];
+          const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
+          acc = acc + val;
+        }
+        if (iy == 1) {
+          const f32x2 r = acc * 0.25f;
+          const int p = s * D + d;
+          const int vo = p < npairs ? ovoff : 0x40000000;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, 0);
+        }
+      });
+    };
+    auto step = [&](auto bb, int s) {
+      if (s >= nst) return;
+      // retire stage s: younger than its DMAs are stage s-1's 2D stores and stage s+1's DMAs
+      if (s + 1 < nst) {
+        issue(s + 1);
+        if (s == 0)
+          wait_vmcnt<D * RP>();
+        else
+          wait_vmcnt<D * RP + 2 * D>();
+      } else if (s == 0) {
+        wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<2 * D>();
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      eval(bb, s);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    issue(0);
+    for (int s = 0; s < nst; s += 2) {
+      step(std::integral_constant<int, 0>{}, s);
+      step(std::integral_constant<int, 1>{}, s + 1);
+    }
+  };
+  if (small)
+    run(std::integral_constant<int, 8>{});
+  else if (ncell <= PairLayout<4, kHalf>::kCells)
+    run(std::integral_constant<int, 4>{});
+  else if (ncell <= PairLayout<2, kHalf>::kCells)
+    run(std::integral_constant<int, 2>{});
+  else
+    run(std::integral_constant<int, 1>{});
+}
+
+static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
+                                                                    const float* __restrict__ gout) {
+  __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];
+  const int64_t k = blockIdx.x;
+  const int c0 = blockIdx.y * kRoiChanChunk;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  fill_taps(g, c, H, W, ty, tx);
+  __syncthreads();
+  const int nbins = c.ph * c.pw;
+  const int nch = min(kRoiChanChunk, c.C - c0);
+  const bool tab = taps_fit(g, c);
+  float* base = lv.grad[l] + (int64_t)g.b * lv.sb[l];
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  const float* go = gout + (k * c.C + c0) * nbins;
+  for (int item = threadIdx.x; item < nch * nbins; item += blockDim.x) {
+    const int cl = item / nbins, bin = item - cl * nbins;
+    const int py = bin / c.pw, px = bin - py * c.pw;
+    float* f = base + (int64_t)(c0 + cl) * scs;
+    const float gv = go[item];
+    for (int iy = 0; iy < g.gh; ++iy) {
+      const Tap a = tab ? ty[py * g.gh + iy] : make_tap(sample_y(g, py, iy), H);
+      if (!a.valid) continue;
+      for (int ix = 0; ix < g.gw; ++ix) {
+        const Tap bx = tab ? tx[px * g.gw + ix] : make_tap(sample_x(g, px, ix), W);
+        if (!bx.valid) continue;
+        float g1 = gv * (a.h * bx.h) / g.count, g2 = gv * (a.h * bx.l) / g.count;
+        float g3 = gv * (a.l * bx.h) / g.count, g4 = gv * (a.l * bx.l) / g.count;
+        atomicAdd(&f[a.lo * sy + bx.lo * sx], g1);
+        atomicAdd(&f[a.lo * sy + bx.hi * sx], g2);
+        atomicAdd(&f[a.hi * sy + bx.lo * sx], g3);
+        atomicAdd(&f[a.hi * sy + bx.hi * sx], g4);
+      }
+    }
+  }
+}
+
+// Backward, window-accumulated (sampling 2, ph*pw <= 64): the default.  The
+// per-tap form above issues 16 scattered global float atomics per (bin, channel)
+// -- 205 M for a cfg2 batch, executed at the memory side at a small fraction of
+// the coalesced atomic rate (MI355X_MICROARCH.md, global float atomics): 7.7 ms
+// per train step.  Here each wave owns 16 channels of one RoI: per channel it
+// sums the 16 weighted taps of every bin into an LDS copy of the RoI's tap window
+// (ds_add_f32), then adds the window to the feature gradient with one global
+// atomic per non-zero cell, lanes along window rows (count = 4 at sampling 2:
+// (g * w) / 4 == (g * w) * 0.25 exactly, without the division sequence).  Windows above kBwdSlab
+// floats keep the per-tap atomics.  Contributions are the reference's
+// grad * w / count; float atomics make the summation order (and the last bits)
+// run-dependent, as in torchvision's own CUDA backward.
+constexpr int kBwdSlab = 1024;  // floats per wave
+
+static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(RoiLevels lv, RoiCfg c,
+                                                                        const float* __restrict__ gout) {
+  constexpr int SR = 2, kCh = kRoiChanChunk / (kRoiThreads / kWave);
+  __shared__ float slab_all[kRoiThreads / kWave][kBwdSlab];
+  const int64_t k = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
+  const int nch = min(kCh, c.C - cw0);
+  if (nch <= 0) return;
+  float* slab = slab_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const int bin = active ? lane : 0;
+  const int py = bin / c.pw, px = bin - py * c.pw;
+  Tap ty[SR], tx[SR];
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {  // sampling 2: the "/ gh" of the sample position is an exact halving
+    ty[i] = make_tap(g.start_h + (float)py * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f, H);
+    tx[i] = make_tap(g.start_w + (float)px * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f, W);
+  }
+  int ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+#pragma unroll
+  for (int i = 0; i < SR; ++i) {
+    if (active && ty[i].valid) ylo = min(ylo, ty[i].lo), yhi = max(yhi, ty[i].hi);
+    if (active && tx[i].valid) xlo = min(xlo, tx[i].lo), xhi = max(xhi, tx[i].hi);
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  if (y1 < y0 || x1 < x0) return;  // no valid tap: no gradient
+  const int WW = x1 - x0 + 1, n = (y1 - y0 + 1) * WW;
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const float* go = gout + (k * c.C + cw0) * nbins;
+  bool ok[SR][SR];
+  float wt[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      ok[iy][ix] = active && a.valid && b.valid;
+      wt[iy][ix][0] = a.h * b.h;
+      wt[iy][ix][1] = a.h * b.l;
+      wt[iy][ix][2] = a.l * b.h;
+      wt[iy][ix][3] = a.l * b.l;
+    }
+  if (n > kBwdSlab) {  // window larger than the slab: per-tap global atomics
+    for (int ch = 0; ch < nch; ++ch) {
+      const float gv = active ? go[ch * nbins + bin] : 0.0f;
+      float* f = gbase + (int64_t)ch * scs;
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          if (!ok[iy][ix]) continue;
+          const Tap a = ty[iy], b = tx[ix];
+          atomicAdd(&f[a.lo * sy + b.lo * sx], gv * wt[iy][ix][0] / g.count);
+          atomicAdd(&f[a.lo * sy + b.hi * sx], gv * wt[iy][ix][1] / g.count);
+          atomicAdd(&f[a.hi * sy + b.lo * sx], gv * wt[iy][ix][2] / g.count);
+          atomicAdd(&f[a.hi * sy + b.hi * sx], gv * wt[iy][ix][3] / g.count);
+        }
+    }
+    return;
+  }
+  int cell[SR][SR][4];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap a = ty[iy], b = tx[ix];
+      const int rl = (a.lo - y0) * WW, rh = (a.hi - y0) * WW, cl = b.lo - x0, chh = b.hi - x0;
+      cell[iy][ix][0] = rl + cl;
+      cell[iy][ix][1] = rl + chh;
+      cell[iy][ix][2] = rh + cl;
+      cell[iy][ix][3] = rh + chh;
+    }
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  const int r0 = lane / WW, col0 = lane - r0 * WW, dr = kWave / WW, dc = kWave - dr * WW;
+  for (int ch = 0; ch < nch; ++ch) {
+    for (int e = lane; e < n; e += kWave) slab[e] = 0.0f;
+    wave_sync();
+    const float gv = active ? go[ch * nbins + bin] : 0.0f;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix)
+        if (ok[iy][ix])
+#pragma unroll
+          for (int q = 0; q < 4; ++q) atomicAdd(&slab[cell[iy][ix][q]], gv * wt[iy][ix][q] * 0.25f);
+    wave_sync();
+    float* f = gbase + (int64_t)ch * scs;
+    int r = r0, col = col0;
+    for (int e = lane; e < n; e += kWave) {
+      const float v = slab[e];
+      if (v != 0.0f) atomicAdd(&f[(int64_t)(y0 + r) * sy + (int64_t)(x0 + col) * sx], v);
+      r += dr;
+      col += dc;
+      if (col >= WW) col -= WW, ++r;
+    }
+    wave_sync();  // the window is re-zeroed for the next channel only after every lane read it
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward, separable tap sums (sampling 2, 4*ph and 4*pw <= 32): the default.
+// LDS float atomics (ds_add_f32) run several times slower than plain LDS
+// traffic on gfx950 (tools/probe/probe_bwd.py: the same accumulation took 7x
+// longer with ds_add_f32 than with a racy read-modify-write), and degenerate
+// RoIs (the random-init proposals clamped to the image border: half the cfg2
+// RoIs are < 1 px tall) pile all their taps on a few cells, which serialises
+// any per-cell scheme.  The taps are separable: cell (y, x) receives
+// (g[py][px] * (wy * wx)) * 0.25 for every y tap entry (py, iy, lo|hi) on row y
+// and every x tap entry (px, ix, lo|hi) on column x; wy * wx is exactly the
+// reference's w1..w4 (hy*hx, hy*lx, ly*hx, ly*lx), so every contribution is the
+// reference's grad * w / count.  A wave sorts its RoI's <= 4*ph y entries by
+// row and <= 4*pw x entries by column once.  Per channel pair, lane (half h,
+// j) owns x entry j of channel h and walks the y entries in row order (a
+// uniform loop): it accumulates its contributions, and at the end of each row
+// a segmented sum over the lanes of equal column leaves each (row, column)
+// cell's total in one lane, which adds it to the feature gradient with one
+// global atomic.  No LDS atomics, no divergence; the order of the float sums
+// differs from the reference's (float atomics already make it run-dependent,
+// as in torchvision's CUDA backward).
+constexpr int kSepEnt = 32;  // tap entries per axis and wave half: 4 * ph, 4 * pw <= 32
+
+static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
+                                                                        const float* __restrict__ gout) {
+  constexpr int kCh = kRoiChanChunk / (kRoiThreads / kWave);  // channels per wave (even)
+  __shared__ int yent_all[kRoiThreads / kWave][kSepEnt];      // row << 16 | py, sorted by (row, entry)
+  __shared__ float yw_all[kRoiThreads / kWave][kSepEnt];
+  __shared__ int xpos_all[kRoiThreads / kWave][kSepEnt];      // position of each x entry, unsorted
+  __shared__ float gv_all[kRoiThreads / kWave][2 * kWave];
+  const int64_t k = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int cw0 = blockIdx.y * kRoiChanChunk + wave * kCh;
+  const int nch = min(kCh, c.C - cw0);
+  if (nch <= 0) return;
+  int* yent = yent_all[wave];
+  float* yw = yw_all[wave];
+  int* xpos = xpos_all[wave];
+  float* gv = gv_all[wave];
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int ph = c.ph, pw = c.pw, nbins = ph * pw;
+  const int nye = 4 * ph, nxe = 4 * pw;
+  const int h = lane >> 5, j = lane & 31;
+  // tap entry e of an axis: sample e / 2 (bin e / 4, sub-sample (e / 2) & 1), lo (e even) or hi
+  auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
+    const Tap t = make_tap(start + (float)(e >> 2) * bin + ((float)((e >> 1) & 1) + 0.5f) * bin * 0.5f, size);
+    *pos = t.valid ? ((e & 1) ? t.hi : t.lo) : -1;
+    *w = (e & 1) ? t.l : t.h;
+  };
+  int yp, xp;
+  float ywv, xwv;
+  entry(j, g.start_h, g.bin_h, H, &yp, &ywv);
+  entry(j, g.start_w, g.bin_w, W, &xp, &xwv);
+  if (j >= nye) yp = -1;
+  if (j >= nxe) xp = -1;
+  if (h == 0) xpos[j] = xp < 0 ? (1 << 20) : xp;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // x entries: rank by (col, entry); lane (h, j) takes the j-th in column order
+  int xrank = 0;
+  for (int e = 0; e < nxe; ++e) {
+    const int pe = xpos[e], pm = xpos[j];
+    xrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
+  }
+  // y entries: rank by (row, entry), written sorted
+  {
+    int yrank = 0;
+    const int pm = yp < 0 ? (1 << 20) : yp;
+    for (int e = 0; e < nye; ++e) {
+      const int pe = __shfl(yp < 0 ? (1 << 20) : yp, e, kWave);
+      yrank += (pe < pm || (pe == pm && e < j)) ? 1 : 0;
+    }
+    if (h == 0 && j < nye && yp >= 0) {
+      yent[yrank] = (yp << 16) | (j >> 2);
+      yw[yrank] = ywv;
+    }
+  }
+  int nyv = 0, nxv = 0;  // valid entries (uniform)
+  {
+    const uint64_t my = __ballot(h == 0 && yp >= 0), mx = __ballot(h == 0 && xp >= 0);
+    nyv = __popcll(my);
+    nxv = __popcll(mx);
+  }
+  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  // this lane's x entry (column order) and the segment of lanes sharing its column
+  int my_col = -1, my_px = 0;
+  float my_wx = 0.0f;
+  // scatter the x entries into column order through LDS
+  __shared__ int xs_all[kRoiThreads / kWave][kSepEnt];
+  __shared__ float xw_all[kRoiThreads / kWave][kSepEnt];
+  int* xs = xs_all[wave];
+  float* xw = xw_all[wave];
+  if (h == 0 && xp >= 0) {
+    xs[xrank] = (xp << 16) | (j >> 2);
+    xw[xrank] = xwv;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool xv = j < nxv;
+  if (xv) {
+    my_col = xs[j] >> 16;
+    my_px = xs[j] & 0xffff;
+    my_wx = xw[j];
+  }
+  // segment of equal columns within the half: [j - lead, j + trail]
+  int trail = 0;
+  for (int d = 1; d < kSepEnt; ++d) {
+    const int jj = j + d;
+    if (jj < nxv && (xs[jj] >> 16) == my_col) trail = d;
+  }
+  const bool head = xv && (j == 0 || (xs[j - 1] >> 16) != my_col);
+  const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
+  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const float* go = gout + (k * c.C + cw0) * nbins;
+  for (int ch = 0; ch < nch; ch += 2) {
+    // grad_out of channels ch, ch + 1 (a missing odd last channel reads 0 and is not written)
+    for (int e = lane; e < 2 * nbins; e += kWave) {
+      const int hh = e >= nbins ? 1 : 0;
+      gv[hh * kWave + (e - hh * nbins)] = (ch + hh < nch) ? go[(ch + hh) * nbins + (e - hh * nbins)] : 0.0f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* f = gbase + (int64_t)(ch + h) * scs;
+    const bool live = xv && ch + h < nch;
+    float acc = 0.0f;
+    for (int i = 0; i < nyv; ++i) {
+      const int ye = yent[i];
+      const int row = ye >> 16, py = ye & 0xffff;
+      const float wy = yw[i];
+      const float gvv = gv[h * kWave + py * pw + my_px];
+      acc = acc + (live ? gvv * (wy * my_wx) * 0.25f : 0.0f);  // (g * w) / count, count = 4
+      if (i + 1 == nyv || (yent[i + 1] >> 16) != row) {  // end of this row's entries (uniform)
+        float sum = acc;
+#pragma unroll
+        for (int d = 1; d < kSepEnt; d <<= 1) {
+          const float t = __shfl_down(sum, d, 32);
+          if (d <= trail) sum = sum + t;
+        }
+        if (head && live && sum != 0.0f) atomicAdd(&f[(int64_t)row * sy + (int64_t)my_col * sx], sum);
+        acc = 0.0f;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+static inline int32_t make_levels(int32_t L, const float* const* feats, float* const* grads, const int32_t* feat_hw,
+                           const int64_t* strides, const float* scales, RoiLevels* lv) {
+  FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "num_levels %d out of range", L);
+  FRH_REQUIRE(feat_hw && scales && strides, "null pointer argument");
+  lv->L = L;
+  for (int l = 0; l < L; ++l) {
+    lv->feat[l] = feats ? feats[l] : nullptr;
+    lv->grad[l] = grads ? grads[l] : nullptr;
+    lv->h[l] = feat_hw[2 * l];
+    lv->w[l] = feat_hw[2 * l + 1];
+    FRH_REQUIRE(lv->h[l] > 0 && lv->w[l] > 0, "level %d has an empty feature map", l);
+    lv->sb[l] = strides[4 * l];
+    lv->sc[l] = strides[4 * l + 1];
+    lv->sy[l] = strides[4 * l + 2];
+    lv->sx[l] = strides[4 * l + 3];
+    lv->scale[l] = scales[l];
+  }
+  return FRH_OK;
+}
+
+
+static inline int32_t roi_common_checks(int32_t batch, int32_t channels, int64_t num_rois, int32_t ph, int32_t pw,
+                                 const float* rois) {
+  FRH_REQUIRE(batch >= 1 && channels >= 1 && num_rois >= 0 && ph >= 1 && pw >= 1, "bad sizes");
+  FRH_REQUIRE(num_rois == 0 || rois, "null rois");
+  FRH_REQUIRE(num_rois < (int64_t)0x7fffffff, "too many rois");
+  return FRH_OK;
+}
+
+// shape classes of the forward kernels
+struct FwdCaps {
+  bool buf;    // 32-bit byte offsets within every (image, level) slice, sampling 2, ph*pw <= 256
+  bool lds;    // + ph*pw <= 64 and 2*ph, 2*pw <= 64
+  bool x4;     // + unit x stride, 16-B aligned rows / channel planes / bases (16-B LDS-DMA)
+};
+
+static inline FwdCaps fwd_caps(const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw, int32_t sr) {
+  FwdCaps f;
+  f.buf = sr == 2 && ph * pw <= kRoiThreads;
+  for (int l = 0; l < lv.L; ++l) {
+    const int64_t ext = ((int64_t)(channels - 1) * lv.sc[l] + (int64_t)(lv.h[l] - 1) * lv.sy[l] +
+                         (int64_t)(lv.w[l] - 1) * lv.sx[l] + 1) * 4;
+    f.buf = f.buf && lv.sc[l] >= 0 && lv.sy[l] >= 0 && lv.sx[l] >= 0 && ext < ((int64_t)1 << 31);
+  }
+  f.lds = f.buf && ph * pw <= 64 && 2 * ph <= 64 && 2 * pw <= 64;
+  f.x4 = f.lds;
+  for (int l = 0; l < lv.L; ++l)
+    f.x4 = f.x4 && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 && lv.sb[l] % 4 == 0 &&
+           (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
+  return f;
+}
+
+
+// kernels of the product's forward, chosen by shape class
+static inline bool pair_ok(const FwdCaps& f, int32_t channels, int32_t ph, int32_t pw) {
+  return f.lds && channels % 2 == 0 && 4 * ph <= kWave && 4 * pw <= kWave &&
+         4 * ph * (4 * pw + 1) <= PairLayout<1>::kCells;
+}
+
+}  // namespace frh

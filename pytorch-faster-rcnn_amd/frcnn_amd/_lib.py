@@ -67,21 +67,8 @@ SIGNATURES = {
                                   c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_align_fwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
-    'frh_roi_align_sweep_workspace': (c_size, [c_i64, c_i32, c_i32]),
-    'frh_roi_align_fwd_sweep': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp,
-                                        c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_bwd_sweep': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp,
-                                        c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_workspace': (c_size, [c_i64]),
-    'frh_roi_align_fwd_ws': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp, c_i64,
-                                     c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_fwd_variant': (c_i32, [c_i32, c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
-                                          c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     'frh_roi_align_bwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
-    'frh_roi_align_bwd_workspace': (c_size, [c_i32, P(c_i32), c_i32, c_i64]),
-    'frh_roi_align_bwd_tiled': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
-                                        c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     'frh_roi_pool_fwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp,
                                  c_vp, c_vp]),
     'frh_roi_pool_bwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,

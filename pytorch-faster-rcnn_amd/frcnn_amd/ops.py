@@ -421,24 +421,6 @@ def _feat_desc(feats):
 ROI_ALIGN_PROFILE = {'on': False, 'records': []}
 
 
-def roi_align_variant(variant, feats, rois, levels, scales, output_size, sampling_ratio):
-    """One named RoIAlign forward kernel (0 direct, 10 per-RoI LDS, 20 channel pairs = default, 50 grouped);
-    parity tests and the micro-benchmark.  The grouped kernel's workspace comes from the
-    caching allocator like every other op's."""
-    _need_cuda(rois, *feats)
-    feats = [_f32(f) for f in feats]
-    rois = _f32(rois).contiguous()
-    K, C = rois.shape[0], feats[0].shape[1]
-    ph, pw = output_size
-    out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
-    hw, st = _feat_desc(feats)
-    ws = workspace(_lib.query('frh_roi_align_workspace', K), rois.device)
-    call('frh_roi_align_fwd_variant', int(variant), len(feats), ptr_array(feats), hw, st, f32_array(scales),
-         feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), 0, ptr(out), ptr(ws),
-         ws.numel(), stream_of(out))
-    return out
-
-
 class _RoIAlignMulti(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, levels, scales, output_size, sampling_ratio, aligned, *feats):
@@ -462,6 +444,8 @@ class _RoIAlignMulti(torch.autograd.Function):
                                                  feats, tuple(scales), sampling_ratio))
         ctx.save_for_backward(rois, levels)
         ctx.cfg = (list(scales), output_size, sampling_ratio, aligned, [f.shape for f in feats])
+        ctx.formats = [torch.channels_last if (f.stride(1) == 1 and f.shape[1] > 1) else torch.contiguous_format
+                       for f in feats]
         return out
 
     @staticmethod
@@ -470,31 +454,14 @@ class _RoIAlignMulti(torch.autograd.Function):
         scales, (ph, pw), sr, aligned, shapes = ctx.cfg
         grad = grad.contiguous()
         K, B, C = rois.shape[0], shapes[0][0], shapes[0][1]
-        if ROI_ALIGN_BWD['mode'] == 'tiled' and sr == 2 and ph * pw <= 64:
-            # tiled gather: writes every gradient cell, no clearing, no global atomics
-            grads = [torch.empty(s, dtype=torch.float32, device=grad.device) for s in shapes]
-            hw, st = _feat_desc(grads)
-            ws = workspace(_lib.query('frh_roi_align_bwd_workspace', len(grads), hw, B, K), grad.device)
-            call('frh_roi_align_bwd_tiled', len(grads), ptr_array(grads), hw, st, f32_array(scales), B, C,
-                 ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), ptr(ws), ws.numel(),
-                 stream_of(grad))
-        else:
-            # 'channels_last': accumulate into [B, H, W, C] (returned as a channels_last view), so every
-            # window cell's 16-channel group is one full 64-B memory-side atomic; 'atomic': NCHW
-            fmt = torch.channels_last if ROI_ALIGN_BWD['mode'] == 'channels_last' else torch.contiguous_format
-            grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt).zero_()
-                     for s in shapes]
-            hw, st = _feat_desc(grads)
-            call('frh_roi_align_bwd_strided', len(grads), ptr_array(grads), hw, st, f32_array(scales), B, C,
-                 ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), stream_of(grad))
+        # the gradient keeps each feature map's memory format (NCHW or channels_last); it is
+        # cleared here and accumulated with float atomics (one per row run of a RoI's taps)
+        grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt).zero_()
+                 for s, fmt in zip(shapes, ctx.formats)]
+        hw, st = _feat_desc(grads)
+        call('frh_roi_align_bwd_strided', len(grads), ptr_array(grads), hw, st, f32_array(scales), B, C,
+             ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), stream_of(grad))
         return (None, None, None, None, None, None) + tuple(grads)
-
-
-# RoIAlign backward kernel: 'atomic' (default: per-RoI LDS window, one global atomic per cell and
-# channel into the NCHW gradient; measured fastest), 'channels_last' (LDS window bands, one 64-B
-# atomic per cell and 16 channels into a channels_last gradient) or 'tiled' (tile lists + LDS
-# gather, no global atomics).  Measurements: DESIGN.md §4.
-ROI_ALIGN_BWD = {'mode': 'atomic'}
 
 
 def roi_align_replay(rec, out=None):

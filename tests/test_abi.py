@@ -58,3 +58,28 @@ def test_errors_are_reported():
     from frcnn_amd import _lib
     with pytest.raises(RuntimeError, match='num_levels'):
         _lib.call('frh_anchor_grid', 0, None, None, None, None, 3, 0, None, 0, None)
+
+
+def test_product_exports_only_the_header():
+    """Every exported frh_* symbol of the product library is declared in the product
+    header: diagnostics and losing variants live in the tools-only library
+    (tools/csrc, tools/lib/libfrcnn_tools.so)."""
+    import subprocess
+    from frcnn_amd import _lib
+    out = subprocess.run(['nm', '-D', '--defined-only', _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.split()[-1].startswith('frh_')}
+    assert exported == set(header_decls()) | {'frh_abi_version', 'frh_last_error'}, exported ^ set(header_decls())
+
+
+def test_tools_header_matches_tools_table():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    import toolslib
+    txt = re.sub(r'/\*.*?\*/', '', open(os.path.join(REPO, 'tools', 'csrc', 'frcnn_tools.h')).read(), flags=re.S)
+    d = {}
+    for m in re.finditer(r'\b(?:int32_t|size_t)\s+(frh_\w+)\s*\(([^;]*?)\)\s*;', txt, flags=re.S):
+        d[m.group(1)] = m.group(2).count(',') + 1
+    assert set(d) == set(toolslib.TOOL_SIGNATURES)
+    for name, n in d.items():
+        assert len(toolslib.TOOL_SIGNATURES[name][1]) == n, name
+    assert not set(d) & set(header_decls())

@@ -360,10 +360,10 @@ def _rois(seed, n, batch):
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
-def test_roi_align_forward_kernels_identical(dev, layout):
-    """Every forward kernel (0 direct, 10 per-RoI LDS, 20 channel-pair, 30 wide-staged, 50 grouped union staging)
-    against the oracle and bit-identical to each other; P2-sized maps and 600 RoIs so the
-    grouped kernel takes both its union path and its per-RoI fallback (large windows)."""
+def test_roi_align_forward_default_vs_oracle_p2(dev, layout):
+    """The product forward (channel-pair kernel) on P2-sized maps, 600 RoIs incl. border /
+    degenerate / outside ones, against the oracle (the variants it was chosen among are
+    compared bit for bit in tests/test_tools_variants.py)."""
     from frcnn_amd import ops
     grids = [(152, 256), (76, 128), (38, 64), (19, 32)]
     feats = inputs.feature_maps(42, grids, 96, 2)
@@ -372,13 +372,13 @@ def test_roi_align_forward_kernels_identical(dev, layout):
     scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
     ref = oracle.roi_align(feats, rois, levels, scales, (7, 7), 2)
     ft = [T(f, dev) for f in feats]
-    if layout == 'nhwc':  # no 16-B staging: unit-stride rows are required
+    if layout == 'nhwc':
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
-    outs = {v: ops.roi_align_variant(v, ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
-            for v in ((0, 10, 20, 30, 50) if layout == 'nchw' else (0, 10, 20, 50))}
-    np.testing.assert_allclose(outs[0], ref, rtol=1e-5, atol=1e-5)
-    for v in outs:
-        assert np.array_equal(outs[v], outs[0]), 'variant %d differs' % v
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+    odd = [T(f[:, :95], dev).contiguous() for f in feats]  # odd C: the per-RoI LDS kernel
+    out2 = ops.roi_align_multilevel(odd, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
+    np.testing.assert_array_equal(out2, out[:, :95])
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
@@ -408,31 +408,31 @@ def test_roi_align_module_and_strided_view(dev):
     np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize('mode', ['channels_last', 'tiled', 'atomic'])
-@pytest.mark.parametrize('case', ['small', 'p2', 'p2_nhwc', 'adaptive'])
-def test_roi_align_backward_vs_oracle(dev, case, mode):
-    """Backward (the NCHW window kernel 'atomic' = the default; window bands + 64-B atomics
-    into a channels_last gradient; tiled gather; per-tap atomics for adaptive sampling)
-    against the oracle:
-    both reorder the float sums, so the tolerance is f32-accumulation level."""
+@pytest.mark.parametrize('case', ['small', 'p2', 'p2_nhwc', 'adaptive', 'bins9x7'])
+def test_roi_align_backward_vs_oracle(dev, case):
+    """Backward against the oracle: the separable row-run kernel (sampling 2, up to 8x8
+    bins; NCHW and channels_last gradients), the LDS-window kernel (9x7 bins) and per-tap
+    atomics (adaptive sampling).  Float atomics reorder the sums, so the tolerance is
+    f32-accumulation level."""
     from frcnn_amd import ops
-    ops.ROI_ALIGN_BWD['mode'] = mode
     if case == 'small' or case == 'adaptive':
         grids, scales, C, K, L = [(38, 64), (19, 32)], [1 / 16, 1 / 32], 16, 120, 2
     else:
         grids, scales, C, K, L = [(152, 256), (76, 128)], [1 / 4, 1 / 8], 80, 300, 2
     sr = 0 if case == 'adaptive' else 2
+    ph, pw = (9, 7) if case == 'bins9x7' else (7, 7)
     feats = inputs.feature_maps(60, grids, C, 2)
     rois = _rois(61, K, 2)
     levels = oracle.roi_level_map(rois, 56.0, L)
-    g = np.random.default_rng(62).standard_normal((K, C, 7, 7)).astype(np.float32)
+    g = np.random.default_rng(62).standard_normal((K, C, ph, pw)).astype(np.float32)
     ft = [T(f, dev) for f in feats]
     if case == 'p2_nhwc':
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
     ft = [f.requires_grad_(True) for f in ft]
-    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), sr)
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (ph, pw), sr)
     out.backward(T(g, dev))
-    ops.ROI_ALIGN_BWD['mode'] = 'atomic'
+    if case == 'p2_nhwc':
+        assert all(f.grad.stride(1) == 1 for f in ft)  # the gradient keeps the features' format
     ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, sr)
     for a, r in zip(ft, ref):
         np.testing.assert_allclose(a.grad.cpu().numpy(), r, rtol=1e-4, atol=2e-5)

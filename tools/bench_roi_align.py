@@ -5,10 +5,11 @@ Prints per-variant average launch time (HIP events), algorithmic GB/s (SURVEY §
 bytes) and the max |difference| to variant 0."""
 import argparse, ctypes, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+sys.path[:0] = [os.path.join(REPO, 'tools'), REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
 import numpy as np, torch
 import bench
-from frcnn_amd import ops, _lib, set_sampler_mode
+from frcnn_amd import ops, _lib, set_sampler_mode  # noqa: E402
+import toolslib  # noqa: E402
 
 
 def calibrate(variants, dev, small=False):
@@ -19,7 +20,7 @@ def calibrate(variants, dev, small=False):
     each plane's 3364 B), exactly once.  small=True: a 12x12 map of 262144 channels (151 MB)
     whose 12x13-float window takes the LDS-staged path of the default kernel; the large map
     takes its block-gather path.  Run under rocprofv3 --pmc FETCH_SIZE."""
-    lib = _lib.load()
+    lib = toolslib.load()
     fn = lib.frh_roi_align_fwd_variant
     C, S = (65536, 29) if small is False else (262144, 12)
     rois = torch.tensor([[0.0, 0.0, 0.0, S - 1.0, S - 1.0]], device=dev)
@@ -73,7 +74,7 @@ def main():
           'side px p10/50/90', np.percentile(side, [10, 50, 90]).round(1).tolist(), 'bytes', nbytes)
     if args.dump:
         np.savez(args.dump, rois=r, levels=lv, shapes=np.array(shapes), scales=np.array(scales))
-    lib = _lib.load()
+    lib = toolslib.load()
     K, C = rois.shape[0], shapes[0][1]
     hw, st = ops._feat_desc(feats)
     outs = {}

@@ -1,21 +1,23 @@
 """Micro-benchmark of the RoIAlign backward kernels on the RoIs of a real cfg2 forward pass.
 
     python tools/bench_roi_bwd.py [--iters 20]
-Times the three backward kernels: frh_roi_align_bwd_strided into a channels_last gradient
-(64-B atomic segments, the default) and into an NCHW one (per-cell atomics), each after
-the gradient clear it needs, and frh_roi_align_bwd_tiled (tile lists + LDS gather), HIP events around back-to-back launches, and prints the
-max |difference| between the two gradients."""
+Times the product backward (frh_roi_align_bwd_strided into an NCHW gradient, separable
+row-run sums) and the tools-library alternatives (frh_roi_align_bwd_cl: channels_last
+gradient with 64-B atomic segments; frh_roi_align_bwd_tiled: tile lists + LDS gather), each
+after the gradient clear it needs, with HIP events around back-to-back launches, and prints
+the max |difference| between the gradients."""
 import argparse
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+sys.path[:0] = [os.path.join(REPO, 'tools'), REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 from frcnn_amd import ops, _lib, set_sampler_mode  # noqa: E402
+import toolslib  # noqa: E402  # noqa: E402
 
 
 def main():
@@ -36,13 +38,13 @@ def main():
     grads['channels_last'] = [torch.empty(s, device=dev, memory_format=torch.channels_last) for s in shapes]
     hw_cl, st_cl = ops._feat_desc(grads['channels_last'])
     hw, st = ops._feat_desc(grads['tiled'])
-    wsb = _lib.query('frh_roi_align_bwd_workspace', len(shapes), hw, B, K)
+    wsb = toolslib.load().frh_roi_align_bwd_workspace(len(shapes), hw, B, K)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     stream = _lib.stream_of(g)
 
     def tiled():
         gr = grads['tiled']
-        _lib.call('frh_roi_align_bwd_tiled', len(gr), _lib.ptr_array(gr), hw, st, _lib.f32_array(scales), B, C,
+        toolslib.call('frh_roi_align_bwd_tiled', len(gr), _lib.ptr_array(gr), hw, st, _lib.f32_array(scales), B, C,
                   _lib.ptr(rois), _lib.ptr(levels), K, ph, pw, sr, 0, _lib.ptr(g), _lib.ptr(ws), wsb, stream)
 
     def atomic():
@@ -56,7 +58,7 @@ def main():
         gr = grads['channels_last']
         for t in gr:
             t.zero_()
-        _lib.call('frh_roi_align_bwd_strided', len(gr), _lib.ptr_array(gr), hw_cl, st_cl, _lib.f32_array(scales), B,
+        toolslib.call('frh_roi_align_bwd_cl', len(gr), _lib.ptr_array(gr), hw_cl, st_cl, _lib.f32_array(scales), B,
                   C, _lib.ptr(rois), _lib.ptr(levels), K, ph, pw, sr, 0, _lib.ptr(g), stream)
 
     print('rois', K, 'level hist', np.bincount(levels.cpu().numpy(), minlength=len(shapes)).tolist(), flush=True)

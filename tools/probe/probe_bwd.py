@@ -8,10 +8,11 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd'), os.path.join(REPO, 'tools', 'probe')]
+sys.path[:0] = [os.path.join(REPO, 'tools'), REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd'), os.path.join(REPO, 'tools', 'probe')]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from frcnn_amd import ops, _lib  # noqa: E402
+from frcnn_amd import ops, _lib
+import toolslib  # noqa: E402
 from probe_roi import timeit  # noqa: E402
 
 
@@ -28,7 +29,7 @@ def main():
     rois = torch.from_numpy(r5).to(dev)
     levels = torch.from_numpy(lv).to(dev)
     K, B, C = rois.shape[0], shapes[0][0], shapes[0][1]
-    lib = _lib.load()
+    lib = toolslib.load()
     gout = torch.randn(K, C, 7, 7, device=dev)
     g_ref = [torch.empty(s, device=dev) for s in shapes]
     g_sw = [torch.full(s, float('nan'), device=dev) for s in shapes]

@@ -12,10 +12,11 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+sys.path[:0] = [os.path.join(REPO, 'tools'), REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from frcnn_amd import ops, _lib  # noqa: E402
+from frcnn_amd import ops, _lib
+import toolslib  # noqa: E402
 
 
 def timeit(fn, iters=30, warm=5):
@@ -40,7 +41,7 @@ def main():
     levels = torch.from_numpy(z['lv'].astype(np.int64)).to(dev)
     scales = [float(s) for s in z['scales']]
     K, C = rois.shape[0], shapes[0][1]
-    lib = _lib.load()
+    lib = toolslib.load()
     hw, st = ops._feat_desc(feats)
     feat_bytes = sum(f.numel() * 4 for f in feats)
     out_bytes = K * C * 49 * 4

@@ -3,9 +3,10 @@ Isolates the per-RoI kernel's cost structure: small vs large windows, repeated
 (L2-hot) RoIs, spatial order."""
 import ctypes, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+sys.path[:0] = [os.path.join(REPO, 'tools'), REPO, os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
 import numpy as np, torch
 from frcnn_amd import ops, _lib
+import toolslib
 
 
 def timeit(fn, iters=30, warm=5):
@@ -39,7 +40,7 @@ def main():
     scales = [float(s) for s in z['scales']]
     r5, lv = z['r5'], z['lv'].astype(np.int64)
     C = shapes[0][1]
-    lib = _lib.load()
+    lib = toolslib.load()
     hw, st = ops._feat_desc(feats)
     area = window_area(r5, lv, shapes, scales)
     sets = {'all': np.arange(len(r5)), 'small<=256': np.nonzero(area <= 256)[0], 'large>256': np.nonzero(area > 256)[0]}
