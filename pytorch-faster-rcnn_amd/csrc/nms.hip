@@ -185,29 +185,50 @@ __device__ __forceinline__ void wait_vmcnt_atmost(int n) {
 
 // Scan, one 256-thread workgroup per segment: wave 0 resolves, waves 1..3 stage.
 //
-//  Staging (wave 1 + (b % 3) stages block b): the span of tiles (j, b), j in
-//  [j0, b], j0 = max(0, b - kNmsSpan + 1), contiguous in the mask, is copied by
-//  16-B LDS-DMA into ring slot b % kNmsRing.  A loader first waits until the
-//  resolver has finished block b - kNmsRing (the slot's previous user), issues
-//  the copies, and keeps up to two of its blocks in flight: when a third is
-//  issued, a counted vmcnt wait retires the oldest, which is then published
-//  (ready[slot] = block + 1).  Three loaders, each with its own vmcnt counter,
-//  keep up to six blocks in flight.
-//  Resolver, block b: waits ready[b % kNmsRing] == b + 1 (acquire), then
-//    acc = OR_j (tile(j, b)[lane] & kept[j]) over j < b  (LDS; global for j < j0)
+//  Loader (wave 1 + (b % 3) owns block b):
+//   (1) once the ring slot b % kNmsRing is free (the resolver has finished block
+//       b - kNmsRing), copies the column span of tiles (j, b), j in [j0, b],
+//       j0 = max(0, b - kNmsSpan + 1) (contiguous in the mask) into the slot by
+//       16-B LDS-DMA;
+//   (2) one block later (after issuing its next block's copies, so the copies
+//       overlap), waits for these copies (counted vmcnt) and for the resolver to
+//       have finished block b - 3, and folds the kept rows of blocks j <= b - 3
+//       into the slot's partial word: lane c = OR_j (tile(j, b)[c] & kept[j])
+//       (LDS; tiles j < j0 from global memory);
+//   (3) publishes ready[slot] = b + 1.
+//  Resolver, block b: waits ready[b % kNmsRing] == b + 1, then
+//    acc = partial | (tile(b-2, b) & kept[b-2]) | (tile(b-1, b) & kept[b-1])
+//  -- the last two blocks' kept sets are in its own scalar registers --,
 //    suppressed = ballot(acc != 0) | past-the-end columns,
 //  resolves the 64 candidates with the diagonal tile (b, b) in bit-parallel
 //  rounds (an undecided candidate with no undecided suppressor before it is kept,
 //  its victims dropped; same keep set as the one-by-one greedy, rounds =
-//  suppression-chain depth), stores the kept indices, kept[b] = kb (LDS, read by
-//  itself only) and s_resolved = b + 1 (release).
-//  No wave waits on a counter that its waiter must advance first: loaders wait
-//  on the resolver (slot reuse), the resolver on the loaders (ready flags), and
-//  a slot is reused only kNmsRing blocks later.  A max_keep stop sets s_stop and
-//  advances s_resolved past the end so every loader exits.
+//  suppression-chain depth), stores the kept indices and kept[b] (LDS), then
+//  publishes s_resolved = b + 1.
+// Ordering.  All flags and shared data are in LDS, which one CU serves in order:
+//  a flag store issued after a wave's LDS writes (or after the counted vmcnt wait
+//  that shows its LDS-DMA copies landed) is observed after them, so plain
+//  (relaxed) flag stores behind an `s_waitcnt lgkmcnt(0)` / vmcnt wait suffice, and
+//  no release fence waits for the keep-list stores to global memory.
+// Progress.  The resolver waits on ready[b], which needs the resolver at b - 3
+//  (two blocks of slack for the loader's fold) and the slot at b - kNmsRing; a
+//  loader waits only on s_resolved.  Every counter advances unconditionally, and a
+//  max_keep stop sets s_stop and pushes s_resolved past the end so every loader exits.
+#ifdef FRH_NMS_TIMELINE  // tools-only build (tools/csrc/nms_timeline.hip): per-block resolver stamps
+__device__ uint64_t* g_nms_tl;
+#define NMS_STAMP(b, k) \
+  if (g_nms_tl && lane == 0) g_nms_tl[((int64_t)s * kMaxNmsWords + (b)) * 8 + (k)] = wall_clock64()
+#else
+#define NMS_STAMP(b, k)
+#endif
 constexpr int kNmsRing = 8;
 constexpr int kNmsSpan = 32;     // tiles per staged span (segments up to 2048 boxes fully staged)
 constexpr int kNmsLoaders = 3;
+
+__device__ __forceinline__ void lds_flag(int* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restrict__ mask,
                                                        const int32_t* __restrict__ counts, int nbw, int span,
@@ -215,6 +236,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
                                                        int32_t* __restrict__ kcounts) {
   extern __shared__ __attribute__((aligned(16))) uint64_t nms_lds[];
   __shared__ uint64_t kept[kMaxNmsWords];
+  __shared__ uint64_t partial[kNmsRing][kWave];
   __shared__ int ready[kNmsRing];
   __shared__ int s_resolved, s_stop;
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
@@ -227,29 +249,25 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   }
   __syncthreads();
   const int slot_words = ((span + 1) & ~1) * 64;  // whole 1 KB copies: an even number of tiles
+  auto tile = [&](const uint64_t* slot, int j0, int j, int b) {
+    return j >= j0 ? slot[(j - j0) * 64 + lane] : mask[tile_word(s, nbw, j, b) + lane];
+  };
   if (wave == 0) {
     int32_t* K = keep + (int64_t)s * kstride;
     int nk = 0;
-    uint64_t keptv = 0;  // lane j: kept set of block j (j < 64); later blocks in kept[]
-    auto kept_at = [&](int j) { return j < 64 ? readlane64(keptv, j) : kept[j]; };
+    uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
     for (int b = 0; b < nb; ++b) {
+      NMS_STAMP(b, 0);
       while (lds_acquire(&ready[b % kNmsRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
+      NMS_STAMP(b, 1);
       const uint64_t* slot = nms_lds + (b % kNmsRing) * slot_words;
       const int j0 = max(0, b - span + 1);
-      uint64_t acc = 0;
-      for (int j = 0; j < j0; ++j) acc |= mask[tile_word(s, nbw, j, b) + lane] & kept_at(j);
-      // eight staged words per batch: their LDS reads overlap
-      int j = j0;
-      for (; j + 8 <= b; j += 8) {
-        uint64_t t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = slot[(j + u - j0) * 64 + lane];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc |= t[u] & kept_at(j + u);
-      }
-      for (; j < b; ++j) acc |= slot[(j - j0) * 64 + lane] & kept_at(j);
+      uint64_t acc = partial[b % kNmsRing][lane];
+      if (b >= 1) acc |= tile(slot, j0, b - 1, b) & kb1;
+      if (b >= 2) acc |= tile(slot, j0, b - 2, b) & kb2;
       const uint64_t d = slot[(b - j0) * 64 + lane];
       uint64_t r = __ballot(acc != 0ull);
+      NMS_STAMP(b, 2);
       const int valid = n - b * 64;
       if (valid < 64) r |= (~0ull) << valid;
       uint64_t kb = 0, und = ~r;
@@ -260,6 +278,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
         const uint64_t vic = __ballot((d & nkp) != 0ull);
         und &= ~(nkp | vic);
       }
+      NMS_STAMP(b, 3);
       bool stop = false;
       if (max_keep >= 0) {
         const int room = max_keep - nk;
@@ -268,16 +287,14 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       }
       if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
       nk += __popcll(kb);
-      if (b < 64) keptv = lane == b ? kb : keptv;
+      kb2 = kb1;
+      kb1 = kb;
       if (lane == 0) {
         kept[b] = kb;
         if (stop) s_stop = b;
-        // the loaders only need this wave's LDS reads of the slot done, not the keep-list
-        // stores to global memory that a release fence would also wait for
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __hip_atomic_store(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_flag(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1);
       }
+      NMS_STAMP(b, 4);
       if (stop) break;
     }
     if (lane == 0) kcounts[s] = nk;
@@ -286,15 +303,29 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
     const int64_t seg_words = (int64_t)nbw * nbw * 64;
     const __amdgpu_buffer_rsrc_t mr = uniform_rsrc(mask + s * seg_words, seg_words * 8);
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint64_t*)nms_lds);
-    // up to two blocks of this loader in flight; a block is published once a counted
-    // vmcnt wait shows its copies landed (LDS-DMA writes are complete in LDS then, and
-    // the flag store goes through the same LDS after them: no fence, which would also
-    // wait for the younger copies)
-    int q0 = -1, q1 = -1, n1 = 0;
-    auto publish = [&](int blk) {  // after a vmcnt wait that covers blk's copies
-      asm volatile("" ::: "memory");
-      if (lane == 0) __hip_atomic_store(&ready[blk % kNmsRing], blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto finish = [&](int p) {  // fold the kept rows of blocks <= p - 3 into p's partial word, publish p
+      while (lds_acquire(&s_resolved) < p - 2) __builtin_amdgcn_s_sleep(1);
+      if (s_stop < p) return;
+      const uint64_t* slot = nms_lds + (p % kNmsRing) * slot_words;
+      const int j0 = max(0, p - span + 1);
+      uint64_t acc = 0;
+      int j = 0;
+      for (; j < j0 && j + 2 < p; ++j) acc |= mask[tile_word(s, nbw, j, p) + lane] & kept[j];
+      for (; j + 8 <= p - 2; j += 8) {  // eight words per batch: their LDS reads overlap
+        uint64_t t[8], k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          t[u] = slot[(j + u - j0) * 64 + lane];
+          k[u] = kept[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc |= t[u] & k[u];
+      }
+      for (; j < p - 2; ++j) acc |= slot[(j - j0) * 64 + lane] & kept[j];
+      partial[p % kNmsRing][lane] = acc;
+      if (lane == 0) lds_flag(&ready[p % kNmsRing], p + 1);
     };
+    int prev = -1;
     for (int b = wave - 1; b < nb; b += kNmsLoaders) {
       while (lds_acquire(&s_resolved) < b - kNmsRing + 1) __builtin_amdgcn_s_sleep(1);
       if (s_stop < b) break;
@@ -303,22 +334,16 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       const uint32_t dst = lds0 + (uint32_t)((b % kNmsRing) * slot_words * 8);
       const int src = (int)((tile_word(s, nbw, j0, b) - s * seg_words) * 8);
       for (int k = 0; k < ninst; ++k) lds_dma_at<16>(mr, dst + (uint32_t)k * 1024u, lane * 16, src + k * 1024);
-      if (q1 >= 0) {  // three in flight: retire the oldest
-        wait_vmcnt_atmost(n1 + ninst);
-        publish(q0);
-        q0 = q1;
-        q1 = b;
-        n1 = ninst;
-      } else if (q0 >= 0) {
-        q1 = b;
-        n1 = ninst;
-      } else {
-        q0 = b;
+      if (prev >= 0) {
+        wait_vmcnt_atmost(ninst);  // prev's copies are older than these ninst
+        asm volatile("" ::: "memory");
+        finish(prev);
       }
+      prev = b;
     }
     wait_vmcnt<0>();
-    if (q0 >= 0) publish(q0);
-    if (q1 >= 0) publish(q1);
+    asm volatile("" ::: "memory");
+    if (prev >= 0 && !(s_stop < prev)) finish(prev);
   }
 }
 

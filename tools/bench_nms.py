@@ -6,7 +6,7 @@ deltas, random scores, sorted per segment; IoU threshold 0.7 (RPN).  Times one
 nms_sorted call (mask + pipelined scan) with HIP events."""
 import argparse, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, 'pytorch-faster-rcnn_amd')]
+sys.path[:0] = [os.path.join(REPO, 'pytorch-faster-rcnn_amd'), os.path.join(REPO, 'tools')]
 import numpy as np, torch
 from frcnn_amd import ops
 
@@ -31,6 +31,7 @@ def main():
     ap.add_argument('--n', type=int, default=2000)
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--thr', type=float, default=0.7)
+    ap.add_argument('--timeline', action='store_true', help='per-block resolver stamps (tools library)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     boxes = torch.from_numpy(make(a.segs, a.n)).to(dev)
@@ -46,6 +47,31 @@ def main():
     torch.cuda.synchronize()
     print('{:.1f} us per nms_sorted (mask + scan), kept {}'.format(e0.elapsed_time(e1) / a.iters * 1e3, kc.tolist()),
           flush=True)
+    if a.timeline:
+        import ctypes
+        import numpy as np
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import toolslib
+        from frcnn_amd import _lib
+        lib = toolslib.load()
+        stamps = torch.zeros(a.segs * 256 * 8, dtype=torch.int64, device=dev)
+        wsb = int(lib.frh_tl_nms_workspace(a.segs, a.n))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        kp = torch.empty(a.segs, a.n, dtype=torch.int32, device=dev)
+        kc2 = torch.empty(a.segs, dtype=torch.int32, device=dev)
+        for on in (False, True):
+            assert lib.frh_tl_nms_timeline(ctypes.c_void_p(stamps.data_ptr() if on else 0)) == 0
+            toolslib.call('frh_tl_nms_sorted', a.segs, _lib.ptr(boxes), a.n * 4, _lib.ptr(counts), a.n, a.thr, -1,
+                          _lib.ptr(kp), a.n, _lib.ptr(kc2), _lib.ptr(ws), wsb, _lib.stream_of(boxes))
+            torch.cuda.synchronize()
+        lib.frh_tl_nms_timeline(ctypes.c_void_p(0))
+        assert torch.equal(kc2, kc)
+        t = stamps.view(a.segs, 256, 8).cpu().numpy().astype(np.int64)
+        nb = (a.n + 63) // 64
+        print('segment 0 resolver, ticks of 10 ns: block, start, ready-wait, span OR, rounds, keep-list + publish')
+        for b in range(nb):
+            r = t[0, b]
+            print(b, r[0] - t[0, 0, 0], r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4] - r[3], flush=True)
 
 if __name__ == '__main__':
     main()

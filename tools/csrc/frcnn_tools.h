@@ -83,6 +83,15 @@ int32_t frh_roi_align_bwd_cl(int32_t num_levels, float* const* grad_feats, const
                              int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
                              const float* grad_out, void* stream);
 
+/* The product NMS rebuilt with per-block resolver timestamps (tools/csrc/nms_timeline.hip):
+ * same arguments as frh_nms_workspace / frh_nms_sorted; frh_tl_nms_timeline sets the
+ * stamp buffer (uint64 [S][256][8] wall_clock64 ticks, nullptr = off). */
+size_t frh_tl_nms_workspace(int32_t num_segs, int32_t n_max);
+int32_t frh_tl_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
+                          int32_t n_max, double iou_thr, int32_t max_keep, int32_t* keep, int64_t keep_seg_stride,
+                          int32_t* keep_counts, void* workspace, size_t ws_bytes, void* stream);
+int32_t frh_tl_nms_timeline(void* stamps);
+
 #ifdef __cplusplus
 }
 #endif

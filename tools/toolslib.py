@@ -23,6 +23,10 @@ TOOL_SIGNATURES = {
     'frh_roi_align_bwd_workspace': (c_size, [c_i32, P(c_i32), c_i32, c_i64]),
     'frh_roi_align_bwd_tiled': (c_i32, _RA + [c_vp, c_vp, c_size, c_vp]),
     'frh_roi_align_bwd_cl': (c_i32, _RA + [c_vp, c_vp]),
+    'frh_tl_nms_workspace': (c_size, [c_i32, c_i32]),
+    'frh_tl_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, _lib.c_f64, c_i32, c_vp, c_i64, c_vp, c_vp,
+                                  c_size, c_vp]),
+    'frh_tl_nms_timeline': (c_i32, [c_vp]),
 }
 _lib_t = None
 
