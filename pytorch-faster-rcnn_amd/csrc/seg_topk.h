@@ -5,15 +5,22 @@
 // workgroup per segment (block_topk_select) reads every key once per radix
 // byte from one CU; here every pass is spread over the whole chip:
 //   hist1   : 4096-bin histogram of key[31:20] per segment (LDS, flushed with
-//             global atomics), all chunks of all segments in one grid
-//   find1   : one wave per segment suffix-scans the histogram -> bucket b1,
-//             remaining slots k1 (also decides "take everything" when n <= k)
-//   hist2   : histogram of key[19:8] for keys in bucket b1
+//             global atomics), all chunks of all segments in one grid; the
+//             last workgroup of a segment to finish (done counter) then runs
+//   find1   : a suffix scan of the histogram -> bucket b1, remaining slots k1
+//             (also decides "take everything" when n <= k), and clears the
+//             histogram for
+//   hist2   : histogram of key[19:8] for keys in bucket b1, whose last
+//             workgroup per segment runs
 //   find2   : bucket b2, remaining slots k2  (prefix P = b1:b2, 24 bits)
-//   collect : keys with key>>8 > P are selected (atomic append, unordered);
-//             keys with key>>8 == P become candidates
+//   collect : keys with key>>8 > P are selected, keys with key>>8 == P become
+//             candidates (appends aggregated per wave: one atomic per wave)
 //   final   : one workgroup per segment sorts the candidates by
 //             (key desc, index asc) and appends the first k2.
+// Four launches per selection.  The last-workgroup hand-off reads the histogram
+// with atomic read-modify-writes (performed at the memory side, like the flush
+// atomics it reads), after every wave's flush atomics have completed (vmcnt(0))
+// and a barrier, so no cross-XCD cache state is involved.
 // Result: out[v][0..k_v) = indices of the k_v largest keys, ties broken by
 // lowest index, in no particular order.  Key 0 means "not a candidate".
 #pragma once
@@ -29,7 +36,7 @@ constexpr int kTkCandCap = 8192;  // candidates sorted in LDS; more -> radix fal
 
 // per-segment state words
 enum { TK_N = 0, TK_K = 1, TK_ALL = 2, TK_B1 = 3, TK_K1 = 4, TK_B2 = 5, TK_K2 = 6, TK_OUT = 7, TK_CAND = 8,
-       TK_WORDS = 16 };
+       TK_DONE0 = 9, TK_DONE1 = 10, TK_WORDS = 16 };
 
 struct TopkBuffers {
   const uint32_t* keys;  // [V][ld]
@@ -46,67 +53,34 @@ struct TopkBuffers {
 // header gets its own copy (no cross-TU device symbols)
 namespace {
 
-__global__ void __launch_bounds__(kTkThreads) tk_hist_kernel(TopkBuffers b, int pass) {
-  __shared__ uint32_t h[kTkBins];
-  const int v = blockIdx.y;
-  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
-  const int32_t* st = b.state + v * TK_WORDS;
-  const int n = st[TK_N];
-  if (base >= n) return;
-  if (pass == 1 && st[TK_ALL]) return;
-  for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) h[i] = 0;
-  __syncthreads();
-  const uint32_t* kk = b.keys + (int64_t)v * b.ld;
-  const uint32_t b1 = (uint32_t)st[TK_B1];
-#pragma unroll 4
-  for (int r = 0; r < kTkPerThread; ++r) {
-    int64_t i = base + r * kTkThreads + threadIdx.x;
-    if (i < n) {
-      uint32_t key = kk[i];
-      if (key) {
-        if (pass == 0)
-          atomicAdd(&h[key >> 20], 1u);
-        else if ((key >> 20) == b1)
-          atomicAdd(&h[(key >> 8) & 0xfffu], 1u);
-      }
-    }
+// The find step of pass `pass` for segment v, run by one whole 256-thread workgroup:
+// suffix scan of the histogram from the highest bin; bucket where the running count
+// reaches the remaining slots.  `rd(i)` reads bin i.
+template <class Rd>
+__device__ __forceinline__ void tk_find(int32_t* st, int pass, Rd rd, int* part, int* sel_bin, int* sel_above) {
+  const int t = threadIdx.x;
+  int bins[16];
+  const int hi = kTkBins - 16 * t;  // thread t owns bins [4096 - 16(t+1), 4096 - 16t) (descending order)
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    bins[i] = rd(hi - 1 - i);
+    s += bins[i];
   }
-  __syncthreads();
-  uint32_t* gh = b.hist + (int64_t)v * kTkBins;
-  for (int i = threadIdx.x; i < kTkBins; i += kTkThreads)
-    if (h[i]) atomicAdd(&gh[i], h[i]);
-}
-
-// one 256-thread block per segment: suffix scan of the histogram from the
-// highest bin; bucket where the running count reaches the remaining slots.
-__global__ void __launch_bounds__(256) tk_find_kernel(TopkBuffers b, int pass) {
-  __shared__ int part[256];
-  __shared__ int sel_bin, sel_above;
-  const int v = blockIdx.x;
-  int32_t* st = b.state + v * TK_WORDS;
-  if (pass == 0) {
-    // total candidates = sum of the histogram
-    int s = 0;
-    const uint32_t* gh = b.hist + (int64_t)v * kTkBins;
-    for (int i = threadIdx.x; i < kTkBins; i += 256) s += (int)gh[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int t = 0;
-      for (int i = 0; i < 256; ++i) t += part[i];
-      st[TK_ALL] = (t <= st[TK_K]) ? 1 : 0;
-      if (st[TK_K] > t) st[TK_K] = t;
+  if (pass == 0) {  // total candidates = sum of the histogram
+    const int tot = block_sum(s, part);
+    if (t == 0) {
+      st[TK_ALL] = (tot <= st[TK_K]) ? 1 : 0;
+      if (st[TK_K] > tot) st[TK_K] = tot;
       st[TK_OUT] = 0;
       st[TK_CAND] = 0;
     }
     __syncthreads();
     if (st[TK_ALL]) return;
-  } else if (st[TK_ALL]) {
-    return;
   }
   const int krem = pass == 0 ? st[TK_K] : st[TK_K1];
   if (krem <= 0) {  // nothing (more) to select: a prefix no key can exceed, zero slots
-    if (threadIdx.x == 0) {
+    if (t == 0) {
       st[pass == 0 ? TK_B1 : TK_B2] = kTkBins - 1;
       st[pass == 0 ? TK_K1 : TK_K2] = 0;
       if (pass == 0) {
@@ -116,41 +90,96 @@ __global__ void __launch_bounds__(256) tk_find_kernel(TopkBuffers b, int pass) {
     }
     return;
   }
-  const uint32_t* gh = b.hist + (int64_t)v * kTkBins;
-  // thread t owns bins [4096 - 16(t+1), 4096 - 16t) (descending order)
-  const int hi = kTkBins - 16 * threadIdx.x;
-  int s = 0;
-  for (int i = hi - 1; i >= hi - 16; --i) s += (int)gh[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    int x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += x;
-    __syncthreads();
+  // inclusive prefix over threads (descending bin order): wave scans + wave totals
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if ((t & (kWave - 1)) >= o) incl += x;
   }
-  int run = part[threadIdx.x] - s;  // count in bins above my range
-  if (run < krem && part[threadIdx.x] >= krem) {
-    for (int i = hi - 1; i >= hi - 16; --i) {
-      int c = (int)gh[i];
-      if (run + c >= krem) {
-        sel_bin = i;
-        sel_above = run;
+  const int w = t / kWave;
+  if ((t & (kWave - 1)) == kWave - 1) part[w] = incl;
+  __syncthreads();
+  for (int i = 0; i < w; ++i) incl += part[i];
+  int run = incl - s;  // count in bins above my range
+  if (run < krem && incl >= krem) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (run + bins[i] >= krem) {
+        *sel_bin = hi - 1 - i;
+        *sel_above = run;
         break;
       }
-      run += c;
+      run += bins[i];
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     if (pass == 0) {
-      st[TK_B1] = sel_bin;
-      st[TK_K1] = krem - sel_above;
+      st[TK_B1] = *sel_bin;
+      st[TK_K1] = krem - *sel_above;
     } else {
-      st[TK_B2] = sel_bin;
-      st[TK_K2] = krem - sel_above;
+      st[TK_B2] = *sel_bin;
+      st[TK_K2] = krem - *sel_above;
     }
   }
+}
+
+// histogram pass + (last workgroup of the segment) the find step
+__global__ void __launch_bounds__(kTkThreads) tk_hist_kernel(TopkBuffers b, int pass) {
+  __shared__ uint32_t h[kTkBins];
+  __shared__ int part[kTkThreads / kWave];
+  __shared__ int last, sel_bin, sel_above;
+  const int v = blockIdx.y;
+  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
+  int32_t* st = b.state + v * TK_WORDS;
+  const int n = st[TK_N];
+  if (pass == 1 && st[TK_ALL]) return;  // uniform per segment: no find either
+  uint32_t* gh = b.hist + (int64_t)v * kTkBins;
+  if (base < n) {
+    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) h[i] = 0;
+    __syncthreads();
+    const uint32_t* kk = b.keys + (int64_t)v * b.ld;
+    const uint32_t b1 = (uint32_t)st[TK_B1];
+#pragma unroll 4
+    for (int r = 0; r < kTkPerThread; ++r) {
+      int64_t i = base + r * kTkThreads + threadIdx.x;
+      if (i < n) {
+        uint32_t key = kk[i];
+        if (key) {
+          if (pass == 0)
+            atomicAdd(&h[key >> 20], 1u);
+          else if ((key >> 20) == b1)
+            atomicAdd(&h[(key >> 8) & 0xfffu], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads)
+      if (h[i]) atomicAdd(&gh[i], h[i]);
+  }
+  // every workgroup of the segment checks in once its flush atomics have completed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&st[pass == 0 ? TK_DONE0 : TK_DONE1], 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  tk_find(st, pass, [&](int i) { return (int)atomicAdd(&gh[i], 0u); }, part, &sel_bin, &sel_above);
+  if (pass == 0) {  // clear for pass 2 (read in the next launch)
+    __syncthreads();
+    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) gh[i] = 0;
+  }
+}
+
+// wave-aggregated append: every lane with `take` gets a distinct slot of `list`
+__device__ __forceinline__ int wave_append(bool take, int* counter) {
+  const uint64_t m = __ballot(take);
+  if (!m) return -1;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if ((int)(threadIdx.x & (kWave - 1)) == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader, kWave);
+  return take ? base + __popcll(m & lanemask_lt()) : -1;
 }
 
 __global__ void __launch_bounds__(kTkThreads) tk_collect_kernel(TopkBuffers b) {
@@ -165,21 +194,15 @@ __global__ void __launch_bounds__(kTkThreads) tk_collect_kernel(TopkBuffers b) {
   int32_t* out = b.out + (int64_t)v * b.out_ld;
   int32_t* cand = b.cand + (int64_t)v * kTkCandCap;
   for (int r = 0; r < kTkPerThread; ++r) {
-    int64_t i = base + r * kTkThreads + threadIdx.x;
-    if (i >= n) break;
-    uint32_t key = kk[i];
-    if (!key) continue;
-    if (all) {
-      out[atomicAdd(&st[TK_OUT], 1)] = (int32_t)i;
-    } else {
-      uint32_t p = key >> 8;
-      if (p > P) {
-        out[atomicAdd(&st[TK_OUT], 1)] = (int32_t)i;
-      } else if (p == P) {
-        int c = atomicAdd(&st[TK_CAND], 1);
-        if (c < kTkCandCap) cand[c] = (int32_t)i;
-      }
-    }
+    const int64_t i = base + r * kTkThreads + threadIdx.x;
+    if (base + r * kTkThreads >= n) break;  // uniform
+    const uint32_t key = i < n ? kk[i] : 0u;
+    const uint32_t p = key >> 8;
+    const bool sel = key && (all || p > P), cnd = key && !all && p == P;
+    const int o = wave_append(sel, &st[TK_OUT]);
+    if (o >= 0) out[o] = (int32_t)i;
+    const int c = wave_append(cnd, &st[TK_CAND]);
+    if (c >= 0 && c < kTkCandCap) cand[c] = (int32_t)i;
   }
 }
 
@@ -229,15 +252,12 @@ inline size_t tk_state_bytes(int V) { return (size_t)V * TK_WORDS * sizeof(int32
 inline size_t tk_hist_bytes(int V) { return (size_t)V * kTkBins * sizeof(uint32_t); }
 inline size_t tk_cand_bytes(int V) { return (size_t)V * kTkCandCap * sizeof(int32_t); }
 
-// Runs hist/find/collect/final.  The caller has written keys and the TK_N /
+// Runs hist+find (x2), collect, final.  The caller has written keys and the TK_N /
 // TK_K words of state (state's other words and hist must be zero).
 static inline void tk_launch(const TopkBuffers& b, int64_t n_max, hipStream_t st) {
   dim3 grid((unsigned)((n_max + kTkChunk - 1) / kTkChunk), (unsigned)b.V);
   hipLaunchKernelGGL(tk_hist_kernel, grid, dim3(kTkThreads), 0, st, b, 0);
-  hipLaunchKernelGGL(tk_find_kernel, dim3(b.V), dim3(256), 0, st, b, 0);
-  hipMemsetAsync(b.hist, 0, tk_hist_bytes(b.V), st);
   hipLaunchKernelGGL(tk_hist_kernel, grid, dim3(kTkThreads), 0, st, b, 1);
-  hipLaunchKernelGGL(tk_find_kernel, dim3(b.V), dim3(256), 0, st, b, 1);
   hipLaunchKernelGGL(tk_collect_kernel, grid, dim3(kTkThreads), 0, st, b);
   hipLaunchKernelGGL(tk_final_kernel, dim3(b.V), dim3(1024), 0, st, b);
 }
