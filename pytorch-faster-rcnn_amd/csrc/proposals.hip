@@ -2,10 +2,11 @@
 // Reference: lib/heads/rpn_head.py:68-120 (predict_single_image), decode from
 // lib/utils.py:83-144, NMS = torchvision.ops.nms semantics (nms.hip).
 //
-//  1. select  (1 block of 1024 per segment): radix top-k of the scores
-//     (score = sigmoid or 2-way softmax of the logits, recomputed per radix
-//     pass straight from the head output), LDS bitonic sort by
-//     (score desc, index asc), decode + clamp, min-size compaction.
+//  1. keys (score = sigmoid or 2-way softmax of the logits -> ordered u32)
+//     + first-level histogram, then refine + collect (seg_topk.h: one
+//     workgroup per 4096 anchors; a selected anchor is decoded + clamped by
+//     the workgroup that selects it), then rank: each selection's position in
+//     (score desc, index asc) order after the min-size compaction, by counting.
 //  2. NMS mask + scan over all segments (nms.hip), keep <= post_nms.
 //  3. merge   (1 block per image): concatenate the levels' survivors and, if
 //     more than max_num, keep the best max_num by (score desc, concat order).
@@ -35,7 +36,8 @@ struct PropArgs {
   // workspace
   float* sel_boxes;   // [S][P][4]
   float* sel_scores;  // [S][P]
-  int32_t* sel_idx;   // [S][P] scratch for the selection
+  uint64_t* sel_keys;  // [S][P] selection records (RpnPol)
+  float4* stage;       // [S][kRpnSelFused] boxes decoded at selection (fused path)
   int32_t* sel_count; // [S]
 };
 
@@ -44,103 +46,216 @@ struct ImgArgs {
   float min_size[64];
 };
 
-__device__ __forceinline__ float score_of(const float* cls, int64_t hwa, int C, int64_t i) {
-  if (C == 1) {
-    float x = cls[i];
-    return 1.0f / (1.0f + expf(-x));
-  }
-  float x0 = cls[i], x1 = cls[hwa + i];  // softmax over the 2 channels, score = channel 1
+// score from the logit(s) of one anchor: sigmoid, or channel 1 of a 2-way softmax
+__device__ __forceinline__ float score_of2(float x0, float x1, int C) {
+  if (C == 1) return 1.0f / (1.0f + expf(-x0));
   float mx = fmaxf(x0, x1);
   float e0 = expf(x0 - mx), e1 = expf(x1 - mx);
   return e1 / (e0 + e1);
 }
 
-// keys = order-preserving u32 of the score; also seeds the top-k state
-__global__ void rpn_keys_kernel(PropArgs p, uint32_t* keys, int64_t kld, int32_t* state) {
+constexpr int kRpnHistBits = 12;
+constexpr int kRpnSelFused = 2048;  // selections decoded at selection time, ordered by rpn_rank_kernel
+
+// keys = order-preserving u32 of the score (never 0: scores are >= 0) and the
+// first-level top-k histogram of their top 12 bits; also seeds the state words
+// read by the large-k sort kernel.  Grid (chunks of 4096, segments).
+static __global__ void __launch_bounds__(kTkThreads) rpn_keys_kernel(PropArgs p, TkBufs b) {
+  __shared__ uint32_t h[1 << kRpnHistBits];
   const int seg = blockIdx.y;
-  const int b = seg / p.L, l = seg % p.L;
+  const int bi = seg / p.L, l = seg % p.L;
   const int64_t hwa = (int64_t)p.A * p.h[l] * p.w[l];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) {
-    int n = (int)hwa;
-    state[seg * TK_WORDS + TK_N] = n;
-    state[seg * TK_WORDS + TK_K] = (p.pre_nms > 0 && p.pre_nms < n) ? p.pre_nms : n;
+  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int n = (int)hwa;
+    b.state[seg * TK_WORDS + TK_N] = n;
+    b.state[seg * TK_WORDS + TK_K] = (p.pre_nms > 0 && p.pre_nms < n) ? p.pre_nms : n;
   }
-  if (i >= hwa) return;
-  const float* cls = p.cls[l] + (int64_t)b * p.C * hwa;
-  keys[(int64_t)seg * kld + i] = float_key(score_of(cls, hwa, p.C, i));
+  if (base >= hwa) return;
+  tk_hist1_clear(h, 1 << kRpnHistBits);
+  const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
+  uint32_t* kk = const_cast<uint32_t*>(b.keys) + (int64_t)seg * b.ld;
+  float x0[kTkPerThread], x1[kTkPerThread];  // every logit load in flight at once
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int64_t i = base + r * kTkThreads + threadIdx.x;
+    x0[r] = i < hwa ? cls[i] : 0.0f;
+    x1[r] = (p.C == 2 && i < hwa) ? cls[hwa + i] : 0.0f;
+  }
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int64_t i = base + r * kTkThreads + threadIdx.x;
+    uint32_t key = 0u;
+    if (i < hwa) {
+      key = float_key(score_of2(x0[r], x1[r], p.C));
+      kk[i] = key;
+    }
+    tk_hist_add(h, i < hwa, key >> (32 - kRpnHistBits));
+  }
+  tk_hist1_flush(h, 1 << kRpnHistBits, b.hist1 + (int64_t)seg * (1 << kRpnHistBits));
 }
 
-// one 1024-thread block per segment: order the selected anchors by
-// (score desc, index asc), decode + clamp, min-size filter (order preserving)
-__global__ void __launch_bounds__(kPropThreads) rpn_sort_decode_kernel(PropArgs p, ImgArgs ia, const uint32_t* keys,
-                                                                       int64_t kld, const int32_t* state,
-                                                                       const int32_t* sel, int64_t sel_ld) {
-  extern __shared__ uint64_t skeys[];
-  __shared__ int wave_tot[kPropThreads / 64];
-  const int seg = blockIdx.x;
+// Decode + clamp of anchor i of segment seg (utils.py:83-144).
+__device__ __forceinline__ float4 rpn_decode_one(const PropArgs& p, const ImgArgs& ia, int seg, int i) {
   const int b = seg / p.L, l = seg % p.L;
   const int64_t hwa = (int64_t)p.A * p.h[l] * p.w[l];
   const float* reg = p.reg[l] + (int64_t)b * 4 * hwa;
+  const float img_h = ia.hw[2 * b], img_w = ia.hw[2 * b + 1];
+  const int64_t ai = p.off[l] + i;
+  const float* an = p.anchors;
+  const int64_t ld = p.anchor_ld;
+  float ax1 = an[ai], ay1 = an[ld + ai], ax2 = an[2 * ld + ai], ay2 = an[3 * ld + ai];
+  float tx = reg[i] * p.sd[0] + p.m[0];
+  float ty = reg[hwa + i] * p.sd[1] + p.m[1];
+  float tw = reg[2 * hwa + i] * p.sd[2] + p.m[2];
+  float th = reg[3 * hwa + i] * p.sd[3] + p.m[3];
+  float bw = (ax2 - ax1) + 1.0f, bh = (ay2 - ay1) + 1.0f;
+  float bcx = (ax2 + ax1) / 2.0f, bcy = (ay2 + ay1) / 2.0f;
+  float cx = tx * bw + bcx, cy = ty * bh + bcy;
+  float ww = expf(tw) * bw, hh = expf(th) * bh;
+  float hw2 = ww / 2.0f, hh2 = hh / 2.0f;
+  float v[4] = {cx - hw2, cy - hh2, cx + hw2, cy + hh2};
+  float hi[4] = {img_w - 1.0f, img_h - 1.0f, img_w - 1.0f, img_h - 1.0f};
+  float box[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float y = (v[q] < 0.0f) ? 0.0f : v[q];
+    box[q] = (y > hi[q]) ? hi[q] : y;
+  }
+  return make_float4(box[0], box[1], box[2], box[3]);
+}
+
+// min-size filter (rpn_head.py:86-90)
+__device__ __forceinline__ bool rpn_big_enough(float4 b, float min_size) {
+  return min_size <= 0.0f || ((((b.z - b.x) + 1.0f) >= min_size) && (((b.w - b.y) + 1.0f) >= min_size));
+}
+
+__device__ __forceinline__ int rpn_k(const PropArgs& p, int n) { return (p.pre_nms > 0 && p.pre_nms < n) ? p.pre_nms : n; }
+
+// RPN policy of the segmented top-k.  Fused (selection <= kRpnSelFused,
+// anchors < 2^20): the workgroup that selects anchor i decodes it at once into
+// stage[slot] and records key << 32 | (~i & 0xfffff) << 12 | big-enough << 11 |
+// slot; rpn_rank_kernel then orders the records.  Otherwise the record is
+// key << 32 | ~i and rpn_sort_decode_kernel follows.  Records and staged boxes
+// cross workgroups and launches (xwg_store, seg_topk.h).
+struct RpnPol {
+  const PropArgs& p;
+  const ImgArgs& ia;
+  const TkBufs& b;
+  int seg;
+  bool fused;
+  __device__ void select(int i, uint32_t key, int slot) {
+    uint64_t* rec = p.sel_keys + (int64_t)seg * p.P + slot;
+    if (!fused) {
+      xwg_store(rec, ((uint64_t)key << 32) | (uint32_t)~(uint32_t)i);
+      return;
+    }
+    const float4 bx = rpn_decode_one(p, ia, seg, i);
+    const bool live = rpn_big_enough(bx, ia.min_size[seg / p.L]);
+    uint64_t* sb = reinterpret_cast<uint64_t*>(p.stage + ((int64_t)seg * kRpnSelFused + slot));
+    xwg_store(sb, ((uint64_t)__float_as_uint(bx.y) << 32) | __float_as_uint(bx.x));
+    xwg_store(sb + 1, ((uint64_t)__float_as_uint(bx.w) << 32) | __float_as_uint(bx.z));
+    xwg_store(rec, ((uint64_t)key << 32) | ((~(uint32_t)i & 0xfffffu) << 12) | (live ? 0x800u : 0u) |
+                       (uint32_t)slot);
+  }
+  __device__ void finish(int kv) {
+    if (threadIdx.x == 0) b.state[seg * TK_WORDS + TK_K] = kv;  // the sort launch's count
+  }
+};
+
+// Fused path, after collect: the order of the kv <= kRpnSelFused records of a
+// segment by (score desc, index asc) without a sort.  Every workgroup holds all
+// records in LDS; 8 threads per record count the big-enough records above it
+// -- its output position after the min-size compaction -- and the first of them
+// moves the staged box and score there.  Grid (kRpnSelFused / 32, segments).
+constexpr int kRankPer = 32;  // records per workgroup
+static __global__ void __launch_bounds__(256) rpn_rank_kernel(PropArgs p, const int32_t* state) {
+  __shared__ uint64_t rec[kRpnSelFused];
+  __shared__ int part[4];
+  const int seg = blockIdx.y, t = threadIdx.x;
+  const int cap = p.P < kRpnSelFused ? p.P : kRpnSelFused;
+  const uint64_t* src = p.sel_keys + (int64_t)seg * p.P;
+  uint64_t r[kRpnSelFused / 256];  // the whole row in flight at once, beside the count
+#pragma unroll
+  for (int e = 0; e < kRpnSelFused / 256; ++e) r[e] = e * 256 + t < cap ? src[e * 256 + t] : 0ull;
+  const int kv = state[seg * TK_WORDS + TK_K];
+#pragma unroll
+  for (int e = 0; e < kRpnSelFused / 256; ++e) rec[e * 256 + t] = e * 256 + t < kv ? r[e] : 0ull;
+  __syncthreads();
+  const int first = blockIdx.x * kRankPer;
+  if (blockIdx.x == 0) {  // the segment's kept count
+    int c = 0;
+    for (int j = t; j < kv; j += 256) c += (int)((rec[j] >> 11) & 1u);
+    c = block_sum(c, part);
+    if (t == 0) p.sel_count[seg] = c;
+  }
+  if (first >= kv) return;
+  const int q = first + (t >> 3), lane8 = t & 7;
+  const uint64_t x = q < kv ? rec[q] : ~0ull;
+  int above = 0;
+  const int kv8 = (kv + 7) & ~7;  // padding records are 0: never above
+#pragma unroll 8
+  for (int j = lane8; j < kv8; j += 8) {
+    const uint64_t y = rec[j];
+    above += (y > x && ((y >> 11) & 1u)) ? 1 : 0;
+  }
+  above += __shfl_xor(above, 1, kWave);
+  above += __shfl_xor(above, 2, kWave);
+  above += __shfl_xor(above, 4, kWave);
+  if (lane8 == 0 && q < kv && ((x >> 11) & 1u)) {
+    const float4 bx = p.stage[(int64_t)seg * kRpnSelFused + (int)(x & 0x7ffu)];
+    reinterpret_cast<float4*>(p.sel_boxes)[(int64_t)seg * p.P + above] = bx;
+    p.sel_scores[(int64_t)seg * p.P + above] = key_float((uint32_t)(x >> 32));
+  }
+}
+
+// Top-k launches: grid (chunks of 4096, segments), 256 threads (seg_topk.h).
+static __global__ void __launch_bounds__(kTkThreads) rpn_refine_kernel(PropArgs p, TkBufs b) {
+  __shared__ TkSmem sm;
+  const int seg = blockIdx.y;
+  const int l = seg % p.L;
+  const int n = p.A * p.h[l] * p.w[l];
+  tk_refine_chunk(b, seg, n, rpn_k(p, n), sm);
+}
+
+static __global__ void __launch_bounds__(kTkThreads) rpn_collect_kernel(PropArgs p, ImgArgs ia, TkBufs b, bool fused) {
+  __shared__ TkSmem sm;
+  const int seg = blockIdx.y;
+  const int l = seg % p.L;
+  const int n = p.A * p.h[l] * p.w[l];
+  RpnPol pol{p, ia, b, seg, fused};
+  tk_collect_chunk(b, seg, n, tk_plan_refined(b, seg), pol, sm);
+}
+
+// ... and one 1024-thread block per segment orders them by (score desc, index
+// asc) in LDS (up to kMaxSort) and decodes
+static __global__ void __launch_bounds__(kPropThreads) rpn_sort_decode_kernel(PropArgs p, ImgArgs ia, const int32_t* state) {
+  extern __shared__ uint64_t skeys[];
+  __shared__ int wave_tot[kPropThreads / 64];
+  const int seg = blockIdx.x;
   const int m = state[seg * TK_WORDS + TK_K];
   const int P2 = next_pow2(m > 1 ? m : 1);
-  const uint32_t* kk = keys + (int64_t)seg * kld;
-  const int32_t* sl = sel + (int64_t)seg * sel_ld;
-  for (int j = threadIdx.x; j < P2; j += blockDim.x) {
-    uint64_t key = 0;
-    if (j < m) {
-      int i = sl[j];
-      key = ((uint64_t)kk[i] << 32) | (uint32_t)(~(uint32_t)i);
-    }
-    skeys[j] = key;
-  }
+  const uint64_t* sl = p.sel_keys + (int64_t)seg * p.P;
+  for (int j = threadIdx.x; j < P2; j += blockDim.x) skeys[j] = j < m ? sl[j] : 0ull;
   __syncthreads();
   block_bitonic_sort_desc(skeys, P2);
-  // decode + clamp + min-size filter, order-preserving compaction
-  const float img_h = ia.hw[2 * b], img_w = ia.hw[2 * b + 1];
-  const float min_size = ia.min_size[b];
+  const float min_size = ia.min_size[seg / p.L];
   float* ob = p.sel_boxes + (int64_t)seg * p.P * 4;
   float* os = p.sel_scores + (int64_t)seg * p.P;
   int written = 0;
   for (int base = 0; base < m; base += blockDim.x) {
-    int j = base + threadIdx.x;
+    const int j = base + threadIdx.x;
     bool live = j < m;
-    float box[4] = {0.f, 0.f, 0.f, 0.f};
-    float score = 0.f;
+    float4 bx = make_float4(0.f, 0.f, 0.f, 0.f);
     if (live) {
-      uint64_t key = skeys[j];
-      int i = (int)(~(uint32_t)key);
-      score = key_float((uint32_t)(key >> 32));
-      int64_t ai = p.off[l] + i;
-      const float* an = p.anchors;
-      const int64_t ld = p.anchor_ld;
-      float ax1 = an[ai], ay1 = an[ld + ai], ax2 = an[2 * ld + ai], ay2 = an[3 * ld + ai];
-      float tx = reg[i] * p.sd[0] + p.m[0];
-      float ty = reg[hwa + i] * p.sd[1] + p.m[1];
-      float tw = reg[2 * hwa + i] * p.sd[2] + p.m[2];
-      float th = reg[3 * hwa + i] * p.sd[3] + p.m[3];
-      float bw = (ax2 - ax1) + 1.0f, bh = (ay2 - ay1) + 1.0f;
-      float bcx = (ax2 + ax1) / 2.0f, bcy = (ay2 + ay1) / 2.0f;
-      float cx = tx * bw + bcx, cy = ty * bh + bcy;
-      float ww = expf(tw) * bw, hh = expf(th) * bh;
-      float hw2 = ww / 2.0f, hh2 = hh / 2.0f;
-      float v[4] = {cx - hw2, cy - hh2, cx + hw2, cy + hh2};
-      float hi[4] = {img_w - 1.0f, img_h - 1.0f, img_w - 1.0f, img_h - 1.0f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float y = (v[q] < 0.0f) ? 0.0f : v[q];
-        box[q] = (y > hi[q]) ? hi[q] : y;
-      }
-      if (min_size > 0.0f) {  // rpn_head.py:86-90
-        live = (((box[2] - box[0]) + 1.0f) >= min_size) && (((box[3] - box[1]) + 1.0f) >= min_size);
-      }
+      bx = rpn_decode_one(p, ia, seg, (int)~(uint32_t)skeys[j]);
+      live = rpn_big_enough(bx, min_size);
     }
     int tot;
-    int r = block_rank(live, wave_tot, &tot);
+    const int r = block_rank(live, wave_tot, &tot);
     if (live) {
-      int o = written + r;
-      reinterpret_cast<float4*>(ob)[o] = make_float4(box[0], box[1], box[2], box[3]);
-      os[o] = score;
+      reinterpret_cast<float4*>(ob)[written + r] = bx;
+      os[written + r] = key_float((uint32_t)(skeys[j] >> 32));
     }
     written += tot;
   }
@@ -169,7 +284,7 @@ __device__ __forceinline__ float kept_score(const MergeArgs& p, int seg, int j) 
   return p.sel_scores[(int64_t)seg * p.P + p.keep[(int64_t)seg * p.P + j]];
 }
 
-__global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
+static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
   const int b = blockIdx.z, l = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int seg = b * p.L + l;
@@ -219,8 +334,8 @@ static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, cnt, keep, kcnt, mask, keys, hist, state, cand, total;
-  int64_t nmax;
+  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, total;
+  int64_t nmax, kld;
 };
 
 static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int32_t A, int32_t pre_nms) {
@@ -238,19 +353,20 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
     if (n > nmax) nmax = n;
   }
   z.nmax = nmax;
+  z.kld = nmax;
   const size_t S = (size_t)B * L;
   z.boxes = 0;
   z.scores = z.boxes + al(S * P * 4 * sizeof(float));
   z.idx = z.scores + al(S * P * sizeof(float));
-  z.cnt = z.idx + al(S * P * sizeof(int32_t));
+  z.stage = z.idx + al(S * P * sizeof(uint64_t));
+  z.cnt = z.stage + al(S * kRpnSelFused * sizeof(float4));
   z.keep = z.cnt + al(S * sizeof(int32_t));
   z.kcnt = z.keep + al(S * P * sizeof(int32_t));
   z.mask = z.kcnt + al(S * sizeof(int32_t));
   z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
-  z.hist = z.keys + al(S * (size_t)nmax * sizeof(uint32_t));
-  z.state = z.hist + al(tk_hist_bytes((int)S));
-  z.cand = z.state + al(tk_state_bytes((int)S));
-  z.total = z.cand + al(tk_cand_bytes((int)S));
+  z.mem = z.keys + al(S * (size_t)z.kld * sizeof(uint32_t));
+  z.zero = z.mem + al(S * (size_t)z.kld * sizeof(uint64_t));
+  z.total = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
   return z;
 }
 
@@ -322,7 +438,8 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   p.P = z.P;
   p.sel_boxes = reinterpret_cast<float*>(ws + z.boxes);
   p.sel_scores = reinterpret_cast<float*>(ws + z.scores);
-  p.sel_idx = reinterpret_cast<int32_t*>(ws + z.idx);
+  p.sel_keys = reinterpret_cast<uint64_t*>(ws + z.idx);
+  p.stage = reinterpret_cast<float4*>(ws + z.stage);
   p.sel_count = reinterpret_cast<int32_t*>(ws + z.cnt);
   // per-image sizes travel by value in the kernel arguments
   ImgArgs ia{};
@@ -332,20 +449,28 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
     ia.min_size[b] = min_size[b];
   }
   const int S = num_imgs * num_levels;
-  // 1. keys + top-k state, 2. segmented top-k, 3. order + decode + min-size
-  uint32_t* keys = reinterpret_cast<uint32_t*>(ws + z.keys);
-  TopkBuffers tb{keys, z.nmax, reinterpret_cast<uint32_t*>(ws + z.hist), reinterpret_cast<int32_t*>(ws + z.state),
-                 p.sel_idx, z.P, reinterpret_cast<int32_t*>(ws + z.cand), S};
-  FRH_HIP(hipMemsetAsync(ws + z.hist, 0, z.cand - z.hist, st));  // hist + state
-  hipLaunchKernelGGL(rpn_keys_kernel, dim3((unsigned)((z.nmax + 255) / 256), (unsigned)S), dim3(256), 0, st, p, keys,
-                     z.nmax, tb.state);
-  tk_launch(tb, z.nmax, st);
-  const size_t lds_sel = (size_t)next_pow2(z.P) * sizeof(uint64_t);
-  if (lds_sel > 65536)
-    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_sort_decode_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sel));
-  hipLaunchKernelGGL(rpn_sort_decode_kernel, dim3(S), dim3(kPropThreads), lds_sel, st, p, ia, keys, z.nmax,
-                     tb.state, p.sel_idx, (int64_t)z.P);
+  // 1. keys + first-level histogram, 2. top-k + order + decode + min-size
+  // (sort + decode fused into the collect launch when the selection is <= kRpnSelFused)
+  char* zb = ws + z.zero;
+  TkBufs tb{reinterpret_cast<uint32_t*>(ws + z.keys), z.kld, reinterpret_cast<uint32_t*>(zb), kRpnHistBits,
+            reinterpret_cast<uint32_t*>(zb + (size_t)S * (1 << kRpnHistBits) * sizeof(uint32_t)),
+            reinterpret_cast<int32_t*>(zb + (size_t)S * ((1 << kRpnHistBits) + kTkBins2) * sizeof(uint32_t)),
+            reinterpret_cast<uint64_t*>(ws + z.mem)};
+  FRH_HIP(hipMemsetAsync(zb, 0, tk_zero_bytes(S, kRpnHistBits), st));
+  const dim3 grid((unsigned)((z.nmax + kTkChunk - 1) / kTkChunk), (unsigned)S);
+  hipLaunchKernelGGL(rpn_keys_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
+  hipLaunchKernelGGL(rpn_refine_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
+  const bool fused = z.P <= kRpnSelFused && z.nmax < (1 << 20);  // record layout limits
+  hipLaunchKernelGGL(rpn_collect_kernel, grid, dim3(kTkThreads), 0, st, p, ia, tb, fused);
+  if (fused) {
+    hipLaunchKernelGGL(rpn_rank_kernel, dim3(kRpnSelFused / kRankPer, (unsigned)S), dim3(256), 0, st, p, tb.state);
+  } else {
+    const size_t lds_sel = (size_t)next_pow2(z.P) * sizeof(uint64_t);
+    if (lds_sel > 65536)
+      FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_sort_decode_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sel));
+    hipLaunchKernelGGL(rpn_sort_decode_kernel, dim3(S), dim3(kPropThreads), lds_sel, st, p, ia, tb.state);
+  }
   int32_t r = check_launch("rpn_select");
   if (r) return r;
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);

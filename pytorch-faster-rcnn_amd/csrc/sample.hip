@@ -121,53 +121,114 @@ __global__ void sample_apply_kernel(const int64_t* lab_in, int64_t label_seg_str
 // device-RNG sampler: virtual top-k segment v = 2s (positives) / 2s+1
 // (negatives); key = candidate ? (~hash(seed, v, box) | 1) : 0, so the k
 // largest keys are a uniform k-subset of the candidates.  Also resets
-// labels_out to -1 and counts the candidates.
-__global__ void sampler_keys_kernel(const int64_t* lab_in, int64_t lstride, const int32_t* num, uint64_t seed,
-                                    uint32_t* keys, int64_t kld, int32_t* counts, int64_t* lab_out) {
-  __shared__ int scratch[4];
-  const int s = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// labels_out to -1 and writes, per 4096-box chunk, the candidate counts and the
+// histograms of the keys' top 8 bits (plain stores: the keys are uniform, so
+// 256 buckets leave ~n/256 keys in the k-th one and no refine launch is
+// needed); chunk 0 zeroes the collect launch's state words.  Grid (chunks,
+// images); no memset.
+constexpr int kSampHistBits = 8;
+constexpr int kSampBins = 1 << kSampHistBits;
+
+struct SampBufs {
+  TkBufs tk;
+  uint32_t* part_hist;   // [V][nchunk][kSampBins]
+  int32_t* part_count;   // [V][nchunk]
+  int nchunk;
+};
+
+static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const int64_t* lab_in, int64_t lstride,
+                                                                         const int32_t* num, uint64_t seed,
+                                                                         SampBufs sb, int64_t* lab_out) {
+  __shared__ uint32_t h[2][kSampBins];
+  __shared__ int scratch[kTkThreads / kWave];
+  const TkBufs& b = sb.tk;
+  const int s = blockIdx.y, c = blockIdx.x;
   const int64_t n = num[s];
-  bool pos = false, neg = false;
-  if (i < n) {
-    int64_t l = lab_in[(int64_t)s * lstride + i];
-    pos = l > 0;
-    neg = l == 0;
-    lab_out[(int64_t)s * lstride + i] = -1;
+  const int64_t base = (int64_t)c * kTkChunk;
+  if (c == 0 && threadIdx.x < 2 * TK_WORDS) b.state[2 * s * TK_WORDS + threadIdx.x] = 0;
+  tk_hist1_clear(&h[0][0], 2 * kSampBins);
+  uint32_t* kp = const_cast<uint32_t*>(b.keys) + (int64_t)(2 * s) * b.ld;
+  uint32_t* kn = kp + b.ld;
+  int cp = 0, cn = 0;
+  int64_t lab[kTkPerThread];  // every label load in flight at once
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int64_t i = base + r * kTkThreads + threadIdx.x;
+    lab[r] = i < n ? lab_in[(int64_t)s * lstride + i] : -1;
   }
-  if (i < kld) {
-    keys[(int64_t)(2 * s) * kld + i] = pos ? ((~hash_u32(seed, 2 * s, (uint32_t)i)) | 1u) : 0u;
-    keys[(int64_t)(2 * s + 1) * kld + i] = neg ? ((~hash_u32(seed, 2 * s + 1, (uint32_t)i)) | 1u) : 0u;
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int64_t i = base + r * kTkThreads + threadIdx.x;
+    const bool pos = lab[r] > 0, neg = lab[r] == 0;
+    if (i < n) lab_out[(int64_t)s * lstride + i] = -1;
+    const uint32_t keyp = pos ? ((~hash_u32(seed, 2 * s, (uint32_t)i)) | 1u) : 0u;
+    const uint32_t keyn = neg ? ((~hash_u32(seed, 2 * s + 1, (uint32_t)i)) | 1u) : 0u;
+    if (i < b.ld) {
+      kp[i] = keyp;
+      kn[i] = keyn;
+    }
+    tk_hist_add(h[0], pos, keyp >> (32 - kSampHistBits));
+    tk_hist_add(h[1], neg, keyn >> (32 - kSampHistBits));
+    cp += pos;
+    cn += neg;
   }
-  int cp = block_sum(pos ? 1 : 0, scratch);
-  int cn = block_sum(neg ? 1 : 0, scratch);
+  cp = block_sum(cp, scratch);
+  cn = block_sum(cn, scratch);
   if (threadIdx.x == 0) {
-    if (cp) atomicAdd(&counts[2 * s], cp);
-    if (cn) atomicAdd(&counts[2 * s + 1], cn);
+    sb.part_count[(int64_t)(2 * s) * sb.nchunk + c] = cp;
+    sb.part_count[(int64_t)(2 * s + 1) * sb.nchunk + c] = cn;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * kSampBins; i += kTkThreads) {
+    const int w = i / kSampBins;
+    sb.part_hist[((int64_t)(2 * s + w) * sb.nchunk + c) * kSampBins + (i % kSampBins)] = h[w][i % kSampBins];
   }
 }
 
-__global__ void sampler_k_kernel(const int32_t* num, const int32_t* counts, int S, int max_num, int pos_num,
-                                 int32_t* state) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= S) return;
-  int npos = counts[2 * s], nneg = counts[2 * s + 1];
-  int kp = npos < pos_num ? npos : pos_num;
-  int slots = max_num - kp;
-  int kn = nneg < slots ? nneg : slots;
-  state[(2 * s) * TK_WORDS + TK_N] = num[s];
-  state[(2 * s) * TK_WORDS + TK_K] = kp;
-  state[(2 * s + 1) * TK_WORDS + TK_N] = num[s];
-  state[(2 * s + 1) * TK_WORDS + TK_K] = kn;
-}
+// sampler policy of the segmented top-k: a selected box gets its input label
+// back (labels_out was reset to -1 by the key kernel)
+struct SampPol {
+  const int64_t* li;
+  int64_t* lo;
+  __device__ void select(int i, uint32_t, int) { lo[i] = li[i]; }
+  __device__ void finish(int) {}
+};
 
-__global__ void sampler_apply_topk_kernel(const int64_t* lab_in, int64_t lstride, const int32_t* state,
-                                          const int32_t* sel, int64_t sel_ld, int64_t* lab_out) {
-  const int v = blockIdx.y, s = v >> 1;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= state[v * TK_WORDS + TK_K]) return;
-  int64_t box = sel[(int64_t)v * sel_ld + j];
-  lab_out[(int64_t)s * lstride + box] = lab_in[(int64_t)s * lstride + box];
+// Collect launch: grid (chunks, 2 x images), 256 threads.  Every workgroup sums
+// the chunk histograms and counts of its segment and of the image's positive
+// segment, derives k -- kp = min(npos, pos_num), kn = min(nneg, max_num - kp)
+// (region.py:43-57) -- and the two-level plan, then collects (seg_topk.h).
+static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(const int64_t* lab_in, int64_t lstride,
+                                                                            const int32_t* num, int max_num,
+                                                                            int pos_num, SampBufs sb,
+                                                                            int64_t* lab_out) {
+  __shared__ TkSmem sm;
+  const int v = blockIdx.y, s = v >> 1, t = threadIdx.x;
+  const int n = num[s];
+  const int nch = (int)((n + kTkChunk - 1) / kTkChunk);
+  int cp = 0, cn = 0;
+  for (int c = t; c < nch; c += kTkThreads) {
+    cp += sb.part_count[(int64_t)(2 * s) * sb.nchunk + c];
+    cn += sb.part_count[(int64_t)(2 * s + 1) * sb.nchunk + c];
+  }
+  const int npos = block_sum(cp, sm.part), nneg = block_sum(cn, sm.part);
+  const int kp = npos < pos_num ? npos : pos_num;
+  const int slots = max_num - kp;
+  const int k = (v & 1) ? (nneg < slots ? nneg : slots) : kp;
+  uint32_t hsum = 0u;  // bin t (kSampBins == kTkThreads); 8 chunk loads in flight per step
+  const uint32_t* ph = sb.part_hist + (int64_t)v * sb.nchunk * kSampBins + t;
+  for (int c0 = 0; c0 < nch; c0 += 8) {
+    uint32_t x[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) x[c] = c0 + c < nch ? ph[(int64_t)(c0 + c) * kSampBins] : 0u;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) hsum += x[c];
+  }
+  sm.h1[t] = hsum;
+  __syncthreads();
+  const TkPlan plan = tk_plan_direct(kSampHistBits, k, sm, [&](int i) { return sm.h1[i]; });
+  SampPol pol{lab_in + (int64_t)s * lstride, lab_out + (int64_t)s * lstride};
+  tk_collect_chunk(sb.tk, v, n, plan, pol, sm);
 }
 
 int32_t launch_compact_lists(int32_t S, const int64_t* labels, int64_t label_seg_stride,
@@ -194,20 +255,23 @@ using namespace frh;
 static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct SampLayout {
-  size_t keys, hist, state, counts, cand, sel, total;
+  size_t keys, cand, state, phist, pcount, total;
+  int64_t kld;
+  int nchunk;
 };
 
 static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   SampLayout z{};
   const size_t n = (size_t)(max_boxes > 0 ? max_boxes : 1);
   const int V = 2 * S;
+  z.kld = (int64_t)n;
+  z.nchunk = (int)((n + kTkChunk - 1) / kTkChunk);
   z.keys = 0;
-  z.hist = z.keys + al256((size_t)V * n * sizeof(uint32_t));
-  z.state = z.hist + al256(tk_hist_bytes(V));
-  z.counts = z.state + al256(tk_state_bytes(V));
-  z.cand = z.counts + al256((size_t)V * sizeof(int32_t));
-  z.sel = z.cand + al256(tk_cand_bytes(V));
-  z.total = z.sel + al256((size_t)V * n * sizeof(int32_t));
+  z.cand = z.keys + al256((size_t)V * n * sizeof(uint32_t));
+  z.state = z.cand + al256((size_t)V * n * sizeof(uint64_t));
+  z.phist = z.state + al256((size_t)V * TK_WORDS * sizeof(int32_t));
+  z.pcount = z.phist + al256((size_t)V * z.nchunk * kSampBins * sizeof(uint32_t));
+  z.total = z.pcount + al256((size_t)V * z.nchunk * sizeof(int32_t));
   return z;
 }
 
@@ -265,25 +329,18 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
   FRH_REQUIRE(labels_in && labels_out && num_boxes, "null pointer argument");
   FRH_REQUIRE(labels_in != labels_out, "labels_out must not alias labels_in");
   FRH_REQUIRE(workspace && ws_bytes >= frh_sample_workspace(num_segs, max_boxes), "workspace too small");
+  FRH_REQUIRE(max_boxes <= INT32_MAX, "max_boxes must fit in int32");
+  static_assert(kSampBins == kTkThreads, "sampler_collect_kernel sums one bin per thread");
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   SampLayout z = samp_layout(num_segs, max_boxes);
   const int V = 2 * num_segs;
-  uint32_t* keys = reinterpret_cast<uint32_t*>(ws + z.keys);
-  int32_t* state = reinterpret_cast<int32_t*>(ws + z.state);
-  int32_t* counts = reinterpret_cast<int32_t*>(ws + z.counts);
-  int32_t* sel = reinterpret_cast<int32_t*>(ws + z.sel);
-  FRH_HIP(hipMemsetAsync(ws + z.hist, 0, z.cand - z.hist, st));  // hist + state + counts
-  dim3 g1((unsigned)((max_boxes + 255) / 256), (unsigned)num_segs);
-  hipLaunchKernelGGL(sampler_keys_kernel, g1, dim3(256), 0, st, labels_in, label_seg_stride, num_boxes, seed, keys,
-                     max_boxes, counts, labels_out);
-  hipLaunchKernelGGL(sampler_k_kernel, dim3((unsigned)((num_segs + 63) / 64)), dim3(64), 0, st, num_boxes, counts,
-                     num_segs, max_num, pos_num, state);
-  TopkBuffers tb{keys, max_boxes, reinterpret_cast<uint32_t*>(ws + z.hist), state, sel, max_boxes,
-                 reinterpret_cast<int32_t*>(ws + z.cand), V};
-  tk_launch(tb, max_boxes, st);
-  dim3 g2((unsigned)((max_num + 255) / 256), (unsigned)V);
-  hipLaunchKernelGGL(sampler_apply_topk_kernel, g2, dim3(256), 0, st, labels_in, label_seg_stride, state, sel,
-                     (int64_t)max_boxes, labels_out);
+  SampBufs sb{TkBufs{reinterpret_cast<uint32_t*>(ws + z.keys), z.kld, nullptr, kSampHistBits, nullptr,
+                     reinterpret_cast<int32_t*>(ws + z.state), reinterpret_cast<uint64_t*>(ws + z.cand)},
+              reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk};
+  hipLaunchKernelGGL(sampler_keys_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
+                     labels_in, label_seg_stride, num_boxes, seed, sb, labels_out);
+  hipLaunchKernelGGL(sampler_collect_kernel, dim3((unsigned)z.nchunk, (unsigned)V), dim3(kTkThreads), 0, st,
+                     labels_in, label_seg_stride, num_boxes, max_num, pos_num, sb, labels_out);
   return check_launch("frh_sample_random");
 }

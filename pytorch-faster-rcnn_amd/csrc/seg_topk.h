@@ -1,265 +1,449 @@
-// Multi-workgroup segmented top-k over precomputed u32 keys.
+// Segmented top-k over u32 keys, spread over the chip: one 256-thread
+// workgroup per 4096-key chunk of every segment.
 //
-// Used by the RPN score selection (pre_nms of ~117k anchors per (image,
-// level)) and the device sampler (k of up to ~130k candidates).  A single
-// workgroup per segment (block_topk_select) reads every key once per radix
-// byte from one CU; here every pass is spread over the whole chip:
-//   hist1   : 4096-bin histogram of key[31:20] per segment (LDS, flushed with
-//             global atomics), all chunks of all segments in one grid; the
-//             last workgroup of a segment to finish (done counter) then runs
-//   find1   : a suffix scan of the histogram -> bucket b1, remaining slots k1
-//             (also decides "take everything" when n <= k), and clears the
-//             histogram for
-//   hist2   : histogram of key[19:8] for keys in bucket b1, whose last
-//             workgroup per segment runs
-//   find2   : bucket b2, remaining slots k2  (prefix P = b1:b2, 24 bits)
-//   collect : keys with key>>8 > P are selected, keys with key>>8 == P become
-//             candidates (appends aggregated per wave: one atomic per wave)
-//   final   : one workgroup per segment sorts the candidates by
-//             (key desc, index asc) and appends the first k2.
-// Four launches per selection.  The last-workgroup hand-off reads the histogram
-// with atomic read-modify-writes (performed at the memory side, like the flush
-// atomics it reads), after every wave's flush atomics have completed (vmcnt(0))
-// and a barrier, so no cross-XCD cache state is involved.
-// Result: out[v][0..k_v) = indices of the k_v largest keys, ties broken by
-// lowest index, in no particular order.  Key 0 means "not a candidate".
+// Used by the RPN score selection (pre_nms of up to ~117k anchors per (image,
+// level); rpn_head.py:84-90) and the device sampler (k of up to ~155k
+// candidates; region.py:43-57).  After one memset, three launches:
+//   keys    : the caller's key kernel writes the keys and, per chunk, an LDS
+//             histogram of their top hb bits (hb <= 12), flushed into the
+//             segment's global histogram with atomics (tk_hist1_*).
+//   refine  : every chunk workgroup finds bucket b1 and the slots k1 left in it
+//             ("take every nonzero key" when there are at most k) from that
+//             histogram and counts its b1 keys into a histogram of the next 12
+//             bits; the segment's last workgroup (done counter) finds bucket b2
+//             and the slots k2 left in the prefix P = b1:b2 and publishes them.
+//   collect : every chunk workgroup selects its keys above P and lists its
+//             keys equal to P (candidates); the last workgroup sorts the
+//             candidates by (key desc, index asc) in LDS, selects the first k2
+//             and runs the caller's finish.
+// When the first-level buckets are small (uniform keys: the device sampler)
+// the refine launch is skipped and P = b1 (tk_plan_direct).
+// Every workgroup loads its 16 keys per thread at once and reserves list slots
+// with one atomic per workgroup, so a launch costs a handful of memory round
+// trips.  Data handed between workgroups inside a launch (second histogram,
+// candidate and selection lists) is written with atomics and read by the last
+// workgroup with atomic read-modify-writes -- both execute at the memory side,
+// no XCD L2 state is involved -- after each writer's vmcnt(0) and its
+// workgroup's done-counter add.
+// Result: k_v = min(k, #nonzero keys) selections -- the k_v largest keys, ties
+// broken by lowest index -- handed to the caller's policy (no order).  Key 0
+// means "not a candidate".
 #pragma once
 #include "block_ops.h"
 
 namespace frh {
 
-constexpr int kTkBins = 4096;
 constexpr int kTkThreads = 256;
 constexpr int kTkPerThread = 16;
-constexpr int kTkChunk = kTkThreads * kTkPerThread;
-constexpr int kTkCandCap = 8192;  // candidates sorted in LDS; more -> radix fallback
+constexpr int kTkChunk = kTkThreads * kTkPerThread;  // keys per workgroup
+constexpr int kTkBins2 = 4096;                       // second level: 12 bits
+constexpr int kTkCandCap = 4096;                     // prefix ties sorted in LDS
 
-// per-segment state words
-enum { TK_N = 0, TK_K = 1, TK_ALL = 2, TK_B1 = 3, TK_K1 = 4, TK_B2 = 5, TK_K2 = 6, TK_OUT = 7, TK_CAND = 8,
-       TK_DONE0 = 9, TK_DONE1 = 10, TK_WORDS = 16 };
+// per-segment state words (zeroed by the caller's memset; TK_N / TK_K may be
+// seeded by the key kernel)
+enum { TK_N = 0, TK_K = 1, TK_OUT = 2, TK_CAND = 3, TK_DONE1 = 4, TK_DONE2 = 5, TK_CNT = 6,
+       TK_ALL = 7, TK_KV = 8, TK_P = 9, TK_K2 = 10, TK_WORDS = 16 };
 
-struct TopkBuffers {
+struct TkBufs {
   const uint32_t* keys;  // [V][ld]
   int64_t ld;
-  uint32_t* hist;        // [V][kTkBins]
-  int32_t* state;        // [V][TK_WORDS]; TK_N and TK_K filled by the key generator
-  int32_t* out;          // [V][out_ld]
-  int64_t out_ld;
-  int32_t* cand;         // [V][kTkCandCap]
-  int V;
+  uint32_t* hist1;       // [V][1 << hb]
+  int hb;                // first-level bits (<= 12)
+  uint32_t* hist2;       // [V][kTkBins2]
+  int32_t* state;        // [V][TK_WORDS]
+  uint64_t* cand;        // [V][ld] candidate list: key << 32 | ~index
 };
 
-// kernels have internal linkage: every translation unit that includes this
-// header gets its own copy (no cross-TU device symbols)
-namespace {
+#ifdef FRH_TK_TIMELINE  // tools-only build (tools/csrc/topk_timeline.hip): segment-0 stamps
+static __device__ uint64_t* g_tk_tl;
+#define TK_STAMP(slot)                                                  \
+  do {                                                                  \
+    if (g_tk_tl && threadIdx.x == 0 && blockIdx.y == 0) g_tk_tl[slot] = wall_clock64(); \
+  } while (0)
+#else
+#define TK_STAMP(slot)
+#endif
 
-// The find step of pass `pass` for segment v, run by one whole 256-thread workgroup:
-// suffix scan of the histogram from the highest bin; bucket where the running count
-// reaches the remaining slots.  `rd(i)` reads bin i.
-template <class Rd>
-__device__ __forceinline__ void tk_find(int32_t* st, int pass, Rd rd, int* part, int* sel_bin, int* sel_above) {
-  const int t = threadIdx.x;
-  int bins[16];
-  const int hi = kTkBins - 16 * t;  // thread t owns bins [4096 - 16(t+1), 4096 - 16t) (descending order)
-  int s = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    bins[i] = rd(hi - 1 - i);
-    s += bins[i];
-  }
-  if (pass == 0) {  // total candidates = sum of the histogram
-    const int tot = block_sum(s, part);
-    if (t == 0) {
-      st[TK_ALL] = (tot <= st[TK_K]) ? 1 : 0;
-      if (st[TK_K] > tot) st[TK_K] = tot;
-      st[TK_OUT] = 0;
-      st[TK_CAND] = 0;
-    }
-    __syncthreads();
-    if (st[TK_ALL]) return;
-  }
-  const int krem = pass == 0 ? st[TK_K] : st[TK_K1];
-  if (krem <= 0) {  // nothing (more) to select: a prefix no key can exceed, zero slots
-    if (t == 0) {
-      st[pass == 0 ? TK_B1 : TK_B2] = kTkBins - 1;
-      st[pass == 0 ? TK_K1 : TK_K2] = 0;
-      if (pass == 0) {
-        st[TK_B2] = kTkBins - 1;
-        st[TK_K2] = 0;
-      }
-    }
-    return;
-  }
-  // inclusive prefix over threads (descending bin order): wave scans + wave totals
-  int incl = s;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int x = __shfl_up(incl, o, kWave);
-    if ((t & (kWave - 1)) >= o) incl += x;
-  }
-  const int w = t / kWave;
-  if ((t & (kWave - 1)) == kWave - 1) part[w] = incl;
-  __syncthreads();
-  for (int i = 0; i < w; ++i) incl += part[i];
-  int run = incl - s;  // count in bins above my range
-  if (run < krem && incl >= krem) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (run + bins[i] >= krem) {
-        *sel_bin = hi - 1 - i;
-        *sel_above = run;
-        break;
-      }
-      run += bins[i];
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    if (pass == 0) {
-      st[TK_B1] = *sel_bin;
-      st[TK_K1] = krem - *sel_above;
-    } else {
-      st[TK_B2] = *sel_bin;
-      st[TK_K2] = krem - *sel_above;
-    }
-  }
+inline size_t tk_zero_bytes(int V, int hb) {  // hist1 + hist2 + state, contiguous
+  return (size_t)V * (((size_t)1 << hb) + kTkBins2 + TK_WORDS) * sizeof(uint32_t);
 }
 
-// histogram pass + (last workgroup of the segment) the find step
-__global__ void __launch_bounds__(kTkThreads) tk_hist_kernel(TopkBuffers b, int pass) {
-  __shared__ uint32_t h[kTkBins];
-  __shared__ int part[kTkThreads / kWave];
-  __shared__ int last, sel_bin, sel_above;
-  const int v = blockIdx.y;
-  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
-  int32_t* st = b.state + v * TK_WORDS;
-  const int n = st[TK_N];
-  if (pass == 1 && st[TK_ALL]) return;  // uniform per segment: no find either
-  uint32_t* gh = b.hist + (int64_t)v * kTkBins;
-  if (base < n) {
-    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) h[i] = 0;
-    __syncthreads();
-    const uint32_t* kk = b.keys + (int64_t)v * b.ld;
-    const uint32_t b1 = (uint32_t)st[TK_B1];
-#pragma unroll 4
-    for (int r = 0; r < kTkPerThread; ++r) {
-      int64_t i = base + r * kTkThreads + threadIdx.x;
-      if (i < n) {
-        uint32_t key = kk[i];
-        if (key) {
-          if (pass == 0)
-            atomicAdd(&h[key >> 20], 1u);
-          else if ((key >> 20) == b1)
-            atomicAdd(&h[(key >> 8) & 0xfffu], 1u);
-        }
-      }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads)
-      if (h[i]) atomicAdd(&gh[i], h[i]);
-  }
-  // every workgroup of the segment checks in once its flush atomics have completed
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&st[pass == 0 ? TK_DONE0 : TK_DONE1], 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  tk_find(st, pass, [&](int i) { return (int)atomicAdd(&gh[i], 0u); }, part, &sel_bin, &sel_above);
-  if (pass == 0) {  // clear for pass 2 (read in the next launch)
-    __syncthreads();
-    for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) gh[i] = 0;
-  }
+// ------------------------------------------- cross-workgroup hand-off words
+// Payload handed from the chunk workgroups of a launch to its last workgroup:
+// written with agent-scope relaxed stores (sc1: write-through, the line leaves
+// the writer's L2) or memory-side atomics, read with agent-scope relaxed loads
+// (sc1: L1 bypassed) after every writer's vmcnt(0) wait and its workgroup's
+// done-counter add has been seen (MI355X_MICROARCH.md, hand-off table row 1).
+__device__ __forceinline__ void xwg_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t xwg_load(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t xwg_load(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t xwg_load(const int32_t* p) {
+  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// wave-aggregated append: every lane with `take` gets a distinct slot of `list`
+// ------------------------------------------------------------ wave helpers
+// histogram add aggregated over the wave's most common bin (the first active
+// lane's): a concentrated key set costs one LDS atomic per wave, not 64
+// conflicting ones.  Wave-uniform call.
+__device__ __forceinline__ void tk_hist_add(uint32_t* h, bool act, uint32_t bin) {
+  const uint64_t am = __ballot(act);
+  if (!am) return;
+  const int l0 = __builtin_ctzll(am);
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, l0);
+  const uint64_t same = __ballot(act && bin == b0);
+  if (lane_id() == l0) atomicAdd(&h[b0], (uint32_t)__popcll(same));
+  if (act && bin != b0) atomicAdd(&h[bin], 1u);
+}
+
+// wave-aggregated append: every lane with `take` gets a distinct slot of the
+// list behind `counter` (LDS or global); -1 for the others.  Wave-uniform call.
 __device__ __forceinline__ int wave_append(bool take, int* counter) {
   const uint64_t m = __ballot(take);
   if (!m) return -1;
   const int leader = __builtin_ctzll(m);
   int base = 0;
-  if ((int)(threadIdx.x & (kWave - 1)) == leader) base = atomicAdd(counter, __popcll(m));
+  if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
   base = __shfl(base, leader, kWave);
   return take ? base + __popcll(m & lanemask_lt()) : -1;
 }
 
-__global__ void __launch_bounds__(kTkThreads) tk_collect_kernel(TopkBuffers b) {
-  const int v = blockIdx.y;
-  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
-  int32_t* st = b.state + v * TK_WORDS;
-  const int n = st[TK_N];
-  if (base >= n) return;
-  const bool all = st[TK_ALL] != 0;
-  const uint32_t P = ((uint32_t)st[TK_B1] << 12) | (uint32_t)st[TK_B2];
-  const uint32_t* kk = b.keys + (int64_t)v * b.ld;
-  int32_t* out = b.out + (int64_t)v * b.out_ld;
-  int32_t* cand = b.cand + (int64_t)v * kTkCandCap;
+// Workgroup-aggregated reservation of `cnt` slots per thread in the list
+// behind the global `counter` (one atomic per workgroup): returns this
+// thread's first slot.  Block-uniform call; part / sh[2]: LDS scratch (sh[0] /
+// sh[1] = the workgroup's first slot / count, valid until the next call).
+__device__ __forceinline__ int block_reserve(int cnt, int* counter, int* part, int* sh) {
+  const int t = threadIdx.x, w = t / kWave;
+  __syncthreads();  // part / sh free
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if (lane_id() >= o) incl += x;
+  }
+  if (lane_id() == kWave - 1) part[w] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int i = 0; i < (int)blockDim.x / kWave; ++i) {
+    const int c = part[i];
+    pre += i < w ? c : 0;
+    tot += c;
+  }
+  if (t == 0) {
+    sh[0] = tot ? atomicAdd(counter, tot) : 0;
+    sh[1] = tot;
+  }
+  __syncthreads();
+  return sh[0] + pre + incl - cnt;  // sh[0] = the workgroup's first slot, sh[1] = its count
+}
+
+// --------------------------------------------- first-level histogram (keys)
+// The key kernels build it per chunk: clear, add, flush (block-uniform calls).
+__device__ __forceinline__ void tk_hist1_clear(uint32_t* h, int bins) {
+  for (int i = threadIdx.x; i < bins; i += blockDim.x) h[i] = 0u;
+  __syncthreads();
+}
+__device__ __forceinline__ void tk_hist1_flush(const uint32_t* h, int bins, uint32_t* gh) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < bins; i += blockDim.x) {
+    const uint32_t c = h[i];
+    if (c) atomicAdd(&gh[i], c);
+  }
+}
+
+// ------------------------------------------------------------ select state
+struct TkSmem {
+  union {
+    struct {
+      uint32_t h1[4096];
+      uint32_t h2[kTkBins2];
+    };
+    uint64_t cand[kTkCandCap];
+  };
+  TopkSmem fb;
+  int part[kTkThreads / kWave];
+  int last, bin, above, tot, ncand;
+  int base, tot_sel;  // block_reserve's (first slot, count); adjacent
+};
+
+// Suffix search over 2^hb bins (highest first), 256 threads: sm.bin / sm.above
+// such that above < krem <= above + h[bin]; sm.tot = the total (no bin written
+// when krem > tot).  rd(i) reads bin i.
+template <class Rd>
+__device__ __forceinline__ void tk_find(TkSmem& sm, int bins, int krem, Rd rd) {
+  const int t = threadIdx.x, w = t / kWave;
+  const int per = bins / kTkThreads;  // 16 or 1 (hb = 12 or 8)
+  const int hi = bins - per * t;      // thread t owns [hi - per, hi), descending
+  int b[16], s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    b[i] = i < per ? (int)rd(hi - 1 - i) : 0;
+    s += b[i];
+  }
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if (lane_id() >= o) incl += x;
+  }
+  if (lane_id() == kWave - 1) sm.part[w] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kTkThreads / kWave; ++i) {
+    const int c = sm.part[i];
+    pre += i < w ? c : 0;
+    tot += c;
+  }
+  incl += pre;
+  int run = incl - s;
+  if (run < krem && incl >= krem) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < per && run + b[i] >= krem) {
+        sm.bin = hi - 1 - i;
+        sm.above = run;
+        break;
+      }
+      run += b[i];
+    }
+  }
+  if (t == 0) sm.tot = tot;
+  __syncthreads();
+}
+
+// This workgroup's 16 keys per thread (key r of thread t = chunk index
+// r * 256 + t), all loads in flight at once; index >= n reads as 0.
+__device__ __forceinline__ void tk_load_chunk(const uint32_t* kk, int64_t base, int n, uint32_t (&key)[kTkPerThread]) {
+#pragma unroll
   for (int r = 0; r < kTkPerThread; ++r) {
     const int64_t i = base + r * kTkThreads + threadIdx.x;
-    if (base + r * kTkThreads >= n) break;  // uniform
-    const uint32_t key = i < n ? kk[i] : 0u;
-    const uint32_t p = key >> 8;
-    const bool sel = key && (all || p > P), cnd = key && !all && p == P;
-    const int o = wave_append(sel, &st[TK_OUT]);
-    if (o >= 0) out[o] = (int32_t)i;
-    const int c = wave_append(cnd, &st[TK_CAND]);
-    if (c >= 0 && c < kTkCandCap) cand[c] = (int32_t)i;
+    key[r] = i < n ? kk[i] : 0u;
   }
 }
 
-// one 1024-thread block per segment: order candidates, append the best k2.
-__global__ void __launch_bounds__(1024) tk_final_kernel(TopkBuffers b) {
-  __shared__ uint64_t sk[kTkCandCap];
-  __shared__ TopkSmem sm;
-  const int v = blockIdx.x;
+// check in once this workgroup's atomics have completed: true in the last
+// workgroup of the segment (block-uniform)
+__device__ __forceinline__ bool tk_check_in(int* done, TkSmem& sm) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) sm.last = atomicAdd(done, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  return sm.last != 0;
+}
+
+// ------------------------------------------------------------- refine launch
+// Chunk blockIdx.x of segment v.  k <= 0 selects nothing.
+__device__ void tk_refine_chunk(const TkBufs& b, int v, int n, int k, TkSmem& sm) {
+  const int t = threadIdx.x;
+  const int bins1 = 1 << b.hb;
+  const int sh1 = 32 - b.hb, sh2 = sh1 - 12;
   int32_t* st = b.state + v * TK_WORDS;
-  if (st[TK_ALL]) return;
-  const int k2 = st[TK_K2];
-  const int ncand = st[TK_CAND];
-  const uint32_t* kk = b.keys + (int64_t)v * b.ld;
-  int32_t* out = b.out + (int64_t)v * b.out_ld;
-  const int base = st[TK_OUT];
-  if (ncand <= kTkCandCap) {
-    const int32_t* cand = b.cand + (int64_t)v * kTkCandCap;
-    const int P2 = next_pow2(ncand > 1 ? ncand : 1);
-    for (int j = threadIdx.x; j < P2; j += blockDim.x) {
-      uint64_t key = 0;
-      if (j < ncand) {
-        int i = cand[j];
-        key = ((uint64_t)kk[i] << 32) | (uint32_t)(~(uint32_t)i);
-      }
-      sk[j] = key;
-    }
+  for (int i = t; i < bins1; i += kTkThreads) sm.h1[i] = b.hist1[(int64_t)v * bins1 + i];
+  for (int i = t; i < kTkBins2; i += kTkThreads) sm.h2[i] = 0u;
+  __syncthreads();
+  tk_find(sm, bins1, k > 0 ? k : 1, [&](int i) { return sm.h1[i]; });
+  const bool all = k <= 0 || sm.tot <= k;
+  const uint32_t b1 = (uint32_t)sm.bin;
+  const int k1 = k - sm.above;
+  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
+  uint32_t* gh2 = b.hist2 + (int64_t)v * kTkBins2;
+  if (!all && base < n) {
+    uint32_t key[kTkPerThread];
+    tk_load_chunk(b.keys + (int64_t)v * b.ld, base, n, key);
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r)
+      tk_hist_add(sm.h2, key[r] != 0u && (key[r] >> sh1) == b1, (key[r] >> sh2) & 0xfffu);
     __syncthreads();
-    block_bitonic_sort_desc(sk, P2);
-    for (int j = threadIdx.x; j < k2; j += blockDim.x) out[base + j] = (int)(~(uint32_t)sk[j]);
-  } else {
-    // degenerate key distribution (> kTkCandCap keys share 24 bits): exact
-    // single-block radix select restricted to the prefix
-    const uint32_t P = ((uint32_t)st[TK_B1] << 12) | (uint32_t)st[TK_B2];
-    const int n = st[TK_N];
-    auto key_of = [&](int i) -> uint32_t {
-      uint32_t key = kk[i];
-      return (key >> 8) == P ? key : 0u;
-    };
-    block_topk_select(key_of, n, k2, out + base, sm);
+    for (int i = t; i < kTkBins2; i += kTkThreads) {
+      const uint32_t c = sm.h2[i];
+      if (c) atomicAdd(&gh2[i], c);
+    }
   }
-  if (threadIdx.x == 0) st[TK_OUT] = base + k2;
+  if (!tk_check_in(&st[TK_DONE1], sm)) return;
+  // last workgroup: find 2 (atomic reads: memory-side values), publish
+  int P = 0, k2 = 0;
+  if (!all) {
+    tk_find(sm, kTkBins2, k1, [&](int i) { return xwg_load(gh2 + i); });
+    P = (int)((b1 << 12) | (uint32_t)sm.bin);
+    k2 = k1 - sm.above;
+  }
+  if (t == 0) {
+    st[TK_ALL] = all ? 1 : 0;
+    st[TK_KV] = k <= 0 ? 0 : (all ? sm.tot : k);
+    st[TK_P] = P;
+    st[TK_K2] = k2;
+  }
 }
 
-}  // namespace
+// ------------------------------------------------------------ collect launch
+// What the collect launch selects: every nonzero key when `all` (kv of them);
+// otherwise keys whose top bits (key >> sh) exceed P, plus the first k2 (by key
+// desc, index asc) of the keys whose top bits equal P.
+struct TkPlan {
+  bool all;
+  int kv;
+  uint32_t P;
+  int sh;
+  int k2;
+};
 
-inline size_t tk_state_bytes(int V) { return (size_t)V * TK_WORDS * sizeof(int32_t); }
-inline size_t tk_hist_bytes(int V) { return (size_t)V * kTkBins * sizeof(uint32_t); }
-inline size_t tk_cand_bytes(int V) { return (size_t)V * kTkCandCap * sizeof(int32_t); }
+// the plan the refine launch published for segment v
+__device__ __forceinline__ TkPlan tk_plan_refined(const TkBufs& b, int v) {
+  const int32_t* st = b.state + v * TK_WORDS;
+  return TkPlan{st[TK_ALL] != 0, st[TK_KV], (uint32_t)st[TK_P], 32 - b.hb - 12, st[TK_K2]};
+}
 
-// Runs hist+find (x2), collect, final.  The caller has written keys and the TK_N /
-// TK_K words of state (state's other words and hist must be zero).
-static inline void tk_launch(const TopkBuffers& b, int64_t n_max, hipStream_t st) {
-  dim3 grid((unsigned)((n_max + kTkChunk - 1) / kTkChunk), (unsigned)b.V);
-  hipLaunchKernelGGL(tk_hist_kernel, grid, dim3(kTkThreads), 0, st, b, 0);
-  hipLaunchKernelGGL(tk_hist_kernel, grid, dim3(kTkThreads), 0, st, b, 1);
-  hipLaunchKernelGGL(tk_collect_kernel, grid, dim3(kTkThreads), 0, st, b);
-  hipLaunchKernelGGL(tk_final_kernel, dim3(b.V), dim3(1024), 0, st, b);
+// Two-level plan straight from a first-level histogram (no refine launch): the
+// bucket b1 holding the k-th key is the prefix; rd(i) reads bin i (all threads).
+template <class Rd>
+__device__ __forceinline__ TkPlan tk_plan_direct(int hb, int k, TkSmem& sm, Rd rd) {
+  tk_find(sm, 1 << hb, k > 0 ? k : 1, rd);
+  const bool all = k <= 0 || sm.tot <= k;
+  return TkPlan{all, k <= 0 ? 0 : (all ? sm.tot : k), (uint32_t)sm.bin, 32 - hb, k - sm.above};
+}
+
+// Chunk blockIdx.x of segment v.  Pol:
+//   void select(int index, uint32_t key, int slot)  one selection; slot = its
+//        position among the segment's k_v selections
+//   void finish(int kv)   last workgroup, all threads, after every select
+// The state words TK_OUT, TK_CAND, TK_DONE2 of v start at 0.
+template <class Pol>
+__device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& plan, Pol& pol, TkSmem& sm) {
+  const int t = threadIdx.x;
+  int32_t* st = b.state + v * TK_WORDS;
+  const bool all = plan.all;
+  const int kv = plan.kv, k2 = plan.k2, sh = plan.sh;
+  const uint32_t P = plan.P;
+  const uint32_t* kk = b.keys + (int64_t)v * b.ld;
+  uint64_t* cand = b.cand + (int64_t)v * b.ld;
+  const int64_t base = (int64_t)blockIdx.x * kTkChunk;
+  TK_STAMP(blockIdx.x * 4);
+  if (kv > 0 && base < n) {
+    uint32_t key[kTkPerThread];
+    tk_load_chunk(kk, base, n, key);
+    uint32_t sel = 0u, eq = 0u;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const uint32_t pre = key[r] >> sh;
+      sel |= (key[r] != 0u && (all || pre > P)) ? 1u << r : 0u;
+      eq |= (key[r] != 0u && !all && pre == P) ? 1u << r : 0u;
+    }
+    // candidates: straight to the segment's list (no dependent loads)
+    int c = block_reserve(__popc(eq), &st[TK_CAND], sm.part, &sm.base);
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r)
+      if (eq & (1u << r))
+        xwg_store(cand + c++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)(base + r * kTkThreads + t));
+    // selections: staged in LDS, then handed to the policy one per thread per
+    // round, so the policy's loads for a round are in flight together
+    int s = block_reserve(__popc(sel), &st[TK_OUT], sm.part, &sm.base);
+    const int gbase = sm.base, nsel = sm.tot_sel;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r)
+      if (sel & (1u << r)) sm.cand[s++ - gbase] = ((uint64_t)key[r] << 32) | (uint32_t)(base + r * kTkThreads + t);
+    __syncthreads();
+    for (int j0 = 0; j0 < nsel; j0 += kTkThreads) {
+      const int j = j0 + t;
+      if (j < nsel) {
+        const uint64_t e = sm.cand[j];
+        pol.select((int)(uint32_t)e, (uint32_t)(e >> 32), gbase + j);
+      }
+    }
+  }
+  TK_STAMP(blockIdx.x * 4 + 1);
+  if (!tk_check_in(&st[TK_DONE2], sm)) return;
+  TK_STAMP(blockIdx.x * 4 + 2);
+  if (kv == 0 || all) {
+    pol.finish(kv);
+    return;
+  }
+  // last workgroup: order the prefix ties, take the first k2
+  const int nabove = kv - k2;
+  const int ncand = xwg_load(st + TK_CAND);
+  if (ncand <= kTkCandCap) {
+    const int P2 = next_pow2(ncand > 1 ? ncand : 1);
+    for (int j = t; j < P2; j += kTkThreads)
+      sm.cand[j] = j < ncand ? xwg_load(cand + j) : 0ull;
+    __syncthreads();
+    TK_STAMP(1024);
+    block_bitonic_sort_desc(sm.cand, P2);
+    TK_STAMP(1025);
+    for (int j = t; j < k2; j += kTkThreads) {
+      const uint64_t e = sm.cand[j];
+      pol.select((int)~(uint32_t)e, (uint32_t)(e >> 32), nabove + j);
+    }
+  } else {
+    // degenerate key set (> kTkCandCap keys share the prefix): exact
+    // radix select restricted to the prefix, lowest index first among equal
+    // keys; indices staged in the (consumed) candidate row, read back in-workgroup
+    int32_t* idx = reinterpret_cast<int32_t*>(cand);
+    auto key_of = [&](int i) -> uint32_t {
+      const uint32_t key = kk[i];
+      return (key >> sh) == P ? key : 0u;
+    };
+    block_topk_select(key_of, n, k2, idx, sm.fb);
+    for (int j = t; j < k2; j += kTkThreads) pol.select(idx[j], kk[idx[j]], nabove + j);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TK_STAMP(1026);
+  pol.finish(kv);
+  TK_STAMP(1031);
+}
+
+// ------------------------------------------- register bitonic sort (desc)
+// kTkThreads threads x E elements (E = 2^LE), P = kTkThreads * E keys, pad with 0.
+// Every compare-exchange happens in registers: before a stage whose partner
+// distance 2^j is not among the element-index bits [r0, r0 + LE) a thread
+// holds, the elements are re-dealt through `lds` (P entries) so that thread t's
+// register e holds element g(t, e) = (t >> r0) << (r0 + LE) | e << r0 | t mod 2^r0
+// with r0 = max(0, j - LE + 1) -- one re-deal per LE stages.  The network is
+// unrolled at compile time.  In and out: x[e] = element t * E + e.
+__device__ __forceinline__ int tk_gidx(int t, int e, int r0, int le) {
+  return ((t >> r0) << (r0 + le)) | (e << r0) | (t & ((1 << r0) - 1));
+}
+
+template <int E>
+__device__ __forceinline__ void reg_bitonic_sort_desc(uint64_t (&x)[E], uint64_t* lds) {
+  constexpr int LE = E == 1 ? 0 : E == 2 ? 1 : E == 4 ? 2 : E == 8 ? 3 : 4;
+  static_assert((1 << LE) == E && E >= 2, "E must be 2, 4, 8 or 16");
+  constexpr int LP = 8 + LE;  // kTkThreads == 256
+  const int t = threadIdx.x;
+  int r0 = 0;
+  auto redeal = [&](int nr0) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) lds[tk_gidx(t, e, r0, LE)] = x[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = lds[tk_gidx(t, e, nr0, LE)];
+    __syncthreads();
+    r0 = nr0;
+  };
+#pragma unroll
+  for (int ls = 1; ls <= LP; ++ls) {
+#pragma unroll
+    for (int j = ls - 1; j >= 0; --j) {
+      if (j < r0 || j >= r0 + LE) redeal(j - LE + 1 < 0 ? 0 : j - LE + 1);
+      const int eb = j - r0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if ((e >> eb) & 1) continue;
+        const int e2 = e | (1 << eb);
+        const bool desc = ((tk_gidx(t, e, r0, LE) >> ls) & 1) == 0;
+        const uint64_t a = x[e], c = x[e2];
+        const bool sw = desc ? (a < c) : (a > c);
+        x[e] = sw ? c : a;
+        x[e2] = sw ? a : c;
+      }
+    }
+  }
+  if (r0 != 0) redeal(0);
 }
 
 }  // namespace frh

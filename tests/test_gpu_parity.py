@@ -204,27 +204,79 @@ def test_rpn_loss_vs_reference(dev, golden):
         np.testing.assert_allclose([float(c), float(r)], g['loss_{}'.format(i)], rtol=2e-5)
 
 
-def test_device_sampler_properties(dev):
+@pytest.mark.parametrize('max_num,pos_num', [(256, 128), (512, 128), (6000, 3000)])
+def test_device_sampler_properties(dev, max_num, pos_num):
+    """Device sampler (one top-k workgroup per (image, pos/neg); max_num > 4096 takes the
+    global-index path): exact pos/neg counts, kept rows keep their labels, rows past num
+    untouched, empty and candidate-poor segments."""
     from frcnn_amd import ops
     rng = np.random.default_rng(3)
-    S, n = 3, 130000
+    S, n = 5, 130001
     lab = rng.choice([-1, 0, 0, 0, 1, 2], size=(S, n), p=[0.3, 0.2, 0.2, 0.2, 0.05, 0.05]).astype(np.int64)
     lab[2, :] = np.where(lab[2] > 0, 0, lab[2])  # a segment with no positives
+    lab[4, :3000] = np.where(lab[4, :3000] == 0, -1, lab[4, :3000])  # fewer negatives than slots
     lt = T(lab, dev)
-    num = torch.tensor([n, n - 5, 1000], dtype=torch.int32, device=dev)
-    out = ops.sample_labels(lt, num, n, 256, 128, mode='device').cpu().numpy()
+    num = torch.tensor([n, n - 5, 1000, 0, 3000], dtype=torch.int32, device=dev)
+    out = ops.sample_labels(lt, num, n, max_num, pos_num, mode='device').cpu().numpy()
     for s in range(S):
         ns = int(num[s])
         src, o = lab[s, :ns], out[s, :ns]
         npos, nneg = int((src > 0).sum()), int((src == 0).sum())
-        kp = min(npos, 128)
+        kp = min(npos, pos_num)
         assert int((o > 0).sum()) == kp
-        assert int((o == 0).sum()) == min(nneg, 256 - kp)
+        assert int((o == 0).sum()) == min(nneg, max_num - kp)
         kept = o >= 0
         np.testing.assert_array_equal(o[kept], src[kept])  # kept rows keep their labels
     # fresh draws differ, and a fixed (seed, call) reproduces
-    out2 = ops.sample_labels(lt, num, n, 256, 128, mode='device').cpu().numpy()
+    out2 = ops.sample_labels(lt, num, n, max_num, pos_num, mode='device').cpu().numpy()
     assert not np.array_equal(out, out2)
+
+
+@pytest.mark.parametrize('case,pre', [('all_equal', 2000), ('four_values', 2000), ('sparse_high', 2000),
+                                      ('near_half', 2000), ('near_half', 6000), ('four_values', 6000)])
+def test_rpn_selection_tie_heavy_vs_oracle(dev, case, pre):
+    """The per-segment top-k (seg_topk.h) on score sets that stress its radix passes: every
+    score equal (bucket and prefix overflow -> restricted radix fallback, lowest indices
+    win), four distinct values (tie groups of ~29k), a few high scores over a flat floor,
+    and scores within 1e-3 of 0.5 (random-init RPN; quantised so that one ulp of sigmoid
+    cannot reorder them).  The oracle orders by (score desc,
+    index asc), as the kernel does, so boxes compare in order with no tie canonicalisation.
+    pre_nms 6000 (> 4096) takes the unfused path (separate sort + decode launch)."""
+    from frcnn_amd.config import wrap
+    head, _ = fpn_setup(dev)
+    rng = np.random.default_rng(7)
+    post, mx, thr = 1000, 1000, 0.7
+    cls_l, reg_l = [], []
+    for i in range(2):
+        cls, reg = inputs.head_outputs(900 + i, inputs.FPN_GRIDS, 3, 1, reg_scale=0.5)
+        for c in cls:
+            if case == 'all_equal':
+                c[...] = 0.0
+            elif case == 'four_values':
+                c[...] = rng.choice(np.array([-1.0, 0.0, 0.5, 2.0], np.float32), size=c.shape)
+            elif case == 'sparse_high':
+                c[...] = -5.0
+                flat = c.reshape(-1)
+                flat[rng.choice(flat.size, min(flat.size, 150), replace=False)] = rng.uniform(1, 3, min(flat.size, 150))
+            else:
+                # 8001 logit values 1e-6 apart: scores >= 4 ulp apart, ~15-way ties at P2
+                c[...] = (rng.integers(-4000, 4001, c.shape) * 1e-6).astype(np.float32)
+        cls_l.append(cls)
+        reg_l.append(reg)
+    cls_b = [T(np.concatenate([cls_l[0][l], cls_l[1][l]], 0), dev) for l in range(5)]
+    reg_b = [T(np.concatenate([reg_l[0][l], reg_l[1][l]], 0), dev) for l in range(5)]
+    tcfg = wrap(dict(pre_nms=pre, post_nms=post, max_num=mx, nms_iou=thr, min_bbox_size=0.0))
+    props, scores, _ = head.predict_bboxes_from_output(cls_b, reg_b, [inputs.img_meta()] * 2, tcfg)
+    anchors = [oracle.anchor_grid(s, [8], [0.5, 1.0, 2.0], s, gr) for s, gr in zip(inputs.FPN_STRIDES, inputs.FPN_GRIDS)]
+    for i in range(2):
+        # identical scores on both sides (the device's sigmoid), so the order is comparable
+        sc = [torch.sigmoid(cls_b[l][i]).reshape(-1).cpu().numpy() for l in range(5)]
+        b, s = oracle.rpn_predict_single_image([c[0] for c in cls_l[i]], [r[0] for r in reg_l[i]], anchors,
+                                               inputs.IMG_SHAPE, 0.0, pre, post, mx, thr, scores=sc)
+        pb, ps = props[i].cpu().numpy(), scores[i].cpu().numpy()
+        assert pb.shape == b.shape, (case, i, pb.shape, b.shape)
+        np.testing.assert_allclose(ps, s, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(pb, b, rtol=1e-5, atol=1e-3)
 
 
 # ----------------------------------------------------------------- a12

@@ -92,6 +92,24 @@ int32_t frh_tl_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stri
                           int32_t* keep_counts, void* workspace, size_t ws_bytes, void* stream);
 int32_t frh_tl_nms_timeline(void* stamps);
 
+/* The product RPN proposals rebuilt with segment-0 top-k timestamps
+ * (tools/csrc/topk_timeline.hip): same arguments as frh_rpn_proposals_workspace /
+ * frh_rpn_proposals / frh_rpn_proposals_nms_view; frh_tl_topk_timeline sets the stamp
+ * buffer (uint64 [2048] wall_clock64 ticks: [4 g + 0..2] per collect workgroup g,
+ * [1024 + 0..7] the last workgroup; nullptr = off). */
+size_t frh_tl_rpn_proposals_workspace(int32_t num_imgs, int32_t num_levels, const int32_t* grid_hw,
+                                      int32_t num_anchors, int32_t pre_nms);
+int32_t frh_tl_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                             const float* const* reg_ptrs, const int32_t* grid_hw, int32_t num_anchors,
+                             int32_t cls_channels, const float* anchors, int64_t anchor_ld, const float* means,
+                             const float* stds, const float* img_hw, const float* min_size, int32_t pre_nms,
+                             int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                             float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
+                             void* stream);
+int32_t frh_tl_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_levels, const int32_t* grid_hw,
+                                      int32_t num_anchors, int32_t pre_nms, int64_t* out);
+int32_t frh_tl_topk_timeline(void* stamps);
+
 #ifdef __cplusplus
 }
 #endif

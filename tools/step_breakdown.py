@@ -18,7 +18,7 @@ CLASSES = [
     ('RoIAlign forward', ('roi_align_fwd',)),
     ('RoIAlign backward', ('roi_align_bwd',)),
     ('NMS', ('nms_',)),
-    ('segmented top-k', ('tk_',)),
+    ('segmented top-k (+ fused sort/decode, label apply)', ('tk_', 'rpn_select', 'sampler_select')),
     ('RPN select/decode/merge', ('rpn_',)),
     ('assignment', ('assign_',)),
     ('sampler compaction', ('chunk_',)),
@@ -69,7 +69,9 @@ def main():
     out = {'window_ms_per_step': (t1 - t0) / 1e6 / k, 'gpu_busy_ms_per_step': busy / 1e6 / k,
            'classes_us_per_step': {c: round(v / 1e3 / k, 1) for c, v in sorted(per_class.items(), key=lambda x: -x[1])},
            'top_kernels_us_per_step': [(n[:90], c // k, round(ns / 1e3 / k, 1)) for n, (c, ns) in
-                                       sorted(per_name.items(), key=lambda x: -x[1][1])[:30]]}
+                                       sorted(per_name.items(), key=lambda x: -x[1][1])[:30]],
+           'frh_kernels_us_per_step': [(n[:90], c // k, round(ns / 1e3 / k, 1)) for n, (c, ns) in
+                                       sorted(per_name.items(), key=lambda x: -x[1][1]) if 'frh::' in n]}
     txt = json.dumps(out, indent=1)
     if args.out:
         open(args.out, 'w').write(txt + '\n')
