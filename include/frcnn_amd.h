@@ -224,6 +224,43 @@ int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride,
                        int32_t* keep, int64_t keep_seg_stride, int32_t* keep_counts,
                        void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- a11: class-wise batched multiclass NMS ------------------------------------
+ * Replaces utils.multiclass_nms + batched_nms (lib/utils.py:211-269), called per
+ * image by anchor_head.py:207-262, fcos_head.py:566-627, bbox_head.py:122-146 --
+ * here for B images at once, one NMS segment per (image, class).  Per image b:
+ * boxes [n_max][4] (box_per_class = 0) or [n_max][4 * C] viewed (n, 4, C), scores
+ * [n_max][C], optional score_factor [n_max] (or [n_max][C] with sf_per_class, official
+ * mode) and row_valid [n_max] (0 = a row the reference removed before the call), rows
+ * < num_rows[b] (device int32).
+ * channel_mask [C] (device uint8) = the nms_channel set; mode 0 official (every
+ * (row, class) pair), 1 strict (argmax class per row); pairs need score >=
+ * min_score; the score is multiplied by score_factor after that test.
+ * by_class = 1: one segment per (image, class); 0: one per image (the reference's
+ * single pass; needed when a candidate coordinate is < 0).  Two calls: prepare
+ * (candidates + per-segment sort; one stream sync; info[0] = the largest segment,
+ * info[1] = 1 if a candidate coordinate is < 0 -- with by_class = 1 the caller then
+ * redoes prepare with by_class = 0), then finish (same mode / by_class; scores
+ * needed in strict mode) with an NMS workspace of frh_mcnms_nms_workspace(...,
+ * info[0]) bytes: torchvision nms per segment,
+ * the keeps of all classes merged in (score desc, candidate asc) order, the first
+ * max_num (<= 0: all) written to out_boxes [B][out_cap][4], out_scores [B][out_cap],
+ * out_labels [B][out_cap] (the class index), out_counts [B] (device). */
+size_t frh_mcnms_workspace(int32_t num_imgs, int32_t num_classes, int64_t n_max);
+int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int64_t n_max, const int32_t* num_rows,
+                          const float* boxes, int64_t box_img_stride, int32_t box_per_class,
+                          const float* scores, int64_t score_img_stride, const float* score_factor,
+                          int64_t sf_img_stride, int32_t sf_per_class, const uint8_t* row_valid,
+                          int64_t valid_img_stride, const uint8_t* channel_mask, int32_t mode,
+                          int32_t by_class, float min_score, void* workspace, size_t ws_bytes,
+                          int32_t* info, void* stream);
+size_t frh_mcnms_nms_workspace(int32_t num_imgs, int32_t num_classes, int32_t max_count);
+int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64_t n_max, int32_t max_count,
+                         const float* boxes, int64_t box_img_stride, int32_t box_per_class,
+                         const float* scores, int64_t score_img_stride, int32_t mode, int32_t by_class,
+                         double nms_iou, int32_t max_num, float* out_boxes, float* out_scores,
+                         int64_t* out_labels, int32_t* out_counts, int64_t out_cap, void* workspace,
+                         size_t ws_bytes, void* nms_ws, size_t nms_ws_bytes, void* stream);
+
 /* ---- a13/a14: BasicRoIExtractor.map_rois_to_levels + RoIAlign ----------------
  * level = clamp(floor(log2(sqrt((x2-x1+1)(y2-y1+1))/finest_scale + 1e-6)),
  * 0, L-1) (lib/region.py:256-264).  rois [K,5] = (batch_idx, x1, y1, x2, y2)

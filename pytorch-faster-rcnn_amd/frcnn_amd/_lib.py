@@ -60,6 +60,12 @@ SIGNATURES = {
     'frh_nms_workspace': (c_size, [c_i32, c_i32]),
     'frh_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, c_f64, c_i32, c_vp, c_i64, c_vp, c_vp, c_size,
                                c_vp]),
+    'frh_mcnms_workspace': (c_size, [c_i32, c_i32, c_i64]),
+    'frh_mcnms_prepare': (c_i32, [c_i32, c_i32, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i32,
+                                  c_vp, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, P(c_i32), c_vp]),
+    'frh_mcnms_nms_workspace': (c_size, [c_i32, c_i32, c_i32]),
+    'frh_mcnms_finish': (c_i32, [c_i32, c_i32, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i32, c_f64,
+                                 c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_size, c_vp, c_size, c_vp]),
     'frh_roi_level_map': (c_i32, [c_vp, c_i64, c_f32, c_i32, c_vp, c_vp]),
     'frh_roi_align_fwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,
                                   c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),

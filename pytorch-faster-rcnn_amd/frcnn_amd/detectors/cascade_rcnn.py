@@ -105,5 +105,4 @@ class CascadeRCNN(nn.Module):
                 props = head.refine_bboxes(props, labels, list(reg_outs), None, img_metas)
         per_img = utils.unpack_multi_result(stage_cls)
         mean_cls = [sum(c) / self.num_stages for c in per_img]
-        return utils.unpack_multi_result(utils.multi_apply(self.rcnn_head[-1].predict_bboxes_single_image, props,
-                                                           mean_cls, list(reg_outs), img_sizes, cfg.rcnn))
+        return self.rcnn_head[-1].predict_bboxes_batched(props, mean_cls, list(reg_outs), img_sizes, cfg.rcnn)

@@ -143,8 +143,10 @@ class AnchorHead(nn.Module):
         return self.loss(cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg)
 
     # ------------------------------------------------------------ inference (multi-class heads)
-    def predict_single_image(self, level_cls_outs, level_reg_outs, level_anchors, img_meta, test_cfg):
-        """anchor_head.py:207-262: per-level top-k, decode, min-size filter, multiclass NMS."""
+    def image_candidates(self, level_cls_outs, level_reg_outs, level_anchors, img_meta, test_cfg):
+        """anchor_head.py:215-249 for one image: per-level top-k by the best class score,
+        decode + clamp.  Returns scores [C, n], boxes [4, n] and the min-size mask [n] (or
+        None) -- rows the reference drops stay in place, masked (no host sync)."""
         cls_outs = [c.reshape(self.cls_channels, -1) for c in level_cls_outs]
         reg_outs = [r.reshape(4, -1) for r in level_reg_outs]
         anchors = [a.reshape(4, -1) for a in level_anchors]
@@ -157,33 +159,52 @@ class AnchorHead(nn.Module):
                 mx = sc.max(0)[0] if self.use_sigmoid else sc[1:, :].max(0)[0]
                 _, idx = mx.topk(test_cfg.pre_nms)
                 sc, ro, an = sc[:, idx], ro[:, idx], an[:, idx]
-            bx = utils.param2bbox(an, ro, self.target_means, self.target_stds, img_size)
-            if min_size > 0:
-                keep = ((bx[2] - bx[0] + 1) >= min_size) & ((bx[3] - bx[1] + 1) >= min_size)
-                sc, bx = sc[:, keep], bx[:, keep]
             scores.append(sc)
-            boxes.append(bx)
+            boxes.append(utils.param2bbox(an, ro, self.target_means, self.target_stds, img_size))
         sc, bx = torch.cat(scores, 1), torch.cat(boxes, 1)
+        valid = None
+        if min_size > 0:
+            valid = ((bx[2] - bx[0] + 1) >= min_size) & ((bx[3] - bx[1] + 1) >= min_size)
+        return sc, bx, valid
+
+    def _nms_labels(self):
         if self.use_sigmoid:
-            labels, adjust = list(range(0, self.num_classes - 1)), 1
-        else:
-            labels, adjust = list(range(1, self.num_classes)), 0
-        kb, ks, kl = utils.multiclass_nms(bx.t(), sc.t(), labels, test_cfg.nms_iou, test_cfg.min_score,
-                                          test_cfg.max_per_img, mode=test_cfg.get('nms_type', 'official'))
-        return kb.t(), ks, kl + adjust
+            return list(range(0, self.num_classes - 1)), 1
+        return list(range(1, self.num_classes)), 0
+
+    def predict_single_image(self, level_cls_outs, level_reg_outs, level_anchors, img_meta, test_cfg):
+        """anchor_head.py:207-262: per-level top-k, decode, min-size filter, multiclass NMS."""
+        return [x[0] for x in self._predict_batch([self.image_candidates(level_cls_outs, level_reg_outs,
+                                                                         level_anchors, img_meta, test_cfg)],
+                                                  test_cfg)]
+
+    def _predict_batch(self, cands, test_cfg):
+        """One class-wise batched multiclass NMS (csrc/mcnms.hip) over the images' candidates
+        (every image has the same row count: the per-level top-k sizes)."""
+        labels, adjust = self._nms_labels()
+        scores = torch.stack([sc.t() for sc, _, _ in cands])
+        boxes = torch.stack([bx.t() for _, bx, _ in cands])
+        valid = None
+        if any(v is not None for _, _, v in cands):
+            valid = torch.stack([v if v is not None else torch.ones_like(sc[0], dtype=torch.bool)
+                                 for sc, _, v in cands])
+        res = ops.multiclass_nms_batched(boxes, scores, labels, test_cfg.nms_iou, test_cfg.min_score,
+                                         test_cfg.max_per_img, mode=test_cfg.get('nms_type', 'official'),
+                                         row_valid=valid)
+        return [[kb.t() for kb, _, _ in res], [ks for _, ks, _ in res], [kl + adjust for _, _, kl in res]]
 
     def predict_bboxes(self, feats, img_metas, test_cfg):
         cls_outs, reg_outs = self.forward(feats)
         return self.predict_bboxes_from_output(cls_outs, reg_outs, img_metas, test_cfg)
 
     def predict_bboxes_from_output(self, cls_outs, reg_outs, img_metas, test_cfg):
+        """anchor_head.py:264-289 batched over the images: per-image candidates (device
+        ops, no sync), then ONE multiclass NMS launch sequence for all images."""
         grid_sizes = [tuple(c.shape[-2:]) for c in cls_outs]
         level_anchors = self.create_anchors(grid_sizes)
-        preds = []
-        for i, meta in enumerate(img_metas):
-            preds.append(self.predict_single_image([c[i] for c in cls_outs], [r[i] for r in reg_outs],
-                                                   level_anchors, meta, test_cfg))
-        return utils.unpack_multi_result(preds)
+        cands = [self.image_candidates([c[i] for c in cls_outs], [r[i] for r in reg_outs], level_anchors, meta,
+                                       test_cfg) for i, meta in enumerate(img_metas)]
+        return self._predict_batch(cands, test_cfg)
 
     def to(self, *args, **kwargs):
         return super().to(*args, **kwargs)

@@ -4,7 +4,7 @@ import logging
 import torch
 from torch import nn
 
-from .. import losses, utils
+from .. import losses, ops, utils
 from ..bbox import bbox_targets_batched
 
 
@@ -84,15 +84,31 @@ class BBoxHead(nn.Module):
 
     def predict_bboxes_single_image(self, props, cls_out, reg_out, img_size=None, cfg=None):
         """bbox_head.py:122-146: softmax, per-class decode, multiclass NMS."""
+        out = self.predict_bboxes_batched([props], [cls_out], [reg_out], [img_size], cfg)
+        return out[0][0], out[1][0], out[2][0]
+
+    def predict_bboxes_batched(self, props, cls_outs, reg_outs, img_sizes, cfg):
+        """bbox_head.py:148-158 (predict_bboxes over the images) with ONE class-wise batched
+        multiclass NMS (csrc/mcnms.hip): per image softmax + per-class decode (device ops),
+        rows padded to the largest image, num_rows from the host-known shapes."""
+        if self.use_sigmoid:
+            raise NotImplementedError('Need to be implemented')
         with torch.no_grad():
-            if self.use_sigmoid:
-                raise NotImplementedError('Need to be implemented')
-            score = cls_out.softmax(dim=1)
-            preds = utils.batched_param2bbox(props, reg_out.t(), self.target_means, self.target_stds, img_size)
-            preds, score, label = utils.multiclass_nms(preds.t(), score, range(1, self.num_classes), cfg.nms_iou,
-                                                       cfg.min_score, cfg.max_per_img,
-                                                       mode=cfg.get('nms_type', 'official'))
-        return preds.t(), score, label
+            B = len(props)
+            n = [int(c.shape[0]) for c in cls_outs]
+            n_max, C = max(n), int(cls_outs[0].shape[1])
+            dev = cls_outs[0].device
+            dec = [utils.batched_param2bbox(props[b], reg_outs[b].t(), self.target_means, self.target_stds,
+                                            img_sizes[b]).t() for b in range(B)]  # [n, 4] agnostic / [n, 4C]
+            scores = cls_outs[0].new_zeros(B, n_max, C)
+            boxes = cls_outs[0].new_zeros(B, n_max, dec[0].shape[1])
+            for b in range(B):
+                scores[b, :n[b]] = cls_outs[b].softmax(dim=1)
+                boxes[b, :n[b]] = dec[b]
+            res = ops.multiclass_nms_batched(boxes, scores, range(1, self.num_classes), cfg.nms_iou, cfg.min_score,
+                                             cfg.max_per_img, mode=cfg.get('nms_type', 'official'),
+                                             num_rows=torch.tensor(n, dtype=torch.int32).to(dev))
+        return [[kb.t() for kb, _, _ in res], [ks for _, ks, _ in res], [kl for _, _, kl in res]]
 
 
 class HeadOutputs(list):

@@ -334,8 +334,10 @@ class FCOSHead(nn.Module):
                               utils.split_by_image(ctr_outs), *tars)
 
     # ------------------------------------------------------------ inference
-    def predict_single_image(self, cls_outs, reg_outs, ctr_outs, img_meta, test_cfg):
-        """fcos_head.py:566-627."""
+    def image_candidates(self, cls_outs, reg_outs, ctr_outs, img_meta, test_cfg):
+        """fcos_head.py:566-620 for one image: per-level decode, clamp, min-size filter, top-k
+        by (centerness x) best class score.  Returns boxes [4, n], scores [C, n] and the
+        centerness factor [n] (or None)."""
         use_center = self.use_centerness
         min_size = img_meta['scale_factor'] * test_cfg['min_bbox_size']
         img_size = img_meta['img_shape'][:2]
@@ -366,14 +368,38 @@ class FCOSHead(nn.Module):
         sc = torch.cat(scores, 1)
         bx = torch.cat(bboxes, 1)
         ct = torch.cat(ctrs, 1).view(-1) if use_center else None
-        kb, ks, kl = utils.multiclass_nms(bx.t(), sc.t(), list(range(0, self.cls_channels)), test_cfg['nms_iou'],
-                                          test_cfg['min_score'], test_cfg['max_per_img'], ct,
-                                          mode=test_cfg.get('nms_type', 'official'))
-        return kb.t(), ks, kl + 1
+        return bx, sc, ct
+
+    def predict_single_image(self, cls_outs, reg_outs, ctr_outs, img_meta, test_cfg):
+        """fcos_head.py:566-627."""
+        out = self._predict_batch([self.image_candidates(cls_outs, reg_outs, ctr_outs, img_meta, test_cfg)],
+                                  test_cfg)
+        return out[0][0], out[1][0], out[2][0]
+
+    def _predict_batch(self, cands, test_cfg):
+        """ONE class-wise batched multiclass NMS (csrc/mcnms.hip) over the images' candidates,
+        rows padded to the largest image (fcos_head.py:621-627)."""
+        B = len(cands)
+        n = [int(bx.shape[1]) for bx, _, _ in cands]
+        n_max = max(n)
+        ref = cands[0][1]
+        scores = ref.new_zeros(B, n_max, self.cls_channels)
+        boxes = ref.new_zeros(B, n_max, 4)
+        ctr = ref.new_zeros(B, n_max) if self.use_centerness else None
+        for b, (bx, sc, ct) in enumerate(cands):
+            scores[b, :n[b]] = sc.t()
+            boxes[b, :n[b]] = bx.t()
+            if ctr is not None:
+                ctr[b, :n[b]] = ct
+        res = ops.multiclass_nms_batched(boxes, scores, list(range(0, self.cls_channels)), test_cfg['nms_iou'],
+                                         test_cfg['min_score'], test_cfg['max_per_img'], ctr,
+                                         mode=test_cfg.get('nms_type', 'official'),
+                                         num_rows=torch.tensor(n, dtype=torch.int32).to(ref.device))
+        return [[kb.t() for kb, _, _ in res], [ks for _, ks, _ in res], [kl + 1 for _, _, kl in res]]
 
     def predict_bboxes(self, feats, img_metas, test_cfg):
         cls_outs, reg_outs, ctr_outs = self.forward(feats)
-        return utils.unpack_multi_result(utils.multi_apply(
-            self.predict_single_image, utils.split_by_image(cls_outs), utils.split_by_image(reg_outs),
-            utils.split_by_image(ctr_outs) if self.use_centerness else [None] * len(img_metas), list(img_metas),
-            test_cfg))
+        ctrs = utils.split_by_image(ctr_outs) if self.use_centerness else [None] * len(img_metas)
+        cands = [self.image_candidates(c, r, t, m, test_cfg) for c, r, t, m in
+                 zip(utils.split_by_image(cls_outs), utils.split_by_image(reg_outs), ctrs, list(img_metas))]
+        return self._predict_batch(cands, test_cfg)

@@ -397,6 +397,70 @@ def nms(boxes, scores, iou_threshold):
     return order[keep[0, :k].long()]
 
 
+# ---------------------------------------------------------------- class-wise batched multiclass NMS (a11)
+def multiclass_nms_batched(boxes, scores, nms_channel, nms_iou, min_score=-1, max_num=None, score_factor=None,
+                           mode='official', num_rows=None, row_valid=None):
+    """utils.multiclass_nms (lib/utils.py:224-269) for B images in one frh_mcnms call.
+
+    boxes [B, n, 4] or [B, n, 4 * C] (viewed (n, 4, C)), scores [B, n, C], score_factor
+    [B, n] or [B, n, C] (official) or None, num_rows int32 [B] (device; None = n each),
+    row_valid bool [B, n] (False = a row the reference drops before the call) or None.
+    Returns per-image lists of (boxes [k, 4], scores [k], labels int64 [k]) in the
+    reference's keep order.  Two host syncs per call (segment sizes, output counts)."""
+    if mode not in ('official', 'strict'):
+        raise AssertionError('unknown mode {}'.format(mode))
+    _need_cuda(boxes, scores)
+    B, n, C = scores.shape
+    dev = scores.device
+    boxes, scores = _f32(boxes).contiguous(), _f32(scores).contiguous()
+    per_class = int(boxes.shape[2] != 4)
+    if per_class and boxes.shape[2] != 4 * C:
+        raise AssertionError('boxes must be [B, n, 4] or [B, n, 4 * classes]')
+    empty = [(boxes.new_zeros(0, 4), scores.new_zeros(0), torch.zeros(0, dtype=torch.long, device=dev))
+             for _ in range(B)]
+    if n == 0 or max_num == 0:
+        return empty
+    if num_rows is None:
+        num_rows = torch.full((B,), n, dtype=torch.int32, device=dev)
+    chan = torch.zeros(C, dtype=torch.uint8)
+    chan[[c for c in nms_channel if 0 <= c < C]] = 1
+    chan = chan.to(dev)
+    sf, sf_pc = None, 0
+    if score_factor is not None:
+        sf = _f32(score_factor).contiguous()
+        sf_pc = int(sf.dim() == 3)
+        if sf_pc and mode == 'strict':
+            raise AssertionError('strict mode takes a per-row score factor')
+    valid = row_valid.to(torch.uint8).contiguous() if row_valid is not None else None
+    ws = workspace(_lib.query('frh_mcnms_workspace', B, C, n), dev)
+    st = stream_of(scores)
+    info = (ctypes.c_int32 * 2)()
+    m = 1 if mode == 'strict' else 0
+    for by_class in (1, 0):  # a negative candidate coordinate: the reference's single pass, by image
+        call('frh_mcnms_prepare', B, C, n, ptr(num_rows), ptr(boxes), boxes.stride(0), per_class, ptr(scores),
+             scores.stride(0), ptr(sf), sf.stride(0) if sf is not None else 0, sf_pc, ptr(valid),
+             valid.stride(0) if valid is not None else 0, ptr(chan), m, by_class, float(min_score), ptr(ws),
+             ws.numel(), info, st)
+        if not info[1]:
+            break
+    P = int(info[0])
+    if P == 0:
+        return empty
+    G = C if by_class else 1
+    mx = int(max_num) if max_num is not None else -1
+    cap = min(mx, G * P) if mx > 0 else G * P
+    ob = torch.empty(B, cap, 4, dtype=torch.float32, device=dev)
+    osc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+    ol = torch.empty(B, cap, dtype=torch.int64, device=dev)
+    oc = torch.empty(B, dtype=torch.int32, device=dev)
+    nws = workspace(_lib.query('frh_mcnms_nms_workspace', B, C, P), dev)
+    call('frh_mcnms_finish', B, C, n, P, ptr(boxes), boxes.stride(0), per_class, ptr(scores), scores.stride(0), m,
+         by_class, float(nms_iou), mx, ptr(ob), ptr(osc), ptr(ol), ptr(oc), cap, ptr(ws), ws.numel(), ptr(nws),
+         nws.numel(), st)
+    counts = oc.cpu().tolist()
+    return [(ob[b, :k], osc[b, :k], ol[b, :k]) for b, k in enumerate(counts)]
+
+
 # ---------------------------------------------------------------- RoI level map + RoIAlign (a13/a14)
 def roi_level_map(rois, finest_scale, num_levels):
     _need_cuda(rois)

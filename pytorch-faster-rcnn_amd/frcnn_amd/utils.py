@@ -127,39 +127,18 @@ def batched_nms(bbox, score, label, nms_iou, class_agnostic=False):
 
 def multiclass_nms(bbox, score, nms_channel, nms_iou, min_score=-1, max_num=None, score_factor=None,
                    mode='official'):
-    """utils.py:224-269: candidate selection (official / strict) + batched_nms + max_num."""
+    """utils.py:224-269 for one image: the class-wise batched kernel (ops.multiclass_nms_batched,
+    csrc/mcnms.hip) with a batch of one."""
     if mode not in ('official', 'strict'):
         raise AssertionError('unknown mode {}'.format(mode))
     if score.dim() != 2:
         raise AssertionError('multiclass_nms only applies to multi-channel score')
-    ncls = score.shape[1]
-    n = bbox.shape[0]
-    simple = bbox.shape[1] == 4
-    channels = torch.tensor(list(nms_channel), dtype=torch.long, device=score.device)
-    if mode == 'official':
-        label = torch.full_like(score, -1, dtype=torch.long)
-        label[:, channels] = channels
-        chosen = label != -1
-        boxes = bbox.unsqueeze(2).expand(-1, -1, ncls) if simple else bbox.view(n, 4, ncls)
-        boxes = boxes.permute(0, 2, 1)
-        chosen = (score >= min_score) & chosen
-        if score_factor is not None:
-            sf = score_factor.unsqueeze(1) if score_factor.dim() == 1 else score_factor
-            score = score * sf
-        nms_bbox, nms_score, nms_label = boxes[chosen], score[chosen], label[chosen]
-    else:
-        score, label = score.max(1)
-        chosen = torch.isin(label, channels)
-        if not simple:
-            bbox = bbox.view(n, 4, ncls)[torch.arange(n, device=bbox.device), :, label]
-        chosen = (score >= min_score) & chosen
-        if score_factor is not None:
-            score = score * score_factor
-        nms_bbox, nms_score, nms_label = bbox[chosen, :], score[chosen], label[chosen]
-    kb, ks, kl = batched_nms(nms_bbox, nms_score, nms_label, nms_iou)
-    if max_num is not None and ks.numel() > max_num:
-        kb, ks, kl = kb[:max_num], ks[:max_num], kl[:max_num]
-    return kb, ks, kl
+    sf = None
+    if score_factor is not None:  # [n] / [n, 1] per row, [n, C] per (row, class)
+        per_row = score_factor.dim() == 1 or score_factor.shape[-1] == 1
+        sf = score_factor.reshape(1, -1) if per_row else score_factor.unsqueeze(0)
+    return ops.multiclass_nms_batched(bbox.unsqueeze(0), score.unsqueeze(0), nms_channel, nms_iou, min_score,
+                                      max_num, sf, mode)[0]
 
 
 def one_hot_embedding(label, n_cls):

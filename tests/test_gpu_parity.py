@@ -643,6 +643,114 @@ def test_multiclass_nms_vs_reference(dev, golden, i):
     np.testing.assert_array_equal(kl.cpu().numpy(), g['labels_{}'.format(i)])
 
 
+def _mcnms_batch(seed, mode, per_class, factor, neg, B=3, C=9):
+    rng = np.random.default_rng(seed)
+    rows = [300, 0, 257][:B]
+    n = 320
+    ctr = rng.uniform(60, 900, (10, 2))
+    boxes, scores, sfs, valid = [], [], [], []
+    for b in range(B):
+        k = rng.integers(0, 10, n)
+        wh = rng.uniform(20, 160, (n, 2))
+        c = ctr[k] + rng.normal(0, 12, (n, 2))
+        base = np.stack([c[:, 0] - wh[:, 0] / 2, c[:, 1] - wh[:, 1] / 2, c[:, 0] + wh[:, 0] / 2,
+                         c[:, 1] + wh[:, 1] / 2], 1)
+        if neg:
+            base[:40] -= 120.0  # coordinates < 0: the by-image fallback
+        else:
+            base = np.clip(base, 0.0, 999.0)
+        if per_class:
+            bx = np.clip(base[:, :, None] + rng.normal(0, 3, (n, 4, C)), 0.0 if not neg else -1e9, 999.0)
+            bx = bx.reshape(n, 4 * C)
+        else:
+            bx = base
+        logits = rng.normal(0, 2, (n, C))
+        sc = 1 / (1 + np.exp(-logits)) if mode == 'strict' else np.exp(logits) / np.exp(logits).sum(1, keepdims=True)
+        sc = np.round(sc * 64) / 64  # exact ties
+        boxes.append(bx.astype(np.float32))
+        scores.append(sc.astype(np.float32))
+        sfs.append(None if factor is None else rng.choice([0.5, 0.75, 1.0], (n,) if factor == 'row' else (n, C))
+                   .astype(np.float32))
+        valid.append(rng.uniform(size=n) > 0.1)
+    chans = list(range(1, C)) if mode == 'official' else [c for c in range(C) if c != 4]
+    return rows, n, boxes, scores, sfs, valid, chans
+
+
+@pytest.mark.parametrize('mode,per_class,factor,neg', [('official', False, None, False),
+                                                       ('official', True, 'row', False),
+                                                       ('official', False, 'class', False),
+                                                       ('strict', False, 'row', False),
+                                                       ('strict', True, None, False),
+                                                       ('official', False, None, True),
+                                                       ('strict', True, 'row', True)])
+def test_mcnms_batched_vs_per_image_oracle(dev, mode, per_class, factor, neg):
+    """a11 as one class-wise batched kernel (csrc/mcnms.hip): 3 images (one empty) of padded
+    rows with removed rows masked (row_valid), score ties (scores on a 1/64 grid), per-row /
+    per-class score factors, class-specific boxes, a channel subset and max_num = 50, against
+    the oracle's per-image restatement of utils.multiclass_nms (lib/utils.py:211-269) on
+    the rows the reference would see: bit-exact boxes, scores, labels and order.  neg: some
+    coordinates < 0, where the reference's shifted classes can overlap -> one segment per
+    image."""
+    from frcnn_amd import ops
+    rows, n, boxes, scores, sfs, valid, chans = _mcnms_batch(70 + 3 * int(neg), mode, per_class, factor, neg)
+    B = len(rows)
+    rv = np.stack(valid)
+    for b in range(B):
+        rv[b, rows[b]:] = False
+    sf = None if factor is None else T(np.stack(sfs), dev)
+    res = ops.multiclass_nms_batched(T(np.stack(boxes), dev), T(np.stack(scores), dev), chans, 0.5, 0.05, 50, sf,
+                                     mode=mode, num_rows=torch.tensor(rows, dtype=torch.int32, device=dev),
+                                     row_valid=T(rv, dev))
+    total = 0
+    for b in range(B):
+        keep = rv[b, :rows[b]]
+        kb, ks, kl = oracle.multiclass_nms(boxes[b][:rows[b]][keep], scores[b][:rows[b]][keep], chans, 0.5, 0.05, 50,
+                                           None if factor is None else sfs[b][:rows[b]][keep], mode=mode)
+        gb, gs, gl = (x.cpu().numpy() for x in res[b])
+        np.testing.assert_array_equal(gb, kb)
+        np.testing.assert_array_equal(gs, ks)
+        np.testing.assert_array_equal(gl, kl)
+        total += len(ks)
+    assert total > 20
+
+
+def test_retina_predict_batched_equals_per_image(dev):
+    """RetinaHead.predict_bboxes_from_output on 2 images (one batched multiclass NMS) equals
+    predict_single_image per image, with the min-size filter active (masked rows)."""
+    from frcnn_amd.config import ConfigDict
+    head = _retina_head(dev)
+    cfg = ConfigDict(dict(pre_nms=1000, min_bbox_size=8, min_score=0.05, nms_iou=0.5, nms_type='official',
+                          max_per_img=100))
+    cls, reg = inputs.head_outputs(951, inputs.RETINA_GRIDS, 9, 20, batch=2, cls_scale=2.0, reg_scale=0.6)
+    cls, reg = [T(c, dev) for c in cls], [T(r, dev) for r in reg]
+    metas = [inputs.img_meta(), dict(inputs.img_meta(), scale_factor=1.2)]
+    bb, ss, ll = head.predict_bboxes_from_output(cls, reg, metas, cfg)
+    anchors = head.create_anchors(inputs.RETINA_GRIDS)
+    for i in range(2):
+        kb, ks, kl = head.predict_single_image([c[i] for c in cls], [r[i] for r in reg], anchors, metas[i], cfg)
+        assert ks.numel() > 10
+        assert torch.equal(bb[i], kb) and torch.equal(ss[i], ks) and torch.equal(ll[i], kl)
+
+
+def test_bbox_head_predict_batched_equals_per_image(dev):
+    """BBoxHead.predict_bboxes_batched (ragged proposals per image, one batched multiclass NMS)
+    equals predict_bboxes_single_image per image."""
+    from frcnn_amd.config import ConfigDict
+    from frcnn_amd.heads.bbox_head import BBoxHead
+    torch.manual_seed(0)
+    head = BBoxHead(21, target_means=[0.0] * 4, target_stds=[0.1, 0.1, 0.2, 0.2])
+    cfg = ConfigDict(dict(min_score=0.05, nms_iou=0.5, max_per_img=100))
+    props = [T(inputs.random_boxes(40 + i, k, min_wh=8, max_wh=300), dev) for i, k in enumerate((600, 437))]
+    cls = [torch.randn(p.shape[1], 21, device=dev) * 3 for p in props]
+    reg = [torch.randn(p.shape[1], 84, device=dev) * 0.3 for p in props]
+    sizes = [(600, 1000), (580, 990)]
+    bb, ss, ll = head.predict_bboxes_batched(props, cls, reg, sizes, cfg)
+    for i in range(2):
+        kb, ks, kl = head.predict_bboxes_single_image(props[i], cls[i], reg[i], sizes[i], cfg)
+        assert ks.numel() > 10
+        assert torch.equal(bb[i], kb) and torch.equal(ss[i], ks) and torch.equal(ll[i], kl)
+
+
 # ----------------------------------------------------------------- a15 Retina dense path, a17 refine
 def _retina_head(dev):
     from frcnn_amd.heads.retina_head import RetinaHead
