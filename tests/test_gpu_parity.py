@@ -356,6 +356,46 @@ def test_nms_keep_bit_exact(dev, n, thr):
     np.testing.assert_array_equal(keep, oracle.nms(boxes, scores, thr))
 
 
+@pytest.mark.parametrize('pattern', ['all_kept', 'chain', 'late_suppressors', 'block_edges'])
+def test_nms_scan_adversarial(dev, pattern):
+    """Deterministic inputs aimed at the scan's resolver / loader hand-offs (nms.hip
+    'Progress' / sync protocol), n = 5000 (79 column blocks, spans wrap the 8-slot ring):
+      all_kept          disjoint boxes: every block keeps 64 rows, so the loaders fold the
+                        largest possible partial sums and the resolver never idles;
+      chain             box i overlaps i+1 only (IoU 0.6 > 0.5): keeps alternate, every
+                        decision depends on the previous one, across every block edge;
+      late_suppressors  rows of block b suppressed only by kept rows of block b-1 / b-2
+                        (the tiles the resolver ORs itself, not the loaders' fold);
+      block_edges       rows 63 / 64 of each block pair overlap (cross-block chains).
+    Keep lists must equal the oracle's exactly, on each of 3 launches."""
+    from frcnn_amd import ops
+    n = 5000
+    i = np.arange(n, dtype=np.float64)
+    if pattern == 'all_kept':
+        x = (i % 100) * 30.0
+        y = (i // 100) * 30.0
+        boxes = np.stack([x, y, x + 20, y + 20], 1)
+    elif pattern == 'chain':
+        x = i * 2.5  # width 10, shift 2.5: IoU(i, i+1) = 0.6 > 0.5, IoU(i, i+2) = 1/3
+        boxes = np.stack([x, np.zeros(n), x + 10.0, np.full(n, 10.0)], 1)
+    elif pattern == 'late_suppressors':
+        blk, r = i // 64, i % 64
+        x = r * 40.0 + (blk % 2) * 5.0  # row r of block b sits near row r of block b-1 (shift 5 / width 30)
+        y = (blk // 2) * 40.0
+        boxes = np.stack([x, y, x + 30.0, y + 30.0], 1)
+    else:
+        blk, r = i // 64, i % 64
+        x = blk * 50.0 + np.where(r == 63, 30.0, np.where(r == 0, 33.0, r * 0.0 - 1000.0 - r * 40.0))
+        boxes = np.stack([x, np.zeros(n), x + 20.0, np.full(n, 20.0)], 1)
+    boxes = boxes.astype(np.float32)
+    scores = (1.0 - i / n).astype(np.float32)  # already in index order
+    want = oracle.nms(boxes, scores, 0.5)
+    assert 0 < len(want) <= n
+    for _ in range(3):
+        keep = ops.nms(T(boxes, dev), T(scores, dev), 0.5).cpu().numpy()
+        np.testing.assert_array_equal(keep, want)
+
+
 @pytest.mark.parametrize('thr', [0.7, 0.5, 0.3])
 def test_nms_threshold_boundary(dev, thr):
     """Pairs of boxes whose IoU straddles the threshold by a few float ulps: the kernel's
