@@ -67,9 +67,11 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
-  if (pair_ok(f, channels, pooled_h, pooled_w)) {
-    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kPairChunk - 1) / kPairChunk));
-    hipLaunchKernelGGL(roi_align_fwd_pair_kernel<>, grid, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  if (pair_ok(f, channels, pooled_h, pooled_w)) {  // chunk-major XCD order (roi_kernels.h kOrder 1)
+    const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
+    FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
+                       dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (f.lds) {
     const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);

@@ -456,15 +456,26 @@ struct PairLayout {
   static_assert(D * RP + 2 * D < 64, "vmcnt is 6 bits");
 };
 
-// kPW: channel pairs per wave; kHalf: dwords per slab buffer.
-template <int kPW = kPairWave, int kHalf = kPairHalf>
+// kPW: channel pairs per wave; kHalf: dwords per slab buffer.  kOrder 0: grid
+// (K, chunks); 1: a 1-D grid of 8 * ceil(K * chunks / 8) workgroups in which XCD
+// x (= linear id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item
+// list, so each XCD's L2 holds the feature planes of its own channel chunks.
+template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0>
 __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   constexpr int SR = 2;
   __shared__ __attribute__((aligned(16))) float slab[2 * kHalf];
   // the slab as an LDS byte address (integer: no generic-pointer casts)
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
-  const int64_t k = blockIdx.x;
-  const int cw0 = blockIdx.y * 2 * kPW;
+  int64_t k = blockIdx.x;
+  int chunk = blockIdx.y;
+  if (kOrder == 1) {
+    const int64_t G = (c.C + 2 * kPW - 1) / (2 * kPW), total = c.K * G, per = (total + 7) / 8;
+    const int64_t w = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (w >= total) return;
+    chunk = (int)(w / c.K);
+    k = w - (int64_t)chunk * c.K;
+  }
+  const int cw0 = chunk * 2 * kPW;
   const int lane = threadIdx.x & (kWave - 1);
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom(c, lv, k);

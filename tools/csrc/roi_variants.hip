@@ -1445,7 +1445,7 @@ using namespace frh;
 
 // variant: 0 = direct gather, 10 = per-RoI LDS windows (9, 11, 12, 15-19: its
 // stage-size / chunk / occupancy variants), 20 = channel pairs (the product default;
-// FRH_PAIR_PW = 4 / 16 / 32 / 64 pairs per wave instead of 8), 25 / 26 = persistent
+// FRH_PAIR_PW = 4 / 16 / 32 / 64 pairs per wave instead of 8; 21 chunk-major XCD order), 25 / 26 = persistent
 // item-walking pair waves, 30-37 = wide-staged (31-34 diagnostics, 35 XCD order,
 // 36 / 37 occupancy), 50 / 51 = grouped union staging (needs the workspace of
 // frh_roi_align_workspace; 51 stamps), -1 = the product's choice.
@@ -1473,7 +1473,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   FRH_REQUIRE(variant == 0 || ((variant >= 9 && variant <= 19 && variant != 13 && variant != 14) && f.lds) ||
-                  ((variant == 50 || variant == 51) && grp_ok) || ((variant == 20 || variant == 25 || variant == 26) && pok) ||
+                  ((variant == 50 || variant == 51) && grp_ok) || ((variant == 20 || variant == 21 || variant == 25 || variant == 26) && pok) ||
                   (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
@@ -1502,6 +1502,10 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (pw == 16) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
     else if (pw == 4) hipLaunchKernelGGL((roi_align_fwd_pair_kernel<4>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
     else hipLaunchKernelGGL((roi_align_fwd_pair_kernel<8>), g2, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 21) {  // pairs, chunk-major XCD order (roi_kernels.h kOrder 1)
+    const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
+                       dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (variant == 25 || variant == 26) {  // 26: registers for 3 waves per SIMD (spills)
     const int G = (channels + 2 * kStrPairs - 1) / (2 * kStrPairs);
     const int64_t nitems = num_rois * G;
