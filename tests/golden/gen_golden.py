@@ -435,6 +435,34 @@ def gen_eval():
     print('wrote eval.json', os.path.getsize(path), 'bytes; AP50', summary['AP50'])
 
 
+def gen_forward_train():
+    """Full forward_train loss dict of the reference's cfg2 model (configs/faster_rcnn_r50_fpn.py
+    built by lib/builder.py, CascadeRCNN.forward_train lib/detectors/cascade_rcnn.py:90-154)
+    on inputs.ftrain_case() with the deterministic inputs.seeded_state weights and
+    np.random.seed(inputs.FTRAIN_NP_SEED) for its samplers.  torchvision's nms / RoIAlign are
+    the shims above (the oracle's restatements).  Only the losses are stored: the weights
+    and inputs are regenerated by the tests from the same seeds."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), '..', 'pytorch-faster-rcnn_amd'))
+    from frcnn_amd.config import Config
+    import lib.builder as rb
+    cfg = Config.fromfile(os.path.join(REF, 'configs', 'faster_rcnn_r50_fpn.py'))
+    cfg.model.backbone.pretrained = False
+    model = rb.build_module(cfg.model, train_cfg=cfg.train_cfg, test_cfg=cfg.test_cfg)
+    sd = inputs.seeded_state({k: tuple(v.shape) for k, v in model.state_dict().items()})
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.train()
+    img, boxes, labels, metas = inputs.ftrain_case()
+    np.random.seed(inputs.FTRAIN_NP_SEED)
+    losses = model.forward_train(torch.from_numpy(img), [torch.from_numpy(b) for b in boxes],
+                                 [torch.from_numpy(l) for l in labels], metas)
+    out = {k: float(v) for k, v in losses.items()}
+    path = os.path.join(HERE, 'ftrain.json')
+    with open(path, 'w') as f:
+        json.dump({'losses': out, 'np_seed': inputs.FTRAIN_NP_SEED, 'config': 'configs/faster_rcnn_r50_fpn.py'}, f,
+                  indent=1)
+    print('wrote ftrain.json', out)
+
+
 def main():
     if not os.path.isdir(os.path.join(REF, 'lib')):
         print('reference not found at {}: nothing to generate (fixtures are committed)'.format(REF))
@@ -455,6 +483,9 @@ def main():
         return 0
     if '--only-eval' in sys.argv:
         gen_eval()
+        return 0
+    if '--only-ftrain' in sys.argv:
+        gen_forward_train()
         return 0
     if '--only-new' in sys.argv:
         import lib.heads.retina_head as retina_mod

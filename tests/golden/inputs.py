@@ -159,3 +159,52 @@ def eval_case():
     gt = {'images': [{'id': int(n[:-4]), 'file_name': n} for n in names], 'annotations': anns,
           'categories': [{'id': c} for c in range(1, 21)]}
     return images, gt
+
+
+# ---------------------------------------------------------------- full forward_train case
+FTRAIN_SHAPE = (256, 384)
+FTRAIN_NP_SEED = 20240607  # np.random.seed before forward_train: the samplers' legacy RNG
+
+
+def seeded_state(shapes):
+    """A deterministic state_dict for a model with these {key: shape} entries (the reference's
+    CascadeRCNN and frcnn_amd's have identical keys / shapes): each tensor from its own
+    PCG64 stream keyed by crc32(key).  Conv / FC weights ~ N(0, 2 / fan_in), the RPN and RCNN
+    output layers ~ N(0, 0.01^2) (scores away from saturation, no exact ties), frozen-BN
+    weights 1 + 0.1 N (0.2 + 0.02 N on each block's last BN and shortcut BN, so the residual
+    stream stays O(1) through 16 blocks), biases / running means 0.05 N, running vars
+    1 + 0.1 U."""
+    import zlib
+    out = {}
+    for key in sorted(shapes):
+        shape = tuple(shapes[key])
+        rng = np.random.default_rng(zlib.crc32(key.encode()))
+        if key.endswith('num_batches_tracked'):
+            out[key] = np.zeros(shape, np.int64)
+            continue
+        if key.endswith('running_var'):
+            v = 1.0 + 0.1 * rng.random(shape)
+        elif key.endswith('running_mean') or key.endswith('bias'):
+            v = 0.05 * rng.standard_normal(shape)
+        elif len(shape) == 1 and (key.endswith('bn3.weight') or key.endswith('downsample.1.weight')):
+            v = 0.2 + 0.02 * rng.standard_normal(shape)  # residual branches / shortcuts damped: bounded stream
+        elif len(shape) == 1:  # BN weight
+            v = 1.0 + 0.1 * rng.standard_normal(shape)
+        elif ('classifier' in key or 'regressor' in key) and ('rpn_head' in key or 'rcnn_head' in key):
+            v = 0.01 * rng.standard_normal(shape)
+        else:
+            v = rng.standard_normal(shape) * np.sqrt(2.0 / float(np.prod(shape[1:])))
+        out[key] = v.astype(np.float32)
+    return out
+
+
+def ftrain_case():
+    """One 256x384 image (N(0,1) pixels) with the 5 boxes of VOC gt set 9 scaled into it: (img
+    [1, 3, H, W] f32, boxes [[4, G] f32], labels [[G] i64], img_metas)."""
+    rng = np.random.default_rng(4242)
+    img = rng.standard_normal((1, 3) + FTRAIN_SHAPE).astype(np.float32)
+    b, l = voc_gts()[9]
+    b = (b * np.float32(0.38)).astype(np.float32)
+    meta = {'img_shape': FTRAIN_SHAPE + (3,), 'pad_shape': FTRAIN_SHAPE + (3,), 'scale_factor': 0.38 * 1.6,
+            'ori_shape': (160, 240, 3)}
+    return img, [b], [l], [meta]

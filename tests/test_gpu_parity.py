@@ -1105,3 +1105,43 @@ def test_graphed_trunk_matches_eager(dev):
         assert not g.matches(imgs)
     finally:
         release_trunk(model)
+
+
+def test_forward_train_loss_dict_vs_reference(dev):
+    """The product's whole cfg2 forward_train against the loss dict the reference produced on
+    the same seeded weights and inputs (tests/golden/ftrain.json; see
+    test_forward_train_loss_dict_oracle_vs_reference).  The trunk (backbone + FPN + RPN head
+    convs) runs on the CPU, as in the fixture, and its outputs enter forward_train through
+    the graphed-trunk hook, so every detection primitive after it -- RPN targets + loss,
+    proposals + NMS, RCNN targets with the numpy-RNG samplers, RoIAlign, the RCNN losses --
+    runs on the HIP path with inputs identical to the reference's.  Only the RCNN FC layers'
+    f32 sums (GPU GEMM vs CPU) differ in rounding: rel 1e-4."""
+    import json
+    import os
+    from frcnn_amd import set_sampler_mode
+    from test_oracle_golden import ftrain_model
+    ref = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'ftrain.json')))
+    model, _ = ftrain_model()
+    img, boxes, labels, metas = inputs.ftrain_case()
+    x = torch.from_numpy(img)
+    with torch.no_grad():
+        feats = model.extract_feat(x)
+        cls, reg = model.rpn_head(feats)
+    model = model.to(dev)
+    trunk = ([f.to(dev) for f in feats], [c.to(dev) for c in cls], [r.to(dev) for r in reg])
+
+    class CpuTrunk(object):  # the graphed-trunk hook of CascadeRCNN.forward_train
+        def matches(self, img_data):
+            return True
+
+        def __call__(self, img_data):
+            return trunk
+
+    model.graphed_trunk = CpuTrunk()
+    set_sampler_mode('numpy')
+    np.random.seed(inputs.FTRAIN_NP_SEED)
+    with torch.no_grad():
+        losses = model.forward_train(x.to(dev), [T(b, dev) for b in boxes], [T(l, dev) for l in labels], metas)
+    assert set(losses) == set(ref['losses'])
+    for k, v in ref['losses'].items():
+        assert float(losses[k]) == pytest.approx(v, rel=1e-4), (k, float(losses[k]), v)
