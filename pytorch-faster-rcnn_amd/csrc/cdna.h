@@ -45,16 +45,17 @@ __device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t r, float* lds, in
 #endif
 }
 
-// the same with the destination given as a wave-uniform LDS byte address
-template <int kBytes>
+// the same with the destination given as a wave-uniform LDS byte address; kAux is
+// the gfx950 cache policy (0 default, 1 sc0, 2 nt, 16 sc1)
+template <int kBytes, int kAux = 0>
 __device__ __forceinline__ void lds_dma_at(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, int voff, int soff) {
 #if defined(__HIP_DEVICE_COMPILE__)
   static_assert(kBytes == 4 || kBytes == 16, "LDS-DMA width");
   auto* p = (__attribute__((address_space(3))) void*)(uintptr_t)lds_addr;
   if constexpr (kBytes == 16)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 16, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 16, voff, soff, 0, kAux);
   else
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 4, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, p, 4, voff, soff, 0, kAux);
 #endif
 }
 

@@ -41,10 +41,11 @@ constexpr int kMaxNmsWords = 256;  // n <= 16384 boxes per segment
 struct NmsThr {
   double thr, mid;
   int tie_up, fast;
+  float hi, lo;  // float bounds around mid (nms_thr): inter > RN(hi * union) => above, < RN(lo * union) => not
 };
 
 static NmsThr nms_thr(double thr) {
-  NmsThr t{thr, 0.0, 0, 0};
+  NmsThr t{thr, 0.0, 0, 0, 0.0f, 0.0f};
   if (!(thr > 0.0 && thr < 1.0)) return t;
   float up = (float)thr;
   if ((double)up <= thr) up = nextafterf(up, 2.0f);
@@ -54,6 +55,12 @@ static NmsThr nms_thr(double thr) {
   memcpy(&bits, &up, 4);
   t.tie_up = (bits & 1u) == 0;
   t.fast = 1;
+  // hi >= mid (1 + 2^-20), lo <= mid (1 - 2^-20): a float product RN(hi * u) is within a
+  // factor (1 +- 2^-24) of hi * u, so for u >= 2^-100 (no underflow) inter > RN(hi * u)
+  // implies inter > mid * u and inter < RN(lo * u) implies inter < mid * u.  Everything
+  // else (IoU within ~1e-6 of thr, tiny / negative / NaN unions) takes the exact test.
+  t.hi = nextafterf((float)(t.mid * (1.0 + 0x1p-20)), 2.0f);
+  t.lo = nextafterf((float)(t.mid * (1.0 - 0x1p-20)), 0.0f);
   return t;
 }
 
@@ -69,6 +76,29 @@ __device__ __forceinline__ bool iou_above(float4 a, float area_a, float4 b, floa
     return (uni > 0.0f) & ((lhs > rhs) | ((lhs == rhs) & (T.tie_up != 0)));
   }
   return (double)(inter / uni) > T.thr;
+}
+
+// min / max of finite non-negative floats as integer min / max of their bits (the same
+// order; no IEEE-mode NaN quieting of memory operands, which doubles fminf / fmaxf)
+__device__ __forceinline__ float nn_min(float x, float y) { return __int_as_float(min(__float_as_int(x), __float_as_int(y))); }
+__device__ __forceinline__ float nn_max(float x, float y) { return __int_as_float(max(__float_as_int(x), __float_as_int(y))); }
+__device__ __forceinline__ bool nn_finite(float4 v) {  // every coordinate in [+0, inf)
+  return ((uint32_t)__float_as_int(v.x) < 0x7f800000u) & ((uint32_t)__float_as_int(v.y) < 0x7f800000u) &
+         ((uint32_t)__float_as_int(v.z) < 0x7f800000u) & ((uint32_t)__float_as_int(v.w) < 0x7f800000u);
+}
+
+// The float filter of the exact test (0 < thr < 1): sets *amb when it cannot decide.
+// kNN: both boxes' coordinates are finite and >= +0 (nn_finite).
+template <bool kNN>
+__device__ __forceinline__ bool iou_above_filter(float4 a, float area_a, float4 b, float area_b, const NmsThr& T,
+                                                 bool* amb) {
+  const float w = kNN ? fmaxf(0.0f, nn_min(a.z, b.z) - nn_max(a.x, b.x)) : fmaxf(0.0f, fminf(a.z, b.z) - fmaxf(a.x, b.x));
+  const float h = kNN ? fmaxf(0.0f, nn_min(a.w, b.w) - nn_max(a.y, b.y)) : fmaxf(0.0f, fminf(a.w, b.w) - fmaxf(a.y, b.y));
+  const float inter = w * h;
+  const float uni = (area_a + area_b) - inter;
+  const bool above = inter > T.hi * uni, below = inter < T.lo * uni;
+  *amb = !(uni >= 0x1p-100f) | !(above | below);
+  return above;
 }
 
 // tile t of a segment's upper triangle, row-major: rows before rb hold
@@ -110,8 +140,10 @@ __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__
   float* rb_area = rb_area_all[wv];
   const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
   const int row = rb * 64 + t;
+  bool row_nn = true;
   if (row < n) {
     const float4 r = bx[row];
+    row_nn = nn_finite(r);
     rb_box[t] = r;
     rb_area[t] = (r.z - r.x) * (r.w - r.y);
   }
@@ -142,8 +174,40 @@ __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__
       colw |= (uint64_t)hit << i0;
     }
   };
-  if (T.fast)
-    sweep(std::true_type{});
+  // rows and column all finite and >= +0 (proposals clipped to the image): integer min / max
+  const bool nn = !__builtin_amdgcn_ballot_w64(!(row_nn & (!cvalid || nn_finite(a))));
+  auto filtered = [&](auto knn) {
+    constexpr bool NN = decltype(knn)::value;
+    // float filter; an 8-row batch with any undecided pair in the wave is redone exactly
+#pragma nounroll
+    for (int i0 = 0; i0 < 64; i0 += 8) {
+      float4 rbx[8];
+      float rba[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        rbx[u] = rb_box[i0 + u];
+        rba[u] = rb_area[i0 + u];
+      }
+      uint32_t hit = 0;
+      uint64_t amb = 0;  // wave masks (SALU): no per-lane bool materialisation
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        bool au;
+        hit |= (uint32_t)iou_above_filter<NN>(rbx[u], rba[u], a, aa, T, &au) << u;
+        amb |= __builtin_amdgcn_ballot_w64(au);
+      }
+      if (amb) {
+        hit = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hit |= (uint32_t)iou_above<true>(rbx[u], rba[u], a, aa, T) << u;
+      }
+      colw |= (uint64_t)hit << i0;
+    }
+  };
+  if (T.fast && nn)
+    filtered(std::true_type{});
+  else if (T.fast)
+    filtered(std::false_type{});
   else
     sweep(std::false_type{});
   const int nrows = min(64, n - rb * 64);

@@ -460,25 +460,37 @@ struct PairLayout {
 // (K, chunks); 1: a 1-D grid of 8 * ceil(K * chunks / 8) workgroups in which XCD
 // x (= linear id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item
 // list, so each XCD's L2 holds the feature planes of its own channel chunks.
-template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0>
-__global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+// kStAux / kLdAux: cache policy of the output stores / staging loads (cdna.h).
+// kStamp (tools-only timing builds): lane 0 writes 8 int64 per item after the
+// output -- s_memrealtime at start / setup done / first stage landed / end, D, cells.
+// kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
+// stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
+// twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
+template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0, int kStAux = 0, int kLdAux = 0,
+          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true>
+__global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   constexpr int SR = 2;
-  __shared__ __attribute__((aligned(16))) float slab[2 * kHalf];
+  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  int64_t t_setup = 0, t_land = 0;
+  __shared__ __attribute__((aligned(16))) float slab[kSingle ? kHalf : 2 * kHalf];
   // the slab as an LDS byte address (integer: no generic-pointer casts)
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   int64_t k = blockIdx.x;
   int chunk = blockIdx.y;
-  if (kOrder == 1) {
-    const int64_t G = (c.C + 2 * kPW - 1) / (2 * kPW), total = c.K * G, per = (total + 7) / 8;
-    const int64_t w = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  int64_t item = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (kOrder == 1) {  // 32-bit item arithmetic (host: K * G < 2^31): no 64-bit software division
+    const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
+    const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+    const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
     if (w >= total) return;
-    chunk = (int)(w / c.K);
-    k = w - (int64_t)chunk * c.K;
+    item = w;
+    chunk = (int)(w / K32);
+    k = (int64_t)(w - (uint32_t)chunk * K32);
   }
   const int cw0 = chunk * 2 * kPW;
   const int lane = threadIdx.x & (kWave - 1);
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
-  const RoiGeom g = roi_geom(c, lv, k);
+  const RoiGeom g = roi_geom_par(c, lv, k);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
   const int nbins = c.ph * c.pw;
@@ -505,7 +517,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
   const int ostep = nbins * 4;
   if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: all bins 0
-    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, 0);
+    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
     return;
   }
   const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;
@@ -545,44 +557,54 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
   const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
   const uint32_t inv = (65536u + (uint32_t)Cs2 - 1u) / (uint32_t)Cs2;  // e / Cs2 == (e * inv) >> 16 for e < 1024
+  if (kStamp) t_setup = (int64_t)__builtin_amdgcn_s_memrealtime();
+  int stamp_d = 0;
 
   auto run = [&](auto dd) {
     constexpr int D = decltype(dd)::value, RS = PairLayout<D, kHalf>::RS, RP = PairLayout<D, kHalf>::RP;
     const int nst = (npairs + D - 1) / D;
     // region dword j * 64 + lane of every pair  <-  channel (lane & 1) of cell (j * 64 + lane) / 2
-    int goff[RP];
-#pragma unroll
-    for (int j = 0; j < RP; ++j) {
+    auto goff_at = [&](int j) {
       int e = (j * kWave + lane) >> 1;
       e = e < ncell ? e : 0;
       const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
-      goff[j] = __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
-    }
+      // dense window: slab cell (r, col) is feature (y0 + r, x0 + col), no lane exchange
+      return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx + (lane & 1) * scs) * 4
+                        : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
+    };
+    int goff[RP];
+#pragma unroll
+    for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
     auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
-      const uint32_t buf = sbase + 4u * (uint32_t)((s & 1) * kHalf);
+      const uint32_t buf = sbase + 4u * (uint32_t)(kSingle ? 0 : (s & 1) * kHalf);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
 #pragma unroll
-        for (int j = 0; j < RP; ++j) lds_dma_at<4>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
+        for (int j = 0; j < RP; ++j) lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
       }
     };
     auto eval = [&](auto bb, int s) {
       constexpr int kBuf = decltype(bb)::value;
       // half-rows h = 2 d + iy: 8 tap reads each; reads of h + 1 in flight while h is summed
-      f32x2 v[2][8];
+      // kRA: the tap reads of half-row h + 1 in flight while h is summed (16 more VGPRs)
+      constexpr int NB = kRA ? 2 : 1;
+      f32x2 v[NB][8];
       f32x2 acc = {0.0f, 0.0f};
       auto load = [&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
+          for (int q = 0; q < 4; ++q) v[h % NB][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
       };
-      load(std::integral_constant<int, 0>{});
+      if constexpr (kRA) load(std::integral_constant<int, 0>{});
       static_for<0, 2 * D>([&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
-        if constexpr (h + 1 < 2 * D) {
+        if constexpr (!kRA) {
+          load(std::integral_constant<int, h>{});
+          lds_wait<0>(v[0]);
+        } else if constexpr (h + 1 < 2 * D) {
           load(std::integral_constant<int, h + 1>{});
           lds_wait<8>(v[h & 1]);
         } else {
@@ -592,7 +614,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix) {
           const float* w = wt[iy][ix];
-          const f32x2* x = &v[h & 1][ix * 4];
+          const f32x2* x = &v[h % NB][ix * 4];
           const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
           acc = acc + val;
         }
@@ -600,8 +622,8 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
           const f32x2 r = acc * 0.25f;
           const int p = s * D + d;
           const int vo = p < npairs ? ovoff : 0x40000000;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
         }
       });
     };
@@ -622,11 +644,28 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (kStamp && s == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
       eval(bb, s);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    stamp_d = D;
+    if constexpr (kSingle) {
+      for (int s = 0; s < nst; ++s) {
+        issue(s);  // the previous stage's tap reads completed (lds_wait<0> + barrier in eval / below)
+        wait_vmcnt<0>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (kStamp && s == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
+        eval(std::integral_constant<int, 0>{}, s);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      return;
+    }
     issue(0);
     for (int s = 0; s < nst; s += 2) {
       step(std::integral_constant<int, 0>{}, s);
@@ -641,6 +680,18 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
     run(std::integral_constant<int, 2>{});
   else
     run(std::integral_constant<int, 1>{});
+  if (kStamp && lane == 0) {
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + item * 8;
+    const int64_t t_end = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[0] = t_start;
+    st[1] = t_setup;
+    st[2] = t_land;
+    st[3] = t_end;
+    st[4] = stamp_d;
+    st[5] = ncell;
+    st[6] = k;
+    st[7] = blockIdx.x & 7;
+  }
 }
 
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,

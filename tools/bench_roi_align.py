@@ -43,6 +43,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=50)
     ap.add_argument('--variants', default='0,10,50')
+    ap.add_argument('--rounds', type=int, default=1, help='repeat the variant list; report medians of back-to-back replays')
     ap.add_argument('--calib', action='store_true', help='known-byte FETCH_SIZE calibration launches only')
     ap.add_argument('--calib-small', action='store_true', help='calibration on the staged (small-window) path')
     ap.add_argument('--sort', action='store_true',
@@ -80,9 +81,12 @@ def main():
     outs = {}
     wsb = int(lib.frh_roi_align_workspace(ctypes.c_int64(K)))
     wsp = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
-    for spec in args.variants.split(','):
+    summary = {}
+    specs = args.variants.split(',') * args.rounds
+    for spec in specs:
         v = int(spec)
-        full = torch.zeros(K * C * ph * pw + (8 * 4096 * 8 if v in (24, 51) else 0), device=dev)  # stamps after
+        extra = 8 * 4096 * 8 if v == 51 else (K * C // 16 * 16 if v in (44, 45, 48) else 0)
+        full = torch.zeros(K * C * ph * pw + extra, device=dev)  # stamps after
         out = full[:K * C * ph * pw].view(K, C, ph, pw)
 
         def launch():
@@ -100,18 +104,36 @@ def main():
             ts.append((e0, e1))
         torch.cuda.synchronize()
         ms = np.array([a.elapsed_time(b) for a, b in ts])
-        if v == 24:  # per-wave stamps [start, setup, ready0, done0, ready1, end, D, roi] (100 MHz)
-            st = full[K * C * ph * pw:].view(torch.int64)[:K * 8 * 8].view(-1, 8).cpu().numpy()
-            st = st[st[:, 0] > 0]
-            t0 = st[:, 0].min()
-            print('  {} waves; span {:.1f} us'.format(len(st), (st[:, 5].max() - t0) / 100.0))
-            for D in sorted(set(st[:, 6].tolist())):
-                m = st[:, 6] == D
-                x = st[m]
-                ph_ = lambda a, b: np.percentile((x[:, b] - x[:, a]) / 100.0, [50, 90]).round(2).tolist()
-                print('  D={} waves {:5d}: start p50/90 {} setup {} wait0 {} eval0 {} wait1 {} total {}'.format(
-                    D, m.sum(), np.percentile((x[:, 0] - t0) / 100.0, [50, 90]).round(1).tolist(), ph_(0, 1),
-                    ph_(1, 2), ph_(2, 3), ph_(3, 4), ph_(0, 5)), flush=True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            launch()
+        e1.record()
+        torch.cuda.synchronize()
+        summary.setdefault(spec, []).append(e0.elapsed_time(e1) / args.iters * 1e3)
+        if v in (44, 45, 48):  # per-wave stamps [start, setup, landed, end, D, cells, roi, xcd] (s_memrealtime, 100 MHz)
+            stm = full[K * C * ph * pw:].view(torch.int64).view(-1, 8).cpu().numpy()
+            stm = stm[stm[:, 0] > 0]
+            t0 = stm[:, 0].min()
+            span = (stm[:, 3].max() - t0) / 100.0
+            print('  {} waves; span {:.1f} us'.format(len(stm), span))
+            for D in sorted(set(stm[:, 4].tolist())):
+                x = stm[stm[:, 4] == D]
+                pc = lambda a: np.percentile(a / 100.0, [50, 90, 99]).round(2).tolist()
+                print('  D={} waves {:5d}: setup {} land {} eval+rest {} life {}'.format(
+                    D, len(x), pc(x[:, 1] - x[:, 0]), pc(x[:, 2] - x[:, 1]), pc(x[:, 3] - x[:, 2]), pc(x[:, 3] - x[:, 0])),
+                    flush=True)
+            nb = int(span) + 1
+            alive = np.zeros(nb)
+            for a, b in zip((stm[:, 0] - t0) / 100.0, (stm[:, 3] - t0) / 100.0):
+                i0, i1 = int(a), int(b)
+                alive[i0:i1 + 1] += 1
+            print('  waves alive per CU by us: ' + ' '.join('%.1f' % (x / 256) for x in alive), flush=True)
+            ends = np.sort((stm[:, 3] - t0) / 100.0)
+            print('  end-time percentiles 50/90/99/100:', np.percentile(ends, [50, 90, 99, 100]).round(1).tolist())
+            late = stm[(stm[:, 3] - t0) / 100.0 > 0.9 * span]
+            print('  last 10% of span: {} waves, D {} cells p50 {}'.format(
+                len(late), np.bincount(late[:, 4]).tolist(), np.median(late[:, 5]) if len(late) else 0), flush=True)
         if v == 51:  # per-workgroup stamps [start, union, end, path | U << 8] (s_memrealtime, 100 MHz)
             allst = full[K * C * ph * pw:].view(torch.int64)
             steps = allst[8192:8192 + 128 * 20 * 4].view(64, 2, 20, 4).cpu().numpy()
@@ -151,6 +173,12 @@ def main():
                 print('   roi {} lvl {} box {} win w {:.1f} h {:.1f} maxdiff {:.3g} ch-diff {}'.format(
                     i, lv[i], r[i, 1:].round(1).tolist(), bx[2] - bx[0], bx[3] - bx[1], per[i],
                     int(((out[i] - ref[i]).abs().flatten(1).max(1).values > 0).sum())), flush=True)
+
+
+    if args.rounds > 1:
+        print('back-to-back replay, median over {} rounds (us per launch):'.format(args.rounds))
+        for spec, v in summary.items():
+            print('  variant {:>4}: {:7.2f}  (all: {})'.format(spec, float(np.median(v)), ' '.join('%.1f' % x for x in v)))
 
 
 if __name__ == '__main__':

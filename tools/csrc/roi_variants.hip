@@ -1473,7 +1473,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   FRH_REQUIRE(variant == 0 || ((variant >= 9 && variant <= 19 && variant != 13 && variant != 14) && f.lds) ||
-                  ((variant == 50 || variant == 51) && grp_ok) || ((variant == 20 || variant == 21 || variant == 25 || variant == 26) && pok) ||
+                  ((variant == 50 || variant == 51) && grp_ok) || (((variant >= 20 && variant <= 28) || (variant >= 39 && variant <= 49)) && pok) ||
                   (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
@@ -1506,6 +1506,57 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
     hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
                        dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 49 || variant == 39) {  // single buffer, no tap read-ahead: 49 registers for 5 waves per SIMD, 39 unconstrained
+    const int pw = variant == 49 ? 8 : 16;
+    const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 49)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<8, kPairHalf, 1, 2, 0, false, true, 5, false>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<8, kPairHalf, 1, 2, 0, false, true, 1, false>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant >= 46 && variant <= 48) {  // single slab buffer: 46 16 pairs, 47 8 pairs, 48 = 46 stamped
+    const int pw = variant == 47 ? 8 : 16;
+    const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 46)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16, kPairHalf, 1, 2, 0, false, true>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else if (variant == 47)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<8, kPairHalf, 1, 2, 0, false, true>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16, kPairHalf, 1, 2, 0, true, true>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 44 || variant == 45) {  // stamped timing builds of variants 40 / 23 (8 int64 per item after out)
+    const int pw = variant == 44 ? 16 : 8;
+    const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 44)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16, kPairHalf, 1, 2, 0, true>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<8, kPairHalf, 1, 2, 0, true>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 40 || variant == 41) {  // chunk-major pairs, nt stores, 16 / 32 pairs per wave
+    const int pw = variant == 40 ? 16 : 32;
+    const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 40)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16, kPairHalf, 1, 2, 0>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<32, kPairHalf, 1, 2, 0>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 27 || variant == 28) {  // chunk-major pairs at 4 / 16 pairs per wave
+    const int pw = variant == 27 ? 4 : 16;
+    const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 27)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<4, kPairHalf, 1>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<16, kPairHalf, 1>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant >= 22 && variant <= 24) {  // chunk-major pairs, cache policy: 22 sc1 stores, 23 nt stores, 24 nt loads
+    const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
+    const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
+    if (variant == 22)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, 16, 0>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else if (variant == 23)
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, 2, 0>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, 0, 2>), g1, dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (variant == 25 || variant == 26) {  // 26: registers for 3 waves per SIMD (spills)
     const int G = (channels + 2 * kStrPairs - 1) / (2 * kStrPairs);
     const int64_t nitems = num_rois * G;

@@ -1,0 +1,5 @@
+set -e
+mkdir -p gpurun_out/s9
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_tools_variants.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s9/t.log 2>&1
+timeout -k 10 300 python tools/bench_roi_align.py --variants 21,47,49,39 --iters 100 --rounds 5 > gpurun_out/s9/roi.log 2>&1
