@@ -45,6 +45,9 @@ __device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t r, float* lds, in
 #endif
 }
 
+// gfx950 cache-policy bits of buffer loads / stores (the builtins' aux operand)
+constexpr int kCpolSC0 = 1, kCpolNT = 2, kCpolSC1 = 16;
+
 // the same with the destination given as a wave-uniform LDS byte address; kAux is
 // the gfx950 cache policy (0 default, 1 sc0, 2 nt, 16 sc1)
 template <int kBytes, int kAux = 0>

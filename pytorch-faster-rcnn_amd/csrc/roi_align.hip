@@ -8,7 +8,7 @@
 // roi_kernels.h):
 //  * roi_align_fwd_pair_kernel -- the default (sampling 2, up to 8x8 bins, even C):
 //    one wave per (RoI, 16 channels); the RoI's tap window staged by LDS-DMA with
-//    channel pairs interleaved, packed-f32 bilinear sums.
+//    channel pairs interleaved into one slab buffer per wave, packed-f32 bilinear sums.
 //  * roi_align_fwd_lds_kernel -- odd channel counts: per-(RoI, 64 channels)
 //    workgroup, windows <= 256 floats staged in LDS, larger ones gathered.
 //  * roi_align_fwd_kernel -- direct gather, any pooled size / sampling ratio.
@@ -67,11 +67,14 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
-  if (pair_ok(f, channels, pooled_h, pooled_w)) {  // chunk-major XCD order (roi_kernels.h kOrder 1)
+  if (pair_ok(f, channels, pooled_h, pooled_w)) {
+    // chunk-major XCD order (kOrder 1), nt output stores, ONE slab buffer per wave (kSingle:
+    // 6.5 KB of LDS, so 16 resident waves per CU instead of 11 -- the register count caps it
+    // there; 37.2 vs 40.9 us on the cfg2 RoIs, tools/bench_roi_align.py variants 47 / 21)
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
-                       dim3(kWave), 0, as_stream(stream), lv, c, out);
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, kCpolNT, 0, false, true>),
+                       dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (f.lds) {
     const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);

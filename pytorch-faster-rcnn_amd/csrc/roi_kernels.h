@@ -440,6 +440,24 @@ __device__ __forceinline__ f32x2 lds_read_b64(uint32_t addr) {
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
   return v;
 }
+// eight ds_read_b64 and their wait in ONE asm statement: no register copy of a value
+// still in flight can be placed between the reads and the wait
+template <int OFF>
+__device__ __forceinline__ void lds_read8_wait(f32x2 (&v)[8], const uint32_t (&a)[8]) {
+  asm volatile(
+      "ds_read_b64 %0, %8 offset:%16\n\t"
+      "ds_read_b64 %1, %9 offset:%16\n\t"
+      "ds_read_b64 %2, %10 offset:%16\n\t"
+      "ds_read_b64 %3, %11 offset:%16\n\t"
+      "ds_read_b64 %4, %12 offset:%16\n\t"
+      "ds_read_b64 %5, %13 offset:%16\n\t"
+      "ds_read_b64 %6, %14 offset:%16\n\t"
+      "ds_read_b64 %7, %15 offset:%16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "i"(OFF)
+      : "memory");
+}
 template <int N>
 __device__ __forceinline__ void lds_wait(f32x2 (&v)[8]) {
   asm volatile("s_waitcnt lgkmcnt(%8)"
@@ -602,8 +620,10 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
       static_for<0, 2 * D>([&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
         if constexpr (!kRA) {
-          load(std::integral_constant<int, h>{});
-          lds_wait<0>(v[0]);
+          constexpr int OFF = 4 * (kBuf * kHalf + d * RS);
+          const uint32_t a8[8] = {ta[iy][0][0], ta[iy][0][1], ta[iy][0][2], ta[iy][0][3],
+                                  ta[iy][1][0], ta[iy][1][1], ta[iy][1][2], ta[iy][1][3]};
+          lds_read8_wait<OFF>(v[0], a8);
         } else if constexpr (h + 1 < 2 * D) {
           load(std::integral_constant<int, h + 1>{});
           lds_wait<8>(v[h & 1]);

@@ -32,6 +32,7 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--thr', type=float, default=0.7)
     ap.add_argument('--timeline', action='store_true', help='per-block resolver stamps (tools library)')
+    ap.add_argument('--ab', action='store_true', help='A/B against the exact-test mask (tools library)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     boxes = torch.from_numpy(make(a.segs, a.n)).to(dev)
@@ -47,6 +48,34 @@ def main():
     torch.cuda.synchronize()
     print('{:.1f} us per nms_sorted (mask + scan), kept {}'.format(e0.elapsed_time(e1) / a.iters * 1e3, kc.tolist()),
           flush=True)
+    if a.ab:  # exact-test mask (tools library) on the same segments: same keep lists, timed alike
+        import ctypes
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import toolslib
+        from frcnn_amd import _lib
+        lib = toolslib.load()
+        wsb = int(lib.frh_ex_nms_workspace(a.segs, a.n))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        kp = torch.full((a.segs, a.n), -1, dtype=torch.int32, device=dev)
+        kc2 = torch.empty(a.segs, dtype=torch.int32, device=dev)
+        for rnd in range(3):
+            for name in ('frh_ex_nms_sorted', 'product'):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    if name == 'product':
+                        keep, kc = ops.nms_sorted(boxes, counts, a.n, a.thr)
+                    else:
+                        toolslib.call(name, a.segs, _lib.ptr(boxes), a.n * 4, _lib.ptr(counts), a.n, a.thr, -1,
+                                      _lib.ptr(kp), a.n, _lib.ptr(kc2), _lib.ptr(ws), wsb, _lib.stream_of(boxes))
+                e1.record()
+                torch.cuda.synchronize()
+                print('  {:>18}: {:.1f} us per call'.format(name, e0.elapsed_time(e1) / a.iters * 1e3), flush=True)
+        assert torch.equal(kc2, kc)
+        for s_ in range(a.segs):
+            n_ = int(kc[s_])
+            assert torch.equal(kp[s_, :n_].cpu(), keep[s_, :n_].cpu()), s_
+        print('  keep lists identical', flush=True)
     if a.timeline:
         import ctypes
         import numpy as np

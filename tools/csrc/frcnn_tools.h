@@ -92,6 +92,12 @@ int32_t frh_tl_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stri
                           int32_t* keep_counts, void* workspace, size_t ws_bytes, void* stream);
 int32_t frh_tl_nms_timeline(void* stamps);
 
+/* tools/csrc/nms_exact.hip: the exact-test mask NMS (A/B of the float-filtered mask) */
+size_t frh_ex_nms_workspace(int32_t num_segs, int32_t n_max);
+int32_t frh_ex_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
+                          int32_t n_max, double iou_thr, int32_t max_keep, int32_t* keep, int64_t keep_seg_stride,
+                          int32_t* keep_counts, void* workspace, size_t ws_bytes, void* stream);
+
 /* The product RPN proposals rebuilt with segment-0 top-k timestamps
  * (tools/csrc/topk_timeline.hip): same arguments as frh_rpn_proposals_workspace /
  * frh_rpn_proposals / frh_rpn_proposals_nms_view; frh_tl_topk_timeline sets the stamp

@@ -1507,7 +1507,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
                        dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (variant == 49 || variant == 39) {  // single buffer, no tap read-ahead: 49 registers for 5 waves per SIMD, 39 unconstrained
-    const int pw = variant == 49 ? 8 : 16;
+    const int pw = 8;
     const int64_t total = num_rois * ((channels + 2 * pw - 1) / (2 * pw));
     const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
     if (variant == 49)

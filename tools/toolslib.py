@@ -26,6 +26,9 @@ TOOL_SIGNATURES = {
     'frh_tl_nms_workspace': (c_size, [c_i32, c_i32]),
     'frh_tl_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, _lib.c_f64, c_i32, c_vp, c_i64, c_vp, c_vp,
                                   c_size, c_vp]),
+    'frh_ex_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, _lib.c_f64, c_i32, c_vp, c_i64, c_vp, c_vp,
+                                  c_size, c_vp]),
+    'frh_ex_nms_workspace': (c_size, [c_i32, c_i32]),
     'frh_tl_nms_timeline': (c_i32, [c_vp]),
     'frh_tl_rpn_proposals_workspace': _lib.SIGNATURES['frh_rpn_proposals_workspace'],
     'frh_tl_rpn_proposals_nms_view': _lib.SIGNATURES['frh_rpn_proposals_nms_view'],
