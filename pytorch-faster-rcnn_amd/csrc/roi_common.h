@@ -85,33 +85,66 @@ __device__ __forceinline__ RoiGeom roi_geom(const RoiCfg& c, const RoiLevels& lv
   return g;
 }
 
-// roi_geom with the RoI's and its level's loads issued together (one memory round trip
-// in the wave's prologue instead of two: the level pointer is selected, not branched on)
-// (k wave-uniform).  The compiler would wait for the level before loading the box, so
-// both scalar loads are issued by hand, followed by ONE lgkmcnt(0) wait.
-__device__ __forceinline__ RoiGeom roi_geom_par(const RoiCfg& c, const RoiLevels& lv, int64_t k) {
-  const float* r = c.rois + k * 5;
-  const int64_t* lp = c.levels ? c.levels + k : reinterpret_cast<const int64_t*>(c.rois);
-  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-  u32x4_t rq;
-  uint32_t r4u, lraw;
+// The RoI's box and level as loaded (RoiRaw), fetched by hand-issued scalar loads: the
+// compiler would wait for the level before loading the box, so the loads of one (or
+// two) RoIs go out together, followed by ONE lgkmcnt(0) wait (k wave-uniform).
+struct RoiRaw {
+  float r0, r1, r2, r3, r4;
+  int lvl;
+};
+
+typedef uint32_t roi_u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ const int64_t* roi_level_ptr(const RoiCfg& c, int64_t k) {
+  return c.levels ? c.levels + k : reinterpret_cast<const int64_t*>(c.rois);  // selected, not branched on
+}
+
+__device__ __forceinline__ RoiRaw roi_raw(const RoiCfg& c, roi_u32x4_t q, uint32_t r4, uint32_t l) {
+  return RoiRaw{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w),
+                __uint_as_float(r4), c.levels ? (int)l : 0};  // level index < 2^31: the low word
+}
+
+__device__ __forceinline__ RoiRaw roi_fetch(const RoiCfg& c, int64_t k) {
+  roi_u32x4_t q;
+  uint32_t r4, l;
   asm volatile(
       "s_load_dwordx4 %0, %3, 0x0\n\t"
       "s_load_dword %1, %3, 0x10\n\t"
       "s_load_dword %2, %4, 0x0\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "=s"(rq), "=s"(r4u), "=s"(lraw)
-      : "s"(r), "s"(lp)
+      : "=&s"(q), "=&s"(r4), "=&s"(l)  // early clobber: later loads of the statement read the inputs
+      : "s"(c.rois + k * 5), "s"(roi_level_ptr(c, k))
       : "memory");
-  const float r0 = __uint_as_float(rq.x), r1 = __uint_as_float(rq.y), r2 = __uint_as_float(rq.z),
-              r3 = __uint_as_float(rq.w), r4 = __uint_as_float(r4u);
+  return roi_raw(c, q, r4, l);
+}
+
+__device__ __forceinline__ void roi_fetch2(const RoiCfg& c, int64_t k0, int64_t k1, RoiRaw* a, RoiRaw* b) {
+  roi_u32x4_t q0, q1;
+  uint32_t r40, r41, l0, l1;
+  asm volatile(
+      "s_load_dwordx4 %0, %6, 0x0\n\t"
+      "s_load_dword %1, %6, 0x10\n\t"
+      "s_load_dword %2, %7, 0x0\n\t"
+      "s_load_dwordx4 %3, %8, 0x0\n\t"
+      "s_load_dword %4, %8, 0x10\n\t"
+      "s_load_dword %5, %9, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(q0), "=&s"(r40), "=&s"(l0), "=&s"(q1), "=&s"(r41), "=&s"(l1)
+      : "s"(c.rois + k0 * 5), "s"(roi_level_ptr(c, k0)), "s"(c.rois + k1 * 5), "s"(roi_level_ptr(c, k1))
+      : "memory");
+  *a = roi_raw(c, q0, r40, l0);
+  *b = roi_raw(c, q1, r41, l1);
+}
+
+// roi_geom from a fetched RoI
+__device__ __forceinline__ RoiGeom roi_geom_raw(const RoiCfg& c, const RoiLevels& lv, const RoiRaw& rr) {
   RoiGeom g;
-  g.b = (int)r0;
-  g.lvl = c.levels ? (int)lraw : 0;  // level index < 2^31: the low word
+  g.b = (int)rr.r0;
+  g.lvl = rr.lvl;
   const float sc = lv.scale[g.lvl];
   const float off = c.aligned ? 0.5f : 0.0f;
-  float sw = r1 * sc - off, sh = r2 * sc - off;
-  float ew = r3 * sc - off, eh = r4 * sc - off;
+  float sw = rr.r1 * sc - off, sh = rr.r2 * sc - off;
+  float ew = rr.r3 * sc - off, eh = rr.r4 * sc - off;
   float rw = ew - sw, rh = eh - sh;
   if (!c.aligned) {
     rw = fmaxf(rw, 1.0f);

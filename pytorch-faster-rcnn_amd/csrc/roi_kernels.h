@@ -484,31 +484,16 @@ struct PairLayout {
 // kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
 // stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
 // twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
-template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0, int kStAux = 0, int kLdAux = 0,
-          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true>
-__global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA>
+__device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
+                                          int chunk, int64_t item, const RoiRaw& raw, uint32_t sbase,
+                                          int64_t t_start) {
   constexpr int SR = 2;
-  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   int64_t t_setup = 0, t_land = 0;
-  __shared__ __attribute__((aligned(16))) float slab[kSingle ? kHalf : 2 * kHalf];
-  // the slab as an LDS byte address (integer: no generic-pointer casts)
-  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
-  int64_t k = blockIdx.x;
-  int chunk = blockIdx.y;
-  int64_t item = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  if (kOrder == 1) {  // 32-bit item arithmetic (host: K * G < 2^31): no 64-bit software division
-    const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
-    const uint32_t total = K32 * G, per = (total + 7u) / 8u;
-    const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-    if (w >= total) return;
-    item = w;
-    chunk = (int)(w / K32);
-    k = (int64_t)(w - (uint32_t)chunk * K32);
-  }
   const int cw0 = chunk * 2 * kPW;
   const int lane = threadIdx.x & (kWave - 1);
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
-  const RoiGeom g = roi_geom_par(c, lv, k);
+  const RoiGeom g = roi_geom_raw(c, lv, raw);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
   const int nbins = c.ph * c.pw;
@@ -711,6 +696,51 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
     st[5] = ncell;
     st[6] = k;
     st[7] = blockIdx.x & 7;
+  }
+}
+
+// kItems (1 or 2): items per wave.  With 2 the second item's RoI and level are fetched
+// with the first's (one memory round trip for both), so its prologue is ALU and
+// kernel-argument loads only.
+template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0, int kStAux = 0, int kLdAux = 0,
+          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true, int kItems = 1>
+__global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  static_assert(kItems == 1 || (kItems == 2 && kOrder == 1), "two items per wave: chunk-major order only");
+  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) float slab[kSingle ? kHalf : 2 * kHalf];
+  // the slab as an LDS byte address (integer: no generic-pointer casts)
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  if (kOrder == 0) {
+    const int64_t k = blockIdx.x;
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k, blockIdx.y,
+                                                                (int64_t)blockIdx.y * gridDim.x + blockIdx.x,
+                                                                roi_fetch(c, k), sbase, t_start);
+    return;
+  }
+  // 32-bit item arithmetic (host: K * G < 2^31): no 64-bit software division.  XCD x (= linear
+  // id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item list.
+  const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3) * (uint32_t)kItems;
+  const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
+  if (w >= wend) return;
+  const int ch0 = (int)(w / K32);
+  const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
+  if constexpr (kItems == 1) {
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, roi_fetch(c, k0), sbase,
+                                                                t_start);
+  } else {
+    const bool two = w + 1 < wend;
+    const uint32_t w1 = two ? w + 1 : w;
+    const int ch1 = (int)(w1 / K32);
+    const int64_t k1 = (int64_t)(w1 - (uint32_t)ch1 * K32);
+    RoiRaw r0, r1;
+    roi_fetch2(c, k0, k1, &r0, &r1);
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, r0, sbase, t_start);
+    if (two) {
+      // the slab is reused: the first item's tap reads are complete (lds_wait<0> + barrier)
+      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k1, ch1, w1, r1, sbase, t_start);
+    }
   }
 }
 

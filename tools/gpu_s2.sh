@@ -1,6 +1,5 @@
 set -e
-mkdir -p gpurun_out/s16
+mkdir -p gpurun_out/s18
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_hand_derived.py -m gpu -x -q --timeout 120 --timeout-method thread -k "nms or mcnms or multiclass or proposals or retina_predict or forward_train or eval" > gpurun_out/s16/t.log 2>&1
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/s16/nmsprof -o run --output-format csv -- python tools/bench_nms.py --ab > gpurun_out/s16/nms.log 2>&1
-timeout -k 10 240 python bench.py --no-cpu-baseline > gpurun_out/s16/bench.json 2> gpurun_out/s16/bench.err
+timeout -k 10 300 python -u -m pytest tests/test_tools_variants.py tests/test_hand_derived.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s18/t.log 2>&1
+timeout -k 10 300 python tools/bench_roi_align.py --variants 21,47,29 --iters 100 --rounds 5 > gpurun_out/s18/roi.log 2>&1
