@@ -487,11 +487,10 @@ struct PairLayout {
 template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA>
 __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, const RoiRaw& raw, uint32_t sbase,
-                                          int64_t t_start) {
+                                          int64_t t_start, int lane) {
   constexpr int SR = 2;
   int64_t t_setup = 0, t_land = 0;
   const int cw0 = chunk * 2 * kPW;
-  const int lane = threadIdx.x & (kWave - 1);
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom_raw(c, lv, raw);
   const int l = g.lvl;
@@ -714,7 +713,7 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
     const int64_t k = blockIdx.x;
     pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k, blockIdx.y,
                                                                 (int64_t)blockIdx.y * gridDim.x + blockIdx.x,
-                                                                roi_fetch(c, k), sbase, t_start);
+                                                                roi_fetch(c, k), sbase, t_start, threadIdx.x & (kWave - 1));
     return;
   }
   // 32-bit item arithmetic (host: K * G < 2^31): no 64-bit software division.  XCD x (= linear
@@ -728,7 +727,7 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
   if constexpr (kItems == 1) {
     pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, roi_fetch(c, k0), sbase,
-                                                                t_start);
+                                                                t_start, threadIdx.x & (kWave - 1));
   } else {
     const bool two = w + 1 < wend;
     const uint32_t w1 = two ? w + 1 : w;
@@ -736,10 +735,12 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
     const int64_t k1 = (int64_t)(w1 - (uint32_t)ch1 * K32);
     RoiRaw r0, r1;
     roi_fetch2(c, k0, k1, &r0, &r1);
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, r0, sbase, t_start);
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, r0, sbase, t_start,
+                                                                threadIdx.x & (kWave - 1));
     if (two) {
       // the slab is reused: the first item's tap reads are complete (lds_wait<0> + barrier)
-      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k1, ch1, w1, r1, sbase, t_start);
+      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k1, ch1, w1, r1, sbase, t_start,
+                                                                  threadIdx.x & (kWave - 1));
     }
   }
 }

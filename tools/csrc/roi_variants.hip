@@ -229,6 +229,87 @@ __device__ __forceinline__ void roi_segment(const RoiLevels& lv, const RoiCfg& c
 }
 
 // ---------------------------------------------------------------------------
+// Measured slower (variants 38, 52, 53) -- kept here, out of the product.
+// Dynamic item scheduling for the pair kernel (kSingle, chunk-major): kDynWaves waves per
+// XCD list stay resident and take (channel chunk, RoI) items of their XCD's list from a
+// per-list counter, so the launch has no tail of late long items, and each wave fetches
+// the NEXT item's index and RoI while it works on the current one (its prologue loses
+// the memory round trips).  Counters: g_roi_dyn[x * 64] (next item of list x) and
+// [x * 64 + 32] (waves of list x that have left); the last wave out of a list resets
+// both, so stream-ordered launches start from zero.  (Two launches of this kernel must
+// not run concurrently on different streams: they would share the counters.)
+static __device__ uint32_t g_roi_dyn[8 * 64];
+
+__device__ __forceinline__ uint32_t lane0_fetch_add(uint32_t* p, uint32_t v) {  // one atomic per wave
+  uint32_t r = 0;
+  if ((threadIdx.x & (kWave - 1)) == 0) r = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;  // lane 0 holds it: read with __builtin_amdgcn_readfirstlane
+}
+
+// kStatic: no counters -- wave j of a list takes items j, j + P, j + 2P, ... (P = waves per
+// list), still with the next item's RoI fetched before the current item's work.
+template <int kPW = kPairWave, int kHalf = kPairHalf, int kStAux = kCpolNT, bool kStatic = false>
+__global__ void __launch_bounds__(kWave) roi_align_fwd_pair_dyn_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out,
+                                                                       uint32_t waves_per_list) {
+  __shared__ __attribute__((aligned(16))) float slab[kHalf];
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const uint32_t x = blockIdx.x & 7u;
+  const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+  const uint32_t lo = x * per, n = min(lo + per, total) > lo ? min(lo + per, total) - lo : 0u;
+  uint32_t* cnt = g_roi_dyn + x * 64u;
+  uint32_t* left = g_roi_dyn + x * 64u + 32u;
+  const uint32_t wj = blockIdx.x >> 3;
+  auto next_index = [&](uint32_t cur) -> uint32_t {  // dynamic: lane 0 holds it; static: uniform
+    return kStatic ? cur + waves_per_list : lane0_fetch_add(cnt, 1u);
+  };
+  uint32_t i0 = kStatic ? wj : __builtin_amdgcn_readfirstlane(lane0_fetch_add(cnt, 1u));
+  if (i0 < n) {
+    auto kc = [&](uint32_t i, int64_t* k, int* ch) {
+      const uint32_t w = lo + i;
+      *ch = (int)(w / K32);
+      *k = (int64_t)(w - (uint32_t)*ch * K32);
+    };
+    int64_t k0;
+    int ch0;
+    kc(i0, &k0, &ch0);
+    RoiRaw r0 = roi_fetch(c, k0);
+    uint32_t i1v = next_index(i0);  // in flight while item i0 runs
+    while (true) {
+      const uint32_t i1 = kStatic ? i1v : __builtin_amdgcn_readfirstlane(i1v);
+      int64_t k1 = k0;
+      int ch1 = ch0;
+      RoiRaw r1 = r0;
+      uint32_t i2v = 0;
+      if (i1 < n) {  // the next item's RoI and the one after's index, before this item's work
+        kc(i1, &k1, &ch1);
+        r1 = roi_fetch(c, k1);
+        i2v = next_index(i1);
+      }
+      // the lane index through an opaque copy: lane-only values of the item (bin, DMA slots)
+      // are recomputed per item instead of hoisted out of the loop into live registers
+      int lane = threadIdx.x & (kWave - 1);
+      asm volatile("" : "+v"(lane));
+      pair_item<kPW, kHalf, kStAux, 0, false, true, true>(lv, c, out, k0, ch0, lo + i0, r0, sbase, 0, lane);
+      if (i1 >= n) break;
+      i0 = i1;
+      k0 = k1;
+      ch0 = ch1;
+      r0 = r1;
+      i1v = i2v;
+    }
+  }
+  if (kStatic) return;
+  // leave: the last wave of this list resets its counters (every other wave of the list has
+  // made its final counter add before its own add to `left`)
+  __builtin_amdgcn_s_waitcnt(0);
+  const uint32_t out_n = __builtin_amdgcn_readfirstlane(lane0_fetch_add(left, 1u));
+  if (out_n == waves_per_list - 1u && (threadIdx.x & (kWave - 1)) == 0) {
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(left, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Persistent channel-pair forward (variant 25).  The staging and evaluation of
 // the channel-pair kernel above, but a grid of resident single-wave workgroups
 // walks the items (RoI, kStrPairs channel pairs): wave w takes items w, w + G,
@@ -1473,7 +1554,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   FRH_REQUIRE(variant == 0 || ((variant >= 9 && variant <= 19 && variant != 13 && variant != 14) && f.lds) ||
-                  ((variant == 50 || variant == 51) && grp_ok) || (((variant >= 20 && variant <= 29) || (variant >= 39 && variant <= 49)) && pok) ||
+                  ((variant == 50 || variant == 51) && grp_ok) || (((variant >= 20 && variant <= 29) || (variant >= 38 && variant <= 49) || variant == 52 || variant == 53) && pok) ||
                   (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
@@ -1506,6 +1587,16 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
     hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1>), dim3((unsigned)(8 * ((total + 7) / 8))),
                        dim3(kWave), 0, as_stream(stream), lv, c, out);
+  } else if (variant == 38 || variant == 52 || variant == 53) {
+    // 38: dynamic item scheduling (roi_align_fwd_pair_dyn_kernel), 512 waves per XCD list;
+    // 52 / 53: static strided items with the next RoI prefetched, 512 / 256 waves per list
+    const uint32_t wpl = variant == 53 ? 256 : 512;
+    if (variant == 38)
+      hipLaunchKernelGGL((roi_align_fwd_pair_dyn_kernel<kPairWave, kPairHalf, kCpolNT>), dim3(8 * wpl), dim3(kWave), 0,
+                         as_stream(stream), lv, c, out, wpl);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_pair_dyn_kernel<kPairWave, kPairHalf, kCpolNT, true>), dim3(8 * wpl), dim3(kWave),
+                         0, as_stream(stream), lv, c, out, wpl);
   } else if (variant == 29) {  // product kernel (single buffer, nt stores) with two items per wave
     const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
     const int64_t per = (total + 7) / 8;
