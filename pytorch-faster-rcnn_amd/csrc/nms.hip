@@ -58,7 +58,8 @@ static NmsThr nms_thr(double thr) {
   // hi >= mid (1 + 2^-20), lo <= mid (1 - 2^-20): a float product RN(hi * u) is within a
   // factor (1 +- 2^-24) of hi * u, so for u >= 2^-100 (no underflow) inter > RN(hi * u)
   // implies inter > mid * u and inter < RN(lo * u) implies inter < mid * u.  Everything
-  // else (IoU within ~1e-6 of thr, tiny / negative / NaN unions) takes the exact test.
+  // else (IoU within ~1e-6 of thr, unions in (0, 2^-100]) takes the exact test; unions <= 0
+  // or NaN are decided (not above) without it -- degenerate boxes are common in RPN output.
   t.hi = nextafterf((float)(t.mid * (1.0 + 0x1p-20)), 2.0f);
   t.lo = nextafterf((float)(t.mid * (1.0 - 0x1p-20)), 0.0f);
   return t;
@@ -96,8 +97,12 @@ __device__ __forceinline__ bool iou_above_filter(float4 a, float area_a, float4 
   const float h = kNN ? fmaxf(0.0f, nn_min(a.w, b.w) - nn_max(a.y, b.y)) : fmaxf(0.0f, fminf(a.w, b.w) - fmaxf(a.y, b.y));
   const float inter = w * h;
   const float uni = (area_a + area_b) - inter;
-  const bool above = inter > T.hi * uni, below = inter < T.lo * uni;
-  *amb = !(uni >= 0x1p-100f) | !(above | below);
+  // union <= 0 or NaN: decided (the exact test needs union > 0); 0 < union <= 2^-100 (the
+  // products could underflow): undecided
+  const bool pos = uni > 0x1p-100f;
+  const bool above = pos & (inter > T.hi * uni);
+  const bool below = !(uni > 0.0f) | (pos & (inter < T.lo * uni));
+  *amb = !(above | below);
   return above;
 }
 

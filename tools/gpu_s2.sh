@@ -1,5 +1,7 @@
 set -e
-mkdir -p gpurun_out/s20
+mkdir -p gpurun_out/s22
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_tools_variants.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s20/t.log 2>&1
-timeout -k 10 300 python tools/bench_roi_align.py --variants 47,52,53 --iters 100 --rounds 5 > gpurun_out/s20/roi.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_hand_derived.py -m gpu -x -q --timeout 120 --timeout-method thread -k "nms or mcnms or multiclass or proposals or retina_predict or forward_train" > gpurun_out/s22/t.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s22/stats -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/s22/stats.log 2>&1
+timeout -k 10 240 python bench.py --no-cpu-baseline > gpurun_out/s22/bench.json 2> gpurun_out/s22/bench.err
+rm -f gpurun_out/s22/stats/run_kernel_trace.csv
