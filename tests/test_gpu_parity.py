@@ -396,6 +396,34 @@ def test_nms_scan_adversarial(dev, pattern):
         np.testing.assert_array_equal(keep, want)
 
 
+@pytest.mark.parametrize('thr', [0.7, 0.5])
+def test_nms_degenerate_boxes(dev, thr):
+    """RPN-like degenerate boxes, the case the mask kernel's float filter decides without
+    the exact test: zero-width / zero-height boxes clamped to the image edge (union 0 with
+    each other), negative-area boxes (union < 0), 1e-30-sized boxes (union in (0, 2^-100],
+    the exact path), duplicates of each, negative coordinates (the float min / max path)
+    mixed with ordinary boxes.  Keep lists must equal the oracle's."""
+    from frcnn_amd import ops
+    rng = np.random.default_rng(7)
+    n = 3000
+    b = inputs.random_boxes(11, n, min_wh=1, max_wh=300).T.copy()
+    k = rng.integers(0, 6, n)
+    edge_y = rng.choice([0.0, 599.0], n).astype(np.float32)
+    b[k == 1, 1] = edge_y[k == 1]
+    b[k == 1, 3] = edge_y[k == 1]          # zero height on the top / bottom edge
+    b[k == 2, 0] = 999.0
+    b[k == 2, 2] = 999.0                   # zero width on the right edge
+    b[k == 3, 2] = b[k == 3, 0] - 5.0      # negative width
+    t = np.float32(1e-30)
+    b[k == 4, 2] = b[k == 4, 0] + t
+    b[k == 4, 3] = b[k == 4, 1] + t        # tiny boxes
+    b[k == 5] -= np.float32(400.0)         # negative coordinates
+    b[1::9] = b[0::9][:len(b[1::9])]       # duplicates
+    scores = rng.random(n).astype(np.float32)
+    keep = ops.nms(T(b, dev), T(scores, dev), thr).cpu().numpy()
+    np.testing.assert_array_equal(keep, oracle.nms(b, scores, thr))
+
+
 @pytest.mark.parametrize('thr', [0.7, 0.5, 0.3])
 def test_nms_threshold_boundary(dev, thr):
     """Pairs of boxes whose IoU straddles the threshold by a few float ulps: the kernel's
