@@ -484,7 +484,7 @@ struct PairLayout {
 // kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
 // stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
 // twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
-template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA>
+template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA, bool kLean = false>
 __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, const RoiRaw& raw, uint32_t sbase,
                                           int64_t t_start, int lane) {
@@ -555,6 +555,32 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
       ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q1) : 0u);
     }
   }
+  // kLean: the 16 weights and 16 tap addresses rebuilt per half-row from per-sample factors
+  // (a.h, a.l, b.h, b.l zeroed for invalid samples: the same products, or +0) and
+  // per-sample bases + row / column deltas -- 16 registers instead of 32
+  float fyh[SR], fyl[SR], fxh[SR], fxl[SR];
+  uint32_t tb0[SR][SR], tdq[SR], tdr[SR];
+  if constexpr (kLean) {
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy) {
+      const Tap a = make_tap(pos_y(py, iy), H);
+      fyh[iy] = a.valid ? a.h : 0.f;
+      fyl[iy] = a.valid ? a.l : 0.f;
+      const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
+      tdr[iy] = 8u * (uint32_t)((r1 - r0) * Cs2);
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const Tap b = make_tap(pos_x(px, ix), W);
+        const int q0 = dx ? b.lo - x0 : 2 * (px * SR + ix), q1 = dx ? b.hi - x0 : 2 * (px * SR + ix) + 1;
+        if (iy == 0) {
+          fxh[ix] = b.valid ? b.h : 0.f;
+          fxl[ix] = b.valid ? b.l : 0.f;
+          tdq[ix] = 8u * (uint32_t)(q1 - q0);
+        }
+        tb0[iy][ix] = lbase + ((a.valid && b.valid) ? 8u * (uint32_t)(r0 * Cs2 + q0) : 0u);
+      }
+    }
+  }
   const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
   const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
   const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
@@ -593,20 +619,40 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
       constexpr int NB = kRA ? 2 : 1;
       f32x2 v[NB][8];
       f32x2 acc = {0.0f, 0.0f};
+      // kLean: the factors pass through an opaque copy per stage, so the products and sums
+      // below are computed here and not hoisted out of the stage loop into live registers
+      float ly_h[SR], ly_l[SR], lx_h[SR], lx_l[SR];
+      uint32_t lb[SR][SR], ldq[SR], ldr[SR];
+      if constexpr (kLean) {
+#pragma unroll
+        for (int i = 0; i < SR; ++i) {
+          ly_h[i] = fyh[i], ly_l[i] = fyl[i], lx_h[i] = fxh[i], lx_l[i] = fxl[i], ldq[i] = tdq[i], ldr[i] = tdr[i];
+          asm volatile("" : "+v"(ly_h[i]), "+v"(ly_l[i]), "+v"(lx_h[i]), "+v"(lx_l[i]), "+v"(ldq[i]), "+v"(ldr[i]));
+#pragma unroll
+          for (int j = 0; j < SR; ++j) {
+            lb[i][j] = tb0[i][j];
+            asm volatile("" : "+v"(lb[i][j]));
+          }
+        }
+      }
+      auto tap = [&](int iy, int ix, int q) -> uint32_t {
+        if constexpr (kLean) return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
+        return ta[iy][ix][q];
+      };
       auto load = [&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[h % NB][ix * 4 + q] = lds_read_b64<OFF>(ta[iy][ix][q]);
+          for (int q = 0; q < 4; ++q) v[h % NB][ix * 4 + q] = lds_read_b64<OFF>(tap(iy, ix, q));
       };
       if constexpr (kRA) load(std::integral_constant<int, 0>{});
       static_for<0, 2 * D>([&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
         if constexpr (!kRA) {
           constexpr int OFF = 4 * (kBuf * kHalf + d * RS);
-          const uint32_t a8[8] = {ta[iy][0][0], ta[iy][0][1], ta[iy][0][2], ta[iy][0][3],
-                                  ta[iy][1][0], ta[iy][1][1], ta[iy][1][2], ta[iy][1][3]};
+          const uint32_t a8[8] = {tap(iy, 0, 0), tap(iy, 0, 1), tap(iy, 0, 2), tap(iy, 0, 3),
+                                  tap(iy, 1, 0), tap(iy, 1, 1), tap(iy, 1, 2), tap(iy, 1, 3)};
           lds_read8_wait<OFF>(v[0], a8);
         } else if constexpr (h + 1 < 2 * D) {
           load(std::integral_constant<int, h + 1>{});
@@ -617,7 +663,14 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
         if (iy == 0) acc = f32x2{0.0f, 0.0f};
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix) {
-          const float* w = wt[iy][ix];
+          float wl[4];
+          if constexpr (kLean) {
+            wl[0] = ly_h[iy] * lx_h[ix];
+            wl[1] = ly_h[iy] * lx_l[ix];
+            wl[2] = ly_l[iy] * lx_h[ix];
+            wl[3] = ly_l[iy] * lx_l[ix];
+          }
+          const float* w = kLean ? wl : wt[iy][ix];
           const f32x2* x = &v[h % NB][ix * 4];
           const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
           acc = acc + val;
@@ -702,7 +755,8 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
 // with the first's (one memory round trip for both), so its prologue is ALU and
 // kernel-argument loads only.
 template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0, int kStAux = 0, int kLdAux = 0,
-          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true, int kItems = 1>
+          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true, int kItems = 1,
+          bool kLean = false>
 __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   static_assert(kItems == 1 || (kItems == 2 && kOrder == 1), "two items per wave: chunk-major order only");
   const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -711,7 +765,7 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   if (kOrder == 0) {
     const int64_t k = blockIdx.x;
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k, blockIdx.y,
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k, blockIdx.y,
                                                                 (int64_t)blockIdx.y * gridDim.x + blockIdx.x,
                                                                 roi_fetch(c, k), sbase, t_start, threadIdx.x & (kWave - 1));
     return;
@@ -726,7 +780,7 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
   if constexpr (kItems == 1) {
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, roi_fetch(c, k0), sbase,
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k0, ch0, w, roi_fetch(c, k0), sbase,
                                                                 t_start, threadIdx.x & (kWave - 1));
   } else {
     const bool two = w + 1 < wend;
@@ -735,11 +789,11 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
     const int64_t k1 = (int64_t)(w1 - (uint32_t)ch1 * K32);
     RoiRaw r0, r1;
     roi_fetch2(c, k0, k1, &r0, &r1);
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k0, ch0, w, r0, sbase, t_start,
+    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k0, ch0, w, r0, sbase, t_start,
                                                                 threadIdx.x & (kWave - 1));
     if (two) {
       // the slab is reused: the first item's tap reads are complete (lds_wait<0> + barrier)
-      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA>(lv, c, out, k1, ch1, w1, r1, sbase, t_start,
+      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k1, ch1, w1, r1, sbase, t_start,
                                                                   threadIdx.x & (kWave - 1));
     }
   }

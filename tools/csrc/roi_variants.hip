@@ -1554,7 +1554,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   for (int l = 0; l < lv.L; ++l) x4_ok = x4_ok && lv.sx[l] == 1 && lv.sy[l] % 4 == 0 && lv.sc[l] % 4 == 0 &&
                                          lv.sb[l] % 4 == 0 && (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) == 0;
   FRH_REQUIRE(variant == 0 || ((variant >= 9 && variant <= 19 && variant != 13 && variant != 14) && f.lds) ||
-                  ((variant == 50 || variant == 51) && grp_ok) || (((variant >= 20 && variant <= 29) || (variant >= 38 && variant <= 49) || variant == 52 || variant == 53) && pok) ||
+                  ((variant == 50 || variant == 51) && grp_ok) || (((variant >= 20 && variant <= 29) || (variant >= 38 && variant <= 49) || variant == 52 || variant == 53 || variant == 55) && pok) ||
                   (variant >= 30 && variant <= 37 && x4_ok),
               "roi_align variant %d unsupported here", variant);
   const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
@@ -1597,6 +1597,10 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else
       hipLaunchKernelGGL((roi_align_fwd_pair_dyn_kernel<kPairWave, kPairHalf, kCpolNT, true>), dim3(8 * wpl), dim3(kWave),
                          0, as_stream(stream), lv, c, out, wpl);
+  } else if (variant == 55) {  // the default with the lean tap state (kLean)
+    const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, kCpolNT, 0, false, true, 1, true, 1, true>),
+                       dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (variant == 29) {  // product kernel (single buffer, nt stores) with two items per wave
     const int64_t total = num_rois * ((channels + 2 * kPairWave - 1) / (2 * kPairWave));
     const int64_t per = (total + 7) / 8;

@@ -1,5 +1,5 @@
 set -e
-mkdir -p gpurun_out/s27
+mkdir -p gpurun_out/s28
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_tools_variants.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s27/t.log 2>&1
-timeout -k 10 300 python tools/bench_roi_align.py --variants 47,54 --iters 100 --rounds 7 > gpurun_out/s27/roi.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_tools_variants.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s28/t.log 2>&1
+timeout -k 10 300 python tools/bench_roi_align.py --variants 47,55 --iters 100 --rounds 7 > gpurun_out/s28/roi.log 2>&1
