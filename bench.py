@@ -328,7 +328,7 @@ def main():
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
                        'sampler': args.sampler, 'mode': args.mode},
-            'roofline': {'kernel': 'roi_align_fwd_pair_kernel<8, 1664, 1, 2, 0, false, true> (single slab buffer, nt stores)', 'bound': 'hbm',
+            'roofline': {'kernel': 'roi_align_fwd_pair_kernel<8, 1664, 1, 2, 0, false, true, 1, true, 1, true> (single slab buffer, nt stores, lean tap state)', 'bound': 'hbm',
                          'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': traffic,
                          'avg_launch_us': avg_ms * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,

@@ -70,10 +70,11 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   if (pair_ok(f, channels, pooled_h, pooled_w)) {
     // chunk-major XCD order (kOrder 1), nt output stores, ONE slab buffer per wave (kSingle:
     // 6.5 KB of LDS, so 16 resident waves per CU instead of 11 -- the register count caps it
-    // there; 37.2 vs 40.9 us on the cfg2 RoIs, tools/bench_roi_align.py variants 47 / 21)
+    // there; 37.2 vs 40.9 us on the cfg2 RoIs, tools/bench_roi_align.py variants 47 / 21), and
+    // the lean tap state (kLean: 95 VGPRs, so 20 resident waves per CU; variant 55)
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, kCpolNT, 0, false, true>),
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, kCpolNT, 0, false, true, 1, true, 1, true>),
                        dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (f.lds) {
     const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
