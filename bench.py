@@ -13,11 +13,19 @@ path (anchor targets, proposals+NMS, RCNN targets, RoIAlign) and the losses.
 Images are independent units: ranks share nothing on the data path
 ("scaling": "weak"); the forward+loss metric has no collective.
 
-The JSON line carries the RoIAlign forward roofline (the timed region's launches
-replayed back to back between one HIP event pair on their stream, algorithmic
-bytes per SURVEY §8(d), PMC traffic from profiles/roi_align_pmc.json) and a CPU
-baseline: the same forward+loss on the host, with the hot path run by the
-oracle's C restatement (oracle/pipeline.py), on a bounded 1-image sample.
+After the timed region (never inside it):
+  * kernel lines: `--trace-steps` more steps run under the ROCm kernel tracer
+    (torch.profiler / kineto), giving every hot-path kernel's in-step device
+    duration and its dispatched name.  The RoIAlign `roofline` is computed from
+    the in-step duration (SURVEY §8(d) algorithmic bytes / in-step µs); the same
+    launches replayed back to back (warm caches) and after a 768 MB read that
+    evicts L2 and the Infinity Cache (cold) are reported beside it.  Assignment,
+    proposal selection/decode and NMS get the same line with their §8(d) bytes.
+  * `cpu_baseline`: the same forward+loss on the host (torch CPU convs + the
+    oracle's C restatement of the hot path), bounded 1-image sample, img/s.
+  * `cpu_baseline_hot_path`: the oracle's C assign / anchor_target /
+    proposals+NMS / RoIAlign timed on this run's own inputs on one host core,
+    beside the GPU µs of the same functions.
 """
 import argparse
 import json
@@ -42,6 +50,17 @@ CONFIG_NAMES = {'faster_rcnn_r50_fpn': 'FasterRCNN_R50_FPN', 'faster_rcnn_r50': 
                 'fcos_r50_fpn_atss': 'ATSS_R50_FPN'}
 IMG_SHAPE, PAD_SHAPE = (600, 1000), (608, 1024)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# in-step kernel groups of the detection path (substrings of the dispatched kernel names)
+KERNEL_GROUPS = [
+    ('roi_align_fwd', ('roi_align_fwd',)),
+    ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
+    ('proposals', ('rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
+    ('assign', ('assign_',)),
+    ('sampler', ('sampler_', 'chunk_count', 'chunk_write_lists')),
+    ('targets', ('anchor_target_kernel', 'bbox_target_kernel', 'prepend_gt', 'gather_levels', 'roi_level')),
+    ('losses', ('cls_loss', 'smooth_l1', 'loss_finalize')),
+]
 
 
 def img_meta():
@@ -93,14 +112,104 @@ def roi_align_bytes(rec):
     return 4 * C * (K * ph * pw + feat_elems) + 20 * K
 
 
-def nms_roofline(recs, dev):
-    """The timed steps' RPN NMS calls (all images x levels per call: mask + scan kernels)
-    replayed back to back between one HIP event pair on their stream, with preallocated
-    outputs; algorithmic bytes per ops.nms_bytes.  NMS at RPN sizes is
-    latency-bound (greedy scan), so the fraction is reported next to the microseconds."""
+# ------------------------------------------------------------------ in-step kernel trace
+def kernel_trace(step, n, dev):
+    """Run `n` steps under the ROCm kernel tracer (torch.profiler, CUDA=HIP activity) and
+    return [(kernel name, device µs)] in dispatch order, or (None, reason)."""
+    try:
+        from torch.profiler import profile, ProfilerActivity
+        from torch.autograd import DeviceType
+    except Exception as e:  # pragma: no cover
+        return None, 'torch.profiler unavailable: {!r}'.format(e)[:200]
+    torch.cuda.synchronize(dev)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize(dev)
+    ks = []
+    for e in prof.events():
+        if e.device_type in (DeviceType.CUDA, getattr(DeviceType, 'HIP', DeviceType.CUDA)) and e.name:
+            ks.append((e.time_range.start, e.name, e.time_range.elapsed_us()))
+    ks.sort()
+    if not any('frh::' in k[1] for k in ks):
+        return None, 'the kernel tracer reported no frcnn_amd kernels ({} device events)'.format(len(ks))
+    return [(name, float(us)) for _, name, us in ks], None
+
+
+def group_of(name):
+    for g, keys in KERNEL_GROUPS:
+        if any(k in name for k in keys):
+            return g
+    return None
+
+
+def summarise_trace(trace, steps):
+    """Per-step µs of each kernel group + the detection-path total (frcnn_amd kernels
+    other than the trunk's bn_act epilogue)."""
+    per = {g: 0.0 for g, _ in KERNEL_GROUPS}
+    names = {g: {} for g, _ in KERNEL_GROUPS}
+    det = 0.0
+    for name, us in trace:
+        if 'frh::' in name and 'bn_act' not in name:
+            det += us
+        g = group_of(name)
+        if g:
+            per[g] += us
+            short = name.split('(')[0].replace('void ', '')
+            names[g][short] = names[g].get(short, 0) + 1
+    return ({g: v / steps for g, v in per.items()}, det / steps,
+            {g: {k: c // steps for k, c in d.items()} for g, d in names.items()})
+
+
+# ------------------------------------------------------------------ RoIAlign replays
+def roi_align_replays(recs, dev, rounds=3):
+    """The recorded launches replayed back to back between one HIP event pair: warm (the
+    same features stay in L2 / Infinity Cache) and cold (each launch after a 768 MB read
+    that evicts both; cold = (evict+launch arm - evict-only arm) / launches, median of
+    `rounds`)."""
+    from frcnn_amd import ops
+    if not recs:
+        return None, None
+    for r in recs[:2]:
+        ops.roi_align_replay(r)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for r in recs:
+        ops.roi_align_replay(r)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    warm = e0.elapsed_time(e1) * 1e3 / len(recs)
+    scratch = torch.ones(768 * 2 ** 20 // 4, dtype=torch.float32, device=dev)
+    sink = torch.empty((), dtype=torch.float32, device=dev)
+
+    def evict():
+        torch.sum(scratch, dim=0, out=sink)  # reads only: no dirty lines for the launch to write back
+
+    evict()
+    colds = []
+    for _ in range(rounds):
+        arms = []
+        for with_launch in (True, False):
+            torch.cuda.synchronize(dev)
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record()
+            for r in recs:
+                evict()
+                if with_launch:
+                    ops.roi_align_replay(r)
+            a1.record()
+            torch.cuda.synchronize(dev)
+            arms.append(a0.elapsed_time(a1) * 1e3)
+        colds.append((arms[0] - arms[1]) / len(recs))
+    del scratch
+    return warm, float(np.median(colds))
+
+
+def nms_replay_us(recs, dev):
+    """The recorded RPN NMS calls replayed back to back (warm); µs per call."""
+    from frcnn_amd import _lib
     if not recs:
         return None
-    from frcnn_amd import ops, _lib
     outs = []
     for ws, rows, cnt, P, thr, max_keep in recs:
         S = rows.shape[0]
@@ -122,18 +231,18 @@ def nms_roofline(recs, dev):
         launch(o)
     e1.record()
     torch.cuda.synchronize(dev)
-    us = e0.elapsed_time(e1) * 1e3 / len(outs)
-    nbytes = float(np.mean([ops.nms_bytes(o[1], o[6]) for o in outs]))
-    achieved = nbytes / (us * 1e-6) / 1e9
-    segs = outs[0][0].shape[0]
-    return {'kernel': 'nms_mask_kernel + nms_scan_kernel (RPN, {} segments of <= {} boxes)'.format(
-                segs, outs[0][2]),
-            'bound': 'latency (greedy scan); hbm for the mask', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'avg_call_us': us,
-            'algorithmic_bytes_per_call': nbytes, 'calls': len(outs),
-            'timing': 'the timed steps\' RPN NMS calls replayed back to back between one HIP event pair'}
+    return e0.elapsed_time(e1) * 1e3 / len(outs), outs
 
 
+def line(us, nbytes, what):
+    if us is None or not us or nbytes is None:
+        return {'us_per_step': us, 'algorithmic_bytes_per_step': nbytes, 'note': what}
+    gbs = nbytes / (us * 1e-6) / 1e9
+    return {'us_per_step': us, 'algorithmic_bytes_per_step': nbytes, 'achieved': gbs, 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS, 'bytes': what}
+
+
+# ------------------------------------------------------------------ CPU baselines
 def cpu_baseline(seed, max_s):
     """Same forward+loss on the host: torch CPU convs + the oracle's C hot path, 1 image."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -154,10 +263,73 @@ def cpu_baseline(seed, max_s):
                       '{} threads)'.format(n, threads)}
 
 
+def hot_path_cpu_baseline(model, cfg, batch, roi_rec, dev, gpu_us, batch_size):
+    """The oracle's C restatement of the hot-path functions on THIS run's inputs (the
+    trunk's RPN outputs, the VOC gts, the timed step's RoIs and features), one host core,
+    each function on every image of the batch; GPU µs of the same functions beside."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import oracle  # oracle/oracle.py (test infrastructure: the timed CPU baseline)
+    imgs, gts, gt_labels, metas = batch
+    with torch.no_grad():
+        feats = model.extract_feat(imgs)
+        cls_outs, reg_outs = model.rpn_head(feats)
+        grids = [tuple(c.shape[-2:]) for c in cls_outs]
+        anchors = model.rpn_head._flat_anchors(grids, dev)
+        masks = model.rpn_head._valid_masks(anchors, grids, metas, cfg.train_cfg.rpn.allowed_border)
+    anc = anchors.cpu().numpy()
+    A = model.rpn_head.num_anchors
+    lv_anc, off = [], 0
+    for h, w in grids:
+        lv_anc.append(anc[:, off:off + A * h * w].reshape(4, A, h, w))
+        off += A * h * w
+    mk = masks.cpu().numpy().astype(bool)
+    cls_np = [c.cpu().numpy() for c in cls_outs]
+    reg_np = [r.cpu().numpy() for r in reg_outs]
+    t = {'assign': 0.0, 'anchor_target': 0.0, 'proposals_nms': 0.0, 'roi_align': 0.0}
+    B = imgs.shape[0]
+    rc = cfg.train_cfg.rpn
+    pc = cfg.train_cfg.rpn_proposal
+    for i in range(B):
+        gt = gts[i].cpu().numpy()
+        in_anc = np.ascontiguousarray(anc[:, mk[i]])
+        t0 = time.perf_counter()
+        oracle.maxiou_assign(in_anc, gt, rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou)
+        t['assign'] += time.perf_counter() - t0
+        co = np.concatenate([c[i].reshape(1, -1) for c in cls_np], 1)
+        ro = np.concatenate([r[i].reshape(4, -1) for r in reg_np], 1)
+        t0 = time.perf_counter()
+        oracle.anchor_target(co, ro, 1, in_anc, mk[i], gt, None,
+                             (rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou),
+                             (rc.sampler.max_num, rc.sampler.pos_num), None, None)
+        t['anchor_target'] += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        oracle.rpn_predict_single_image([c[i] for c in cls_np], [r[i] for r in reg_np], lv_anc, IMG_SHAPE,
+                                        float(pc.min_bbox_size), pc.pre_nms, pc.post_nms, pc.max_num, pc.nms_iou)
+        t['proposals_nms'] += time.perf_counter() - t0
+    if roi_rec is not None:
+        _, _, rois, levels, shapes, (ph, pw) = roi_rec[:6]
+        scales = roi_rec[7]
+        fnp = [f.cpu().numpy() for f in feats[:len(shapes)]]
+        t0 = time.perf_counter()
+        oracle.roi_align(fnp, rois.cpu().numpy(), levels.cpu().numpy(), scales, (ph, pw), 2)
+        t['roi_align'] = time.perf_counter() - t0
+    per_img = {k: v * 1e3 / B for k, v in t.items()}
+    out = {'unit': 'ms per image', 'cores': 1, 'kind': 'port',
+           'sample': 'oracle C restatement on this run\'s {} images: trunk RPN outputs, VOC gts, the timed step\'s '
+                     'RoIs + P2-P5 features'.format(B),
+           'cpu_ms_per_image': per_img, 'gpu_us_per_image': {k: (v / batch_size if v is not None else None)
+                                                              for k, v in gpu_us.items()}}
+    out['speedup'] = {k: (per_img[k] * 1e3 / out['gpu_us_per_image'][k]) if out['gpu_us_per_image'].get(k) else None
+                      for k in per_img}
+    return out
+
+
 def max_over_ranks(elapsed, dev, world):
     """Job time = the slowest rank's (weak scaling: every rank has its own shard)."""
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
+        if dist.get_backend() == 'gloo':
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -177,6 +349,14 @@ def main():
     ap.add_argument('--sampler', default='device', choices=['device', 'numpy'])
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--trace-steps', type=int, default=3,
+                    help='extra steps (after the timed region) run under the kernel tracer for the kernel lines; 0 = off')
+    ap.add_argument('--proposal-stream', default='on', choices=['on', 'off'],
+                    help='RPN proposal chain on a side stream, concurrent with the RPN target / loss chain')
+    ap.add_argument('--rpn-order', default='finest-last', choices=['finest-last', 'reference'],
+                    help='level order of the RPN head convs (finest-last keeps P2 cache-resident for RoIAlign)')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='torch.distributed backend for N > 1 (nccl = RCCL; gloo lets several ranks share one GPU)')
     ap.add_argument('--mode', default='fwd', choices=['fwd', 'train'],
                     help='fwd: forward+loss (the BASELINE metric); train: forward+loss+backward with the '
                          'DDP gradient all-reduce (RCCL) + grad clip + SGD step (frcnn_amd.train)')
@@ -197,12 +377,17 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local % ndev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group('gloo')
+    dev = torch.device('cuda', torch.cuda.current_device() if world > 1 else local)
     import frcnn_amd
     from frcnn_amd import ops
     frcnn_amd.set_sampler_mode(args.sampler, seed=1234 + rank)
+    frcnn_amd.set_proposal_stream(args.proposal_stream == 'on')
     np.random.seed(rank)
 
     if args.conv_search == 'auto':
@@ -211,6 +396,8 @@ def main():
     torch.backends.cudnn.benchmark = args.conv_search
     model, cfg = make_model(dev, seed=0, config=os.path.join(CONFIG_DIR, args.config + '.py'))
     batch = make_batch(dev, args.batch, seed=0, rank=rank)
+    if hasattr(model, 'rpn_head'):
+        model.rpn_head.finest_last = args.rpn_order == 'finest-last'
 
     if args.mode == 'train':
         from frcnn_amd.train import TrainStep, DEFAULT_BUCKET_MB
@@ -262,50 +449,43 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    ops.ROI_ALIGN_PROFILE['records'].clear()
-    ops.ROI_ALIGN_PROFILE['on'] = True
-    ops.NMS_PROFILE['records'].clear()
-    ops.NMS_PROFILE['on'] = True
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     barrier()
     elapsed = time.perf_counter() - t0
-    ops.ROI_ALIGN_PROFILE['on'] = False
-    ops.NMS_PROFILE['on'] = False
     assert torch.isfinite(loss).all()
-
     t_max = max_over_ranks(elapsed, dev, world)
 
-    recs = ops.ROI_ALIGN_PROFILE['records']
-    ms = [r[0].elapsed_time(r[1]) for r in recs]  # per-launch event pairs inside the steps
-    bytes_per = [roi_align_bytes(r) for r in recs]
-    # Kernel duration: the timed region's launches replayed back to back on their stream
-    # between one HIP event pair (per-launch pairs add the event packets' own latency).
-    avg_ms = float('nan')
-    if recs:
-        for r in recs[:2]:
-            ops.roi_align_replay(r)  # warm
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        r0.record()
-        for r in recs:
-            ops.roi_align_replay(r)
-        r1.record()
-        torch.cuda.synchronize(dev)
-        avg_ms = r0.elapsed_time(r1) / len(recs)
-    avg_bytes = float(np.mean(bytes_per)) if bytes_per else float('nan')
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if ms else None
-
-    nms_line = nms_roofline(ops.NMS_PROFILE['records'], dev)
-    ops.NMS_PROFILE['records'].clear()
-
-    traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json')
-    if os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
-
+    # ---- after the timed region: kernel lines (rank 0 only; other ranks idle)
+    out = None
     if rank == 0:
+        ops.ROI_ALIGN_PROFILE['records'].clear()
+        ops.NMS_PROFILE['records'].clear()
+        ops.ROI_ALIGN_PROFILE['on'] = ops.NMS_PROFILE['on'] = True
+        ops.ROI_ALIGN_PROFILE['events'] = False  # records only: no event packets around the launches
+        trace, trace_err = (None, 'disabled') if args.trace_steps <= 0 else kernel_trace(step, args.trace_steps, dev)
+        if args.trace_steps <= 0:  # still record the launches of one step for the replays
+            step()
+        ops.ROI_ALIGN_PROFILE['on'] = ops.NMS_PROFILE['on'] = False
+        ops.ROI_ALIGN_PROFILE['events'] = True
+        steps_traced = max(args.trace_steps, 1)
+        recs = list(ops.ROI_ALIGN_PROFILE['records'])
+        nrecs = list(ops.NMS_PROFILE['records'])
+        per_group, det_us, group_names = summarise_trace(trace, steps_traced) if trace else ({}, None, {})
+        roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]
+        roi_in_step = float(np.mean([us for _, us in roi_launches])) if roi_launches else None
+        roi_kernel = roi_launches[0][0].split('(')[0].replace('void ', '') if roi_launches else None
+        warm, cold = roi_align_replays(recs, dev)
+        avg_bytes = float(np.mean([roi_align_bytes(r) for r in recs])) if recs else None
+        us_for_frac = roi_in_step if roi_in_step else warm
+        achieved = avg_bytes / (us_for_frac * 1e-6) / 1e9 if recs and us_for_frac else None
+        traffic = None
+        pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json')
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+
         imgs_total = world * args.batch * args.steps
         out = {
             'metric': 'img/s ' + CONFIG_NAMES[args.config] + ' 1000x600 ' + ('fwd+loss' if args.mode == 'fwd' else
@@ -327,32 +507,90 @@ def main():
                        'trunk': 'hipGraph replay (backbone + neck + RPN head convs)' if graphed else 'eager',
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
-                       'sampler': args.sampler, 'mode': args.mode},
-            'roofline': {'kernel': 'roi_align_fwd_pair_kernel<8, 1664, 1, 2, 0, false, true, 1, true, 1, true> (single slab buffer, nt stores, lean tap state)', 'bound': 'hbm',
-                         'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': traffic,
-                         'avg_launch_us': avg_ms * 1e3, 'algorithmic_bytes_per_launch': avg_bytes,
-                         'launches': len(ms), 'avg_launch_us_in_step_events': float(np.mean(ms)) * 1e3,
-                         'timing': 'the timed steps\' RoIAlign launches replayed back to back between one HIP event '
-                                   'pair on their stream; traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '
-                                   'launch, profiles/roi_align_pmc.json'},
+                       'backend': args.backend if world > 1 else None,
+                       'sampler': args.sampler, 'mode': args.mode, 'proposal_stream': args.proposal_stream,
+                       'rpn_order': args.rpn_order},
         }
-        if not recs:
+        if recs:
+            out['roofline'] = {
+                'kernel': roi_kernel or 'frh_roi_align_fwd_strided (name unavailable: {})'.format(trace_err),
+                'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS if achieved else None, 'traffic': traffic,
+                'avg_launch_us': us_for_frac, 'algorithmic_bytes_per_launch': avg_bytes,
+                'launches': len(roi_launches) or len(recs),
+                'avg_launch_us_in_step': roi_in_step, 'avg_launch_us_replay_warm': warm,
+                'avg_launch_us_replay_cold': cold,
+                'timing': ('in-step device durations from the ROCm kernel tracer (torch.profiler) over {} steps '
+                           'after the timed region'.format(steps_traced) if roi_in_step else
+                           'kernel tracer unavailable ({}): back-to-back replay, warm caches'.format(trace_err)) +
+                          '; replay_warm = the same launches back to back, replay_cold = each after a 768 MB read '
+                          '(L2 + Infinity Cache evicted); traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '
+                          'launch, profiles/roi_align_pmc.json'}
+        else:
             out['roofline'] = None  # no RoIAlign on this model's path
-        if nms_line:
-            out['nms'] = nms_line
-            if recs:  # the two kernels the north star names, as one HBM fraction per step
-                b = avg_bytes + nms_line['algorithmic_bytes_per_call']
-                t = avg_ms * 1e-3 + nms_line['avg_call_us'] * 1e-6
-                out['roi_align_nms_combined'] = {'bytes': b, 'us': t * 1e6, 'achieved': b / t / 1e9,
-                                                 'frac': b / t / 1e9 / HBM_PEAK_GBS, 'unit': 'GB/s'}
+        if trace:
+            B = args.batch
+            lines = {}
+            nbytes_nms = float(np.mean([ops.nms_bytes(r[2], torch.clamp(r[2], max=r[5] if r[5] > 0 else r[3]))
+                                        for r in nrecs])) if nrecs else None
+            nrep = nms_replay_us(nrecs, dev)
+            if nrep:  # algorithmic bytes with the real keep counts of the replayed calls
+                nbytes_nms = float(np.mean([ops.nms_bytes(o[1], o[6]) for o in nrep[1]]))
+            lines['nms'] = line(per_group.get('nms'), nbytes_nms,
+                                '20*N + 16*N*ceil(N/64) + 8*K_keep per segment (SURVEY §8(d)); RPN call, {} '
+                                'segments'.format(nrecs[0][1].shape[0] if nrecs else 0))
+            if nrep:
+                lines['nms']['us_replay_warm'] = nrep[0]
+            if args.config in ('faster_rcnn_r50_fpn', 'cascade_rcnn_r50_fpn'):
+                n_all = sum(model.rpn_head.num_anchors * h * w for h, w in
+                            [(int(np.ceil(PAD_SHAPE[0] / s)), int(np.ceil(PAD_SHAPE[1] / s)))
+                             for s in model.rpn_head.anchor_strides])
+                n_in = 130833  # inside anchors of a 600x1000 image at cfg2 (tests pin the mask)
+                assign_trace = [(n, us) for n, us in trace if 'assign_' in n]
+                per_call = len(assign_trace) // steps_traced  # RPN call first, then the RCNN call(s)
+                rpn_assign = (sum(sum(us for _, us in assign_trace[i * per_call:i * per_call + 2])
+                                  for i in range(steps_traced)) / steps_traced) if per_call >= 2 else None
+                lines['assign_rpn'] = line(rpn_assign, B * (16 * n_all + n_all + 12 * n_in),
+                                           '16*N_all + N_all + 12*N_in per image (SURVEY §8(d)), RPN anchors')
+                lines['assign_all'] = {'us_per_step': per_group.get('assign'), 'note': 'RPN + RCNN assignment'}
+                lines['proposals'] = line(per_group.get('proposals'), B * (36 * n_all + 20 * 2000),
+                                          '36*N_all + 20*2000 per image (SURVEY §8(d)): selection, decode, merge')
+                for g in ('sampler', 'targets', 'losses'):
+                    lines[g] = {'us_per_step': per_group.get(g)}
+            lines['roi_align_fwd'] = {'us_per_step': per_group.get('roi_align_fwd')}
+            out['kernels'] = {'per_step': lines, 'detection_path_us_per_step': det_us, 'dispatched': group_names,
+                              'timing': 'in-step device durations, ROCm kernel tracer, {} steps'.format(steps_traced)}
+            if recs and lines.get('nms', {}).get('us_per_step'):
+                b = avg_bytes + lines['nms']['algorithmic_bytes_per_step']
+                t = us_for_frac + lines['nms']['us_per_step']
+                out['roi_align_nms_combined'] = {'bytes': b, 'us': t, 'achieved': b / (t * 1e-6) / 1e9,
+                                                 'frac': b / (t * 1e-6) / 1e9 / HBM_PEAK_GBS, 'unit': 'GB/s',
+                                                 'timing': 'in-step'}
+        else:
+            out['kernels'] = {'error': trace_err}
         if not args.no_cpu_baseline and world == 1 and args.config == 'faster_rcnn_r50_fpn':
             try:
-                out['cpu_baseline'] = cpu_baseline(0, args.cpu_baseline_seconds)
+                k = out.get('kernels', {}).get('per_step', {})
+                gpu_us = {'assign': k.get('assign_rpn', {}).get('us_per_step'),
+                          'anchor_target': (sum(k.get(g, {}).get('us_per_step') or 0 for g in ('assign_rpn',)) +
+                                            ((k.get('sampler', {}).get('us_per_step') or 0) +
+                                             (k.get('targets', {}).get('us_per_step') or 0)) / 2) if k else None,
+                          'proposals_nms': ((k.get('proposals', {}).get('us_per_step') or 0) +
+                                            (k.get('nms', {}).get('us_per_step') or 0)) if k else None,
+                          'roi_align': us_for_frac}
+                out['cpu_baseline_hot_path'] = hot_path_cpu_baseline(model, cfg, batch, recs[-1] if recs else None,
+                                                                     dev, gpu_us, args.batch)
+                out['cpu_baseline_hot_path']['gpu_note'] = ('anchor_target GPU = RPN assignment + half the per-step '
+                                                            'sampler and target kernels (the RPN call of two)')
             except Exception as e:  # the baseline must never hide the GPU number
+                out['cpu_baseline_hot_path'] = {'error': repr(e)[:300]}
+            try:
+                out['cpu_baseline'] = cpu_baseline(0, args.cpu_baseline_seconds)
+            except Exception as e:
                 out['cpu_baseline'] = {'value': None, 'error': repr(e)[:200]}
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -97,7 +97,11 @@ int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
  *      keep_counts [S,2]) and writes labels_out (-1 for everything else).
  *  (2) device RNG: frh_sample_random keeps min(npos,pos_num) positives and
  *      min(nneg, max_num-kept_pos) negatives, each chosen uniformly without
- *      replacement by the smallest 32-bit hash(seed, seg, box) keys. */
+ *      replacement by the smallest 32-bit hash(seed, seg, box) keys.  Outputs
+ *      (either or both): labels_out (the sampled labels, -1 elsewhere) and / or
+ *      sel [S][2][max_num] (the kept positives / negatives, in no order) with
+ *      sel_counts [S][2] -- the form frh_anchor_target / frh_bbox_target take
+ *      without a compaction pass over every box. */
 size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes);
 int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                               const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
@@ -110,8 +114,8 @@ int32_t frh_sample_apply(int32_t num_segs, const int64_t* labels_in, int64_t lab
                          const int32_t* keep_counts, int64_t* labels_out, void* stream);
 int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                           const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
-                          int32_t pos_num, uint64_t seed, int64_t* labels_out,
-                          void* workspace, size_t ws_bytes, void* stream);
+                          int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
+                          int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- a6: anchor_target (lib/anchor.py:11-76) after assign+sample -------------
  * Chosen = boxes with sampled label >= 0, ascending.  Segment outputs are
@@ -121,13 +125,18 @@ int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t la
  *   chosen_idx[j] (int64, index into the per-segment box space),
  *   seg_of[j] (int32), tar_labels[j] (int64: gt_label[g] or 0 for negatives;
  *   gt_label == nullptr => 1/0), tar_anchors/tar_bbox/tar_param [4, out_ld].
- * tar_param = (bbox2param(anchor, gt) - means) / stds (anchor.py:69-73). */
+ * tar_param = (bbox2param(anchor, gt) - means) / stds (anchor.py:69-73).
+ * sel / sel_counts (nullable; frh_sample_random's lists, max_num = max_out_per_seg
+ * <= 8192): the chosen boxes are those lists (ranked into ascending box order in
+ * the gather itself) and `labels` are the assignment labels before sampling; no
+ * workspace is needed. */
 int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                           const int32_t* num_boxes, int64_t max_boxes, const float* anchors,
                           int64_t anchor_ld, int64_t anchor_seg_stride, const float* gts,
                           int64_t gt_ld, int64_t gt_seg_stride, const int64_t* gt_labels,
                           int64_t gt_label_seg_stride, const float* means, const float* stds,
-                          int64_t max_out_per_seg, int64_t* chosen_idx, int32_t* seg_of,
+                          int64_t max_out_per_seg, const int32_t* sel, const int32_t* sel_counts,
+                          int64_t* chosen_idx, int32_t* seg_of,
                           int64_t* tar_labels, float* tar_anchors, float* tar_bbox,
                           float* tar_param, int64_t out_ld, int32_t* out_counts,
                           void* workspace, size_t ws_bytes, void* stream);
@@ -155,7 +164,8 @@ int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
  * frh_bbox_target (labels = the sampled rows, num_rows from the prepend)
  * gathers the chosen rows (ascending) into concatenated
  * outputs: tar_props/tar_bbox/tar_param [4, out_ld], tar_label (int64, gt
- * class or 0), tar_is_gt (int64 0/1), out_counts[S+1] as in frh_anchor_target. */
+ * class or 0), tar_is_gt (int64 0/1), out_counts[S+1] as in frh_anchor_target;
+ * sel / sel_counts as in frh_anchor_target (labels = the prepended rows). */
 int32_t frh_prepend_gt_labels(int32_t num_segs, const int64_t* prop_labels,
                               int64_t prop_label_seg_stride, const int32_t* num_props,
                               const int32_t* num_gts, int64_t max_rows, int64_t* rows_out,
@@ -167,6 +177,7 @@ int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int64_t label_s
                         const float* gts, int64_t gt_ld, int64_t gt_seg_stride,
                         const int64_t* gt_labels, int64_t gt_label_seg_stride,
                         const float* means, const float* stds, int64_t max_out_per_seg,
+                        const int32_t* sel, const int32_t* sel_counts,
                         float* tar_props, float* tar_bbox, int64_t* tar_label,
                         float* tar_param, int64_t* tar_is_gt, int64_t out_ld,
                         int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream);
@@ -216,8 +227,11 @@ int32_t frh_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_levels, const i
 
 /* ---- a10: torchvision.ops.nms on pre-sorted segments --------------------------
  * boxes [S, n_max, 4] row-major xyxy, already in descending-score order
- * (stable); count[s] valid rows.  keep[s, :] = kept row positions (ascending
- * = score order), keep_counts[s].  max_keep >= 0 stops after that many. */
+ * (stable); count[s] valid rows, n_max <= 65536 (the offset-trick batched_nms of
+ * lib/utils.py:211-221 runs one NMS over up to 1000 proposals x 20 classes).
+ * keep[s, :] = kept row positions (ascending = score order), keep_counts[s].
+ * max_keep >= 0 stops after that many.  Workspace: one upper-triangle suppression
+ * mask of ceil(n_max / 64) column blocks per segment (512 B per 64x64 tile). */
 size_t frh_nms_workspace(int32_t num_segs, int32_t n_max);
 int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride,
                        const int32_t* counts, int32_t n_max, double iou_thr, int32_t max_keep,
@@ -236,15 +250,18 @@ int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride,
  * (row, class) pair), 1 strict (argmax class per row); pairs need score >=
  * min_score; the score is multiplied by score_factor after that test.
  * by_class = 1: one segment per (image, class); 0: one per image (the reference's
- * single pass; needed when a candidate coordinate is < 0).  Two calls: prepare
- * (candidates + per-segment sort; one stream sync; info[0] = the largest segment,
- * info[1] = 1 if a candidate coordinate is < 0 -- with by_class = 1 the caller then
- * redoes prepare with by_class = 0), then finish (same mode / by_class; scores
- * needed in strict mode) with an NMS workspace of frh_mcnms_nms_workspace(...,
- * info[0]) bytes: torchvision nms per segment,
- * the keeps of all classes merged in (score desc, candidate asc) order, the first
- * max_num (<= 0: all) written to out_boxes [B][out_cap][4], out_scores [B][out_cap],
- * out_labels [B][out_cap] (the class index), out_counts [B] (device). */
+ * single pass; needed when a candidate coordinate is < 0).  Two calls, neither of
+ * which allocates or synchronises: prepare (candidates + per-segment NMS mask
+ * offsets) writes the device int32 info[4]: info[0] = the largest segment (limit
+ * 65536), info[1] = 1 if a candidate coordinate is < 0 (with by_class = 1 the caller
+ * then redoes prepare with by_class = 0), info[2] | info[3] << 32 = the NMS mask
+ * tiles.  The caller copies info to the host, then calls finish (same mode /
+ * by_class; scores needed in strict mode) with max_count = info[0], mask_tiles =
+ * info[2..3] and an NMS workspace of frh_mcnms_nms_workspace(..., max_count,
+ * mask_tiles) bytes: per-segment sort (score desc, candidate asc), torchvision nms per
+ * segment, the keeps of all classes merged in (score desc, candidate asc) order, the
+ * first max_num (<= 0: all) written to out_boxes [B][out_cap][4], out_scores
+ * [B][out_cap], out_labels [B][out_cap] (the class index), out_counts [B] (device). */
 size_t frh_mcnms_workspace(int32_t num_imgs, int32_t num_classes, int64_t n_max);
 int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int64_t n_max, const int32_t* num_rows,
                           const float* boxes, int64_t box_img_stride, int32_t box_per_class,
@@ -253,9 +270,9 @@ int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int64_t n_max, 
                           int64_t valid_img_stride, const uint8_t* channel_mask, int32_t mode,
                           int32_t by_class, float min_score, void* workspace, size_t ws_bytes,
                           int32_t* info, void* stream);
-size_t frh_mcnms_nms_workspace(int32_t num_imgs, int32_t num_classes, int32_t max_count);
+size_t frh_mcnms_nms_workspace(int32_t num_imgs, int32_t num_classes, int32_t max_count, int64_t mask_tiles);
 int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64_t n_max, int32_t max_count,
-                         const float* boxes, int64_t box_img_stride, int32_t box_per_class,
+                         int64_t mask_tiles, const float* boxes, int64_t box_img_stride, int32_t box_per_class,
                          const float* scores, int64_t score_img_stride, int32_t mode, int32_t by_class,
                          double nms_iou, int32_t max_num, float* out_boxes, float* out_scores,
                          int64_t* out_labels, int32_t* out_counts, int64_t out_cap, void* workspace,

@@ -18,9 +18,15 @@
 //                         (score desc, candidate asc) -- the reference's stable
 //                         sort order -- in LDS and writes the shifted boxes
 //                         (box + float(label) * max, in f32 as the reference).
-//            -> the largest segment count comes back to the host (one sync)
-//               to size the NMS mask.
-//   finish   nms        : nms.hip over all segments, max_num keeps per segment.
+//            summary    : one workgroup: the largest segment count, the negative-
+//                         coordinate flag and each segment's NMS mask offset (its
+//                         own triangle of 64x64 tiles) into a caller-provided device
+//                         `info` / the workspace.  The caller copies `info` back (its
+//                         one sync) to size the sort and the NMS workspace.
+//   finish   sort       : as above; segments above 16384 candidates are sorted in
+//                         16384-record chunks and merged by rank (binary searches).
+//            nms        : nms.hip over all segments, max_num keeps per segment, each
+//                         segment's mask sized by its own count.
 //            merge      : per image, the kept pairs of all classes ranked by
 //                         (score desc, candidate asc) with binary searches
 //                         into the other classes' keep lists; the first
@@ -42,10 +48,10 @@ namespace frh {
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, hipStream_t st);
-size_t nms_mask_bytes(int32_t S, int32_t n_max);
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st);
 
-constexpr int kMcMaxSeg = 16384;  // per-segment candidates (NMS and LDS sort limit)
+constexpr int kMcMaxSeg = 65536;    // per-segment candidates (the NMS limit)
+constexpr int kMcSortChunk = 16384; // records sorted per workgroup in LDS (128 KB)
 
 struct McArgs {
   int B, C;
@@ -71,6 +77,7 @@ struct McArgs {
   uint32_t* maxk;    // [B] float_key of the largest candidate coordinate
   uint32_t* negk;    // [B] ~float_key of the smallest (nonzero: some coordinate < 0)
   uint64_t* rec;     // [segments][seg_ld] (B * C * n_max entries in all)
+  int64_t* seg_base; // [S + 1] NMS mask tile offset of each segment (summary kernel)
   float4* rows;      // shifted boxes, sorted
   float* ssc;        // scores, sorted
   int32_t* scand;    // candidates, sorted
@@ -145,33 +152,117 @@ static __global__ void __launch_bounds__(256) mc_candidates_kernel(McArgs a) {
   if (lane_id() == 0 && nk) atomicMax(&a.negk[b], nk);
 }
 
-// one 1024-thread workgroup per segment; dynamic LDS next_pow2(max count) u64
-static __global__ void __launch_bounds__(1024) mc_sort_kernel(McArgs a) {
+// sorted record r of segment seg at position j: the shifted box, the score, the candidate
+__device__ __forceinline__ void mc_emit(const McArgs& a, int seg, int b, int64_t j, uint64_t r) {
+  const float M = key_float(a.maxk[b]);
+  const uint32_t cand = ~(uint32_t)r;
+  int c;
+  const int64_t i = mc_row(a, b, cand, &c);
+  const float off = (float)c * M;  // (label * max_range) in f32, utils.py:218-219
+  float4 v;
+  v.x = mc_coord(a, b, i, 0, c) + off;
+  v.y = mc_coord(a, b, i, 1, c) + off;
+  v.z = mc_coord(a, b, i, 2, c) + off;
+  v.w = mc_coord(a, b, i, 3, c) + off;
+  const int64_t o = (int64_t)seg * a.seg_ld + j;
+  a.rows[o] = v;
+  a.ssc[o] = key_float((uint32_t)(r >> 32));
+  a.scand[o] = (int32_t)cand;
+}
+
+// one 1024-thread workgroup per (segment, 16384-record chunk); dynamic LDS
+// next_pow2(chunk) u64.  One chunk: the sorted records are emitted directly; several:
+// each chunk is written back sorted (descending; keys are unique: the candidate is in
+// the low word) and mc_rank_kernel merges them.
+static __global__ void __launch_bounds__(1024) mc_sort_kernel(McArgs a, int chunked) {
   extern __shared__ uint64_t sk[];
   const int seg = blockIdx.x, b = a.by_class ? seg / a.C : seg;
   const int m = a.cnt[seg];
-  if (m == 0) return;
-  const int P2 = next_pow2(m);
-  const uint64_t* rec = a.rec + (int64_t)seg * a.seg_ld;
-  for (int j = threadIdx.x; j < P2; j += blockDim.x) sk[j] = j < m ? rec[j] : 0ull;
+  const int q0 = blockIdx.y * kMcSortChunk;
+  if (q0 >= m) return;
+  const int mq = min(m - q0, kMcSortChunk);
+  const int P2 = next_pow2(mq);
+  uint64_t* rec = a.rec + (int64_t)seg * a.seg_ld + q0;
+  for (int j = threadIdx.x; j < P2; j += blockDim.x) sk[j] = j < mq ? rec[j] : 0ull;
   __syncthreads();
   block_bitonic_sort_desc(sk, P2);
-  const float M = key_float(a.maxk[b]);
-  for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    const uint64_t r = sk[j];
-    const uint32_t cand = ~(uint32_t)r;
-    int c;
-    const int64_t i = mc_row(a, b, cand, &c);
-    const float off = (float)c * M;  // (label * max_range) in f32, utils.py:218-219
-    float4 v;
-    v.x = mc_coord(a, b, i, 0, c) + off;
-    v.y = mc_coord(a, b, i, 1, c) + off;
-    v.z = mc_coord(a, b, i, 2, c) + off;
-    v.w = mc_coord(a, b, i, 3, c) + off;
-    const int64_t o = (int64_t)seg * a.seg_ld + j;
-    a.rows[o] = v;
-    a.ssc[o] = key_float((uint32_t)(r >> 32));
-    a.scand[o] = (int32_t)cand;
+  for (int j = threadIdx.x; j < mq; j += blockDim.x) {
+    if (chunked)
+      rec[j] = sk[j];
+    else
+      mc_emit(a, seg, b, j, sk[j]);
+  }
+}
+
+// position of each record among all chunks of its segment: its index in its own chunk
+// plus, per other chunk, the number of records ordered before it (binary search)
+static __global__ void __launch_bounds__(256) mc_rank_kernel(McArgs a) {
+  const int seg = blockIdx.y, b = a.by_class ? seg / a.C : seg;
+  const int m = a.cnt[seg];
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint64_t* rec = a.rec + (int64_t)seg * a.seg_ld;
+  const uint64_t key = rec[j];
+  const int q = (int)(j / kMcSortChunk);
+  int64_t rank = j - (int64_t)q * kMcSortChunk;
+  for (int q2 = 0; q2 * kMcSortChunk < m; ++q2) {
+    if (q2 == q) continue;
+    const uint64_t* c = rec + (int64_t)q2 * kMcSortChunk;
+    int lo = 0, hi = min(m - q2 * kMcSortChunk, kMcSortChunk);
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (c[mid] > key)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    rank += lo;
+  }
+  mc_emit(a, seg, b, rank, key);
+}
+
+// one workgroup: info = {largest segment count, some coordinate < 0, total NMS mask
+// tiles (lo, hi)} and seg_base[s] = sum over earlier segments of tri(ceil(cnt / 64))
+static __global__ void __launch_bounds__(1024) mc_summary_kernel(McArgs a, int S, int32_t* info) {
+  __shared__ int64_t scan[1024];
+  __shared__ int smax[1024];
+  __shared__ int64_t carry;
+  const int t = threadIdx.x;
+  int mx = 0;
+  if (t == 0) carry = 0;
+  for (int c0 = 0; c0 < S; c0 += 1024) {
+    const int s = c0 + t;
+    const int64_t n = s < S ? a.cnt[s] : 0;
+    mx = max(mx, (int)n);
+    const int64_t nb = (n + 63) / 64;
+    scan[t] = nb * (nb + 1) / 2;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+      const int64_t v = t >= d ? scan[t - d] : 0;
+      __syncthreads();
+      scan[t] += v;
+      __syncthreads();
+    }
+    const int64_t excl = carry + (t ? scan[t - 1] : 0);
+    if (s < S) a.seg_base[s] = excl;
+    __syncthreads();
+    if (t == 1023) carry += scan[1023];
+    __syncthreads();
+  }
+  smax[t] = mx;
+  __syncthreads();
+  for (int d = 512; d > 0; d >>= 1) {
+    if (t < d) smax[t] = max(smax[t], smax[t + d]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    int neg = 0;
+    for (int b = 0; b < a.B; ++b) neg |= a.negk[b] != 0u;
+    a.seg_base[S] = carry;
+    info[0] = smax[0];
+    info[1] = neg;
+    info[2] = (int32_t)(uint32_t)(carry & 0xffffffffll);
+    info[3] = (int32_t)(uint32_t)(carry >> 32);
   }
 }
 
@@ -233,7 +324,7 @@ static __global__ void __launch_bounds__(256) mc_merge_kernel(McMerge m) {
 static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct McLayout {
-  size_t cnt, maxk, negk, rec, rows, ssc, scand, total;
+  size_t cnt, maxk, negk, seg_base, rec, rows, ssc, scand, total;
 };
 
 static McLayout mc_layout(int B, int C, int64_t n_max) {
@@ -242,7 +333,8 @@ static McLayout mc_layout(int B, int C, int64_t n_max) {
   z.cnt = 0;
   z.maxk = z.cnt + S * sizeof(int32_t);  // cnt + maxk + negk contiguous: one memset
   z.negk = z.maxk + (size_t)B * sizeof(uint32_t);
-  z.rec = al(z.negk + (size_t)B * sizeof(uint32_t));
+  z.seg_base = al(z.negk + (size_t)B * sizeof(uint32_t));
+  z.rec = al(z.seg_base + (S + 1) * sizeof(int64_t));
   z.rows = z.rec + al(S * n * sizeof(uint64_t));
   z.ssc = z.rows + al(S * n * sizeof(float4));
   z.scand = z.ssc + al(S * n * sizeof(float));
@@ -258,6 +350,7 @@ static void mc_bind(McArgs& a, char* ws, int B, int C, int64_t n_max, int strict
   a.cnt = reinterpret_cast<int32_t*>(ws + z.cnt);
   a.maxk = reinterpret_cast<uint32_t*>(ws + z.maxk);
   a.negk = reinterpret_cast<uint32_t*>(ws + z.negk);
+  a.seg_base = reinterpret_cast<int64_t*>(ws + z.seg_base);
   a.rec = reinterpret_cast<uint64_t*>(ws + z.rec);
   a.rows = reinterpret_cast<float4*>(ws + z.rows);
   a.ssc = reinterpret_cast<float*>(ws + z.ssc);
@@ -285,6 +378,7 @@ extern "C" int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int6
   FRH_REQUIRE(num_rows && boxes && scores && channel_mask && info, "null pointer argument");
   FRH_REQUIRE(n_max * num_classes < INT32_MAX, "candidate index overflow");
   FRH_REQUIRE(workspace && ws_bytes >= frh_mcnms_workspace(num_imgs, num_classes, n_max), "workspace too small");
+  FRH_REQUIRE(!(mode == 1 && sf_per_class), "strict mode takes a per-row score factor");
   hipStream_t st = as_stream(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   McArgs a{};
@@ -299,7 +393,6 @@ extern "C" int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int6
   a.sf = score_factor;
   a.sf_ld = sf_img_stride;
   a.sf_per_class = sf_per_class;
-  FRH_REQUIRE(!(mode == 1 && sf_per_class), "strict mode takes a per-row score factor");
   a.valid = row_valid;
   a.valid_ld = valid_img_stride;
   a.chan = channel_mask;
@@ -307,55 +400,36 @@ extern "C" int32_t frh_mcnms_prepare(int32_t num_imgs, int32_t num_classes, int6
   a.min_score = min_score;
   mc_bind(a, ws, num_imgs, num_classes, n_max > 0 ? n_max : 1, mode, by_class);
   const int S = by_class ? num_imgs * num_classes : num_imgs;
-  FRH_HIP(hipMemsetAsync(ws, 0, mc_layout(num_imgs, num_classes, a.n_max).rec, st));
-  info[0] = info[1] = 0;
-  if (n_max == 0) return FRH_OK;
-  const int64_t per_img = mode ? n_max : n_max * num_classes;
-  hipLaunchKernelGGL(mc_candidates_kernel, dim3((unsigned)((per_img + 255) / 256), (unsigned)num_imgs), dim3(256), 0,
-                     st, a);
-  // one sync: the largest segment sizes the sort's LDS and the NMS mask; a
-  // negative candidate coordinate tells the caller to redo the call by image
-  const size_t hn = (size_t)S + 2 * (size_t)num_imgs;  // cnt, maxk, negk are contiguous
-  int32_t* hc = static_cast<int32_t*>(malloc(hn * sizeof(int32_t)));
-  FRH_REQUIRE(hc, "host allocation failed");
-  hipError_t e1 = hipMemcpyAsync(hc, a.cnt, (size_t)S * sizeof(int32_t), hipMemcpyDeviceToHost, st);
-  if (e1 == hipSuccess)
-    e1 = hipMemcpyAsync(hc + S, a.negk, (size_t)num_imgs * sizeof(int32_t), hipMemcpyDeviceToHost, st);
-  hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(st) : e1;
-  int mx = 0, neg = 0;
-  for (int s = 0; s < S && e2 == hipSuccess; ++s) mx = hc[s] > mx ? hc[s] : mx;
-  for (int b = 0; b < num_imgs && e2 == hipSuccess; ++b) neg |= hc[S + b] != 0;
-  free(hc);
-  FRH_HIP(e2);
-  info[0] = mx;
-  info[1] = neg;
-  if (by_class && neg) return FRH_OK;  // the caller switches to by_class = 0
-  FRH_REQUIRE(mx <= kMcMaxSeg, "a segment has %d candidates (limit %d): raise min_score / pre_nms", mx, kMcMaxSeg);
-  if (mx == 0) return FRH_OK;
-  const size_t lds = (size_t)next_pow2(mx) * sizeof(uint64_t);
-  if (lds > 65536)
-    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc_sort_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(mc_sort_kernel, dim3((unsigned)S), dim3(1024), lds, st, a);
+  FRH_HIP(hipMemsetAsync(ws, 0, mc_layout(num_imgs, num_classes, a.n_max).seg_base, st));
+  if (n_max > 0) {
+    const int64_t per_img = mode ? n_max : n_max * num_classes;
+    hipLaunchKernelGGL(mc_candidates_kernel, dim3((unsigned)((per_img + 255) / 256), (unsigned)num_imgs), dim3(256),
+                       0, st, a);
+  }
+  hipLaunchKernelGGL(mc_summary_kernel, dim3(1), dim3(1024), 0, st, a, S, info);
   return check_launch("frh_mcnms_prepare");
 }
 
-extern "C" size_t frh_mcnms_nms_workspace(int32_t num_imgs, int32_t num_classes, int32_t max_count) {
-  if (num_imgs <= 0 || num_classes <= 0 || max_count <= 0) return 0;
+extern "C" size_t frh_mcnms_nms_workspace(int32_t num_imgs, int32_t num_classes, int32_t max_count,
+                                         int64_t mask_tiles) {
+  if (num_imgs <= 0 || num_classes <= 0 || max_count <= 0 || mask_tiles < 0) return 0;
   const size_t S = (size_t)num_imgs * num_classes;  // enough for either segmentation
-  return al(nms_mask_bytes((int32_t)S, max_count)) + al(S * (size_t)max_count * sizeof(int32_t)) +
+  return al((size_t)mask_tiles * 64 * sizeof(uint64_t)) + al(S * (size_t)max_count * sizeof(int32_t)) +
          al(S * sizeof(int32_t));
 }
 
 extern "C" int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64_t n_max, int32_t max_count,
-                                    const float* boxes, int64_t box_img_stride, int32_t box_per_class,
-                                    const float* scores, int64_t score_img_stride, int32_t mode, int32_t by_class,
-                                    double nms_iou, int32_t max_num, float* out_boxes, float* out_scores,
-                                    int64_t* out_labels, int32_t* out_counts, int64_t out_cap, void* workspace,
-                                    size_t ws_bytes, void* nms_ws, size_t nms_ws_bytes, void* stream) {
-  FRH_REQUIRE(num_imgs >= 1 && num_classes >= 1 && n_max >= 0 && max_count >= 0, "bad sizes");
+                                    int64_t mask_tiles, const float* boxes, int64_t box_img_stride,
+                                    int32_t box_per_class, const float* scores, int64_t score_img_stride,
+                                    int32_t mode, int32_t by_class, double nms_iou, int32_t max_num,
+                                    float* out_boxes, float* out_scores, int64_t* out_labels, int32_t* out_counts,
+                                    int64_t out_cap, void* workspace, size_t ws_bytes, void* nms_ws,
+                                    size_t nms_ws_bytes, void* stream) {
+  FRH_REQUIRE(num_imgs >= 1 && num_classes >= 1 && n_max >= 0 && max_count >= 0 && mask_tiles >= 0, "bad sizes");
   FRH_REQUIRE(boxes && out_counts, "null pointer argument");
   FRH_REQUIRE(workspace && ws_bytes >= frh_mcnms_workspace(num_imgs, num_classes, n_max), "workspace too small");
+  FRH_REQUIRE(max_count <= kMcMaxSeg, "a segment has %d candidates (limit %d): raise min_score / pre_nms", max_count,
+              kMcMaxSeg);
   hipStream_t st = as_stream(stream);
   const int S = by_class ? num_imgs * num_classes : num_imgs;
   if (max_count == 0) return hipMemsetAsync(out_counts, 0, (size_t)num_imgs * sizeof(int32_t), st) == hipSuccess
@@ -365,7 +439,7 @@ extern "C" int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64
   const int64_t per_img = (int64_t)(S / num_imgs) * max_count;
   FRH_REQUIRE(out_cap >= (max_num > 0 ? std::min<int64_t>(max_num, per_img) : per_img), "out_cap too small");
   FRH_REQUIRE(!mode || scores, "strict mode needs the scores (labels)");
-  FRH_REQUIRE(nms_ws && nms_ws_bytes >= frh_mcnms_nms_workspace(num_imgs, num_classes, max_count),
+  FRH_REQUIRE(nms_ws && nms_ws_bytes >= frh_mcnms_nms_workspace(num_imgs, num_classes, max_count, mask_tiles),
               "nms workspace too small");
   McArgs a{};
   a.B = num_imgs;
@@ -377,13 +451,24 @@ extern "C" int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64
   a.score_ld = score_img_stride;
   a.strict = mode;
   mc_bind(a, reinterpret_cast<char*>(workspace), num_imgs, num_classes, n_max > 0 ? n_max : 1, mode, by_class);
+  // sort: one workgroup per (segment, chunk of 16384 records), then a rank merge if chunked
+  const int nq = (max_count + kMcSortChunk - 1) / kMcSortChunk;
+  const size_t lds = (size_t)next_pow2(std::min(max_count, kMcSortChunk)) * sizeof(uint64_t);
+  if (lds > 65536)
+    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc_sort_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(mc_sort_kernel, dim3((unsigned)S, (unsigned)nq), dim3(1024), lds, st, a, (int)(nq > 1));
+  if (nq > 1)
+    hipLaunchKernelGGL(mc_rank_kernel, dim3((unsigned)((max_count + 255) / 256), (unsigned)S), dim3(256), 0, st, a);
+  int32_t r = check_launch("mcnms sort");
+  if (r) return r;
   char* nw = reinterpret_cast<char*>(nms_ws);
   uint64_t* mask = reinterpret_cast<uint64_t*>(nw);
-  int32_t* keep = reinterpret_cast<int32_t*>(nw + al(nms_mask_bytes(S, max_count)));
-  int32_t* kcnt = reinterpret_cast<int32_t*>(nw + al(nms_mask_bytes(S, max_count)) +
-                                             al((size_t)S * max_count * sizeof(int32_t)));
-  int32_t r = launch_nms_sorted(S, reinterpret_cast<const float*>(a.rows), a.seg_ld * 4, a.cnt, max_count, nms_iou,
-                                max_num > 0 ? max_num : -1, keep, max_count, kcnt, mask, st);
+  const size_t mask_b = al((size_t)mask_tiles * 64 * sizeof(uint64_t));
+  int32_t* keep = reinterpret_cast<int32_t*>(nw + mask_b);
+  int32_t* kcnt = reinterpret_cast<int32_t*>(nw + mask_b + al((size_t)S * max_count * sizeof(int32_t)));
+  r = launch_nms_sorted(S, reinterpret_cast<const float*>(a.rows), a.seg_ld * 4, a.cnt, max_count, nms_iou,
+                        max_num > 0 ? max_num : -1, keep, max_count, kcnt, mask, a.seg_base, st);
   if (r) return r;
   McMerge m{a, keep, kcnt, max_count, max_num, out_cap, out_boxes, out_scores, out_labels, out_counts};
   const int kmax = max_num > 0 ? std::min(max_num, max_count) : max_count;

@@ -5,9 +5,12 @@
 //  mask: one wave per (segment, 64-row block rb, 64-col block cb >= rb) -- the
 //        grid covers the upper triangle only.  The suppression relation is
 //        stored as COLUMN words: for column j of the tile, the 64-bit set of
-//        rows of block rb whose box suppresses box j (row < column, IoU > thr),
-//        Layout [segment][cb][rb][64 columns]: the tiles of one column block
-//        are contiguous.
+//        rows of block rb whose box suppresses box j (row < column, IoU > thr).
+//        Layout: per segment the upper triangle, column-block-major (tile
+//        (rb, cb) at cb (cb + 1) / 2 + rb, 64 words each), so the tiles of one
+//        column block are contiguous; a segment's tiles start at seg_base[s]
+//        (caller-computed, e.g. sized by each segment's own count) or at
+//        s * tri(nbw) when seg_base is null.
 //  scan: one workgroup per segment walks the blocks in score order (the
 //        resolve chain of a segment is inherently sequential).  For block b the
 //        column span of tiles (0..b, b) is staged in LDS by LDS-DMA ahead of
@@ -20,6 +23,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "block_ops.h"
@@ -27,7 +31,7 @@
 
 namespace frh {
 
-constexpr int kMaxNmsWords = 256;  // n <= 16384 boxes per segment
+constexpr int kMaxNmsWords = 1024;  // n <= 65536 boxes per segment
 
 // The suppression test IoU > thr without the division.  v = RN(inter / union) is
 // a float, so v > thr (double) <=> v >= t_up, the smallest float above thr, <=>
@@ -106,20 +110,26 @@ __device__ __forceinline__ bool iou_above_filter(float4 a, float area_a, float4 
   return above;
 }
 
-// tile t of a segment's upper triangle, row-major: rows before rb hold
-// T(rb) = rb * nbw - rb * (rb - 1) / 2 tiles; rb = max{r : T(r) <= t}
-__device__ __forceinline__ void tri_tile(int t, int nbw, int* rb, int* cb) {
-  const float b = 2.0f * (float)nbw + 1.0f;
-  int r = (int)((b - sqrtf(fmaxf(b * b - 8.0f * (float)t, 0.0f))) * 0.5f);
-  r = max(0, min(r, nbw - 1));
-  while (r > 0 && r * nbw - r * (r - 1) / 2 > t) --r;
-  while (r + 1 < nbw && (r + 1) * nbw - (r + 1) * r / 2 <= t) ++r;
-  *rb = r;
-  *cb = r + (t - (r * nbw - r * (r - 1) / 2));
+__host__ __device__ __forceinline__ int64_t tri_tiles(int64_t nbw) { return nbw * (nbw + 1) / 2; }
+
+// tile t of a segment's upper triangle, column-block-major: column blocks before cb
+// hold cb (cb + 1) / 2 tiles; cb = max{c : c (c + 1) / 2 <= t}
+__device__ __forceinline__ void tri_tile(int t, int* rb, int* cb) {
+  int c = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+  c = max(c, 0);
+  while (c > 0 && c * (c + 1) / 2 > t) --c;
+  while ((c + 1) * (c + 2) / 2 <= t) ++c;
+  *cb = c;
+  *rb = t - c * (c + 1) / 2;
 }
 
-__device__ __forceinline__ int64_t tile_word(int s, int nbw, int rb, int cb) {
-  return (((int64_t)s * nbw + cb) * nbw + rb) * 64;
+// first word of tile (rb, cb) of the segment whose tiles start at tile `base`
+__device__ __forceinline__ int64_t tile_word(int64_t base, int rb, int cb) {
+  return (base + (int64_t)cb * (cb + 1) / 2 + rb) * 64;
+}
+
+__device__ __forceinline__ int64_t seg_tile_base(const int64_t* seg_base, int s, int nbw) {
+  return seg_base ? seg_base[s] : (int64_t)s * tri_tiles(nbw);
 }
 
 // Four tiles per 256-thread workgroup, each wave staging its tile's 64 ROW boxes in
@@ -129,14 +139,15 @@ __device__ __forceinline__ int64_t tile_word(int s, int nbw, int rb, int cb) {
 // kept box i against candidate j.
 __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
                                                        const int32_t* __restrict__ counts, int n_max, int nbw,
-                                                       NmsThr T, uint64_t* __restrict__ mask) {
+                                                       NmsThr T, uint64_t* __restrict__ mask,
+                                                       const int64_t* __restrict__ seg_base) {
   __shared__ float4 rb_box_all[4][64];
   __shared__ float rb_area_all[4][64];
   const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
   if (tile >= nbw * (nbw + 1) / 2) return;
   int rb, cb;
-  tri_tile(__builtin_amdgcn_readfirstlane(tile), nbw, &rb, &cb);
+  tri_tile(__builtin_amdgcn_readfirstlane(tile), &rb, &cb);
   rb = __builtin_amdgcn_readfirstlane(rb);
   cb = __builtin_amdgcn_readfirstlane(cb);
   // the count, the row box and the column box in flight together (indices clamped to
@@ -216,7 +227,7 @@ __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__
   const int nrows = min(64, n - rb * 64);
   if (nrows < 64) colw &= (1ull << nrows) - 1ull;
   if (cb == rb) colw &= t == 0 ? 0ull : (~0ull >> (64 - t));  // rows before the column only
-  mask[tile_word(s, nbw, rb, cb) + t] = cvalid ? colw : 0ull;
+  mask[tile_word(seg_tile_base(seg_base, s, nbw), rb, cb) + t] = cvalid ? colw : 0ull;
 }
 
 __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
@@ -292,13 +303,6 @@ __device__ __forceinline__ void wait_vmcnt_atmost(int n) {
 //  (two blocks of slack for the loader's fold) and the slot at b - kNmsRing; a
 //  loader waits only on s_resolved.  Every counter advances unconditionally, and a
 //  max_keep stop sets s_stop and pushes s_resolved past the end so every loader exits.
-#ifdef FRH_NMS_TIMELINE  // tools-only build (tools/csrc/nms_timeline.hip): per-block resolver stamps
-__device__ uint64_t* g_nms_tl;
-#define NMS_STAMP(b, k) \
-  if (g_nms_tl && lane == 0) g_nms_tl[((int64_t)s * kMaxNmsWords + (b)) * 8 + (k)] = wall_clock64()
-#else
-#define NMS_STAMP(b, k)
-#endif
 constexpr int kNmsRing = 8;
 constexpr int kNmsSpan = 32;     // tiles per staged span (segments up to 2048 boxes fully staged)
 constexpr int kNmsLoaders = 3;
@@ -311,7 +315,8 @@ __device__ __forceinline__ void lds_flag(int* p, int v) {
 __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restrict__ mask,
                                                        const int32_t* __restrict__ counts, int nbw, int span,
                                                        int max_keep, int32_t* __restrict__ keep, int64_t kstride,
-                                                       int32_t* __restrict__ kcounts) {
+                                                       int32_t* __restrict__ kcounts,
+                                                       const int64_t* __restrict__ seg_base) {
   extern __shared__ __attribute__((aligned(16))) uint64_t nms_lds[];
   __shared__ uint64_t kept[kMaxNmsWords];
   __shared__ uint64_t partial[kNmsRing][kWave];
@@ -327,17 +332,16 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   }
   __syncthreads();
   const int slot_words = ((span + 1) & ~1) * 64;  // whole 1 KB copies: an even number of tiles
+  const int64_t base = seg_tile_base(seg_base, s, nbw);
   auto tile = [&](const uint64_t* slot, int j0, int j, int b) {
-    return j >= j0 ? slot[(j - j0) * 64 + lane] : mask[tile_word(s, nbw, j, b) + lane];
+    return j >= j0 ? slot[(j - j0) * 64 + lane] : mask[tile_word(base, j, b) + lane];
   };
   if (wave == 0) {
     int32_t* K = keep + (int64_t)s * kstride;
     int nk = 0;
     uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
     for (int b = 0; b < nb; ++b) {
-      NMS_STAMP(b, 0);
       while (lds_poll(&ready[b % kNmsRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
-      NMS_STAMP(b, 1);
       const uint64_t* slot = nms_lds + (b % kNmsRing) * slot_words;
       const int j0 = max(0, b - span + 1);
       uint64_t acc = partial[b % kNmsRing][lane];
@@ -345,7 +349,6 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       if (b >= 2) acc |= tile(slot, j0, b - 2, b) & kb2;
       const uint64_t d = slot[(b - j0) * 64 + lane];
       uint64_t r = __ballot(acc != 0ull);
-      NMS_STAMP(b, 2);
       const int valid = n - b * 64;
       if (valid < 64) r |= (~0ull) << valid;
       uint64_t kb = 0, und = ~r;
@@ -356,7 +359,6 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
         const uint64_t vic = __ballot((d & nkp) != 0ull);
         und &= ~(nkp | vic);
       }
-      NMS_STAMP(b, 3);
       bool stop = false;
       if (max_keep >= 0) {
         const int room = max_keep - nk;
@@ -372,14 +374,14 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
         if (stop) s_stop = b;
         lds_flag(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1);
       }
-      NMS_STAMP(b, 4);
       if (stop) break;
     }
     if (lane == 0) kcounts[s] = nk;
   } else {
-    // descriptor over this segment's tiles (32-bit byte range)
-    const int64_t seg_words = (int64_t)nbw * nbw * 64;
-    const __amdgpu_buffer_rsrc_t mr = uniform_rsrc(mask + s * seg_words, seg_words * 8);
+    // descriptor over this segment's tiles (its own count's triangle; a span copy that runs
+    // one tile past the last column block reads zeros from the range check)
+    const int64_t seg_words = tri_tiles(nb) * 64;
+    const __amdgpu_buffer_rsrc_t mr = uniform_rsrc(mask + base * 64, seg_words * 8);
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint64_t*)nms_lds);
     auto finish = [&](int p) {  // fold the kept rows of blocks <= p - 3 into p's partial word, publish p
       while (lds_poll(&s_resolved) < p - 2) __builtin_amdgcn_s_sleep(1);
@@ -388,7 +390,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       const int j0 = max(0, p - span + 1);
       uint64_t acc = 0;
       int j = 0;
-      for (; j < j0 && j + 2 < p; ++j) acc |= mask[tile_word(s, nbw, j, p) + lane] & kept[j];
+      for (; j < j0 && j + 2 < p; ++j) acc |= mask[tile_word(base, j, p) + lane] & kept[j];
       for (; j + 8 <= p - 2; j += 8) {  // eight words per batch: their LDS reads overlap
         uint64_t t[8], k[8];
 #pragma unroll
@@ -410,7 +412,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       const int j0 = max(0, b - span + 1);
       const int ninst = (b - j0 + 2) >> 1;  // 1 KB (two tiles) per wave-instruction
       const uint32_t dst = lds0 + (uint32_t)((b % kNmsRing) * slot_words * 8);
-      const int src = (int)((tile_word(s, nbw, j0, b) - s * seg_words) * 8);
+      const int src = (int)((tile_word(0, j0, b)) * 8);
       for (int k = 0; k < ninst; ++k) lds_dma_at<16>(mr, dst + (uint32_t)k * 1024u, lane * 16, src + k * 1024);
       if (prev >= 0) {
         wait_vmcnt_atmost(ninst);  // prev's copies are older than these ninst
@@ -425,28 +427,41 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   }
 }
 
+// The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
+// set for every device the first time a launch runs on it (one bit per device id;
+// setting it twice from racing threads is harmless).
+static std::atomic<uint64_t> g_scan_attr_devices{0};
+
+static int32_t nms_scan_attr() {
+  int dev = 0;
+  FRH_HIP(hipGetDevice(&dev));
+  const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
+  if (bit && (g_scan_attr_devices.load(std::memory_order_acquire) & bit)) return FRH_OK;
+  FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kNmsRing * kNmsSpan * 64 * 8));
+  g_scan_attr_devices.fetch_or(bit, std::memory_order_acq_rel);
+  return FRH_OK;
+}
+
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, hipStream_t st) {
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st) {
   const int nbw = (n_max + 63) / 64;
-  dim3 g((nbw * (nbw + 1) / 2 + 3) / 4, S);
-  hipLaunchKernelGGL(nms_mask_kernel, g, dim3(256), 0, st, boxes, seg_stride, counts, n_max, nbw, nms_thr(thr), mask);
+  FRH_REQUIRE(nbw <= kMaxNmsWords, "n_max %d exceeds %d", n_max, 64 * kMaxNmsWords);
+  const int32_t r = nms_scan_attr();
+  if (r) return r;
+  dim3 g((unsigned)((tri_tiles(nbw) + 3) / 4), S);
+  hipLaunchKernelGGL(nms_mask_kernel, g, dim3(256), 0, st, boxes, seg_stride, counts, n_max, nbw, nms_thr(thr), mask,
+                     seg_base);
   const int span = std::min(nbw, kNmsSpan);
   const size_t lds = (size_t)kNmsRing * ((span + 1) & ~1) * 64 * sizeof(uint64_t);
-  static bool attr = false;
-  if (!attr) {
-    FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kNmsRing * kNmsSpan * 64 * 8));
-    attr = true;
-  }
   hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep, kstride,
-                     kcounts);
+                     kcounts, seg_base);
   return check_launch("nms");
 }
 
-size_t nms_mask_bytes(int32_t S, int32_t n_max) {  // [S][cb][rb][64] column words
-  const size_t nbw = (size_t)((n_max + 63) / 64);
-  return (size_t)S * nbw * nbw * 64 * sizeof(uint64_t);
+size_t nms_mask_bytes(int32_t S, int32_t n_max) {  // S triangles of the n_max segment, 64 column words per tile
+  return (size_t)S * (size_t)tri_tiles((n_max + 63) / 64) * 64 * sizeof(uint64_t);
 }
 
 }  // namespace frh
@@ -471,5 +486,5 @@ extern "C" int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t 
     return FRH_OK;
   }
   return launch_nms_sorted(num_segs, boxes, seg_stride, counts, n_max, iou_thr, max_keep, keep, keep_seg_stride,
-                           keep_counts, reinterpret_cast<uint64_t*>(workspace), as_stream(stream));
+                           keep_counts, reinterpret_cast<uint64_t*>(workspace), nullptr, as_stream(stream));
 }

@@ -16,7 +16,7 @@ namespace frh {
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, hipStream_t st);
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st);
 size_t nms_mask_bytes(int32_t S, int32_t n_max);
 
 constexpr int kPropThreads = 1024;
@@ -476,7 +476,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);
   int32_t* kcnt = reinterpret_cast<int32_t*>(ws + z.kcnt);
   r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
-                        (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, reinterpret_cast<uint64_t*>(ws + z.mask), st);
+                        (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, reinterpret_cast<uint64_t*>(ws + z.mask), nullptr, st);
   if (r) return r;
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};

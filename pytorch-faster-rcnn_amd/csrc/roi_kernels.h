@@ -10,6 +10,10 @@
 
 #include "roi_common.h"
 
+#ifndef FRH_ONLY8
+#define FRH_ONLY8 0
+#endif
+
 namespace frh {
 
 constexpr int kRoiThreads = 256;
@@ -484,10 +488,17 @@ struct PairLayout {
 // kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
 // stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
 // twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
-template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA, bool kLean = false>
+// kDynR (kSingle only): a stage issues only the DMA rounds its window needs
+// (ceil(cells / 32)) instead of the region's RP rounds -- the slab region of a pair is
+// sized for the largest window the stage's D admits, most windows need one or two rounds.
+// kWideSt (kSingle only): a stage's outputs go to LDS at obase ([channel][bin]) and leave
+// by 16-B (or 8-B) stores, 4x fewer store instructions than one 4-B store per channel.
+template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA, bool kLean = false,
+          bool kDynR = false, bool kWideSt = false>
 __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, const RoiRaw& raw, uint32_t sbase,
-                                          int64_t t_start, int lane) {
+                                          int64_t t_start, int lane, uint32_t obase = 0) {
+  static_assert(kSingle || !(kDynR || kWideSt), "dynamic rounds / wide stores need the single slab buffer");
   constexpr int SR = 2;
   int64_t t_setup = 0, t_land = 0;
   const int cw0 = chunk * 2 * kPW;
@@ -600,16 +611,34 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
       return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx + (lane & 1) * scs) * 4
                         : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
     };
-    int goff[RP];
+    // kDynR with many rounds per pair (the big windows of D <= 2): the per-lane DMA offsets are
+    // recomputed per stage instead of held in RP registers, which would set the register
+    // budget of the whole kernel for a few percent of its items
+    constexpr bool kFly = kDynR && RP > 4;
+    int goff[kFly ? 1 : RP];
+    if constexpr (!kFly) {
 #pragma unroll
-    for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
+      for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
+    }
+    const int nr = kDynR ? min(RP, (ncell + 31) >> 5) : RP;  // 32 cells (64 dwords) per round
     auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
       const uint32_t buf = sbase + 4u * (uint32_t)(kSingle ? 0 : (s & 1) * kHalf);
+      if constexpr (kFly) {
+        for (int j = 0; j < nr; ++j) {
+          const int g = goff_at(j);
+#pragma unroll
+          for (int d = 0; d < D; ++d)
+            lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), g,
+                                  (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4);
+        }
+        return;
+      }
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
 #pragma unroll
-        for (int j = 0; j < RP; ++j) lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
+        for (int j = 0; j < RP; ++j)
+          if (!kDynR || j < nr) lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
       }
     };
     auto eval = [&](auto bb, int s) {
@@ -678,11 +707,35 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
         if (iy == 1) {
           const f32x2 r = acc * 0.25f;
           const int p = s * D + d;
-          const int vo = p < npairs ? ovoff : 0x40000000;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
+          if constexpr (kWideSt) {  // idle lanes write past the block (obase has 64 spare floats)
+            auto* ol = (__attribute__((address_space(3))) float*)(uintptr_t)obase;
+            const int o0 = active ? (2 * d) * nbins + lane : 2 * kPW * kWave + lane;
+            ol[o0] = r.x;
+            ol[o0 + (active ? nbins : 0)] = r.y;
+            asm volatile("" ::: "memory");  // written here: the results do not stay live in registers
+          } else {
+            const int vo = p < npairs ? ovoff : 0x40000000;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
+          }
         }
       });
+      if constexpr (kWideSt) {  // the stage's [channel][bin] block: 16-B pieces (8-B when not a multiple of 4 floats)
+        const int nd = min(D, npairs - s * D);
+        const int nf = 2 * nd * nbins, base = 2 * s * D * ostep;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if ((nf & 3) == 0 && (base & 15) == 0) {
+          auto* o4 = (__attribute__((address_space(3))) u32x4*)(uintptr_t)obase;
+          for (int q = lane; 4 * q < nf; q += kWave)
+            __builtin_amdgcn_raw_buffer_store_b128(o4[q], orr, 16 * q, base, kStAux);
+        } else {
+          auto* o2 = (__attribute__((address_space(3))) u32x2*)(uintptr_t)obase;
+          for (int q = lane; 2 * q < nf; q += kWave)
+            __builtin_amdgcn_raw_buffer_store_b64(o2[q], orr, 8 * q, base, kStAux);
+        }
+      }
     };
     auto step = [&](auto bb, int s) {
       if (s >= nst) return;
@@ -731,6 +784,8 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
   };
   if (small)
     run(std::integral_constant<int, 8>{});
+  else if (FRH_ONLY8)
+    return;
   else if (ncell <= PairLayout<4, kHalf>::kCells)
     run(std::integral_constant<int, 4>{});
   else if (ncell <= PairLayout<2, kHalf>::kCells)

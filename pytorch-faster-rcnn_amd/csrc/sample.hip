@@ -134,6 +134,9 @@ struct SampBufs {
   uint32_t* part_hist;   // [V][nchunk][kSampBins]
   int32_t* part_count;   // [V][nchunk]
   int nchunk;
+  int32_t* sel;          // nullable: [V][sel_ld] the selected indices (any order)
+  int64_t sel_ld;
+  int32_t* sel_cnt;      // [V] how many
 };
 
 static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const int64_t* lab_in, int64_t lstride,
@@ -160,7 +163,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const i
   for (int r = 0; r < kTkPerThread; ++r) {
     const int64_t i = base + r * kTkThreads + threadIdx.x;
     const bool pos = lab[r] > 0, neg = lab[r] == 0;
-    if (i < n) lab_out[(int64_t)s * lstride + i] = -1;
+    if (lab_out && i < n) lab_out[(int64_t)s * lstride + i] = -1;
     const uint32_t keyp = pos ? ((~hash_u32(seed, 2 * s, (uint32_t)i)) | 1u) : 0u;
     const uint32_t keyn = neg ? ((~hash_u32(seed, 2 * s + 1, (uint32_t)i)) | 1u) : 0u;
     if (i < b.ld) {
@@ -186,12 +189,20 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const i
 }
 
 // sampler policy of the segmented top-k: a selected box gets its input label
-// back (labels_out was reset to -1 by the key kernel)
+// back (labels_out was reset to -1 by the key kernel) and / or is listed at its
+// selection slot (the target gathers order the lists themselves)
 struct SampPol {
   const int64_t* li;
-  int64_t* lo;
-  __device__ void select(int i, uint32_t, int) { lo[i] = li[i]; }
-  __device__ void finish(int) {}
+  int64_t* lo;      // nullable
+  int32_t* sel;     // nullable: this virtual segment's list
+  int32_t* sel_cnt;
+  __device__ void select(int i, uint32_t, int slot) {
+    if (lo) lo[i] = li[i];
+    if (sel) sel[slot] = i;
+  }
+  __device__ void finish(int kv) {
+    if (sel_cnt && threadIdx.x == 0) *sel_cnt = kv;
+  }
 };
 
 // Collect launch: grid (chunks, 2 x images), 256 threads.  Every workgroup sums
@@ -227,7 +238,8 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
   sm.h1[t] = hsum;
   __syncthreads();
   const TkPlan plan = tk_plan_direct(kSampHistBits, k, sm, [&](int i) { return sm.h1[i]; });
-  SampPol pol{lab_in + (int64_t)s * lstride, lab_out + (int64_t)s * lstride};
+  SampPol pol{lab_in + (int64_t)s * lstride, lab_out ? lab_out + (int64_t)s * lstride : nullptr,
+              sb.sel ? sb.sel + (int64_t)v * sb.sel_ld : nullptr, sb.sel ? sb.sel_cnt + v : nullptr};
   tk_collect_chunk(sb.tk, v, n, plan, pol, sm);
 }
 
@@ -321,12 +333,13 @@ extern "C" int32_t frh_sample_apply(int32_t num_segs, const int64_t* labels_in, 
 
 extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                      const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
-                                     int32_t pos_num, uint64_t seed, int64_t* labels_out,
-                                     void* workspace, size_t ws_bytes, void* stream) {
+                                     int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
+                                     int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream) {
   FRH_REQUIRE(num_segs >= 0 && max_boxes >= 0, "negative sizes");
   FRH_REQUIRE(pos_num <= max_num && pos_num >= 0, "pos_num must be in [0, max_num]");
   if (num_segs == 0 || max_boxes == 0) return FRH_OK;
-  FRH_REQUIRE(labels_in && labels_out && num_boxes, "null pointer argument");
+  FRH_REQUIRE(labels_in && num_boxes && (labels_out || sel), "null pointer argument");
+  FRH_REQUIRE(!sel == !sel_counts, "sel and sel_counts go together");
   FRH_REQUIRE(labels_in != labels_out, "labels_out must not alias labels_in");
   FRH_REQUIRE(workspace && ws_bytes >= frh_sample_workspace(num_segs, max_boxes), "workspace too small");
   FRH_REQUIRE(max_boxes <= INT32_MAX, "max_boxes must fit in int32");
@@ -337,7 +350,8 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
   const int V = 2 * num_segs;
   SampBufs sb{TkBufs{reinterpret_cast<uint32_t*>(ws + z.keys), z.kld, nullptr, kSampHistBits, nullptr,
                      reinterpret_cast<int32_t*>(ws + z.state), reinterpret_cast<uint64_t*>(ws + z.cand)},
-              reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk};
+              reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
+              sel, (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
   hipLaunchKernelGGL(sampler_keys_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
                      labels_in, label_seg_stride, num_boxes, seed, sb, labels_out);
   hipLaunchKernelGGL(sampler_collect_kernel, dim3((unsigned)z.nchunk, (unsigned)V), dim3(kTkThreads), 0, st,

@@ -54,15 +54,6 @@ struct TkBufs {
   uint64_t* cand;        // [V][ld] candidate list: key << 32 | ~index
 };
 
-#ifdef FRH_TK_TIMELINE  // tools-only build (tools/csrc/topk_timeline.hip): segment-0 stamps
-static __device__ uint64_t* g_tk_tl;
-#define TK_STAMP(slot)                                                  \
-  do {                                                                  \
-    if (g_tk_tl && threadIdx.x == 0 && blockIdx.y == 0) g_tk_tl[slot] = wall_clock64(); \
-  } while (0)
-#else
-#define TK_STAMP(slot)
-#endif
 
 inline size_t tk_zero_bytes(int V, int hb) {  // hist1 + hist2 + state, contiguous
   return (size_t)V * (((size_t)1 << hb) + kTkBins2 + TK_WORDS) * sizeof(uint32_t);
@@ -323,7 +314,6 @@ __device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& pl
   const uint32_t* kk = b.keys + (int64_t)v * b.ld;
   uint64_t* cand = b.cand + (int64_t)v * b.ld;
   const int64_t base = (int64_t)blockIdx.x * kTkChunk;
-  TK_STAMP(blockIdx.x * 4);
   if (kv > 0 && base < n) {
     uint32_t key[kTkPerThread];
     tk_load_chunk(kk, base, n, key);
@@ -356,9 +346,7 @@ __device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& pl
       }
     }
   }
-  TK_STAMP(blockIdx.x * 4 + 1);
   if (!tk_check_in(&st[TK_DONE2], sm)) return;
-  TK_STAMP(blockIdx.x * 4 + 2);
   if (kv == 0 || all) {
     pol.finish(kv);
     return;
@@ -371,9 +359,7 @@ __device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& pl
     for (int j = t; j < P2; j += kTkThreads)
       sm.cand[j] = j < ncand ? xwg_load(cand + j) : 0ull;
     __syncthreads();
-    TK_STAMP(1024);
     block_bitonic_sort_desc(sm.cand, P2);
-    TK_STAMP(1025);
     for (int j = t; j < k2; j += kTkThreads) {
       const uint64_t e = sm.cand[j];
       pol.select((int)~(uint32_t)e, (uint32_t)(e >> 32), nabove + j);
@@ -392,9 +378,7 @@ __device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& pl
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  TK_STAMP(1026);
   pol.finish(kv);
-  TK_STAMP(1031);
 }
 
 // ------------------------------------------- register bitonic sort (desc)

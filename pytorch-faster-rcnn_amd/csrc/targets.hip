@@ -123,7 +123,12 @@ struct AnchorTargetArgs {
   int64_t out_ld;
   int32_t* out_counts;
   int S;
+  const int32_t* sel;      // nullable: the device sampler's lists [S][2][sel_ld] (positives, negatives)
+  const int32_t* sel_cnt;  // [S][2]
+  int64_t sel_ld;
 };
+
+__device__ void anchor_target_item(const AnchorTargetArgs& p, int s, int64_t n, int64_t o);
 
 __global__ void anchor_target_kernel(AnchorTargetArgs p) {
   const int s = blockIdx.y;
@@ -136,7 +141,45 @@ __global__ void anchor_target_kernel(AnchorTargetArgs p) {
     if (s == p.S - 1) p.out_counts[p.S] = (int32_t)(off + cnt);
   }
   if (j >= cnt) return;
-  const int64_t n = p.chosen[(int64_t)s * p.list_seg_stride + j];
+  anchor_target_item(p, s, p.chosen[(int64_t)s * p.list_seg_stride + j], off + j);
+}
+
+// The image's selected boxes = its two sampler lists (disjoint, any order), in ascending
+// box order: each item's output position is the number of listed boxes below it (rank by
+// counting over the list staged in LDS) -- the reference's nonzero(labels >= 0) order
+// (anchor.py:49-50, bbox.py:52-58) without a compaction pass over every box.
+// Dynamic LDS: 2 * sel_ld int32.
+template <class F>
+__device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32_t* sel_cnt, int64_t sel_ld, int S,
+                                                 int32_t* out_counts, F&& item) {
+  extern __shared__ int32_t su[];
+  const int s = blockIdx.y;
+  const int np = sel_cnt[2 * s], cnt = np + sel_cnt[2 * s + 1];
+  int64_t off = 0;
+  for (int q = 0; q < s; ++q) off += sel_cnt[2 * q] + sel_cnt[2 * q + 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out_counts[s] = cnt;
+    if (s == S - 1) out_counts[S] = (int32_t)(off + cnt);
+  }
+  if ((int64_t)blockIdx.x * blockDim.x >= cnt) return;  // uniform per workgroup
+  const int32_t* pos = sel + (int64_t)(2 * s) * sel_ld;
+  const int32_t* neg = pos + sel_ld;
+  for (int q = threadIdx.x; q < cnt; q += blockDim.x) su[q] = q < np ? pos[q] : neg[q - np];
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cnt) return;
+  const int32_t x = su[j];
+  int rank = 0;
+  for (int q = 0; q < cnt; ++q) rank += su[q] < x;
+  item(s, (int64_t)x, off + rank);
+}
+
+__global__ void anchor_target_sel_kernel(AnchorTargetArgs p) {
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts,
+                   [&](int s, int64_t n, int64_t o) { anchor_target_item(p, s, n, o); });
+}
+
+__device__ void anchor_target_item(const AnchorTargetArgs& p, int s, int64_t n, int64_t o) {
   const int64_t lab = p.labels[(int64_t)s * p.label_seg_stride + n];
   const int64_t g = lab > 0 ? lab - 1 : 0;
   const float* a = p.anchors + (int64_t)s * p.anchor_seg_stride;
@@ -145,7 +188,6 @@ __global__ void anchor_target_kernel(AnchorTargetArgs p) {
   float gx1 = gt[g], gy1 = gt[p.gt_ld + g], gx2 = gt[2 * p.gt_ld + g], gy2 = gt[3 * p.gt_ld + g];
   float r[4];
   encode(ax1, ay1, ax2, ay2, gx1, gy1, gx2, gy2, p.nm.has ? p.nm.m : nullptr, p.nm.s, r);
-  const int64_t o = off + j;
   p.chosen_idx[o] = n;
   p.seg_of[o] = s;
   int64_t tl = 0;
@@ -224,7 +266,12 @@ struct BBoxTargetArgs {
   int64_t out_ld;
   int32_t* out_counts;
   int S;
+  const int32_t* sel;      // nullable: the device sampler's lists [S][2][sel_ld]
+  const int32_t* sel_cnt;  // [S][2]
+  int64_t sel_ld;
 };
+
+__device__ void bbox_target_item(const BBoxTargetArgs& p, int s, int64_t row, int64_t o);
 
 __global__ void bbox_target_kernel(BBoxTargetArgs p) {
   const int s = blockIdx.y;
@@ -237,7 +284,15 @@ __global__ void bbox_target_kernel(BBoxTargetArgs p) {
     if (s == p.S - 1) p.out_counts[p.S] = (int32_t)(off + cnt);
   }
   if (j >= cnt) return;
-  const int64_t row = p.chosen[(int64_t)s * p.list_seg_stride + j];
+  bbox_target_item(p, s, p.chosen[(int64_t)s * p.list_seg_stride + j], off + j);
+}
+
+__global__ void bbox_target_sel_kernel(BBoxTargetArgs p) {
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts,
+                   [&](int s, int64_t row, int64_t o) { bbox_target_item(p, s, row, o); });
+}
+
+__device__ void bbox_target_item(const BBoxTargetArgs& p, int s, int64_t row, int64_t o) {
   const int64_t lab = p.labels[(int64_t)s * p.label_seg_stride + row];
   const int64_t G = p.num_gts[s];
   const int64_t g = lab > 0 ? lab - 1 : 0;
@@ -256,7 +311,6 @@ __global__ void bbox_target_kernel(BBoxTargetArgs p) {
   for (int k = 0; k < 4; ++k) gv[k] = gt[k * p.gt_ld + g];
   float r[4];
   encode(bv[0], bv[1], bv[2], bv[3], gv[0], gv[1], gv[2], gv[3], p.nm.has ? p.nm.m : nullptr, p.nm.s, r);
-  const int64_t o = off + j;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     p.tar_props[k * p.out_ld + o] = bv[k];
@@ -318,7 +372,8 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
                                      int64_t anchor_ld, int64_t anchor_seg_stride, const float* gts,
                                      int64_t gt_ld, int64_t gt_seg_stride, const int64_t* gt_labels,
                                      int64_t gt_label_seg_stride, const float* means, const float* stds,
-                                     int64_t max_out_per_seg, int64_t* chosen_idx, int32_t* seg_of,
+                                     int64_t max_out_per_seg, const int32_t* sel, const int32_t* sel_counts,
+                                     int64_t* chosen_idx, int32_t* seg_of,
                                      int64_t* tar_labels, float* tar_anchors, float* tar_bbox,
                                      float* tar_param, int64_t out_ld, int32_t* out_counts, void* workspace,
                                      size_t ws_bytes, void* stream) {
@@ -327,8 +382,20 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
                   tar_bbox && tar_param && out_counts,
               "null pointer argument");
   FRH_REQUIRE(out_ld >= (int64_t)num_segs * max_out_per_seg, "out_ld too small");
-  FRH_REQUIRE(workspace && ws_bytes >= frh_anchor_target_workspace(num_segs, max_boxes), "workspace too small");
+  FRH_REQUIRE(!sel == !sel_counts, "sel and sel_counts go together");
   hipStream_t st = as_stream(stream);
+  unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
+  if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
+    FRH_REQUIRE(2 * max_out_per_seg * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
+    AnchorTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, anchors, anchor_ld, anchor_seg_stride,
+                       gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
+                       max_out_per_seg, chosen_idx, seg_of, tar_labels, tar_anchors, tar_bbox, tar_param, out_ld,
+                       out_counts, num_segs, sel, sel_counts, max_out_per_seg};
+    hipLaunchKernelGGL(anchor_target_sel_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256),
+                       2 * max_out_per_seg * sizeof(int32_t), st, p);
+    return check_launch("frh_anchor_target");
+  }
+  FRH_REQUIRE(workspace && ws_bytes >= frh_anchor_target_workspace(num_segs, max_boxes), "workspace too small");
   char* ws = reinterpret_cast<char*>(workspace);
   int32_t* chunk_counts = reinterpret_cast<int32_t*>(ws);
   size_t a = align256(compact_workspace(num_segs, max_boxes));
@@ -343,8 +410,7 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
   AnchorTargetArgs p{labels, label_seg_stride, chosen, counts, max_boxes, anchors, anchor_ld, anchor_seg_stride,
                      gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                      max_out_per_seg, chosen_idx, seg_of, tar_labels, tar_anchors, tar_bbox, tar_param, out_ld,
-                     out_counts, num_segs};
-  unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
+                     out_counts, num_segs, nullptr, nullptr, 0};
   hipLaunchKernelGGL(anchor_target_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256), 0, st, p);
   return check_launch("frh_anchor_target");
 }
@@ -416,7 +482,8 @@ extern "C" int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int6
                                    const float* props, int64_t prop_ld, int64_t prop_seg_stride, const float* gts,
                                    int64_t gt_ld, int64_t gt_seg_stride, const int64_t* gt_labels,
                                    int64_t gt_label_seg_stride, const float* means, const float* stds,
-                                   int64_t max_out_per_seg, float* tar_props, float* tar_bbox,
+                                   int64_t max_out_per_seg, const int32_t* sel, const int32_t* sel_counts,
+                                   float* tar_props, float* tar_bbox,
                                    int64_t* tar_label, float* tar_param, int64_t* tar_is_gt, int64_t out_ld,
                                    int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream) {
   FRH_REQUIRE(num_segs >= 1 && max_rows >= 0 && max_out_per_seg >= 0, "bad sizes");
@@ -424,8 +491,20 @@ extern "C" int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int6
                   tar_param && tar_is_gt && out_counts,
               "null pointer argument");
   FRH_REQUIRE(out_ld >= (int64_t)num_segs * max_out_per_seg, "out_ld too small");
-  FRH_REQUIRE(workspace && ws_bytes >= frh_bbox_target_workspace(num_segs, max_rows), "workspace too small");
+  FRH_REQUIRE(!sel == !sel_counts, "sel and sel_counts go together");
   hipStream_t st = as_stream(stream);
+  unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
+  if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
+    FRH_REQUIRE(2 * max_out_per_seg * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
+    BBoxTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, num_gts, props, prop_ld, prop_seg_stride,
+                     gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
+                     max_out_per_seg, tar_props, tar_bbox, tar_param, tar_label, tar_is_gt, out_ld, out_counts,
+                     num_segs, sel, sel_counts, max_out_per_seg};
+    hipLaunchKernelGGL(bbox_target_sel_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256),
+                       2 * max_out_per_seg * sizeof(int32_t), st, p);
+    return check_launch("frh_bbox_target");
+  }
+  FRH_REQUIRE(workspace && ws_bytes >= frh_bbox_target_workspace(num_segs, max_rows), "workspace too small");
   char* ws = reinterpret_cast<char*>(workspace);
   int32_t* chunk_counts = reinterpret_cast<int32_t*>(ws);
   size_t a = align256(compact_workspace(num_segs, max_rows));
@@ -440,8 +519,7 @@ extern "C" int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int6
   BBoxTargetArgs p{labels, label_seg_stride, chosen, counts, max_rows, num_gts, props, prop_ld, prop_seg_stride,
                    gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                    max_out_per_seg, tar_props, tar_bbox, tar_param, tar_label, tar_is_gt, out_ld, out_counts,
-                   num_segs};
-  unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
+                   num_segs, nullptr, nullptr, 0};
   hipLaunchKernelGGL(bbox_target_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256), 0, st, p);
   return check_launch("frh_bbox_target");
 }

@@ -34,12 +34,12 @@ SIGNATURES = {
                                       c_vp]),
     'frh_sample_apply': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                  c_vp, c_vp]),
-    'frh_sample_random': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_u64, c_vp, c_vp, c_size,
-                                  c_vp]),
+    'frh_sample_random': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp, c_vp,
+                                  c_size, c_vp]),
     'frh_anchor_target_workspace': (c_size, [c_i32, c_i64]),
     'frh_anchor_target': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
                                   c_vp, c_i64, P(c_f32), P(c_f32), c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                  c_i64, c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     'frh_gather_level_outputs': (c_i32, [c_i32, P(c_vp), P(c_i64), P(c_i64), c_i32, c_i64, c_vp, c_vp, c_vp,
                                          c_i64, c_vp]),
     'frh_scatter_level_grads': (c_i32, [c_i32, P(c_vp), P(c_i64), P(c_i64), c_i32, c_i64, c_vp, c_vp, c_vp,
@@ -47,8 +47,8 @@ SIGNATURES = {
     'frh_prepend_gt_labels': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'frh_bbox_target_workspace': (c_size, [c_i32, c_i64]),
     'frh_bbox_target': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
-                                c_vp, c_i64, P(c_f32), P(c_f32), c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                c_vp, c_vp, c_size, c_vp]),
+                                c_vp, c_i64, P(c_f32), P(c_f32), c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                c_vp, c_i64, c_vp, c_vp, c_size, c_vp]),
     'frh_bbox2param': (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, P(c_f32), P(c_f32), c_vp, c_i64, c_vp]),
     'frh_param2bbox': (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, P(c_f32), P(c_f32), c_i32, c_f32, c_f32,
                                c_vp, c_i64, c_vp]),
@@ -62,9 +62,9 @@ SIGNATURES = {
                                c_vp]),
     'frh_mcnms_workspace': (c_size, [c_i32, c_i32, c_i64]),
     'frh_mcnms_prepare': (c_i32, [c_i32, c_i32, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_i32,
-                                  c_vp, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, P(c_i32), c_vp]),
-    'frh_mcnms_nms_workspace': (c_size, [c_i32, c_i32, c_i32]),
-    'frh_mcnms_finish': (c_i32, [c_i32, c_i32, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i32, c_f64,
+                                  c_vp, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_vp]),
+    'frh_mcnms_nms_workspace': (c_size, [c_i32, c_i32, c_i32, c_i64]),
+    'frh_mcnms_finish': (c_i32, [c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i32, c_f64,
                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_size, c_vp, c_size, c_vp]),
     'frh_roi_level_map': (c_i32, [c_vp, c_i64, c_f32, c_i32, c_vp, c_vp]),
     'frh_roi_align_fwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,

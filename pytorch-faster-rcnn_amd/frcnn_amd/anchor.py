@@ -64,8 +64,9 @@ def in_grid_sizes(img_size, grid_sizes, strides):
 def anchor_targets_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, sampler, means, stds):
     """Sample (optional) + gather/encode for all images: the per-image anchor_target
     results concatenated in image order (anchor_head.py:177-192)."""
-    if sampler is not None:
-        labels = ops.sample_labels(labels, num_boxes, max_boxes, sampler.max_num, sampler.pos_num)
+    if sampler is not None:  # device mode: the sampler's lists feed the gather (no compaction pass)
+        labels = ops.sample_labels(labels, num_boxes, max_boxes, sampler.max_num, sampler.pos_num,
+                                   lists=ops.sampler_mode() == 'device')
         cap = sampler.max_num
     else:
         cap = max_boxes

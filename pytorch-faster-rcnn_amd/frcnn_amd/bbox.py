@@ -42,7 +42,8 @@ def bbox_targets_batched(props_list, gt_bboxes, gt_labels, assigner, sampler, ta
                                   assigner.min_pos_iou, num_segs=S)
     max_rows = gmax + pmax
     rows, num_rows = ops.prepend_gt_labels(labels, pcount, gcnt, max_rows)
-    rows = ops.sample_labels(rows, num_rows, max_rows, sampler.max_num, sampler.pos_num)
+    rows = ops.sample_labels(rows, num_rows, max_rows, sampler.max_num, sampler.pos_num,
+                             lists=ops.sampler_mode() == 'device')
     r = ops.bbox_target_batched(rows, num_rows, gcnt, max_rows, props, pstride, gts, glab,
                                 target_means, target_stds, sampler.max_num)
     out = {k: [] for k in ('tar_props', 'tar_bbox', 'tar_label', 'tar_param', 'tar_is_gt')}

@@ -141,19 +141,32 @@ def sampler_mode():
     return _SAMPLER['mode']
 
 
-def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None):
-    """Batched RandomSampler over labels [S, >=max_boxes] (region.py:43-57,112-126)."""
+class SampleLists(object):
+    """The device sampler's selection (frh_sample_random's sel / sel_counts): per segment the
+    kept positives and negatives, in no order, for the target gathers; `labels` are the
+    assignment labels they select from (unchanged)."""
+
+    def __init__(self, labels, sel, sel_counts, max_num):
+        self.labels, self.sel, self.sel_counts, self.max_num = labels, sel, sel_counts, int(max_num)
+
+
+def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None, lists=False):
+    """Batched RandomSampler over labels [S, >=max_boxes] (region.py:43-57,112-126).
+    lists=True (device mode only): return a SampleLists instead of the sampled labels."""
     mode = mode or _SAMPLER['mode']
     S = labels.shape[0]
     dev = labels.device
-    out = torch.empty_like(labels)
     if mode == 'device':
         ws = workspace(_lib.query('frh_sample_workspace', S, max(max_boxes, 1)), dev)
         _SAMPLER['calls'] += 1
         seed = (_SAMPLER['seed'] * 0x9E3779B97F4A7C15 + _SAMPLER['calls']) & 0xFFFFFFFFFFFFFFFF
+        out = None if lists else torch.empty_like(labels)
+        sel = torch.empty(S, 2, max(int(max_num), 1), dtype=torch.int32, device=dev) if lists else None
+        sel_cnt = torch.empty(S, 2, dtype=torch.int32, device=dev) if lists else None
         call('frh_sample_random', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, int(max_num),
-             int(pos_num), seed, ptr(out), ptr(ws), ws.numel(), stream_of(labels))
-        return out
+             int(pos_num), seed, ptr(out), ptr(sel), ptr(sel_cnt), ptr(ws), ws.numel(), stream_of(labels))
+        return SampleLists(labels, sel, sel_cnt, max_num) if lists else out
+    out = torch.empty_like(labels)
     ld = max(max_boxes, 1)
     pos_list = torch.empty(S, ld, dtype=torch.int32, device=dev)
     neg_list = torch.empty(S, ld, dtype=torch.int32, device=dev)
@@ -193,6 +206,10 @@ def _numpy_keep(n, cap):
 
 # ---------------------------------------------------------------- target gathers (a6/a12)
 def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, max_out_per_seg):
+    """labels: the sampled labels [S, n] (chosen = label >= 0) or a SampleLists."""
+    sl = labels if isinstance(labels, SampleLists) else None
+    if sl is not None:
+        labels = sl.labels
     S = labels.shape[0]
     dev = labels.device
     cap = max(int(max_out_per_seg), 1)
@@ -202,13 +219,16 @@ def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels,
     tar_labels = torch.empty(T, dtype=torch.int64, device=dev)
     tars = torch.empty(3, 4, T, dtype=torch.float32, device=dev)
     counts = torch.empty(S + 1, dtype=torch.int32, device=dev)
-    ws = workspace(_lib.query('frh_anchor_target_workspace', S, max(max_boxes, 1)), dev)
+    ws = None if sl is not None else workspace(_lib.query('frh_anchor_target_workspace', S, max(max_boxes, 1)), dev)
     m = f32_array(means) if means is not None else None
     sd = f32_array(stds) if stds is not None else None
+    if sl is not None and sl.max_num != cap:
+        raise AssertionError('sampler lists of max_num {} for a cap of {}'.format(sl.max_num, cap))
     call('frh_anchor_target', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, ptr(anchors),
          anchors.stride(0), 0, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_labels),
-         gt_labels.stride(0) if gt_labels is not None else 0, m, sd, cap, ptr(chosen_idx), ptr(seg_of),
-         ptr(tar_labels), ptr(tars[0]), ptr(tars[1]), ptr(tars[2]), T, ptr(counts), ptr(ws), ws.numel(),
+         gt_labels.stride(0) if gt_labels is not None else 0, m, sd, cap, ptr(sl.sel if sl else None),
+         ptr(sl.sel_counts if sl else None), ptr(chosen_idx), ptr(seg_of), ptr(tar_labels), ptr(tars[0]),
+         ptr(tars[1]), ptr(tars[2]), T, ptr(counts), ptr(ws), ws.numel() if ws is not None else 0,
          stream_of(labels))
     cnt = counts.cpu().tolist()  # output sizes are data dependent: one sync per batch
     n = cnt[S]
@@ -272,6 +292,10 @@ def prepend_gt_labels(prop_labels, num_props, num_gts, max_rows):
 
 def bbox_target_batched(rows, num_rows, num_gts, max_rows, props, prop_seg_stride, gts, gt_labels, means, stds,
                         max_out_per_seg):
+    """rows: the sampled prepended rows [S, n] (chosen = label >= 0) or a SampleLists."""
+    sl = rows if isinstance(rows, SampleLists) else None
+    if sl is not None:
+        rows = sl.labels
     S = rows.shape[0]
     dev = rows.device
     cap = max(int(max_out_per_seg), 1)
@@ -279,13 +303,16 @@ def bbox_target_batched(rows, num_rows, num_gts, max_rows, props, prop_seg_strid
     tars = torch.empty(3, 4, T, dtype=torch.float32, device=dev)
     lab = torch.empty(2, T, dtype=torch.int64, device=dev)
     counts = torch.empty(S + 1, dtype=torch.int32, device=dev)
-    ws = workspace(_lib.query('frh_bbox_target_workspace', S, max(max_rows, 1)), dev)
+    ws = None if sl is not None else workspace(_lib.query('frh_bbox_target_workspace', S, max(max_rows, 1)), dev)
     m = f32_array(means) if means is not None else None
     sd = f32_array(stds) if stds is not None else None
+    if sl is not None and sl.max_num != cap:
+        raise AssertionError('sampler lists of max_num {} for a cap of {}'.format(sl.max_num, cap))
     call('frh_bbox_target', S, ptr(rows), rows.stride(0), ptr(num_rows), ptr(num_gts), max_rows, ptr(props),
          props.stride(-2), prop_seg_stride, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_labels),
-         gt_labels.stride(0), m, sd, cap, ptr(tars[0]), ptr(tars[1]), ptr(lab[0]), ptr(tars[2]), ptr(lab[1]), T,
-         ptr(counts), ptr(ws), ws.numel(), stream_of(rows))
+         gt_labels.stride(0), m, sd, cap, ptr(sl.sel if sl else None), ptr(sl.sel_counts if sl else None),
+         ptr(tars[0]), ptr(tars[1]), ptr(lab[0]), ptr(tars[2]), ptr(lab[1]), T, ptr(counts), ptr(ws),
+         ws.numel() if ws is not None else 0, stream_of(rows))
     cnt = counts.cpu().tolist()
     n = cnt[S]
     return dict(tar_props=tars[0][:, :n], tar_bbox=tars[1][:, :n], tar_label=lab[0][:n], tar_param=tars[2][:, :n],
@@ -362,6 +389,14 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
 
 NMS_PROFILE = {'on': False, 'records': []}
 
+# CascadeRCNN.forward_train runs the RPN proposal chain on a side stream of the device,
+# concurrently with the RPN target / loss chain (one stream per device, created on first use).
+PROPOSAL_STREAM = {'on': True, 'streams': {}}
+
+
+def set_proposal_stream(on):
+    PROPOSAL_STREAM['on'] = bool(on)
+
 
 def nms_bytes(counts, kept):
     """Algorithmic bytes of one segmented NMS call: per segment of N boxes
@@ -434,16 +469,18 @@ def multiclass_nms_batched(boxes, scores, nms_channel, nms_iou, min_score=-1, ma
     valid = row_valid.to(torch.uint8).contiguous() if row_valid is not None else None
     ws = workspace(_lib.query('frh_mcnms_workspace', B, C, n), dev)
     st = stream_of(scores)
-    info = (ctypes.c_int32 * 2)()
+    info_d = torch.empty(4, dtype=torch.int32, device=dev)
     m = 1 if mode == 'strict' else 0
     for by_class in (1, 0):  # a negative candidate coordinate: the reference's single pass, by image
         call('frh_mcnms_prepare', B, C, n, ptr(num_rows), ptr(boxes), boxes.stride(0), per_class, ptr(scores),
              scores.stride(0), ptr(sf), sf.stride(0) if sf is not None else 0, sf_pc, ptr(valid),
              valid.stride(0) if valid is not None else 0, ptr(chan), m, by_class, float(min_score), ptr(ws),
-             ws.numel(), info, st)
+             ws.numel(), ptr(info_d), st)
+        info = info_d.cpu().tolist()  # the call's one sync: segment sizes size the sort and the NMS mask
         if not info[1]:
             break
     P = int(info[0])
+    tiles = (info[2] & 0xffffffff) | (info[3] << 32)
     if P == 0:
         return empty
     G = C if by_class else 1
@@ -453,10 +490,10 @@ def multiclass_nms_batched(boxes, scores, nms_channel, nms_iou, min_score=-1, ma
     osc = torch.empty(B, cap, dtype=torch.float32, device=dev)
     ol = torch.empty(B, cap, dtype=torch.int64, device=dev)
     oc = torch.empty(B, dtype=torch.int32, device=dev)
-    nws = workspace(_lib.query('frh_mcnms_nms_workspace', B, C, P), dev)
-    call('frh_mcnms_finish', B, C, n, P, ptr(boxes), boxes.stride(0), per_class, ptr(scores), scores.stride(0), m,
-         by_class, float(nms_iou), mx, ptr(ob), ptr(osc), ptr(ol), ptr(oc), cap, ptr(ws), ws.numel(), ptr(nws),
-         nws.numel(), st)
+    nws = workspace(_lib.query('frh_mcnms_nms_workspace', B, C, P, tiles), dev)
+    call('frh_mcnms_finish', B, C, n, P, tiles, ptr(boxes), boxes.stride(0), per_class, ptr(scores),
+         scores.stride(0), m, by_class, float(nms_iou), mx, ptr(ob), ptr(osc), ptr(ol), ptr(oc), cap, ptr(ws),
+         ws.numel(), ptr(nws), nws.numel(), st)
     counts = oc.cpu().tolist()
     return [(ob[b, :k], osc[b, :k], ol[b, :k]) for b, k in enumerate(counts)]
 
@@ -482,7 +519,7 @@ def _feat_desc(feats):
 # feature tensors only to replay the same launch shape for timing; with a graphed
 # trunk they alias the graph's output buffers, so a replay reads the newest step's
 # values -- never use a record's features for their contents.
-ROI_ALIGN_PROFILE = {'on': False, 'records': []}
+ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True}
 
 
 class _RoIAlignMulti(torch.autograd.Function):
@@ -496,14 +533,16 @@ class _RoIAlignMulti(torch.autograd.Function):
         out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
         hw, st = _feat_desc(feats)
         prof = ROI_ALIGN_PROFILE['on']
-        if prof:
+        e0 = e1 = None
+        if prof and ROI_ALIGN_PROFILE['events']:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales),
              feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
              ptr(out), stream_of(out))
         if prof:
-            e1.record()
+            if e1 is not None:
+                e1.record()
             ROI_ALIGN_PROFILE['records'].append((e0, e1, rois, levels, [tuple(f.shape) for f in feats], (ph, pw),
                                                  feats, tuple(scales), sampling_ratio))
         ctx.save_for_backward(rois, levels)

@@ -463,6 +463,63 @@ def gen_forward_train():
     print('wrote ftrain.json', out)
 
 
+def _topk_by_center_floor(fcos_head_mod):
+    def topk_by_center(anchors, bbox, k):  # fcos_head.py:106-116 with `//`
+        h, w = anchors.shape[-2:]
+        flat = anchors.view(4, -1)
+        ctr = torch.stack(list(fcos_head_mod.utils.center_of(flat)))
+        bctr = torch.stack(list(fcos_head_mod.utils.center_of(bbox))).view(-1, 1)
+        l2 = (ctr - bctr).norm(dim=0)
+        _, k_inds = l2.topk(k, largest=False)
+        return k_inds % w, k_inds // w, flat[:, k_inds], k_inds.numel()
+    fcos_head_mod.topk_by_center = topk_by_center
+
+
+def gen_whole_detectors():
+    """forward_train loss dict AND forward_test detections of the reference's own detector for
+    each BASELINE config in inputs.WHOLE_DETECTORS (lib/builder.py; CascadeRCNN
+    lib/detectors/cascade_rcnn.py:90-203, RetinaNet retinanet.py:43-59, FCOS fcos.py:42-57) on
+    inputs.ftrain_case() with inputs.seeded_state weights; np.random seeded for the samplers.
+    Writes whole_<tag>.json (losses) and whole_<tag>.npz (per-image boxes / scores / labels of
+    forward_test in the reference's order).  torchvision nms / RoIAlign are the oracle shims."""
+    sys.path.insert(0, os.path.join(REPO, 'pytorch-faster-rcnn_amd'))
+    from frcnn_amd.config import Config
+    import lib.builder as rb
+    import lib.heads.fcos_head as fcos_head_mod
+    _topk_by_center_floor(fcos_head_mod)
+    for tag, fname, over, shape in inputs.WHOLE_DETECTORS:
+        img, boxes, labels, metas = inputs.ftrain_case(shape)
+        cfg = Config.fromfile(os.path.join(REF, 'configs', fname))
+        cfg.model.backbone.pretrained = False
+        for k, v in over.items():
+            cfg.test_cfg[k].update(v)
+        model = rb.build_module(cfg.model, train_cfg=cfg.train_cfg, test_cfg=cfg.test_cfg)
+        sd = inputs.seeded_state({k: tuple(v.shape) for k, v in model.state_dict().items()})
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        model.train()
+        np.random.seed(inputs.FTRAIN_NP_SEED)
+        with torch.no_grad():
+            losses = model.forward_train(torch.from_numpy(img), [torch.from_numpy(b) for b in boxes],
+                                         [torch.from_numpy(l) for l in labels], metas)
+        out = {k: float(v) for k, v in losses.items()}
+        with open(os.path.join(HERE, 'whole_{}.json'.format(tag)), 'w') as f:
+            json.dump({'losses': out, 'np_seed': inputs.FTRAIN_NP_SEED, 'config': 'configs/' + fname,
+                       'test_cfg_overrides': over, 'image_shape': list(shape)}, f, indent=1)
+        model.eval()
+        with torch.no_grad():
+            dets = model.forward_test(torch.from_numpy(img), metas)
+        dets = list(zip(*dets[:3]))  # unpack_multi_result: ([boxes_i], [scores_i], [labels_i]) -> per image
+        res = {'n': np.int64(len(dets))}
+        for i, d in enumerate(dets):
+            b, sc, lb = d
+            b = b.detach().numpy().astype(np.float32)
+            res['boxes_{}'.format(i)] = (b.T if b.shape[0] == 4 and b.ndim == 2 and b.shape[1] != 4 else b).reshape(-1, 4)
+            res['scores_{}'.format(i)] = sc.detach().numpy().astype(np.float32).reshape(-1)
+            res['labels_{}'.format(i)] = lb.detach().numpy().astype(np.int64).reshape(-1)
+        save('whole_{}.npz'.format(tag), **res)
+        print(tag, out, [len(d[1]) for d in dets], flush=True)
+
+
 def main():
     if not os.path.isdir(os.path.join(REF, 'lib')):
         print('reference not found at {}: nothing to generate (fixtures are committed)'.format(REF))
@@ -487,6 +544,9 @@ def main():
     if '--only-ftrain' in sys.argv:
         gen_forward_train()
         return 0
+    if '--only-whole' in sys.argv:
+        gen_whole_detectors()
+        return 0
     if '--only-new' in sys.argv:
         import lib.heads.retina_head as retina_mod
         import lib.heads.bbox_head as bbox_head_mod
@@ -506,6 +566,8 @@ def main():
     gen_multiclass_nms(utils)
     gen_retina(retina_mod, bbox_head_mod)
     gen_eval()
+    gen_forward_train()
+    gen_whole_detectors()
     return 0
 
 

@@ -58,6 +58,10 @@ def random_boxes(seed, n, img=IMG_SHAPE, min_wh=2.0, max_wh=400.0):
     return np.stack([x1, y1, x2, y2]).astype(np.float32)
 
 
+def golden_path(name):
+    return os.path.join(HERE, name)
+
+
 def feature_maps(seed, grids, channels, batch):
     rng = np.random.default_rng(seed)
     return [rng.standard_normal((batch, channels, h, w)).astype(np.float32) for h, w in grids]
@@ -198,13 +202,28 @@ def seeded_state(shapes):
     return out
 
 
-def ftrain_case():
-    """One 256x384 image (N(0,1) pixels) with the 5 boxes of VOC gt set 9 scaled into it: (img
-    [1, 3, H, W] f32, boxes [[4, G] f32], labels [[G] i64], img_metas)."""
+def ftrain_case(shape=FTRAIN_SHAPE):
+    """One image (default 256x384, N(0,1) pixels) with the 5 boxes of VOC gt set 9 scaled into
+    it: (img [1, 3, H, W] f32, boxes [[4, G] f32], labels [[G] i64], img_metas)."""
+    shape = tuple(shape)
     rng = np.random.default_rng(4242)
-    img = rng.standard_normal((1, 3) + FTRAIN_SHAPE).astype(np.float32)
+    img = rng.standard_normal((1, 3) + shape).astype(np.float32)
     b, l = voc_gts()[9]
-    b = (b * np.float32(0.38)).astype(np.float32)
-    meta = {'img_shape': FTRAIN_SHAPE + (3,), 'pad_shape': FTRAIN_SHAPE + (3,), 'scale_factor': 0.38 * 1.6,
+    f = 0.38 * shape[0] / FTRAIN_SHAPE[0]
+    b = (b * np.float32(f)).astype(np.float32)
+    meta = {'img_shape': shape + (3,), 'pad_shape': shape + (3,), 'scale_factor': f * 1.6,
             'ori_shape': (160, 240, 3)}
     return img, [b], [l], [meta]
+
+
+# BASELINE configs whose whole detector (forward_train losses + forward_test detections) is
+# pinned to the reference's own outputs (gen_golden.gen_whole_detectors): (tag, config file,
+# test_cfg overrides, image shape).  The two-stage configs' RCNN classifiers are N(0, 0.01^2)
+# under seeded_state, so every softmax score sits near 1/21 < 0.05: their fixtures lower
+# min_score to 0 (every (proposal, class) pair is a multiclass-NMS candidate: one offset NMS
+# over up to 20 000 boxes).  cfg5 runs on 384x640: the reference's ATSS top-9 per level needs
+# 9 cells on P7 (stride 128).
+WHOLE_DETECTORS = [('cfg2', 'faster_rcnn_r50_fpn.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
+                   ('cfg3', 'retinanet_r50_fpn.py', {}, FTRAIN_SHAPE),
+                   ('cfg4', 'cascade_rcnn_r50_fpn.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
+                   ('cfg5', 'fcos_r50_fpn_atss.py', {}, (384, 640))]

@@ -232,6 +232,35 @@ def test_device_sampler_properties(dev, max_num, pos_num):
     assert not np.array_equal(out, out2)
 
 
+@pytest.mark.parametrize('max_num,pos_num', [(256, 128), (512, 128)])
+def test_device_sampler_lists_feed_targets(dev, max_num, pos_num):
+    """The device sampler's selection lists (frh_sample_random sel / sel_counts) fed straight
+    into the target gathers (rank-by-counting into ascending box order, no compaction pass)
+    give exactly the targets of the sampled-labels path (labels >= 0 compacted in order), for
+    the same draw; also for an image with fewer candidates than slots and an empty one."""
+    from frcnn_amd import ops
+    rng = np.random.default_rng(8)
+    S, n = 4, 20000
+    lab = rng.choice([-1, 0, 1, 2, 3], size=(S, n), p=[0.3, 0.6, 0.04, 0.03, 0.03]).astype(np.int64)
+    lab[3, :] = np.where(lab[3] >= 0, -1, lab[3])
+    lab[3, :40] = 0  # 40 candidates for max_num slots
+    lt = T(lab, dev)
+    num = torch.tensor([n, n - 7, 0, n], dtype=torch.int32, device=dev)
+    anchors = T(inputs.random_boxes(12, n), dev)
+    gts, gcnt, gmax = ops.pack_boxes([T(inputs.random_boxes(13 + s, 3), dev) for s in range(S)], dev)
+    glab = ops.pack_labels([torch.tensor([4, 9, 17], device=dev)] * S, gmax, dev)
+    res = []
+    for lists in (False, True):
+        ops.set_sampler_mode('device', seed=77)
+        sl = ops.sample_labels(lt, num, n, max_num, pos_num, mode='device', lists=lists)
+        res.append(ops.anchor_target_batched(sl, num, n, anchors, gts, glab, None, None, max_num))
+    a, b = res
+    assert a['counts'] == b['counts'] and a['counts'][2] == 0 and a['counts'][3] == 40
+    for k in ('chosen_idx', 'seg_of', 'tar_labels', 'tar_anchors', 'tar_bbox', 'tar_param'):
+        assert torch.equal(a[k], b[k]), k
+    ops.set_sampler_mode('numpy')
+
+
 @pytest.mark.parametrize('case,pre', [('all_equal', 2000), ('four_values', 2000), ('sparse_high', 2000),
                                       ('near_half', 2000), ('near_half', 6000), ('four_values', 6000)])
 def test_rpn_selection_tie_heavy_vs_oracle(dev, case, pre):
@@ -461,6 +490,27 @@ def test_nms_empty_and_batched(dev):
     np.testing.assert_array_equal(ks.cpu().numpy(), scores[k])
 
 
+@pytest.mark.parametrize('n', [16385, 20000])
+def test_nms_above_16384_boxes(dev, n):
+    """torchvision.ops.nms takes any n; the reference's offset-trick batched_nms
+    (lib/utils.py:211-221) runs one NMS over up to 1000 proposals x 20 classes = 20 000
+    boxes at RCNN test.  Keep list bit-exact vs the oracle, through ops.nms and through
+    utils.batched_nms on 20 class labels."""
+    from frcnn_amd import ops, utils
+    rng = np.random.default_rng(n)
+    boxes = inputs.random_boxes(n, n, min_wh=5, max_wh=120).T.copy()
+    scores = rng.random(n).astype(np.float32)
+    scores[::11] = scores[1]
+    keep = ops.nms(T(boxes, dev), T(scores, dev), 0.5).cpu().numpy()
+    np.testing.assert_array_equal(keep, oracle.nms(boxes, scores, 0.5))
+    labels = rng.integers(1, 21, n)
+    kb, ks, kl = utils.batched_nms(T(boxes, dev), T(scores, dev), T(labels, dev), 0.5)
+    off = boxes + (labels.astype(np.float32) * np.float32(boxes.max()))[:, None]
+    k = oracle.nms(off, scores, 0.5)
+    np.testing.assert_array_equal(kl.cpu().numpy(), labels[k])
+    np.testing.assert_array_equal(ks.cpu().numpy(), scores[k])
+
+
 # ----------------------------------------------------------------- a13/a14
 def test_roi_level_map(dev, golden):
     from frcnn_amd import ops
@@ -482,8 +532,7 @@ def _rois(seed, n, batch):
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
 def test_roi_align_forward_default_vs_oracle_p2(dev, layout):
     """The product forward (channel-pair kernel) on P2-sized maps, 600 RoIs incl. border /
-    degenerate / outside ones, against the oracle (the variants it was chosen among are
-    compared bit for bit in tests/test_tools_variants.py)."""
+    degenerate / outside ones, against the oracle: bit-identical."""
     from frcnn_amd import ops
     grids = [(152, 256), (76, 128), (38, 64), (19, 32)]
     feats = inputs.feature_maps(42, grids, 96, 2)
@@ -495,10 +544,27 @@ def test_roi_align_forward_default_vs_oracle_p2(dev, layout):
     if layout == 'nhwc':
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
     out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
-    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(out, ref)  # same operation order as the oracle: bit-identical
     odd = [T(f[:, :95], dev).contiguous() for f in feats]  # odd C: the per-RoI LDS kernel
     out2 = ops.roi_align_multilevel(odd, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
     np.testing.assert_array_equal(out2, out[:, :95])
+
+
+def test_roi_align_forward_bench_config_bit_exact(dev):
+    """The forward at the bench's own configuration: the 1024 RoIs of a cfg2 training step
+    (tests/golden/cfg2_rois.npz, 873 / 102 / 42 / 7 on P2..P5), C = 256, P2-P5 of a
+    2-image 608x1024 batch (152x256 ... 19x32), NCHW: every output bit-identical to the
+    oracle (lib/region.py:271-296, torchvision legacy RoIAlign semantics)."""
+    from frcnn_amd import ops
+    z = np.load(inputs.golden_path('cfg2_rois.npz'))
+    rois, levels = z['r5'], z['lv']
+    shapes = [tuple(int(v) for v in s) for s in z['shapes']]
+    scales = [float(v) for v in z['scales']]
+    feats = inputs.feature_maps(44, [s[2:] for s in shapes], shapes[0][1], shapes[0][0])
+    ref = oracle.roi_align(feats, rois, levels, scales, (7, 7), 2)
+    out = ops.roi_align_multilevel([T(f, dev) for f in feats], T(rois, dev), T(levels, dev), scales, (7, 7),
+                                   2).cpu().numpy()
+    np.testing.assert_array_equal(out, ref)
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
@@ -780,6 +846,57 @@ def test_mcnms_batched_vs_per_image_oracle(dev, mode, per_class, factor, neg):
         np.testing.assert_array_equal(gl, kl)
         total += len(ks)
     assert total > 20
+
+
+def _mcnms_check(dev, boxes, scores, chans, thr, min_score, max_num, mode='official'):
+    from frcnn_amd import ops
+    res = ops.multiclass_nms_batched(T(np.stack(boxes), dev), T(np.stack(scores), dev), chans, thr, min_score,
+                                     max_num, None, mode=mode)
+    total = 0
+    for b in range(len(boxes)):
+        kb, ks, kl = oracle.multiclass_nms(boxes[b], scores[b], chans, thr, min_score, max_num, None, mode=mode)
+        gb, gs, gl = (x.cpu().numpy() for x in res[b])
+        np.testing.assert_array_equal(gb, kb)
+        np.testing.assert_array_equal(gs, ks)
+        np.testing.assert_array_equal(gl, kl)
+        total += len(ks)
+    return total
+
+
+def test_mcnms_one_dense_class_many_segments(dev):
+    """8 images x 80 classes (640 segments) where one class per image keeps ~5000
+    candidates above min_score and the others a handful: each segment's NMS mask is sized
+    by its own count (a square per segment sized by the largest would need ~2 GB here);
+    bit-exact vs the per-image oracle (lib/utils.py:224-269)."""
+    rng = np.random.default_rng(91)
+    B, C, n = 8, 80, 5000
+    boxes, scores = [], []
+    for b in range(B):
+        ctr = rng.uniform(50, 950, (n, 2))
+        wh = rng.uniform(10, 120, (n, 2))
+        bx = np.clip(np.concatenate([ctr - wh / 2, ctr + wh / 2], 1), 0, 999).astype(np.float32)
+        sc = np.full((n, C), 0.01, np.float32)
+        sc[:, 1 + b % (C - 1)] = rng.uniform(0.06, 1.0, n).astype(np.float32)  # the dense class
+        few = rng.integers(0, n, 40)
+        sc[few, rng.integers(1, C, 40)] = 0.5
+        boxes.append(bx)
+        scores.append(sc)
+    assert _mcnms_check(dev, boxes, scores, list(range(1, C)), 0.5, 0.05, 100) > 100 * B // 2
+
+
+def test_mcnms_by_image_above_sort_chunk(dev):
+    """Negative coordinates send every class of an image into ONE segment (the reference's
+    single offset pass); 1000 rows x 20 classes = 20 000 candidates exceed the 16 384 records
+    one workgroup sorts in LDS, so the chunked sort + rank merge runs.  Bit-exact vs the oracle."""
+    rng = np.random.default_rng(92)
+    n, C = 1000, 21
+    ctr = rng.uniform(-50, 950, (n, 2))
+    wh = rng.uniform(10, 200, (n, 2))
+    bx = np.concatenate([ctr - wh / 2, ctr + wh / 2], 1).astype(np.float32)
+    sc = rng.uniform(0.06, 1.0, (n, C)).astype(np.float32)
+    sc = (np.round(sc * 256) / 256).astype(np.float32)  # exact ties across the chunks
+    assert bx.min() < 0
+    assert _mcnms_check(dev, [bx], [sc], list(range(1, C)), 0.5, 0.05, None) > 1000
 
 
 def test_retina_predict_batched_equals_per_image(dev):

@@ -2,10 +2,10 @@
 
     python tools/build_tools.py
 It links the product objects (pytorch-faster-rcnn_amd/build/obj, built first by
-build_lib.build()) with tools/csrc/*.hip: the RoIAlign variants measured on the way to
-the product kernels, with the entry points declared in tools/csrc/frcnn_tools.h.  The
-micro-benchmarks (tools/bench_*.py, tools/probe/) and tests/test_tools_variants.py load
-it through tools/toolslib.py.
+build_lib.build()) with tools/csrc/*.hip: the RoIAlign laboratory (the product default
+kernel, a stamped build of it and candidates under measurement), entry points declared
+in tools/csrc/frcnn_tools.h.  tools/bench_roi_align.py loads it through tools/toolslib.py.
+Not part of __graft_entry__.build(): run it by hand before a measurement.
 """
 import concurrent.futures as cf
 import glob
@@ -38,7 +38,10 @@ def _compile(src, hdr_mtime):
 def build():
     build_lib.build()
     os.makedirs(OBJ, exist_ok=True)
-    hm = max([build_lib._deps_mtime()] + [os.path.getmtime(h) for h in glob.glob(os.path.join(SRC, '*.h'))])
+    # any product header / source or tools header / include can change a tools object
+    deps = glob.glob(os.path.join(SRC, '*.h')) + glob.glob(os.path.join(SRC, '*.inc')) + \
+        glob.glob(os.path.join(build_lib.CSRC, '*.hip'))
+    hm = max([build_lib._deps_mtime()] + [os.path.getmtime(h) for h in deps])
     srcs = sorted(glob.glob(os.path.join(SRC, '*.hip')))
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(lambda s: _compile(s, hm), srcs))

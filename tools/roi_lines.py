@@ -2,7 +2,7 @@
 (NCHW, per channel), against the line-uses of the per-RoI staging -- the floor on the
 forward's feature traffic when every reuse hits in L2.
 
-    python tools/roi_lines.py [tools/data/cfg2_rois_cpu.npz]
+    python tools/roi_lines.py [tests/golden/cfg2_rois.npz]
 Window rule as roi_align_fwd_pair_kernel stages it (torchvision legacy taps, 7x7 bins,
 sampling 2; dense rows / columns while the window is at most 28 wide, else the tap list)."""
 import sys
@@ -29,7 +29,7 @@ def taps(start, binsz, n):
 
 
 def main():
-    d = np.load(sys.argv[1] if len(sys.argv) > 1 else 'tools/data/cfg2_rois_cpu.npz')
+    d = np.load(sys.argv[1] if len(sys.argv) > 1 else 'tests/golden/cfg2_rois.npz')
     r5, lv, shapes, sc = d['r5'], d['lv'], d['shapes'], d['scales']
     uniq, uses = set(), 0
     for k in range(len(r5)):

@@ -1,7 +1,7 @@
 """ctypes loader of the TOOLS-ONLY library tools/lib/libfrcnn_tools.so (see
-tools/build_tools.py): the product ABI (frcnn_amd._lib.SIGNATURES) plus the variant
-entry points of tools/csrc/frcnn_tools.h.  Used by the micro-benchmarks and
-tests/test_tools_variants.py only."""
+tools/build_tools.py): the product ABI (frcnn_amd._lib.SIGNATURES) plus the RoIAlign
+laboratory entry points of tools/csrc/frcnn_tools.h.  Used by tools/bench_roi_align.py and
+tests/test_abi.py only; never by the product."""
 import ctypes
 import os
 import sys
@@ -16,24 +16,6 @@ _RA = [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp, c
 TOOL_SIGNATURES = {
     'frh_roi_align_fwd_variant': (c_i32, [c_i32] + _RA + [c_vp, c_vp, c_size, c_vp]),
     'frh_roi_align_workspace': (c_size, [c_i64]),
-    'frh_roi_align_fwd_ws': (c_i32, _RA + [c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_sweep_workspace': (c_size, [c_i64, c_i32, c_i32]),
-    'frh_roi_align_fwd_sweep': (c_i32, _RA + [c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_bwd_sweep': (c_i32, _RA + [c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_bwd_workspace': (c_size, [c_i32, P(c_i32), c_i32, c_i64]),
-    'frh_roi_align_bwd_tiled': (c_i32, _RA + [c_vp, c_vp, c_size, c_vp]),
-    'frh_roi_align_bwd_cl': (c_i32, _RA + [c_vp, c_vp]),
-    'frh_tl_nms_workspace': (c_size, [c_i32, c_i32]),
-    'frh_tl_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, _lib.c_f64, c_i32, c_vp, c_i64, c_vp, c_vp,
-                                  c_size, c_vp]),
-    'frh_ex_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, _lib.c_f64, c_i32, c_vp, c_i64, c_vp, c_vp,
-                                  c_size, c_vp]),
-    'frh_ex_nms_workspace': (c_size, [c_i32, c_i32]),
-    'frh_tl_nms_timeline': (c_i32, [c_vp]),
-    'frh_tl_rpn_proposals_workspace': _lib.SIGNATURES['frh_rpn_proposals_workspace'],
-    'frh_tl_rpn_proposals_nms_view': _lib.SIGNATURES['frh_rpn_proposals_nms_view'],
-    'frh_tl_rpn_proposals': _lib.SIGNATURES['frh_rpn_proposals'],
-    'frh_tl_topk_timeline': (c_i32, [c_vp]),
 }
 _lib_t = None
 
@@ -49,10 +31,3 @@ def load():
             fn.restype, fn.argtypes = res, args
         _lib_t = lib
     return _lib_t
-
-
-def call(name, *args):
-    lib = load()
-    st = getattr(lib, name)(*args)
-    if st != 0:
-        raise RuntimeError('{} failed ({}): {}'.format(name, st, lib.frh_last_error().decode(errors='replace')))
