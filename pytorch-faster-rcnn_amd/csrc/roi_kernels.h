@@ -854,6 +854,261 @@ __global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLev
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent pipelined channel-pair forward.  Each wave walks a static list of items
+// (RoI, 16 channels) and treats their stages (D channel pairs of one item, the slab
+// layout of pair_item) as one stream: while it evaluates stage k from one slab buffer,
+// the DMA of stage k+1 -- the same item's next pairs or the next item's first -- is
+// landing in the other.  The next RoI's record and window are loaded / computed while
+// the current stage's copies are in flight, so the per-item prologue (RoI load, window,
+// DMA issue) leaves the critical path that bounds the one-item-per-wave kernel (DESIGN
+// §4).  DMA rounds are issued only as far as the window needs (ceil(cells / 32)) and
+// their per-lane offsets computed per round.  Two kHalf-dword buffers per wave.  Same
+// taps, weights and operation order as pair_item: bit-identical.
+struct PipeItem {
+  int k, chunk, empty, l, b, H, W, sy, sx, scs;
+  int y0, x0, Cs, Cs2, ncell, dense, dy, dx;
+  int D, RS, nr, nst, npairs, cw0;
+  uint32_t inv;
+  float start_h, start_w, bin_h, bin_w;
+  int rsrc, csrc;  // per lane: feature byte offsets of slab row / column `lane` (sparse windows)
+};
+
+template <int kPW, int kHalf>
+__device__ __forceinline__ PipeItem pipe_prep(const RoiLevels& lv, const RoiCfg& c, int64_t k, int chunk, int lane) {
+  constexpr int SR = 2;
+  PipeItem it;
+  const RoiGeom g = roi_geom_raw(c, lv, roi_fetch(c, k));
+  it.k = (int)k;
+  it.chunk = chunk;
+  it.l = g.lvl;
+  it.b = g.b;
+  it.H = lv.h[it.l];
+  it.W = lv.w[it.l];
+  it.sy = (int)lv.sy[it.l];
+  it.sx = (int)lv.sx[it.l];
+  it.scs = (int)lv.sc[it.l];
+  it.start_h = g.start_h;
+  it.start_w = g.start_w;
+  it.bin_h = g.bin_h;
+  it.bin_w = g.bin_w;
+  it.cw0 = chunk * 2 * kPW;
+  it.npairs = min(kPW, (c.C - it.cw0) / 2);
+  auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
+  auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
+  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
+  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
+  if (lane < nly) {
+    const int s = lane >> 1;
+    const Tap t = make_tap(pos_y(s >> 1, s & 1), it.H);
+    if (t.valid) yrow = (lane & 1) ? t.hi : t.lo, ylo = t.lo, yhi = t.hi;
+  }
+  if (lane < nlx) {
+    const int s = lane >> 1;
+    const Tap t = make_tap(pos_x(s >> 1, s & 1), it.W);
+    if (t.valid) xcol = (lane & 1) ? t.hi : t.lo, xlo = t.lo, xhi = t.hi;
+  }
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
+  it.empty = !(y1 >= y0 && x1 >= x0);
+  it.y0 = y0;
+  it.x0 = x0;
+  it.dy = y1 - y0 + 1 <= nly;
+  it.dx = x1 - x0 + 1 <= nlx;
+  it.dense = it.dy && it.dx;
+  const int R = it.dy ? y1 - y0 + 1 : nly;
+  it.Cs = it.dx ? x1 - x0 + 1 : nlx;
+  it.Cs2 = it.Cs | 1;
+  it.ncell = it.empty ? 0 : R * it.Cs2;
+  it.rsrc = (it.dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * it.sy * 4;
+  it.csrc = (it.dx ? x0 + min(lane, it.Cs - 1) : (xcol >= 0 ? xcol : x0)) * it.sx * 4;
+  it.D = it.ncell <= PairLayout<8, kHalf>::kCells ? 8
+       : it.ncell <= PairLayout<4, kHalf>::kCells ? 4
+       : it.ncell <= PairLayout<2, kHalf>::kCells ? 2 : 1;
+  it.RS = (kHalf / it.D) / kWave * kWave;
+  it.nr = it.empty ? 0 : min(it.RS / kWave, (it.ncell + 31) >> 5);
+  it.nst = it.empty ? 1 : (it.npairs + it.D - 1) / it.D;
+  it.inv = (65536u + (uint32_t)it.Cs2 - 1u) / (uint32_t)it.Cs2;
+  return it;
+}
+
+// issue the DMA rounds of stage s of `it` into the buffer at LDS byte address buf;
+// returns the number of vector-memory operations issued (wave-uniform)
+template <int kLdAux>
+__device__ __forceinline__ int pipe_issue(const RoiLevels& lv, const RoiCfg& c, const PipeItem& it, int s,
+                                          uint32_t buf, int lane) {
+  if (it.empty) return 0;
+  const float* base = lv.feat[it.l] + (int64_t)it.b * lv.sb[it.l];
+  const int64_t extent = ((int64_t)(c.C - 1) * it.scs + (int64_t)(it.H - 1) * it.sy + (int64_t)(it.W - 1) * it.sx + 1) * 4;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
+  for (int j = 0; j < it.nr; ++j) {
+    int e = (j * kWave + lane) >> 1;
+    e = e < it.ncell ? e : 0;
+    const int r = (int)(((uint32_t)e * it.inv) >> 16), col = min(e - r * it.Cs2, it.Cs - 1);
+    const int goff = it.dense ? ((it.y0 + r) * it.sy + (it.x0 + col) * it.sx + (lane & 1) * it.scs) * 4
+                              : __shfl(it.rsrc, r, kWave) + __shfl(it.csrc, col, kWave) + (lane & 1) * it.scs * 4;
+    for (int d = 0; d < it.D; ++d)
+      lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * it.RS + j * kWave), goff,
+                            (it.cw0 + 2 * min(s * it.D + d, it.npairs - 1)) * it.scs * 4);
+  }
+  return it.nr * it.D;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n < 32
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define FRH_VM(i) \
+  case i:         \
+    wait_vmcnt<i>(); \
+    break;
+    FRH_VM(0) FRH_VM(1) FRH_VM(2) FRH_VM(3) FRH_VM(4) FRH_VM(5) FRH_VM(6) FRH_VM(7) FRH_VM(8) FRH_VM(9) FRH_VM(10)
+    FRH_VM(11) FRH_VM(12) FRH_VM(13) FRH_VM(14) FRH_VM(15) FRH_VM(16) FRH_VM(17) FRH_VM(18) FRH_VM(19) FRH_VM(20)
+    FRH_VM(21) FRH_VM(22) FRH_VM(23) FRH_VM(24) FRH_VM(25) FRH_VM(26) FRH_VM(27) FRH_VM(28) FRH_VM(29) FRH_VM(30)
+    FRH_VM(31)
+#undef FRH_VM
+    default:
+      wait_vmcnt<0>();
+  }
+}
+
+// evaluate stage s of `it` (D pairs from the buffer at `buf`) and store its outputs
+template <int D, int kPW, int kHalf, int kStAux>
+__device__ __forceinline__ void pipe_eval(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out,
+                                          const PipeItem& it, int s, uint32_t buf, int lane) {
+  constexpr int SR = 2, RS = PairLayout<D, kHalf>::RS;
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr =
+      uniform_rsrc(out + ((int64_t)it.k * c.C + it.cw0) * nbins, (int64_t)2 * it.npairs * nbins * 4);
+  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  const int ostep = nbins * 4;
+  if (it.empty) {
+    for (int ch = 0; ch < 2 * it.npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
+    return;
+  }
+  auto pos_y = [&](int p, int i) { return it.start_h + (float)p * it.bin_h + ((float)i + 0.5f) * it.bin_h * 0.5f; };
+  auto pos_x = [&](int p, int i) { return it.start_w + (float)p * it.bin_w + ((float)i + 0.5f) * it.bin_w * 0.5f; };
+  const int bin = active ? lane : 0;
+  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
+  // lean tap state (pair_item kLean): per-sample factors (zero for invalid samples) and bases
+  float fyh[SR], fyl[SR], fxh[SR], fxl[SR];
+  uint32_t tb0[SR][SR], tdq[SR], tdr[SR];
+#pragma unroll
+  for (int iy = 0; iy < SR; ++iy) {
+    const Tap a = make_tap(pos_y(py, iy), it.H);
+    fyh[iy] = a.valid ? a.h : 0.f;
+    fyl[iy] = a.valid ? a.l : 0.f;
+    const int r0 = it.dy ? a.lo - it.y0 : 2 * (py * SR + iy), r1 = it.dy ? a.hi - it.y0 : 2 * (py * SR + iy) + 1;
+    tdr[iy] = 8u * (uint32_t)((r1 - r0) * it.Cs2);
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      const Tap b = make_tap(pos_x(px, ix), it.W);
+      const int q0 = it.dx ? b.lo - it.x0 : 2 * (px * SR + ix), q1 = it.dx ? b.hi - it.x0 : 2 * (px * SR + ix) + 1;
+      if (iy == 0) {
+        fxh[ix] = b.valid ? b.h : 0.f;
+        fxl[ix] = b.valid ? b.l : 0.f;
+        tdq[ix] = 8u * (uint32_t)(q1 - q0);
+      }
+      tb0[iy][ix] = buf + ((a.valid && b.valid) ? 8u * (uint32_t)(r0 * it.Cs2 + q0) : 0u);
+    }
+  }
+  f32x2 v[2][8];
+  f32x2 acc = {0.0f, 0.0f};
+  auto tap = [&](int iy, int ix, int q) -> uint32_t {
+    return tb0[iy][ix] + ((q & 1) ? tdq[ix] : 0u) + ((q & 2) ? tdr[iy] : 0u);
+  };
+  auto load = [&](auto hh) {
+    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * d * RS;
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[h % 2][ix * 4 + q] = lds_read_b64<OFF>(tap(iy, ix, q));
+  };
+  load(std::integral_constant<int, 0>{});
+  static_for<0, 2 * D>([&](auto hh) {
+    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
+    if constexpr (h + 1 < 2 * D) {
+      load(std::integral_constant<int, h + 1>{});
+      lds_wait<8>(v[h & 1]);
+    } else {
+      lds_wait<0>(v[h & 1]);
+    }
+    if (iy == 0) acc = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int ix = 0; ix < SR; ++ix) {
+      float wl[4];
+      wl[0] = fyh[iy] * fxh[ix];
+      wl[1] = fyh[iy] * fxl[ix];
+      wl[2] = fyl[iy] * fxh[ix];
+      wl[3] = fyl[iy] * fxl[ix];
+      const f32x2* x = &v[h % 2][ix * 4];
+      const f32x2 val = ((f32x2(wl[0]) * x[0] + f32x2(wl[1]) * x[1]) + f32x2(wl[2]) * x[2]) + f32x2(wl[3]) * x[3];
+      acc = acc + val;
+    }
+    if (iy == 1) {
+      const f32x2 r = acc * 0.25f;
+      const int p = s * D + d;
+      const int vo = p < it.npairs ? ovoff : 0x40000000;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
+    }
+  });
+}
+
+// The wave's items: XCD x (= workgroup id % 8) walks the x-th eighth of the chunk-major
+// (chunk, RoI) list; the Q waves of an XCD interleave over it (wave q: items q, q + Q, ...).
+template <int kPW = kPairWave, int kHalf = kPairHalf, int kStAux = kCpolNT, int kLdAux = 0>
+__global__ void __launch_bounds__(kWave) roi_align_fwd_pipe_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float slab[2 * kHalf];
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u, Q = gridDim.x >> 3;
+  const uint32_t lo = (blockIdx.x & 7u) * per, hi = min(lo + per, total);
+  uint32_t w = lo + (blockIdx.x >> 3);
+  if (w >= hi) return;
+  auto prep = [&](uint32_t item) {
+    const int ch = (int)(item / K32);
+    return pipe_prep<kPW, kHalf>(lv, c, (int64_t)(item - (uint32_t)ch * K32), ch, lane);
+  };
+  PipeItem cur = prep(w);
+  int cs = 0, buf = 0;
+  pipe_issue<kLdAux>(lv, c, cur, 0, sbase, lane);
+  for (;;) {
+    // the next stage: the current item's, or the next item's first
+    PipeItem nxt = cur;
+    int ns = cs + 1;
+    bool have = true;
+    if (ns >= cur.nst) {
+      w += Q;
+      have = w < hi;
+      if (have) nxt = prep(w);  // the RoI record loads while the current stage's copies land
+      ns = 0;
+    }
+    const uint32_t nb = sbase + 4u * (uint32_t)((buf ^ 1) * kHalf);
+    const int nvm = have ? pipe_issue<kLdAux>(lv, c, nxt, ns, nb, lane) : 0;
+    wait_vmcnt_dyn(nvm);  // the current stage landed (older: its copies, the previous stage's stores)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t cb = sbase + 4u * (uint32_t)(buf * kHalf);
+    switch (cur.D) {
+      case 8: pipe_eval<8, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
+      case 4: pipe_eval<4, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
+      case 2: pipe_eval<2, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
+      default: pipe_eval<1, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
+    }
+    // every tap read of this buffer completed (lds_wait<0> in the evaluation) before it is refilled
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!have) break;
+    cur = nxt;
+    cs = ns;
+    buf ^= 1;
+  }
+}
+
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
                                                                     const float* __restrict__ gout) {
   __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];

@@ -90,6 +90,10 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (variant == 26) launch_mw<2, 1, false, true, false>(lv, c, out, total, st);  // 20, 2 waves per WG
     else if (variant == 27) launch_mw<4, 1, false, true, false>(lv, c, out, total, st);  // 20, 4 waves per WG
     else FRH_REQUIRE(false, "roi_align variant %d unknown", variant);
+  } else if (variant >= 30 && variant <= 33) {  // persistent pipelined waves: Q per XCD
+    FRH_REQUIRE(pok, "the pair kernel does not take this shape");
+    const unsigned q = variant == 30 ? 384 : variant == 31 ? 256 : variant == 32 ? 320 : 448;
+    hipLaunchKernelGGL((roi_align_fwd_pipe_kernel<>), dim3(8 * q), dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else {
     FRH_REQUIRE(false, "roi_align variant %d unknown", variant);
   }
