@@ -149,16 +149,20 @@ def summarise_trace(trace, steps):
     per = {g: 0.0 for g, _ in KERNEL_GROUPS}
     names = {g: {} for g, _ in KERNEL_GROUPS}
     det = 0.0
+    det_k = {}
     for name, us in trace:
         if 'frh::' in name and 'bn_act' not in name:
             det += us
+            short = name.split('(')[0].replace('void ', '')
+            det_k[short] = det_k.get(short, 0.0) + us
         g = group_of(name)
         if g:
             per[g] += us
             short = name.split('(')[0].replace('void ', '')
             names[g][short] = names[g].get(short, 0) + 1
     return ({g: v / steps for g, v in per.items()}, det / steps,
-            {g: {k: c // steps for k, c in d.items()} for g, d in names.items()})
+            {g: {k: c // steps for k, c in d.items()} for g, d in names.items()},
+            {k: round(v / steps, 2) for k, v in sorted(det_k.items(), key=lambda kv: -kv[1])})
 
 
 # ------------------------------------------------------------------ RoIAlign replays
@@ -351,10 +355,6 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--trace-steps', type=int, default=3,
                     help='extra steps (after the timed region) run under the kernel tracer for the kernel lines; 0 = off')
-    ap.add_argument('--proposal-stream', default='on', choices=['on', 'off'],
-                    help='RPN proposal chain on a side stream, concurrent with the RPN target / loss chain')
-    ap.add_argument('--rpn-order', default='finest-last', choices=['finest-last', 'reference'],
-                    help='level order of the RPN head convs (finest-last keeps P2 cache-resident for RoIAlign)')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='torch.distributed backend for N > 1 (nccl = RCCL; gloo lets several ranks share one GPU)')
     ap.add_argument('--mode', default='fwd', choices=['fwd', 'train'],
@@ -387,7 +387,6 @@ def main():
     import frcnn_amd
     from frcnn_amd import ops
     frcnn_amd.set_sampler_mode(args.sampler, seed=1234 + rank)
-    frcnn_amd.set_proposal_stream(args.proposal_stream == 'on')
     np.random.seed(rank)
 
     if args.conv_search == 'auto':
@@ -396,8 +395,6 @@ def main():
     torch.backends.cudnn.benchmark = args.conv_search
     model, cfg = make_model(dev, seed=0, config=os.path.join(CONFIG_DIR, args.config + '.py'))
     batch = make_batch(dev, args.batch, seed=0, rank=rank)
-    if hasattr(model, 'rpn_head'):
-        model.rpn_head.finest_last = args.rpn_order == 'finest-last'
 
     if args.mode == 'train':
         from frcnn_amd.train import TrainStep, DEFAULT_BUCKET_MB
@@ -473,7 +470,8 @@ def main():
         steps_traced = max(args.trace_steps, 1)
         recs = list(ops.ROI_ALIGN_PROFILE['records'])
         nrecs = list(ops.NMS_PROFILE['records'])
-        per_group, det_us, group_names = summarise_trace(trace, steps_traced) if trace else ({}, None, {})
+        per_group, det_us, group_names, det_kernels = (summarise_trace(trace, steps_traced) if trace else
+                                                        ({}, None, {}, {}))
         roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]
         roi_in_step = float(np.mean([us for _, us in roi_launches])) if roi_launches else None
         roi_kernel = roi_launches[0][0].split('(')[0].replace('void ', '') if roi_launches else None
@@ -508,8 +506,7 @@ def main():
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
                        'backend': args.backend if world > 1 else None,
-                       'sampler': args.sampler, 'mode': args.mode, 'proposal_stream': args.proposal_stream,
-                       'rpn_order': args.rpn_order},
+                       'sampler': args.sampler, 'mode': args.mode},
         }
         if recs:
             out['roofline'] = {
@@ -558,7 +555,8 @@ def main():
                 for g in ('sampler', 'targets', 'losses'):
                     lines[g] = {'us_per_step': per_group.get(g)}
             lines['roi_align_fwd'] = {'us_per_step': per_group.get('roi_align_fwd')}
-            out['kernels'] = {'per_step': lines, 'detection_path_us_per_step': det_us, 'dispatched': group_names,
+            out['kernels'] = {'per_step': lines, 'detection_path_us_per_step': det_us,
+                              'detection_path_kernels_us_per_step': det_kernels, 'dispatched': group_names,
                               'timing': 'in-step device durations, ROCm kernel tracer, {} steps'.format(steps_traced)}
             if recs and lines.get('nms', {}).get('us_per_step'):
                 b = avg_bytes + lines['nms']['algorithmic_bytes_per_step']

@@ -76,8 +76,14 @@ int32_t frh_elem_iou(const float* a, int64_t lda, const float* b, int64_t ldb, i
  * ([4, gt_ld]), count num_gts[s] (device).  Labels are int64:
  * -1 ignore, 0 negative, g+1 positive for gt g; max_iou f32.  Thresholds are
  * compared in f32 like the reference (`f32 tensor < python float`).
- * max_boxes / max_gts bound the launch (host-known maxima of the counts). */
-size_t frh_maxiou_assign_workspace(int32_t num_segs, int32_t max_gts);
+ * max_boxes / max_gts bound the launch (host-known maxima of the counts).  One launch: the
+ * last workgroup of each segment labels the boxes tied at a gt's maximum (hand-off inside
+ * the launch).  Workspace: frh_maxiou_assign_workspace bytes whose leading
+ * frh_maxiou_assign_zero_bytes(num_segs, max_gts) bytes are zero before the call; every call
+ * leaves them zero, so a caller zero-fills them once per (num_segs, max_gts) layout and reuses
+ * the buffer for calls ordered on one stream. */
+size_t frh_maxiou_assign_zero_bytes(int32_t num_segs, int32_t max_gts);
+size_t frh_maxiou_assign_workspace(int32_t num_segs, int32_t max_gts, int64_t max_boxes);
 int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
                           int64_t box_seg_stride, const int32_t* num_boxes,
                           const uint8_t* valid, int64_t valid_seg_stride,
@@ -287,6 +293,15 @@ int32_t frh_mcnms_finish(int32_t num_imgs, int32_t num_classes, int64_t n_max, i
  * (layout 0) or NHWC (layout 1, i.e. channels_last strides); out [K, C, ph, pw]. */
 int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float finest_scale,
                           int32_t num_levels, int64_t* levels, void* stream);
+/* The RoI rows the extractor feeds RoIAlign: rois [K, 5] = (image b, x1, y1, x2, y2) for the
+ * boxes of num_segs images (<= 64) concatenated in image order (the reference attaches the
+ * index per image, region.py:266-269, in its per-image forward, :303-306), and with
+ * num_levels > 1 their levels as frh_roi_level_map computes them (region.py:256-264).  seg_offsets: HOST array [num_segs + 1] of row offsets
+ * (0, n_0, n_0 + n_1, ...).  Boxes are [4, box_ld] coordinate-major: image b's box j at column
+ * j of boxes + b * box_seg_stride, or (flat != 0) at column offsets[b] + j of boxes. */
+int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t box_ld, int64_t box_seg_stride,
+                     int32_t flat, const int64_t* seg_offsets, float finest_scale, int32_t num_levels,
+                     float* rois, int64_t* levels, void* stream);
 int32_t frh_roi_align_fwd(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
                           const float* scales, int32_t batch, int32_t channels, int32_t layout,
                           const float* rois, const int64_t* roi_levels, int64_t num_rois,
@@ -369,6 +384,9 @@ int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gam
  * Backward writes grad_x (i, k) at grad_x[i*gsr + k*gsc] = grad_out[0] * dL/dx.
  * Callers: AnchorHead.calc_loss (anchor_head.py:113-139), BBoxHead.calc_loss
  * (bbox_head.py:56-87), FCOSHead losses (fcos_head.py:418-534). */
+/* Forward workspace: frh_loss_workspace() bytes whose first 256 bytes (the arrival counter of
+ * the in-launch finalisation) are zero before the first call; every call leaves them zero, so
+ * a caller zero-fills the buffer once and reuses it for calls ordered on one stream. */
 size_t frh_loss_workspace(void);
 int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr,
                          int64_t sc, const void* target, int32_t target_is_float, float alpha,

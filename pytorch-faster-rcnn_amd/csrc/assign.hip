@@ -1,14 +1,23 @@
 // a3/a4: IoU tables and MaxIoU assignment, batched over segments (images).
 // Reference: lib/utils.py:151-182 (calc_iou/elem_iou), lib/region.py:60-107 (MaxIoUAssigner).
 //
-// Assignment runs in two passes over the boxes of every segment:
-//   pass 1: per-gt max IoU over all valid boxes (wave max-reduce + one
-//           atomicMax per wave on an order-preserving u32 key),
-//   pass 2: recompute the box's G IoUs (cheaper than storing the N x G
-//           table), apply the neg/pos thresholds on the row max and the
-//           "every box tied at a gt's max" rule with the first tied gt.
-// The IoU expression is identical in both passes, so the equality test of
-// pass 2 sees exactly the values pass 1 reduced.
+// Assignment is ONE launch, one thread per box, gts in LDS:
+//   every workgroup computes its boxes' row maxima (first argmax, NaN wins like
+//   torch.max) and threshold labels, and its own per-gt maxima (wave max + LDS
+//   atomicMax on order-preserving u32 keys), which it folds into the segment's
+//   per-gt maxima with a device atomicMax (skipped when the value there is
+//   already as large).  A box can take the "tied at a gt's maximum" rule
+//   (region.py:95-106) only if it ties its own workgroup's maximum of that gt
+//   (the segment maximum is >= the workgroup's): such candidate boxes, found by
+//   re-evaluating only the gts whose workgroup maximum reaches min_pos_iou, are
+//   appended to a per-segment list instead of being labelled; every other box
+//   is final.  The workgroup then arrives at the segment's counter; the last to
+//   arrive labels the candidates against the final maxima and resets the
+//   counters.  Hand-off (MI355X_MICROARCH.md hand-off table, row 1): list
+//   entries stored write-through (agent-scope relaxed stores) and drained before
+//   the arrival, maxima by device atomics, all read with agent-scope loads.
+// The IoU expression is identical everywhere, so the equality tests see exactly
+// the values the maxima were reduced from.
 #include "common.h"
 
 namespace frh {
@@ -54,7 +63,10 @@ struct AssignArgs {
   int64_t label_seg_stride;
   float* max_iou;
   int64_t iou_seg_stride;
-  uint32_t* colmax;  // [S, max_gts] order-preserving keys
+  uint32_t* colmax;  // [S, max_gts] order-preserving keys; zero between calls
+  int32_t* state;    // [S, 4]: arrivals, candidates; zero between calls
+  int32_t* cand;     // [S, cand_ld] candidate box indices
+  int64_t cand_ld;
   int32_t max_gts;
 };
 
@@ -64,91 +76,148 @@ __device__ __forceinline__ void load_gts(const AssignArgs& p, int s, int G, floa
     sg[j] = make_float4(g[j], g[p.gt_ld + j], g[2 * p.gt_ld + j], g[3 * p.gt_ld + j]);
 }
 
-__global__ void __launch_bounds__(kAssignThreads) assign_colmax_kernel(AssignArgs p) {
-  __shared__ float4 sg[kMaxGts];
-  __shared__ uint32_t scol[kMaxGts];
-  const int s = blockIdx.y;
-  const int n = p.num_boxes[s];
-  const int G = p.num_gts[s];
-  if ((int64_t)blockIdx.x * blockDim.x >= n || G <= 0) return;  // uniform per block
-  load_gts(p, s, G, sg);
-  for (int j = threadIdx.x; j < G; j += blockDim.x) scol[j] = 0u;
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool live = i < n;
-  if (live && p.valid) live = p.valid[(int64_t)s * p.valid_seg_stride + i] != 0;
-  float x1 = 0.f, y1 = 0.f, x2 = 0.f, y2 = 0.f;
-  if (live) {
-    const float* b = p.boxes + (int64_t)s * p.box_seg_stride;
-    x1 = b[i];
-    y1 = b[p.box_ld + i];
-    x2 = b[2 * p.box_ld + i];
-    y2 = b[3 * p.box_ld + i];
-  }
-  for (int j = 0; j < G; ++j) {
-    float4 g = sg[j];
-    uint32_t key = live ? float_key(iou_plus1(x1, y1, x2, y2, g.x, g.y, g.z, g.w)) : 0u;
-    key = wave_max_u32(key);
-    if (lane_id() == 0 && key) atomicMax(&scol[j], key);
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < G; j += blockDim.x)
-    if (scol[j]) atomicMax(&p.colmax[(int64_t)s * p.max_gts + j], scol[j]);
+__device__ __forceinline__ float4 load_box(const AssignArgs& p, int s, int64_t i) {
+  const float* b = p.boxes + (int64_t)s * p.box_seg_stride;
+  return make_float4(b[i], b[p.box_ld + i], b[2 * p.box_ld + i], b[3 * p.box_ld + i]);
 }
 
-__global__ void __launch_bounds__(kAssignThreads) assign_label_kernel(AssignArgs p) {
+__device__ __forceinline__ float iou_box(const float4& a, const float4& g) {
+  return iou_plus1(a.x, a.y, a.z, a.w, g.x, g.y, g.z, g.w);
+}
+
+// row max / first argmax with NaN winning like torch.max (region.py:88)
+__device__ __forceinline__ void row_step(int j, float v, float& m, int& arg) {
+  if (j == 0) {
+    m = v;
+  } else if (!(v <= m) && !isnan(m)) {
+    m = v;
+    arg = j;
+  }
+}
+
+// thresholds (region.py:90-92) on the row maximum
+__device__ __forceinline__ int64_t threshold_label(const AssignArgs& p, float m, int arg) {
+  int64_t lab = -1;
+  if (m < p.neg_iou) lab = 0;
+  if (m >= p.pos_iou) lab = (int64_t)arg + 1;
+  return lab;
+}
+
+// The last workgroup of segment s: every candidate box gets its full label -- the
+// first gt whose final maximum it ties (>= min_pos_iou) overrides the thresholds
+// (region.py:95-106).  scm: the final maxima as floats (NaN where no valid box
+// reached the gt: never equal).
+__device__ void label_candidates(const AssignArgs& p, int s, int G, const float4* sg, float* scm) {
+  for (int j = threadIdx.x; j < G; j += blockDim.x) {
+    const uint32_t k = __hip_atomic_load(p.colmax + (int64_t)s * p.max_gts + j, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    scm[j] = k ? key_float(k) : __uint_as_float(0x7fc00000u);
+  }
+  int32_t* st = p.state + 4 * s;
+  const int ncand = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  int64_t* lab_out = p.labels + (int64_t)s * p.label_seg_stride;
+  float* iou_out = p.max_iou ? p.max_iou + (int64_t)s * p.iou_seg_stride : nullptr;
+  for (int t = threadIdx.x; t < ncand; t += blockDim.x) {
+    const int64_t i = __hip_atomic_load(p.cand + (int64_t)s * p.cand_ld + t, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    const float4 a = load_box(p, s, i);
+    float m = 0.f, m_eq = 0.f;
+    int arg = 0, eq = -1;
+    for (int j = 0; j < G; ++j) {
+      const float v = iou_box(a, sg[j]);
+      row_step(j, v, m, arg);
+      if (eq < 0 && v == scm[j] && scm[j] >= p.min_pos_iou) {
+        eq = j;
+        m_eq = v;
+      }
+    }
+    int64_t lab = threshold_label(p, m, arg);
+    float out_iou = m;
+    if (eq >= 0) {
+      lab = (int64_t)eq + 1;
+      out_iou = m_eq;
+    }
+    lab_out[i] = lab;
+    if (iou_out) iou_out[i] = out_iou;
+  }
+  __syncthreads();  // every read of the maxima and the list is done: reset for the next call
+  for (int j = threadIdx.x; j < G; j += blockDim.x)
+    __hip_atomic_store(p.colmax + (int64_t)s * p.max_gts + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(st + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(st + 0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(kAssignThreads) maxiou_assign_kernel(AssignArgs p) {
   __shared__ float4 sg[kMaxGts];
-  __shared__ float scm[kMaxGts];
+  __shared__ uint32_t scol[kMaxGts];  // this workgroup's per-gt maxima (keys); later the final maxima
+  __shared__ int snear[kMaxGts];      // gts whose workgroup maximum reaches min_pos_iou
+  __shared__ int nnear, last;
   const int s = blockIdx.y;
   const int n = p.num_boxes[s];
   const int G = p.num_gts[s];
-  if ((int64_t)blockIdx.x * blockDim.x >= n) return;
-  load_gts(p, s, G, sg);
-  for (int j = threadIdx.x; j < G; j += blockDim.x) {
-    uint32_t k = p.colmax[(int64_t)s * p.max_gts + j];
-    // a gt that no valid box reached keeps key 0: never equal to any IoU
-    scm[j] = k ? key_float(k) : __uint_as_float(0x7fc00000u);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool any = (int64_t)blockIdx.x * blockDim.x < n && G > 0;  // uniform per block
+  if (any) {
+    load_gts(p, s, G, sg);
+    for (int j = threadIdx.x; j < G; j += blockDim.x) scol[j] = 0u;
+  }
+  if (threadIdx.x == 0) nnear = 0;
+  __syncthreads();
+  bool live = i < n;
+  if (live && p.valid) live = p.valid[(int64_t)s * p.valid_seg_stride + i] != 0;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) a = load_box(p, s, i);
+  float m = 0.f;
+  int arg = 0;
+  if (any) {
+    for (int j = 0; j < G; ++j) {
+      const float v = iou_box(a, sg[j]);
+      if (live) row_step(j, v, m, arg);
+      const uint32_t key = wave_max_u32(live ? float_key(v) : 0u);
+      if (lane_id() == 0 && key) atomicMax(&scol[j], key);
+    }
   }
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int64_t* lab_out = p.labels + (int64_t)s * p.label_seg_stride;
-  float* iou_out = p.max_iou ? p.max_iou + (int64_t)s * p.iou_seg_stride : nullptr;
-  bool live = !p.valid || p.valid[(int64_t)s * p.valid_seg_stride + i] != 0;
-  if (!live || G <= 0) {
-    lab_out[i] = -1;
-    if (iou_out) iou_out[i] = 0.0f;
-    return;
-  }
-  const float* b = p.boxes + (int64_t)s * p.box_seg_stride;
-  float x1 = b[i], y1 = b[p.box_ld + i], x2 = b[2 * p.box_ld + i], y2 = b[3 * p.box_ld + i];
-  // row max / first argmax, NaN wins like torch.max (region.py:88)
-  float m = 0.f, m_eq = 0.f;
-  int arg = 0, eq = -1;
-  for (int j = 0; j < G; ++j) {
-    float4 g = sg[j];
-    float v = iou_plus1(x1, y1, x2, y2, g.x, g.y, g.z, g.w);
-    if (j == 0) {
-      m = v;
-    } else if (!(v <= m) && !isnan(m)) {
-      m = v;
-      arg = j;
-    }
-    if (eq < 0 && v == scm[j] && scm[j] >= p.min_pos_iou) {  // region.py:95-101
-      eq = j;
-      m_eq = v;
+  if (any) {
+    uint32_t* cm = p.colmax + (int64_t)s * p.max_gts;
+    for (int j = threadIdx.x; j < G; j += blockDim.x) {
+      const uint32_t k = scol[j];
+      if (!k) continue;
+      if (k > __hip_atomic_load(cm + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cm + j, k);
+      if (key_float(k) >= p.min_pos_iou) snear[atomicAdd(&nnear, 1)] = j;
     }
   }
-  int64_t lab = -1;
-  if (m < p.neg_iou) lab = 0;                    // region.py:90
-  if (m >= p.pos_iou) lab = (int64_t)arg + 1;    // region.py:92,106
-  float out_iou = m;
-  if (eq >= 0) {                                 // region.py:101-106
-    lab = (int64_t)eq + 1;
-    out_iou = m_eq;
+  __syncthreads();
+  // candidates: ties of this workgroup's maximum of a gt that reaches min_pos_iou
+  bool cand = false;
+  if (live) {
+    for (int t = 0; t < nnear && !cand; ++t) {
+      const int j = snear[t];
+      cand = iou_box(a, sg[j]) == key_float(scol[j]);
+    }
   }
-  lab_out[i] = lab;
-  if (iou_out) iou_out[i] = out_iou;
+  const int slot = wave_append(cand, p.state + 4 * s + 1);
+  if (cand) {
+    __hip_atomic_store(p.cand + (int64_t)s * p.cand_ld + slot, (int32_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (i < n) {
+    p.labels[(int64_t)s * p.label_seg_stride + i] = (live && G > 0) ? threshold_label(p, m, arg) : -1;
+    if (p.max_iou) p.max_iou[(int64_t)s * p.iou_seg_stride + i] = (live && G > 0) ? m : 0.0f;
+  }
+  // arrival: every wave drains its stores, then one lane adds for the workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(p.state + 4 * s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (!any && G > 0) load_gts(p, s, G, sg);  // the last workgroup may be one past the boxes
+  __syncthreads();
+  if (G > 0) label_candidates(p, s, G, sg, reinterpret_cast<float*>(scol));
+  else if (threadIdx.x == 0) __hip_atomic_store(p.state + 4 * s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace frh
@@ -176,8 +245,19 @@ extern "C" int32_t frh_elem_iou(const float* a, int64_t lda, const float* b, int
   return check_launch("frh_elem_iou");
 }
 
-extern "C" size_t frh_maxiou_assign_workspace(int32_t num_segs, int32_t max_gts) {
-  return (size_t)num_segs * (size_t)(max_gts > 0 ? max_gts : 1) * sizeof(uint32_t);
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// [zeroed: state S x 4 int32 | colmax S x max_gts u32] [candidates S x max_boxes int32]
+static size_t assign_zero_bytes(int32_t num_segs, int32_t max_gts) {
+  return al256((size_t)num_segs * 16) + al256((size_t)num_segs * (size_t)(max_gts > 0 ? max_gts : 1) * 4);
+}
+
+extern "C" size_t frh_maxiou_assign_zero_bytes(int32_t num_segs, int32_t max_gts) {
+  return assign_zero_bytes(num_segs, max_gts);
+}
+
+extern "C" size_t frh_maxiou_assign_workspace(int32_t num_segs, int32_t max_gts, int64_t max_boxes) {
+  return assign_zero_bytes(num_segs, max_gts) + al256((size_t)num_segs * (size_t)(max_boxes > 0 ? max_boxes : 1) * 4);
 }
 
 extern "C" int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
@@ -194,14 +274,14 @@ extern "C" int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64
   FRH_REQUIRE(max_gts <= kMaxGts, "max_gts %d exceeds %d", max_gts, kMaxGts);
   FRH_REQUIRE(max_boxes <= (int64_t)0x7fffffff, "too many boxes");
   int32_t mg = max_gts > 0 ? max_gts : 1;
-  FRH_REQUIRE(workspace && ws_bytes >= frh_maxiou_assign_workspace(num_segs, mg), "workspace too small");
+  FRH_REQUIRE(workspace && ws_bytes >= frh_maxiou_assign_workspace(num_segs, mg, max_boxes), "workspace too small");
+  char* ws = static_cast<char*>(workspace);
+  const size_t zs = al256((size_t)num_segs * 16);
   AssignArgs p{boxes, box_ld, box_seg_stride, num_boxes, valid, valid_seg_stride, gts, gt_ld,
                gt_seg_stride, num_gts, pos_iou, neg_iou, min_pos_iou, labels, label_seg_stride,
-               max_iou, iou_seg_stride, reinterpret_cast<uint32_t*>(workspace), mg};
-  FRH_HIP(hipMemsetAsync(workspace, 0, frh_maxiou_assign_workspace(num_segs, mg), as_stream(stream)));
+               max_iou, iou_seg_stride, reinterpret_cast<uint32_t*>(ws + zs), reinterpret_cast<int32_t*>(ws),
+               reinterpret_cast<int32_t*>(ws + assign_zero_bytes(num_segs, mg)), max_boxes, mg};
   dim3 grid((unsigned)((max_boxes + kAssignThreads - 1) / kAssignThreads), (unsigned)num_segs);
-  if (max_gts > 0)
-    hipLaunchKernelGGL(assign_colmax_kernel, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
-  hipLaunchKernelGGL(assign_label_kernel, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
+  hipLaunchKernelGGL(maxiou_assign_kernel, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
   return check_launch("frh_maxiou_assign");
 }

@@ -89,4 +89,16 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return (lane_id() == 0) ? 0ull : ((~0ull) >> (kWave - lane_id()));
 }
 
+// wave-aggregated append: every lane with `take` gets a distinct slot of the
+// list behind `counter` (LDS or global); -1 for the others.  Wave-uniform call.
+__device__ __forceinline__ int wave_append(bool take, int* counter) {
+  const uint64_t m = __ballot(take);
+  if (!m) return -1;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader, kWave);
+  return take ? base + __popcll(m & lanemask_lt()) : -1;
+}
+
 }  // namespace frh

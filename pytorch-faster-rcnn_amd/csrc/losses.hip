@@ -13,10 +13,18 @@
 // is one streaming pass: the element (i, k) of the logits is read through
 // explicit strides (so the channel-major [C, S] views the target gathers
 // produce need no copy), the one-hot target is the comparison label[i] == k+1,
-// and the per-block partial sums are finalised by one single-block kernel in a
-// fixed order (deterministic; no float atomics).  Backward recomputes the
+// and the per-block partial sums are finalised in a fixed order by the last
+// workgroup (deterministic; no float atomics).  Backward recomputes the
 // element's derivative and writes g * dL/dx, reading the upstream gradient
 // from device memory (no host sync).
+//
+// The forward's finalisation rides in the same launch: every workgroup stores
+// its partial write-through (agent-scope relaxed store), drains, and adds to an
+// arrival counter; the workgroup whose add returns nb - 1 sums the nb partials
+// (agent-scope loads) in the fixed order of the former separate finalise
+// launch and resets the counter (MI355X_MICROARCH.md hand-off table, row 1:
+// one signalling lane per workgroup, one unsharded counter, last adder told by
+// its add's return value; grids capped at 256 workgroups).
 //
 // Bytes per element: forward 4 (logit) + 8/C (label); backward 4 + 4 + 8/C.
 // Numerics follow torch's formulas (binary_cross_entropy_with_logits via
@@ -30,7 +38,8 @@ namespace frh {
 namespace {
 
 constexpr int kLossThreads = 256;
-constexpr int kMaxPartials = 1024;
+constexpr int kMaxPartials = 256;   // forward grid cap = partial slots
+constexpr int kCounterBytes = 256;  // arrival counter block at the workspace start
 
 enum ClsKind { kFocal = 0, kSigmoidBce = 1, kSoftmaxCe = 2 };
 
@@ -109,8 +118,43 @@ __device__ __forceinline__ float block_sum_f(float v, float* scratch) {
   return t;
 }
 
+struct FanIn {
+  uint32_t* counter;  // zero between calls
+  float* partial;     // [gridDim.x]
+  float* out;
+};
+
+// Thread 0 holds the workgroup's partial sum.  The last workgroup to arrive sums
+// all partials in a fixed order (double accumulation: one slot per thread, then
+// a tree) and writes the loss.
+__device__ void fan_in_finalize(float block_total, const FanIn& f) {
+  __shared__ double s[kLossThreads];
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(f.partial + blockIdx.x, block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(f.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  double v = 0.0;
+  for (int j = threadIdx.x; j < (int)gridDim.x; j += kLossThreads)
+    v += (double)__hip_atomic_load(f.partial + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = kLossThreads / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    f.out[0] = (float)s[0];
+    __hip_atomic_store(f.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int kKind>
-__global__ void __launch_bounds__(kLossThreads) cls_loss_fwd_kernel(ClsArgs a, float* partial) {
+__global__ void __launch_bounds__(kLossThreads) cls_loss_fwd_kernel(ClsArgs a, FanIn f) {
   __shared__ float scratch[kLossThreads / kWave];
   float acc = 0.0f;
   if constexpr (kKind == kSoftmaxCe) {
@@ -136,8 +180,7 @@ __global__ void __launch_bounds__(kLossThreads) cls_loss_fwd_kernel(ClsArgs a, f
       acc += kKind == kFocal ? focal_elem(x, t, a.alpha, a.gamma, nullptr) : bce_logits(x, t);
     }
   }
-  float s = block_sum_f(acc, scratch);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  fan_in_finalize(block_sum_f(acc, scratch), f);
 }
 
 template <int kKind>
@@ -196,7 +239,7 @@ __device__ __forceinline__ bool l1_row(const L1Args& a, int64_t i, int64_t* off)
   return true;
 }
 
-__global__ void __launch_bounds__(kLossThreads) smooth_l1_fwd_kernel(L1Args a, float* partial) {
+__global__ void __launch_bounds__(kLossThreads) smooth_l1_fwd_kernel(L1Args a, FanIn f) {
   __shared__ float scratch[kLossThreads / kWave];
   float acc = 0.0f;
   const int64_t total = a.n * a.m;
@@ -211,8 +254,7 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_fwd_kernel(L1Args a, f
     float d = fabsf(a.x[off + j * a.xs_j] - a.y[i * a.ys_i + j * a.ys_j]);
     acc += d < a.beta ? (d * d) / (2.0f * a.beta) : d - 0.5f * a.beta;
   }
-  float s = block_sum_f(acc, scratch);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  fan_in_finalize(block_sum_f(acc, scratch), f);
 }
 
 // gx must be zero-filled by the caller: only the selected, unmasked elements are written.
@@ -234,19 +276,6 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_bwd_kernel(L1Args a, c
   }
 }
 
-// Fixed-order sum of the per-block partials (double accumulation).
-__global__ void __launch_bounds__(kLossThreads) loss_finalize_kernel(const float* partial, int nb, float* out) {
-  __shared__ double s[kLossThreads];
-  double v = 0.0;
-  for (int j = threadIdx.x; j < nb; j += kLossThreads) v += (double)partial[j];
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = kLossThreads / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = (float)s[0];
-}
 
 int grid_for(int64_t work) {
   int64_t b = (work + kLossThreads - 1) / kLossThreads;
@@ -314,7 +343,12 @@ using namespace frh;
 
 extern "C" {
 
-size_t frh_loss_workspace(void) { return kMaxPartials * sizeof(float); }
+size_t frh_loss_workspace(void) { return kCounterBytes + kMaxPartials * sizeof(float); }
+
+static FanIn fan_in(void* workspace, float* out) {
+  char* w = static_cast<char*>(workspace);
+  return FanIn{reinterpret_cast<uint32_t*>(w), reinterpret_cast<float*>(w + kCounterBytes), out};
+}
 
 int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr, int64_t sc,
                          const void* target, int32_t target_is_float, float alpha, float gamma, float* out,
@@ -324,16 +358,15 @@ int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
   if (st != FRH_OK) return st;
   FRH_REQUIRE(out, "cls loss: null output");
   FRH_REQUIRE(workspace && ws_bytes >= frh_loss_workspace(), "cls loss: workspace too small");
-  float* partial = static_cast<float*>(workspace);
+  const FanIn f = fan_in(workspace, out);
   int nb = grid_for(kind == kSoftmaxCe ? n : n * c);
   hipStream_t s = as_stream(stream);
   if (kind == kFocal)
-    hipLaunchKernelGGL(cls_loss_fwd_kernel<kFocal>, dim3(nb), dim3(kLossThreads), 0, s, a, partial);
+    hipLaunchKernelGGL(cls_loss_fwd_kernel<kFocal>, dim3(nb), dim3(kLossThreads), 0, s, a, f);
   else if (kind == kSigmoidBce)
-    hipLaunchKernelGGL(cls_loss_fwd_kernel<kSigmoidBce>, dim3(nb), dim3(kLossThreads), 0, s, a, partial);
+    hipLaunchKernelGGL(cls_loss_fwd_kernel<kSigmoidBce>, dim3(nb), dim3(kLossThreads), 0, s, a, f);
   else
-    hipLaunchKernelGGL(cls_loss_fwd_kernel<kSoftmaxCe>, dim3(nb), dim3(kLossThreads), 0, s, a, partial);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(kLossThreads), 0, s, partial, nb, out);
+    hipLaunchKernelGGL(cls_loss_fwd_kernel<kSoftmaxCe>, dim3(nb), dim3(kLossThreads), 0, s, a, f);
   return check_launch("frh_cls_loss_fwd");
 }
 
@@ -366,11 +399,9 @@ int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
   if (st != FRH_OK) return st;
   FRH_REQUIRE(out, "smooth l1: null output");
   FRH_REQUIRE(workspace && ws_bytes >= frh_loss_workspace(), "smooth l1: workspace too small");
-  float* partial = static_cast<float*>(workspace);
   int nb = grid_for(n * m);
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(smooth_l1_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, s, a, partial);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(kLossThreads), 0, s, partial, nb, out);
+  hipLaunchKernelGGL(smooth_l1_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, as_stream(stream), a,
+                     fan_in(workspace, out));
   return check_launch("frh_smooth_l1_fwd");
 }
 

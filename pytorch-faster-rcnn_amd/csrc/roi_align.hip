@@ -23,11 +23,9 @@
 
 namespace frh {
 
-__global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int L, int64_t* levels) {
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const float* r = rois + k * 5;
-  float area = ((r[3] - r[1]) + 1.0f) * ((r[4] - r[2]) + 1.0f);
+// region.py:256-264: floor(log2(sqrt(area) / finest + 1e-6)) clamped to [0, L-1]
+__device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, float y2, float finest, int L) {
+  float area = ((x2 - x1) + 1.0f) * ((y2 - y1) + 1.0f);
   float s = sqrtf(area);
   float v = s / finest + 1e-6f;
   // correctly rounded f32 log2, then floor (region.py:262); clamp to [0, L-1]
@@ -35,7 +33,47 @@ __global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int
   float fl = floorf(lg);
   float hi = (float)(L - 1);
   fl = fl < 0.0f ? 0.0f : (fl > hi ? hi : fl);
-  levels[k] = (int64_t)fl;
+  return (int64_t)fl;
+}
+
+__global__ void roi_level_kernel(const float* rois, int64_t K, float finest, int L, int64_t* levels) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const float* r = rois + k * 5;
+  levels[k] = roi_level_of(r[1], r[2], r[3], r[4], finest, L);
+}
+
+constexpr int kRowSegs = 64;
+
+struct RowsArgs {
+  const float* boxes;
+  int64_t ld, seg_stride;
+  int32_t S, flat, L;
+  float finest;
+  int64_t K;
+  float* rois;
+  int64_t* levels;
+  int64_t offs[kRowSegs + 1];
+};
+
+// RoI rows [K, 5] = (image, x1, y1, x2, y2) of the images' boxes, concatenated in image
+// order, and (L > 1) their FPN levels: the reference's batch-index column
+// (_attach_idx_to_rois_, region.py:266-269) and map_rois_to_levels (:256-264) in one pass.
+__global__ void roi_rows_kernel(RowsArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.K) return;
+  int b = 0;
+  while (b + 1 < a.S && k >= a.offs[b + 1]) ++b;
+  const int64_t col = a.flat ? k : k - a.offs[b];
+  const float* p = a.boxes + (int64_t)b * a.seg_stride + col;
+  const float x1 = p[0], y1 = p[a.ld], x2 = p[2 * a.ld], y2 = p[3 * a.ld];
+  float* r = a.rois + k * 5;
+  r[0] = (float)b;
+  r[1] = x1;
+  r[2] = y1;
+  r[3] = x2;
+  r[4] = y2;
+  if (a.levels) a.levels[k] = roi_level_of(x1, y1, x2, y2, a.finest, a.L);
 }
 
 }  // namespace frh
@@ -52,6 +90,23 @@ extern "C" int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float 
   return check_launch("frh_roi_level_map");
 }
 
+extern "C" int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t box_ld, int64_t box_seg_stride,
+                                int32_t flat, const int64_t* seg_offsets, float finest_scale, int32_t num_levels,
+                                float* rois, int64_t* levels, void* stream) {
+  FRH_REQUIRE(num_segs >= 1 && num_segs <= kRowSegs, "num_segs must be in [1, %d]", kRowSegs);
+  FRH_REQUIRE(seg_offsets && num_levels >= 1, "bad arguments");
+  RowsArgs a{boxes, box_ld, box_seg_stride, num_segs, flat ? 1 : 0, num_levels, finest_scale, 0, rois,
+             num_levels > 1 ? levels : nullptr, {}};
+  for (int b = 0; b <= num_segs; ++b) {
+    a.offs[b] = seg_offsets[b];
+    FRH_REQUIRE(b == 0 ? a.offs[0] == 0 : a.offs[b] >= a.offs[b - 1], "seg_offsets must start at 0 and not decrease");
+  }
+  a.K = a.offs[num_segs];
+  if (a.K == 0) return FRH_OK;
+  FRH_REQUIRE(boxes && rois && (num_levels == 1 || levels), "null pointer argument");
+  hipLaunchKernelGGL(roi_rows_kernel, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+  return check_launch("frh_roi_rows");
+}
 
 extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
                                              const int64_t* strides, const float* scales, int32_t batch,

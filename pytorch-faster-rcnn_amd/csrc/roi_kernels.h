@@ -484,7 +484,8 @@ struct PairLayout {
 // list, so each XCD's L2 holds the feature planes of its own channel chunks.
 // kStAux / kLdAux: cache policy of the output stores / staging loads (cdna.h).
 // kStamp (tools-only timing builds): lane 0 writes 8 int64 per item after the
-// output -- s_memrealtime at start / setup done / first stage landed / end, D, cells.
+// output -- s_memrealtime at start / setup done / first stage landed / end, D, cells,
+// RoI record landed, XCD.
 // kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
 // stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
 // twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
@@ -501,6 +502,7 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
   static_assert(kSingle || !(kDynR || kWideSt), "dynamic rounds / wide stores need the single slab buffer");
   constexpr int SR = 2;
   int64_t t_setup = 0, t_land = 0;
+  const int64_t t_fetched = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;  // the RoI record has landed
   const int cw0 = chunk * 2 * kPW;
   const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom_raw(c, lv, raw);
@@ -801,7 +803,7 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
     st[3] = t_end;
     st[4] = stamp_d;
     st[5] = ncell;
-    st[6] = k;
+    st[6] = t_fetched;
     st[7] = blockIdx.x & 7;
   }
 }

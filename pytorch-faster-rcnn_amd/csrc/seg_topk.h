@@ -92,18 +92,6 @@ __device__ __forceinline__ void tk_hist_add(uint32_t* h, bool act, uint32_t bin)
   if (act && bin != b0) atomicAdd(&h[bin], 1u);
 }
 
-// wave-aggregated append: every lane with `take` gets a distinct slot of the
-// list behind `counter` (LDS or global); -1 for the others.  Wave-uniform call.
-__device__ __forceinline__ int wave_append(bool take, int* counter) {
-  const uint64_t m = __ballot(take);
-  if (!m) return -1;
-  const int leader = __builtin_ctzll(m);
-  int base = 0;
-  if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader, kWave);
-  return take ? base + __popcll(m & lanemask_lt()) : -1;
-}
-
 // Workgroup-aggregated reservation of `cnt` slots per thread in the list
 // behind the global `counter` (one atomic per workgroup): returns this
 // thread's first slot.  Block-uniform call; part / sh[2]: LDS scratch (sh[0] /

@@ -7,9 +7,9 @@ primitives run as hand-written HIP kernels in libfrcnn_amd.so (C-ABI in
 include/frcnn_amd.h).  There is no CPU fallback.
 """
 from . import _lib
-from .ops import set_sampler_mode, sampler_mode, set_proposal_stream
+from .ops import set_sampler_mode, sampler_mode
 
-__all__ = ['set_sampler_mode', 'sampler_mode', 'set_proposal_stream', 'load_library']
+__all__ = ['set_sampler_mode', 'sampler_mode', 'load_library']
 
 
 def load_library():

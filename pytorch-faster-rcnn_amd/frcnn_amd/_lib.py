@@ -25,7 +25,8 @@ SIGNATURES = {
     'frh_inside_mask': (c_i32, [c_vp, c_i64, c_i32, P(c_i32), P(c_i32), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_iou_table': (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     'frh_elem_iou': (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
-    'frh_maxiou_assign_workspace': (c_size, [c_i32, c_i32]),
+    'frh_maxiou_assign_zero_bytes': (c_size, [c_i32, c_i32]),
+    'frh_maxiou_assign_workspace': (c_size, [c_i32, c_i32, c_i64]),
     'frh_maxiou_assign': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
                                   c_f32, c_f32, c_f32, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_size,
                                   c_vp]),
@@ -67,6 +68,7 @@ SIGNATURES = {
     'frh_mcnms_finish': (c_i32, [c_i32, c_i32, c_i64, c_i32, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i32, c_f64,
                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_size, c_vp, c_size, c_vp]),
     'frh_roi_level_map': (c_i32, [c_vp, c_i64, c_f32, c_i32, c_vp, c_vp]),
+    'frh_roi_rows': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i32, P(c_i64), c_f32, c_i32, c_vp, c_vp, c_vp]),
     'frh_roi_align_fwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,
                                   c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_align_bwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,

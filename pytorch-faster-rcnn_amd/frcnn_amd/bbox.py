@@ -13,9 +13,19 @@ from . import ops
 
 class PropBatch(list):
     """Per-image proposal views [4, n_i] that also expose the batched buffer
-    [B, 4, cap] and the device counts they were cut from (RPN output)."""
+    [B, 4, cap] and the device counts they were cut from (RPN output), or the flat
+    [4, sum n_i] buffer they are consecutive column slices of (RCNN targets)."""
     buffer = None
     counts_dev = None
+    flat_buffer = None
+
+
+class FlatList(list):
+    """Per-image views that are consecutive slices (last dimension) of `flat`."""
+
+    def __init__(self, flat):
+        super().__init__()
+        self.flat = flat
 
 
 def _as_batch(props_list, dev):
@@ -46,7 +56,9 @@ def bbox_targets_batched(props_list, gt_bboxes, gt_labels, assigner, sampler, ta
                              lists=ops.sampler_mode() == 'device')
     r = ops.bbox_target_batched(rows, num_rows, gcnt, max_rows, props, pstride, gts, glab,
                                 target_means, target_stds, sampler.max_num)
-    out = {k: [] for k in ('tar_props', 'tar_bbox', 'tar_label', 'tar_param', 'tar_is_gt')}
+    out = {k: FlatList(r[k]) for k in ('tar_bbox', 'tar_label', 'tar_param', 'tar_is_gt')}
+    out['tar_props'] = PropBatch()
+    out['tar_props'].flat_buffer = r['tar_props']  # [4, n]: the images' rows back to back
     off = 0
     for c in r['counts']:
         for k in out:

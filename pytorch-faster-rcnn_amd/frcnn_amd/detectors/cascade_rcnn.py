@@ -53,19 +53,6 @@ class CascadeRCNN(nn.Module):
         if self.with_shared_head:
             self.shared_head.init_weights()
 
-    def _side_stream(self, ref):
-        """A second HIP stream of ref's device for the proposal chain (None on CPU tensors or
-        when frcnn_amd.set_proposal_stream(False))."""
-        from .. import ops
-        if not ref.is_cuda or not ops.PROPOSAL_STREAM['on']:
-            return None
-        key = ref.device.index
-        st = ops.PROPOSAL_STREAM['streams'].get(key)
-        if st is None:
-            st = torch.cuda.Stream(ref.device)
-            ops.PROPOSAL_STREAM['streams'][key] = st
-        return st
-
     def extract_feat(self, x):
         x = self.backbone(x)
         return self.neck(x) if self.with_neck else x
@@ -80,23 +67,10 @@ class CascadeRCNN(nn.Module):
             rpn_cls, rpn_reg = self.rpn_head(feats)
         cfg = self.train_cfg
         rpn_gt_labels = [torch.ones_like(g) for g in gt_labels]
-        # The proposal chain (selection, decode, NMS, merge) and the RPN target / loss chain
-        # both read only the RPN outputs: the proposals run on a side stream, concurrently.
-        side = self._side_stream(rpn_cls[0])
-        if side is not None:
-            main = torch.cuda.current_stream(rpn_cls[0].device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
-        else:
-            props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
+        props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
         l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
         losses['rpn_cls_loss'] = l_cls
         losses['rpn_reg_loss'] = l_reg
-        if side is not None:
-            main.wait_stream(side)
-            for t in (props.buffer, props.counts_dev):  # allocated on the side stream, used on main
-                t.record_stream(main)
         for i in range(self.num_stages):
             head, extractor, scfg = self.rcnn_head[i], self.roi_extractors[i], cfg.rcnn[i]
             tar_props, tar_bboxes, tar_labels, tar_params, tar_is_gts = head.bbox_targets(

@@ -66,17 +66,19 @@ class AnchorHead(nn.Module):
         return out
 
     def _valid_masks(self, anchors, grid_sizes, img_metas, allowed_border):
-        rows = []
+        keys = []
         for m in img_metas:
             img = tuple(int(v) for v in m['img_shape'][:2])
             key = (tuple((int(h), int(w)) for h, w in grid_sizes), img, int(allowed_border), anchors.data_ptr())
-            mk = self._mask_cache.get(key)
-            if mk is None:
+            if key not in self._mask_cache:
                 ins = in_grid_sizes(img, grid_sizes, self.anchor_strides)
-                mk = ops.inside_mask(anchors, grid_sizes, ins, self.num_anchors, img[0], img[1], allowed_border)
-                self._mask_cache[key] = mk
-            rows.append(mk)
-        return torch.stack(rows)
+                self._mask_cache[key] = ops.inside_mask(anchors, grid_sizes, ins, self.num_anchors, img[0], img[1],
+                                                        allowed_border)
+            keys.append(key)
+        bkey = ('batch',) + tuple(keys)  # the [B, N] stack of a batch of image shapes, cached as well
+        if bkey not in self._mask_cache:
+            self._mask_cache[bkey] = torch.stack([self._mask_cache[k] for k in keys])
+        return self._mask_cache[bkey]
 
     # ------------------------------------------------------------ targets
     def targets_batched(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg):
@@ -96,7 +98,10 @@ class AnchorHead(nn.Module):
             sampler = build_module(sampler)
         gts, gcnt, gmax = ops.pack_boxes([g.float() for g in gt_bboxes], dev)
         glab = ops.pack_labels(gt_labels, gmax, dev) if gt_labels is not None else None
-        num = torch.full((B,), N, dtype=torch.int32, device=dev)
+        nkey = ('num', B, N, dev)
+        if nkey not in self._mask_cache:
+            self._mask_cache[nkey] = torch.full((B,), N, dtype=torch.int32, device=dev)
+        num = self._mask_cache[nkey]
         labels, _ = ops.maxiou_assign(anchors, 0, num, N, gts, gcnt, gmax, assigner.pos_iou, assigner.neg_iou,
                                       assigner.min_pos_iou, valid=masks, valid_seg_stride=masks.stride(0))
         r = anchor_targets_batched(labels, num, N, anchors, gts, glab, sampler, self.target_means,
@@ -119,15 +124,14 @@ class AnchorHead(nn.Module):
         dev = tar_cls_out.device
         cls_loss, reg_loss = losses.zero_loss(dev), losses.zero_loss(dev)
         sampling = 'sampler' in train_cfg
-        pos = tar_labels > 0
-        avg_factor = len(tar_labels) if sampling else pos.sum()
+        avg_factor = len(tar_labels) if sampling else (tar_labels > 0).sum()
         if tar_labels.numel() != 0:
             cls_loss = self.loss_cls(tar_cls_out.t(), tar_labels) / avg_factor
             if isinstance(self.loss_bbox, losses.SmoothL1Loss):
                 # fused masked smooth-L1 over the positive columns of [4, S] (one kernel, no sync)
                 reg_loss = self.loss_bbox.masked(tar_reg_out, tar_param, tar_labels, rows_dim=1) / avg_factor
             else:
-                m = pos.view(1, -1)
+                m = (tar_labels > 0).view(1, -1)
                 z = tar_reg_out.new_zeros(())
                 reg_loss = self.loss_bbox(torch.where(m, tar_reg_out, z), torch.where(m, tar_param, z)) / avg_factor
         else:

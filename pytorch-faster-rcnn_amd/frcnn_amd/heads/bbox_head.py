@@ -34,9 +34,8 @@ class BBoxHead(nn.Module):
         """bbox_head.py:56-80."""
         dev = cls_out.device
         cls_loss, reg_loss = losses.zero_loss(dev), losses.zero_loss(dev)
-        pos = tar_label > 0
         n = len(tar_label)
-        avg_factor = pos.sum() if 'sampler' not in train_cfg else n
+        avg_factor = (tar_label > 0).sum() if 'sampler' not in train_cfg else n
         if avg_factor == 0:
             logging.warning('return zero loss due to zero avg_factor')
             return cls_loss, reg_loss
@@ -53,7 +52,7 @@ class BBoxHead(nn.Module):
                 reg_out = reg_out.view(-1, 4, self.num_classes)
                 reg_out = reg_out[torch.arange(n, device=dev), :, tar_label]
             # masked sum over positive rows (see AnchorHead.calc_loss): no host sync
-            m = pos.view(-1, 1)
+            m = (tar_label > 0).view(-1, 1)
             z = reg_out.new_zeros(())
             reg_loss = self.loss_bbox(torch.where(m, reg_out, z), torch.where(m, tar_param.t(), z)) / avg_factor
         return cls_loss, reg_loss
@@ -62,7 +61,9 @@ class BBoxHead(nn.Module):
         flat = getattr(cls_outs, 'flat', None)
         cls_out = flat[0] if flat is not None else torch.cat(cls_outs, 0)
         reg_out = flat[1] if flat is not None else torch.cat(reg_outs, 0)
-        return self.calc_loss_all(cls_out, reg_out, torch.cat(tar_labels), torch.cat(tar_params, 1), train_cfg)
+        tl, tp = getattr(tar_labels, 'flat', None), getattr(tar_params, 'flat', None)  # the targets' own buffers
+        return self.calc_loss_all(cls_out, reg_out, tl if tl is not None else torch.cat(tar_labels),
+                                  tp if tp is not None else torch.cat(tar_params, 1), train_cfg)
 
     def refine_bboxes(self, props, labels, reg_outs, is_gts=None, img_metas=None):
         return utils.multi_apply(self.refine_bboxes_single_image, props, labels, reg_outs,

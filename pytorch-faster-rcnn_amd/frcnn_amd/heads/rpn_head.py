@@ -60,7 +60,6 @@ class RPNHead(AnchorHead):
                  target_stds=(1.0, 1.0, 1.0, 1.0), loss_cls=None, loss_bbox=None):
         self.in_channels = in_channels
         self.feat_channels = feat_channels
-        self.finest_last = True  # level order of forward (same outputs either way)
         super().__init__(num_classes=2, anchor_scales=anchor_scales, anchor_ratios=anchor_ratios,
                          anchor_strides=anchor_strides, anchor_center_lt=anchor_center_lt,
                          target_means=target_means, target_stds=target_stds, loss_cls=loss_cls,
@@ -78,16 +77,8 @@ class RPNHead(AnchorHead):
             init_module_normal(m, mean=0.0, std=0.01)
 
     def forward(self, xs):
-        """rpn_head.py:62-66, one level at a time and the finest level last: each hidden map is
-        read by the 1x1 classifier / regressor while still cache-resident, and P2 (the level
-        ~85 % of the sampled RoIs map to) and its hidden map are the trunk's most recently
-        touched data when the RoI extractor reads P2.  Same outputs as the reference's order."""
-        cls_outs, reg_outs = [None] * len(xs), [None] * len(xs)
-        for i in (reversed(range(len(xs))) if self.finest_last else range(len(xs))):
-            h = self.relu(self.conv(xs[i]))
-            cls_outs[i] = self.classifier(h)
-            reg_outs[i] = self.regressor(h)
-        return cls_outs, reg_outs
+        hidden = [self.relu(self.conv(x)) for x in xs]
+        return [self.classifier(h) for h in hidden], [self.regressor(h) for h in hidden]
 
     def predict_bboxes_from_output(self, cls_outs, reg_outs, img_metas, test_cfg):
         """Returns [props, scores, labels] lists like unpack_multi_result of

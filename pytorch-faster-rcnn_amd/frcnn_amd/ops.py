@@ -84,8 +84,32 @@ def device_ints(vals, device, dtype=torch.int32):
     return t.pin_memory().to(device, non_blocking=True)
 
 
+_PACKED = []  # (inputs, their versions, key, result): the packs of the last few distinct input lists
+
+
+def _memo(inputs, key, make):
+    """A batch's gt boxes / labels are packed once and reused by the RPN and every RCNN stage:
+    hit only for the same tensor objects (held by the entry, so their storage cannot be
+    reused) with unchanged version counters."""
+    vers = tuple(t._version for t in inputs)
+    for ent in _PACKED:
+        if ent[2] == key and len(ent[0]) == len(inputs) and all(a is b for a, b in zip(ent[0], inputs)) \
+                and ent[1] == vers:
+            return ent[3]
+    res = make()
+    _PACKED.insert(0, (tuple(inputs), vers, key, res))
+    del _PACKED[8:]
+    return res
+
+
 def pack_boxes(box_list, device, min_cols=1):
     """list of [4, n_i] -> ([S, 4, n_max] f32, counts int32 device, n_max)."""
+    if all(torch.is_tensor(b) and b.dtype == torch.float32 for b in box_list):
+        return _memo(list(box_list), ('boxes', device, min_cols), lambda: _pack_boxes(box_list, device, min_cols))
+    return _pack_boxes(box_list, device, min_cols)
+
+
+def _pack_boxes(box_list, device, min_cols):
     S = len(box_list)
     nmax = max([int(b.shape[1]) for b in box_list] + [min_cols])
     out = torch.zeros(S, 4, nmax, dtype=torch.float32, device=device)
@@ -97,6 +121,12 @@ def pack_boxes(box_list, device, min_cols=1):
 
 
 def pack_labels(label_list, nmax, device):
+    if all(torch.is_tensor(l) for l in label_list):
+        return _memo(list(label_list), ('labels', device, nmax), lambda: _pack_labels(label_list, nmax, device))
+    return _pack_labels(label_list, nmax, device)
+
+
+def _pack_labels(label_list, nmax, device):
     S = len(label_list)
     out = torch.zeros(S, max(nmax, 1), dtype=torch.int64, device=device)
     for s, l in enumerate(label_list):
@@ -106,6 +136,23 @@ def pack_labels(label_list, nmax, device):
 
 
 # ---------------------------------------------------------------- MaxIoU assignment (a4)
+_ASSIGN_WS = {}
+
+
+def _assign_workspace(dev, S, mg, max_boxes):
+    """One buffer per (device, stream): its leading counters / maxima are zero-filled when
+    the (segments, gts) layout changes; every call leaves them zero."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    need = int(_lib.query('frh_maxiou_assign_workspace', S, mg, max_boxes))
+    layout = (S, mg)
+    ent = _ASSIGN_WS.get(key)
+    if ent is None or ent[1].numel() < need:
+        ent = _ASSIGN_WS[key] = [layout, torch.zeros(need, dtype=torch.uint8, device=dev)]
+    elif ent[0] != layout:
+        ent[1][:int(_lib.query('frh_maxiou_assign_zero_bytes', S, mg))].zero_()
+        ent[0] = layout
+    return ent[1]
+
 def maxiou_assign(boxes, box_seg_stride, num_boxes, max_boxes, gts, gt_counts, max_gts, pos_iou, neg_iou,
                   min_pos_iou, valid=None, valid_seg_stride=0, num_segs=None):
     """Batched MaxIoUAssigner: boxes [.., 4, ld] (segment stride given), gts [S, 4, Gmax]."""
@@ -114,7 +161,7 @@ def maxiou_assign(boxes, box_seg_stride, num_boxes, max_boxes, gts, gt_counts, m
     dev = boxes.device
     labels = torch.empty(S, max(max_boxes, 1), dtype=torch.int64, device=dev)
     max_iou = torch.empty(S, max(max_boxes, 1), dtype=torch.float32, device=dev)
-    ws = workspace(_lib.query('frh_maxiou_assign_workspace', S, max(max_gts, 1)), dev)
+    ws = _assign_workspace(dev, S, max(max_gts, 1), max_boxes)
     call('frh_maxiou_assign', S, ptr(boxes), boxes.stride(-2), box_seg_stride, ptr(num_boxes),
          ptr(valid), valid_seg_stride, ptr(gts), gts.stride(1), gts.stride(0), ptr(gt_counts),
          float(pos_iou), float(neg_iou), float(min_pos_iou), ptr(labels), labels.stride(0), ptr(max_iou),
@@ -389,15 +436,6 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
 
 NMS_PROFILE = {'on': False, 'records': []}
 
-# CascadeRCNN.forward_train runs the RPN proposal chain on a side stream of the device,
-# concurrently with the RPN target / loss chain (one stream per device, created on first use).
-PROPOSAL_STREAM = {'on': True, 'streams': {}}
-
-
-def set_proposal_stream(on):
-    PROPOSAL_STREAM['on'] = bool(on)
-
-
 def nms_bytes(counts, kept):
     """Algorithmic bytes of one segmented NMS call: per segment of N boxes
     20*N + 16*N*ceil(N/64) + 8*K_keep (boxes + scores read, 64-bit mask written and read once)."""
@@ -499,6 +537,23 @@ def multiclass_nms_batched(boxes, scores, nms_channel, nms_iou, min_score=-1, ma
 
 
 # ---------------------------------------------------------------- RoI level map + RoIAlign (a13/a14)
+def roi_rows(boxes, counts, finest_scale, num_levels, seg_stride=0, flat=True):
+    """RoI rows [K, 5] (image, x1, y1, x2, y2) + levels ([K] int64, None for one level) of the
+    images' boxes (frh_roi_rows): `boxes` [4, ld] with image b's boxes at columns
+    offsets[b]... (flat) or [B, 4, cap] with image b's at boxes[b, :, :counts[b]]."""
+    _need_cuda(boxes)
+    K = int(sum(counts))
+    dev = boxes.device
+    rois = torch.empty(K, 5, dtype=torch.float32, device=dev)
+    lv = torch.empty(K, dtype=torch.int64, device=dev) if num_levels > 1 else None
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + int(c))
+    call('frh_roi_rows', len(counts), ptr(boxes), boxes.stride(-2), seg_stride, int(bool(flat)), i64_array(offs),
+         float(finest_scale), int(num_levels), ptr(rois), ptr(lv), stream_of(boxes))
+    return rois, lv
+
+
 def roi_level_map(rois, finest_scale, num_levels):
     _need_cuda(rois)
     rois = _f32(rois).contiguous()
@@ -733,6 +788,16 @@ def bn_act(x, bn, skip=None, relu=True):
 
 # ---------------------------------------------------------------- f1: fused losses
 CLS_FOCAL, CLS_SIGMOID_BCE, CLS_SOFTMAX_CE = 0, 1, 2
+_LOSS_WS = {}
+
+
+def _loss_workspace(x):
+    """Zero-filled once per (device, stream): each forward call leaves its arrival counter zero."""
+    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
+    ws = _LOSS_WS.get(key)
+    if ws is None:
+        ws = _LOSS_WS[key] = torch.zeros(int(_lib.query('frh_loss_workspace')), dtype=torch.uint8, device=x.device)
+    return ws
 
 
 class _ClsLoss(torch.autograd.Function):
@@ -741,7 +806,7 @@ class _ClsLoss(torch.autograd.Function):
         n, c = x.shape
         tfloat = int(target.dtype == torch.float32)
         out = torch.empty((), dtype=torch.float32, device=x.device)
-        ws = workspace(_lib.query('frh_loss_workspace'), x.device)
+        ws = _loss_workspace(x)
         call('frh_cls_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
              float(gamma), ptr(out), ptr(ws), ws.numel(), stream_of(x))
         ctx.save_for_backward(x, target)
@@ -779,7 +844,7 @@ class _SmoothL1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, label, xs, ys, n, m, n_sel, beta):
         out = torch.empty((), dtype=torch.float32, device=x.device)
-        ws = workspace(_lib.query('frh_loss_workspace'), x.device)
+        ws = _loss_workspace(x)
         call('frh_smooth_l1_fwd', ptr(x), xs[0], xs[1], xs[2], ptr(y), ys[0], ys[1], ptr(label), n, m, n_sel,
              float(beta), ptr(out), ptr(ws), ws.numel(), stream_of(x))
         ctx.save_for_backward(x, y, label)

@@ -124,11 +124,7 @@ class BasicRoIExtractor(nn.Module):
         counts = [int(r.shape[1]) for r in rois_list]
         dev = level_feats[0].device
         if self._fusable():
-            boxes = torch.cat([r.float() for r in rois_list], 1) if rois_list else torch.zeros(4, 0, device=dev)
-            bidx = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.float32),
-                                           ops.device_ints(counts, dev, torch.int64), output_size=sum(counts))
-            rois = torch.cat([bidx.view(1, -1), boxes], 0).t().contiguous()
-            levels = ops.roi_level_map(rois, self.finest_scale, n_lvls) if n_lvls > 1 else None
+            rois, levels = self._rows(rois_list, counts, n_lvls, dev)
             first = self.roi_layers[0]
             out = ops.roi_align_multilevel(list(level_feats[:n_lvls]), rois, levels,
                                            [l.spatial_scale for l in self.roi_layers], first.output_size,
@@ -142,6 +138,23 @@ class BasicRoIExtractor(nn.Module):
             off += c
         res.flat = out
         return res
+
+    def _rows(self, rois_list, counts, n_lvls, dev):
+        """(image, box) rows + levels in one kernel (frh_roi_rows), reading the RCNN targets'
+        flat buffer or the RPN's batched proposal buffer in place when the list carries one."""
+        if not 0 < len(counts) <= 64:
+            boxes = torch.cat([r.float() for r in rois_list], 1) if rois_list else torch.zeros(4, 0, device=dev)
+            bidx = torch.repeat_interleave(torch.arange(len(counts), device=dev, dtype=torch.float32),
+                                           ops.device_ints(counts, dev, torch.int64), output_size=sum(counts))
+            rois = torch.cat([bidx.view(1, -1), boxes], 0).t().contiguous()
+            return rois, (ops.roi_level_map(rois, self.finest_scale, n_lvls) if n_lvls > 1 else None)
+        flat = getattr(rois_list, 'flat_buffer', None)
+        if flat is not None and flat.dtype == torch.float32:
+            return ops.roi_rows(flat, counts, self.finest_scale, n_lvls)
+        buf = getattr(rois_list, 'buffer', None)
+        if buf is not None and buf.dtype == torch.float32 and buf.dim() == 3:
+            return ops.roi_rows(buf, counts, self.finest_scale, n_lvls, seg_stride=buf.stride(0), flat=False)
+        return ops.roi_rows(torch.cat([r.float() for r in rois_list], 1), counts, self.finest_scale, n_lvls)
 
     def _forward_per_level(self, level_feats, rois_list, counts):
         # generic path for non-RoIAlign layers (e.g. RoIPool): per level, all images at once

@@ -127,6 +127,39 @@ def test_assign_ties_and_nan_free_edges(dev):
         np.testing.assert_array_equal(miou.cpu().numpy(), ri)
 
 
+def test_assign_one_launch_handoff_cases(dev):
+    """The single-launch assignment's hand-off: boxes tied at a gt's maximum in many
+    workgroups (the last workgroup labels them), a gt no box overlaps with min_pos_iou 0
+    (every box a candidate: the whole segment goes through the hand-off), a segment with no
+    gts and an empty segment in the same launch, and the same workspace reused (its
+    counters must come back zero)."""
+    from frcnn_amd import ops
+    gts = np.array([[10, 10, 50, 50], [100, 100, 140, 180], [9000, 9000, 9050, 9050]], np.float32).T
+    n = 20000
+    boxes = inputs.random_boxes(8, n)
+    for pos in (3, 300, 301, 700, 5000, 12345, 19999):  # one gt's exact copy in many workgroups
+        boxes[:, pos] = gts[:, pos % 2]
+    segs = [(boxes, gts), (boxes[:, :9000], gts[:, :2]), (boxes[:, :5000], gts[:, :0]), (boxes[:, :0], gts)]
+    S = len(segs)
+    bb = torch.zeros(S, 4, n, device=dev)
+    for s, (b, _) in enumerate(segs):
+        bb[s, :, :b.shape[1]] = T(b, dev)
+    num = torch.tensor([b.shape[1] for b, _ in segs], dtype=torch.int32, device=dev)
+    gb, gc, gm = ops.pack_boxes([T(g, dev) for _, g in segs], dev)
+    for thr in ((0.7, 0.3, 0.3), (0.5, 0.4, 0.0), (0.5, 0.5, 0.5), (0.7, 0.3, 0.3)):
+        labels, miou = ops.maxiou_assign(bb, bb.stride(0), num, n, gb, gc, gm, *thr)
+        for s, (b, g) in enumerate(segs):
+            k = b.shape[1]
+            if k == 0:
+                continue
+            if g.shape[1] == 0:
+                assert bool((labels[s, :k] == -1).all()) and bool((miou[s, :k] == 0).all())
+                continue
+            rl, ri = oracle.maxiou_assign(b, g, *thr)
+            np.testing.assert_array_equal(labels[s, :k].cpu().numpy(), rl)
+            np.testing.assert_array_equal(miou[s, :k].cpu().numpy(), ri)
+
+
 # ----------------------------------------------------------------- a5/a6 anchor targets (numpy-parity sampler)
 def test_anchor_target_single_image_vs_reference(dev, golden):
     from frcnn_amd import anchor as A
@@ -518,6 +551,33 @@ def test_roi_level_map(dev, golden):
     r = g['rois']
     r5 = np.concatenate([np.zeros((1, r.shape[1]), np.float32), r], 0).T.copy()
     np.testing.assert_array_equal(ops.roi_level_map(T(r5, dev), 56, 4).cpu().numpy(), g['levels'])
+
+
+def test_roi_rows_flat_and_batched(dev, golden):
+    """frh_roi_rows: the (image, box) rows and levels of three images' boxes from a flat
+    [4, sum n] buffer and from a padded [B, 4, cap] buffer (including an empty image) equal
+    the reference's per-image index column + concatenation, and the level fixture."""
+    from frcnn_amd import ops
+    g = golden('levels.npz')
+    r = g['rois']
+    n = r.shape[1]
+    counts = [n // 3, 0, n - n // 3]
+    bidx = np.repeat(np.arange(3, dtype=np.float32), counts)
+    want = np.concatenate([bidx[None], r], 0).T
+    rois, lv = ops.roi_rows(T(r, dev), counts, 56, 4)
+    np.testing.assert_array_equal(rois.cpu().numpy(), want)
+    np.testing.assert_array_equal(lv.cpu().numpy(), g['levels'])
+    cap = max(counts) + 5
+    buf = torch.full((3, 4, cap), 7.0, device=dev)
+    off = 0
+    for b, c in enumerate(counts):
+        buf[b, :, :c] = T(r[:, off:off + c], dev)
+        off += c
+    rois2, lv2 = ops.roi_rows(buf, counts, 56, 4, seg_stride=buf.stride(0), flat=False)
+    np.testing.assert_array_equal(rois2.cpu().numpy(), want)
+    np.testing.assert_array_equal(lv2.cpu().numpy(), g['levels'])
+    rois1, lv1 = ops.roi_rows(T(r, dev), [n], 56, 1)
+    assert lv1 is None and np.array_equal(rois1.cpu().numpy()[:, 1:], r.T)
 
 
 def _rois(seed, n, batch):

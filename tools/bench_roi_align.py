@@ -50,8 +50,8 @@ def calibrate(variants, dev, small=False):
 
 
 def stamps_report(stm):
-    """Per-item stamps [start, setup done, first stage landed, end, D, cells, roi, xcd]
-    (s_memrealtime, 100 MHz)."""
+    """Per-item stamps [start, setup done, first stage landed, end, D, cells, RoI record
+    landed, xcd] (s_memrealtime, 100 MHz)."""
     stm = stm[stm[:, 0] > 0]
     t0 = stm[:, 0].min()
     span = (stm[:, 3].max() - t0) / 100.0
@@ -59,8 +59,9 @@ def stamps_report(stm):
     pc = lambda a: np.percentile(a / 100.0, [50, 90, 99]).round(2).tolist()  # noqa: E731
     for D in sorted(set(stm[:, 4].tolist())):
         x = stm[stm[:, 4] == D]
-        print('  D={} waves {:5d}: setup {} land {} eval+rest {} life {}'.format(
-            D, len(x), pc(x[:, 1] - x[:, 0]), pc(x[:, 2] - x[:, 1]), pc(x[:, 3] - x[:, 2]), pc(x[:, 3] - x[:, 0])))
+        print('  D={} waves {:5d}: fetch {} taps {} land {} eval+rest {} life {}'.format(
+            D, len(x), pc(x[:, 6] - x[:, 0]), pc(x[:, 1] - x[:, 6]), pc(x[:, 2] - x[:, 1]), pc(x[:, 3] - x[:, 2]),
+            pc(x[:, 3] - x[:, 0])))
     alive = np.zeros(int(span) + 1)
     for a, b in zip((stm[:, 0] - t0) / 100.0, (stm[:, 3] - t0) / 100.0):
         alive[int(a):int(b) + 1] += 1
@@ -75,6 +76,8 @@ def main():
     ap.add_argument('--variants', default='0')
     ap.add_argument('--rounds', type=int, default=1)
     ap.add_argument('--cold', action='store_true')
+    ap.add_argument('--after-write', action='store_true',
+                    help='also time each launch right after the features are rewritten in place (x *= 1)')
     ap.add_argument('--calib', action='store_true')
     ap.add_argument('--calib-small', action='store_true')
     ap.add_argument('--dump', help='save the RoIs / levels / level shapes of the recorded launch to this .npz')
@@ -143,6 +146,22 @@ def main():
                 torch.cuda.synchronize()
                 arms.append(e0.elapsed_time(e1) * 1e3)
             cold = (arms[0] - arms[1]) / args.iters
+        aw = None
+        if args.after_write:  # does the Infinity Cache keep lines the trunk has just written?
+            arms = []
+            for with_launch in (True, False):
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(args.iters):
+                    for f in feats:
+                        f.mul_(1.0)
+                    if with_launch:
+                        launch()
+                e1.record()
+                torch.cuda.synchronize()
+                arms.append(e0.elapsed_time(e1) * 1e3)
+            aw = (arms[0] - arms[1]) / args.iters
+            print('variant {:>3}: after a rewrite of the features {:7.2f} us'.format(v, aw), flush=True)
         summary.setdefault(v, []).append((warm, cold))
         if v in STAMPED:
             stamps_report(full[K * C * ph * pw:].view(torch.int64).view(-1, 8).cpu().numpy())
