@@ -53,12 +53,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # in-step kernel groups of the detection path (substrings of the dispatched kernel names)
 KERNEL_GROUPS = [
-    ('roi_align_fwd', ('roi_align_fwd',)),
+    ('roi_align_fwd', ('roi_align_fwd', 'roi_align_pair_desc')),
     ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
     ('proposals', ('rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
     ('sampler', ('sampler_', 'chunk_count', 'chunk_write_lists')),
-    ('targets', ('anchor_target_kernel', 'bbox_target_kernel', 'prepend_gt', 'gather_levels', 'roi_level')),
+    ('targets', ('anchor_target', 'bbox_target', 'prepend_gt', 'gather_levels', 'roi_level', 'roi_rows')),
     ('losses', ('cls_loss', 'smooth_l1', 'loss_finalize')),
 ]
 
@@ -136,6 +136,11 @@ def kernel_trace(step, n, dev):
     return [(name, float(us)) for _, name, us in ks], None
 
 
+def kernel_short(name):
+    """Kernel name without its return type and parameter list."""
+    return name.replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '')
+
+
 def group_of(name):
     for g, keys in KERNEL_GROUPS:
         if any(k in name for k in keys):
@@ -153,12 +158,12 @@ def summarise_trace(trace, steps):
     for name, us in trace:
         if 'frh::' in name and 'bn_act' not in name:
             det += us
-            short = name.split('(')[0].replace('void ', '')
+            short = kernel_short(name)
             det_k[short] = det_k.get(short, 0.0) + us
         g = group_of(name)
         if g:
             per[g] += us
-            short = name.split('(')[0].replace('void ', '')
+            short = kernel_short(name)
             names[g][short] = names[g].get(short, 0) + 1
     return ({g: v / steps for g, v in per.items()}, det / steps,
             {g: {k: c // steps for k, c in d.items()} for g, d in names.items()},
@@ -472,9 +477,14 @@ def main():
         nrecs = list(ops.NMS_PROFILE['records'])
         per_group, det_us, group_names, det_kernels = (summarise_trace(trace, steps_traced) if trace else
                                                         ({}, None, {}, {}))
+        # one forward call = the descriptor launch (frh_roi_align_fwd_ws) + the pair kernel
         roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]
-        roi_in_step = float(np.mean([us for _, us in roi_launches])) if roi_launches else None
-        roi_kernel = roi_launches[0][0].split('(')[0].replace('void ', '') if roi_launches else None
+        roi_desc = [us for n, us in (trace or []) if 'roi_align_pair_desc' in n]
+        roi_in_step = (float(np.sum([us for _, us in roi_launches]) + np.sum(roi_desc)) / len(roi_launches)
+                       if roi_launches else None)
+        roi_kernel = kernel_short(roi_launches[0][0]) if roi_launches else None
+        if roi_kernel and roi_desc:
+            roi_kernel = 'frh::roi_align_pair_desc_kernel + ' + roi_kernel
         warm, cold = roi_align_replays(recs, dev)
         avg_bytes = float(np.mean([roi_align_bytes(r) for r in recs])) if recs else None
         us_for_frac = roi_in_step if roi_in_step else warm
@@ -518,7 +528,8 @@ def main():
                 'avg_launch_us_in_step': roi_in_step, 'avg_launch_us_replay_warm': warm,
                 'avg_launch_us_replay_cold': cold,
                 'timing': ('in-step device durations from the ROCm kernel tracer (torch.profiler) over {} steps '
-                           'after the timed region'.format(steps_traced) if roi_in_step else
+                           'after the timed region, per forward call (descriptor launch + pair kernel)'.format(
+                               steps_traced) if roi_in_step else
                            'kernel tracer unavailable ({}): back-to-back replay, warm caches'.format(trace_err)) +
                           '; replay_warm = the same launches back to back, replay_cold = each after a 768 MB read '
                           '(L2 + Infinity Cache evicted); traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '
@@ -544,9 +555,9 @@ def main():
                              for s in model.rpn_head.anchor_strides])
                 n_in = 130833  # inside anchors of a 600x1000 image at cfg2 (tests pin the mask)
                 assign_trace = [(n, us) for n, us in trace if 'assign_' in n]
-                per_call = len(assign_trace) // steps_traced  # RPN call first, then the RCNN call(s)
-                rpn_assign = (sum(sum(us for _, us in assign_trace[i * per_call:i * per_call + 2])
-                                  for i in range(steps_traced)) / steps_traced) if per_call >= 2 else None
+                per_step = len(assign_trace) // steps_traced  # one launch per call: the RPN's first
+                rpn_assign = (sum(assign_trace[i * per_step][1] for i in range(steps_traced)) / steps_traced
+                              if per_step >= 1 else None)
                 lines['assign_rpn'] = line(rpn_assign, B * (16 * n_all + n_all + 12 * n_in),
                                            '16*N_all + N_all + 12*N_in per image (SURVEY §8(d)), RPN anchors')
                 lines['assign_all'] = {'us_per_step': per_group.get('assign'), 'note': 'RPN + RCNN assignment'}

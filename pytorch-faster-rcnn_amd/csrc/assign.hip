@@ -150,6 +150,10 @@ __device__ void label_candidates(const AssignArgs& p, int s, int G, const float4
   }
 }
 
+// R boxes per thread (box base + r * 256 + tid: coalesced): 4 for anchor sets, so a
+// workgroup pays its gt staging and its arrival once per 1024 boxes; 1 for a few
+// thousand proposals, which need the workgroups more
+template <int R>
 __global__ void __launch_bounds__(kAssignThreads) maxiou_assign_kernel(AssignArgs p) {
   __shared__ float4 sg[kMaxGts];
   __shared__ uint32_t scol[kMaxGts];  // this workgroup's per-gt maxima (keys); later the final maxima
@@ -158,25 +162,40 @@ __global__ void __launch_bounds__(kAssignThreads) maxiou_assign_kernel(AssignArg
   const int s = blockIdx.y;
   const int n = p.num_boxes[s];
   const int G = p.num_gts[s];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool any = (int64_t)blockIdx.x * blockDim.x < n && G > 0;  // uniform per block
+  const int64_t base = (int64_t)blockIdx.x * (kAssignThreads * R) + threadIdx.x;
+  const bool any = (int64_t)blockIdx.x * (kAssignThreads * R) < n && G > 0;  // uniform per block
   if (any) {
     load_gts(p, s, G, sg);
     for (int j = threadIdx.x; j < G; j += blockDim.x) scol[j] = 0u;
   }
   if (threadIdx.x == 0) nnear = 0;
+  bool live[R];
+  float4 a[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = base + r * kAssignThreads;
+    live[r] = i < n;
+    if (live[r] && p.valid) live[r] = p.valid[(int64_t)s * p.valid_seg_stride + i] != 0;
+    a[r] = live[r] ? load_box(p, s, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   __syncthreads();
-  bool live = i < n;
-  if (live && p.valid) live = p.valid[(int64_t)s * p.valid_seg_stride + i] != 0;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (live) a = load_box(p, s, i);
-  float m = 0.f;
-  int arg = 0;
+  float m[R];
+  int arg[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) m[r] = 0.f, arg[r] = 0;
   if (any) {
     for (int j = 0; j < G; ++j) {
-      const float v = iou_box(a, sg[j]);
-      if (live) row_step(j, v, m, arg);
-      const uint32_t key = wave_max_u32(live ? float_key(v) : 0u);
+      const float4 g = sg[j];
+      uint32_t key = 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float v = iou_box(a[r], g);
+        if (live[r]) {
+          row_step(j, v, m[r], arg[r]);
+          key = max(key, float_key(v));
+        }
+      }
+      key = wave_max_u32(key);
       if (lane_id() == 0 && key) atomicMax(&scol[j], key);
     }
   }
@@ -186,32 +205,41 @@ __global__ void __launch_bounds__(kAssignThreads) maxiou_assign_kernel(AssignArg
     for (int j = threadIdx.x; j < G; j += blockDim.x) {
       const uint32_t k = scol[j];
       if (!k) continue;
-      if (k > __hip_atomic_load(cm + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cm + j, k);
+      atomicMax(cm + j, k);
       if (key_float(k) >= p.min_pos_iou) snear[atomicAdd(&nnear, 1)] = j;
     }
   }
   __syncthreads();
   // candidates: ties of this workgroup's maximum of a gt that reaches min_pos_iou
-  bool cand = false;
-  if (live) {
-    for (int t = 0; t < nnear && !cand; ++t) {
-      const int j = snear[t];
-      cand = iou_box(a, sg[j]) == key_float(scol[j]);
-    }
+  bool cand[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    cand[r] = false;
+    if (live[r])
+      for (int t = 0; t < nnear && !cand[r]; ++t) {
+        const int j = snear[t];
+        cand[r] = iou_box(a[r], sg[j]) == key_float(scol[j]);
+      }
+    const int slot = wave_append(cand[r], p.state + 4 * s + 1);
+    if (cand[r])
+      __hip_atomic_store(p.cand + (int64_t)s * p.cand_ld + slot, (int32_t)(base + r * kAssignThreads),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const int slot = wave_append(cand, p.state + 4 * s + 1);
-  if (cand) {
-    __hip_atomic_store(p.cand + (int64_t)s * p.cand_ld + slot, (int32_t)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (i < n) {
-    p.labels[(int64_t)s * p.label_seg_stride + i] = (live && G > 0) ? threshold_label(p, m, arg) : -1;
-    if (p.max_iou) p.max_iou[(int64_t)s * p.iou_seg_stride + i] = (live && G > 0) ? m : 0.0f;
-  }
-  // arrival: every wave drains its stores, then one lane adds for the workgroup
+  // arrival: every wave drains its list entries and maxima, then one lane adds for the
+  // workgroup; the labels of the other boxes (which no other workgroup touches) go after it
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
     last = __hip_atomic_fetch_add(p.state + 4 * s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
            (int)gridDim.x - 1;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = base + r * kAssignThreads;
+    if (cand[r] || i >= n) continue;
+    const bool lab = live[r] && G > 0;
+    p.labels[(int64_t)s * p.label_seg_stride + i] = lab ? threshold_label(p, m[r], arg[r]) : -1;
+    if (p.max_iou) p.max_iou[(int64_t)s * p.iou_seg_stride + i] = lab ? m[r] : 0.0f;
+  }
   __syncthreads();
   if (!last) return;
   if (!any && G > 0) load_gts(p, s, G, sg);  // the last workgroup may be one past the boxes
@@ -281,7 +309,12 @@ extern "C" int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64
                gt_seg_stride, num_gts, pos_iou, neg_iou, min_pos_iou, labels, label_seg_stride,
                max_iou, iou_seg_stride, reinterpret_cast<uint32_t*>(ws + zs), reinterpret_cast<int32_t*>(ws),
                reinterpret_cast<int32_t*>(ws + assign_zero_bytes(num_segs, mg)), max_boxes, mg};
-  dim3 grid((unsigned)((max_boxes + kAssignThreads - 1) / kAssignThreads), (unsigned)num_segs);
-  hipLaunchKernelGGL(maxiou_assign_kernel, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
+  if (max_boxes >= 32768) {
+    const dim3 grid((unsigned)((max_boxes + 4 * kAssignThreads - 1) / (4 * kAssignThreads)), (unsigned)num_segs);
+    hipLaunchKernelGGL(maxiou_assign_kernel<4>, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
+  } else {
+    const dim3 grid((unsigned)((max_boxes + kAssignThreads - 1) / kAssignThreads), (unsigned)num_segs);
+    hipLaunchKernelGGL(maxiou_assign_kernel<1>, grid, dim3(kAssignThreads), 0, as_stream(stream), p);
+  }
   return check_launch("frh_maxiou_assign");
 }

@@ -279,12 +279,17 @@ struct MergeArgs {
 // (score desc) order, so the rank of survivor j of level l among all levels
 // (score desc, concatenation order on ties) is j + sum over other levels of
 // a binary search (upper bound for earlier levels, lower bound for later).
-// Grid: (survivor chunks of 256, level, image); no sort, no LDS.
+// Grid: (survivor chunks of 256, level, image); no sort.  kLds: the image's
+// survivor scores of every level are gathered into LDS first (L * P floats,
+// two memory round trips), so the searches are LDS reads instead of chains of
+// dependent global loads.
 __device__ __forceinline__ float kept_score(const MergeArgs& p, int seg, int j) {
   return p.sel_scores[(int64_t)seg * p.P + p.keep[(int64_t)seg * p.P + j]];
 }
 
+template <bool kLds>
 static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
+  extern __shared__ float ms[];  // kLds: [L][P] survivor scores of image b
   const int b = blockIdx.z, l = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int seg = b * p.L + l;
@@ -297,6 +302,14 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
   }
   const bool cut = p.max_num > 0 && total > p.max_num;
   if (blockIdx.x == 0 && threadIdx.x == 0 && l == 0) p.out_counts[b] = cut ? p.max_num : total;
+  if (kLds && cut) {
+    for (int q = 0; q < p.L; ++q) {
+      const int oseg = b * p.L + q, c = p.keep_count[oseg];
+      for (int i = threadIdx.x; i < c; i += blockDim.x)
+        ms[q * p.P + i] = p.sel_scores[(int64_t)oseg * p.P + p.keep[(int64_t)oseg * p.P + i]];
+    }
+    __syncthreads();
+  }
   if (j >= cnt) return;
   const int pos = p.keep[(int64_t)seg * p.P + j];
   const float s = p.sel_scores[(int64_t)seg * p.P + pos];
@@ -310,7 +323,7 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
       // count of survivors of level q ordered before (s, this level)
       while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        float o = kept_score(p, oseg, mid);
+        float o = kLds ? ms[q * p.P + mid] : kept_score(p, oseg, mid);
         bool before = q < l ? (o >= s) : (o > s);
         if (before)
           lo = mid + 1;
@@ -481,6 +494,10 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};
   dim3 mg((unsigned)((post + 255) / 256), (unsigned)num_levels, (unsigned)num_imgs);
-  hipLaunchKernelGGL(rpn_merge_kernel, mg, dim3(256), 0, st, mp);
+  const size_t merge_lds = (size_t)num_levels * z.P * sizeof(float);
+  if (merge_lds <= 65536)
+    hipLaunchKernelGGL(rpn_merge_kernel<true>, mg, dim3(256), merge_lds, st, mp);
+  else
+    hipLaunchKernelGGL(rpn_merge_kernel<false>, mg, dim3(256), 0, st, mp);
   return check_launch("rpn_merge");
 }

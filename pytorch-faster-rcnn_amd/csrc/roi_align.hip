@@ -17,8 +17,8 @@
 // roi_align_bwd_kernel (per-tap atomics, any shape).
 // Feature tensors are addressed through explicit (batch, channel, y, x) element
 // strides: NCHW, channels_last and strided views (FPN P6 = P5[..., ::2, ::2]) all
-// run.  The losing / diagnostic variants measured along the way live in the
-// tools-only library (tools/csrc/roi_variants.hip).
+// run.  The forward laboratory (stamped builds, candidate kernels) is the tools-only
+// library (tools/csrc/roi_lab.hip).
 #include "roi_kernels.h"
 
 namespace frh {
@@ -123,14 +123,11 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
   if (pair_ok(f, channels, pooled_h, pooled_w)) {
-    // chunk-major XCD order (kOrder 1), nt output stores, ONE slab buffer per wave (kSingle:
-    // 6.5 KB of LDS, so 16 resident waves per CU instead of 11 -- the register count caps it
-    // there; 37.2 vs 40.9 us on the cfg2 RoIs, tools/bench_roi_align.py variants 47 / 21), and
-    // the lean tap state (kLean: 95 VGPRs, so 20 resident waves per CU; variant 55)
+    // chunk-major XCD order, nt output stores, one 6.5 KB slab per wave, lean tap state
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kPairWave, kPairHalf, 1, kCpolNT, 0, false, true, 1, true, 1, true>),
-                       dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave), 0, as_stream(stream), lv, c, out);
+    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kCpolNT, false>), dim3((unsigned)(8 * ((total + 7) / 8))),
+                       dim3(kWave), 0, as_stream(stream), lv, c, out);
   } else if (f.lds) {
     const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
     hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);

@@ -10,10 +10,6 @@
 
 #include "roi_common.h"
 
-#ifndef FRH_ONLY8
-#define FRH_ONLY8 0
-#endif
-
 namespace frh {
 
 constexpr int kRoiThreads = 256;
@@ -401,27 +397,30 @@ roi_align_fwd_lds_kernel(RoiLevels lv, RoiCfg c,
 
 
 // ---------------------------------------------------------------------------
-// Channel-pair forward (the default).  One wave per (RoI, 2 * kPW channels), lane =
-// bin.  The RoI's tap grid is staged into the wave's LDS slab by 4-B LDS-DMA
-// with the two channels of a pair interleaved ([cell][2]), so every tap of a
-// bin is ONE aligned ds_read_b64 (2 LDS cycles per wave-instruction, twice the
-// bytes of ds_read_b32) and the bilinear sums run as packed f32 (v_pk_mul_f32
-// / v_pk_add_f32) on both channels at once -- halving the two per-output
-// costs (LDS tap reads, VALU) that bound the per-RoI kernels.  Each slab
-// dimension is either the dense tap window [y0, y1] (at most 4*ph rows) or the
-// list of the 2*ph samples' (lo, hi) taps, so every RoI fits (<= 28 x 29 cells
-// at 7x7) and large RoIs need no per-bin gather.  A DMA round moves 32
-// consecutive cells of one pair (two feature planes, one or two lines each).
-// The slab is two buffers; a stage is the D pairs (D = 8, 4, 2, 1, as the cell
-// count allows) one buffer holds, and stage s+1 is in flight while stage s is
-// evaluated (counted vmcnt waits); the tap reads of half-sample-row h+1 are in
-// flight while h is summed.  The RoI geometry is set up once per kPW pairs
-// (kPW = 8 measured fastest on the cfg2 RoIs: 45 us vs 62 us at 64 pairs).
+// Channel-pair forward (the default).  One wave per (RoI, 16 channels = 8 channel
+// pairs), lane = bin.  The RoI's tap grid is staged into the wave's LDS slab by 4-B
+// LDS-DMA with the two channels of a pair interleaved ([cell][2]), so every tap of a
+// bin is ONE aligned ds_read_b64 and the bilinear sums run as packed f32
+// (v_pk_mul_f32 / v_pk_add_f32) on both channels at once.  Each slab dimension is
+// either the dense tap window [y0, y1] (at most 4*ph rows) or the list of the 2*ph
+// samples' (lo, hi) taps, so every RoI fits (<= 28 x 29 cells at 7x7) and large RoIs
+// need no per-bin gather.  A DMA round moves 32 consecutive cells of one pair.  ONE
+// slab buffer of kPairHalf dwords per wave (6.5 KB: 20 resident waves per CU, the
+// register count's cap); a stage is the D pairs (D = 8, 4, 2, 1, as the cell count
+// allows) it holds; the tap reads of half-sample-row h+1 are in flight while h is
+// summed.  Lean tap state: per-sample weight factors and tap bases, the 16 weights
+// and addresses rebuilt per half-row behind an opaque copy (95 VGPRs).
 // Invalid samples have zero weights and read cell 0 (finite features: +0, the
 // reference's own 0 * feature term).  Same operation order as torchvision:
 // bit-identical to the other kernels.
+//
+// The per-wave prologue (RoI geometry, tap window, per-bin tap state) is the same for
+// the 16 channel chunks of a RoI and is still recomputed by each: loading it from a
+// per-RoI descriptor written by a first launch measured slower (under
+// this kernel's memory load the descriptor's loads take longer than the ~450
+// instructions they replace).
 constexpr int kPairWave = 8;                    // channel pairs per wave (= workgroup): 16 channels
-constexpr int kPairHalf = 1664;                 // dwords per buffer (13 KB per wave for both)
+constexpr int kPairHalf = 1664;                 // dwords per slab buffer (6.5 KB)
 constexpr int kPairChunk = 2 * kPairWave;       // channels per workgroup
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -444,24 +443,6 @@ __device__ __forceinline__ f32x2 lds_read_b64(uint32_t addr) {
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
   return v;
 }
-// eight ds_read_b64 and their wait in ONE asm statement: no register copy of a value
-// still in flight can be placed between the reads and the wait
-template <int OFF>
-__device__ __forceinline__ void lds_read8_wait(f32x2 (&v)[8], const uint32_t (&a)[8]) {
-  asm volatile(
-      "ds_read_b64 %0, %8 offset:%16\n\t"
-      "ds_read_b64 %1, %9 offset:%16\n\t"
-      "ds_read_b64 %2, %10 offset:%16\n\t"
-      "ds_read_b64 %3, %11 offset:%16\n\t"
-      "ds_read_b64 %4, %12 offset:%16\n\t"
-      "ds_read_b64 %5, %13 offset:%16\n\t"
-      "ds_read_b64 %6, %14 offset:%16\n\t"
-      "ds_read_b64 %7, %15 offset:%16\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "i"(OFF)
-      : "memory");
-}
 template <int N>
 __device__ __forceinline__ void lds_wait(f32x2 (&v)[8]) {
   asm volatile("s_waitcnt lgkmcnt(%8)"
@@ -478,38 +459,35 @@ struct PairLayout {
   static_assert(D * RP + 2 * D < 64, "vmcnt is 6 bits");
 };
 
-// kPW: channel pairs per wave; kHalf: dwords per slab buffer.  kOrder 0: grid
-// (K, chunks); 1: a 1-D grid of 8 * ceil(K * chunks / 8) workgroups in which XCD
-// x (= linear id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item
-// list, so each XCD's L2 holds the feature planes of its own channel chunks.
-// kStAux / kLdAux: cache policy of the output stores / staging loads (cdna.h).
-// kStamp (tools-only timing builds): lane 0 writes 8 int64 per item after the
-// output -- s_memrealtime at start / setup done / first stage landed / end, D, cells,
-// RoI record landed, XCD.
-// kSingle: ONE slab buffer (kHalf dwords): a stage's DMA is issued after the previous
-// stage's evaluation (no overlap inside the wave) for half the LDS per wave, i.e.
-// twice the resident waves (the LDS, not registers, caps the double-buffered kernel).
-// kDynR (kSingle only): a stage issues only the DMA rounds its window needs
-// (ceil(cells / 32)) instead of the region's RP rounds -- the slab region of a pair is
-// sized for the largest window the stage's D admits, most windows need one or two rounds.
-// kWideSt (kSingle only): a stage's outputs go to LDS at obase ([channel][bin]) and leave
-// by 16-B (or 8-B) stores, 4x fewer store instructions than one 4-B store per channel.
-template <int kPW, int kHalf, int kStAux, int kLdAux, bool kStamp, bool kSingle, bool kRA, bool kLean = false,
-          bool kDynR = false, bool kWideSt = false>
-__device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
-                                          int chunk, int64_t item, const RoiRaw& raw, uint32_t sbase,
-                                          int64_t t_start, int lane, uint32_t obase = 0) {
-  static_assert(kSingle || !(kDynR || kWideSt), "dynamic rounds / wide stores need the single slab buffer");
+// The RoI's wave-uniform slab geometry and the feature plane it reads.
+struct PairGeom {
+  int empty;             // no valid sample: every bin is 0
+  int y0, x0, R, Cs, Cs2;
+  int dy, dx;            // dense window rows / columns (else the sample tap lists)
+  int sy, sx, scs;       // feature element strides (row, column, channel)
+  uint32_t inv;          // e / Cs2 == (e * inv) >> 16 for e < 1024
+  uint32_t extent;       // feature bytes addressable from base
+  const float* base;     // image b of the RoI's level
+};
+
+// This lane's share: the slab-row / column source offsets of its tap-list entries and
+// its bin's lean tap state (tap bases relative to the slab start).
+struct PairLane {
+  int rsrc, csrc;
+  float fyh[2], fyl[2], fxh[2], fxl[2];
+  uint32_t tb0[2][2], tdq[2], tdr[2];
+};
+
+__device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c, const RoiRaw& raw, int lane,
+                                           PairGeom& G, PairLane& P) {
   constexpr int SR = 2;
-  int64_t t_setup = 0, t_land = 0;
-  const int64_t t_fetched = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;  // the RoI record has landed
-  const int cw0 = chunk * 2 * kPW;
-  const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
   const RoiGeom g = roi_geom_raw(c, lv, raw);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
   const int nbins = c.ph * c.pw;
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l], scs = (int)lv.sc[l];
+  G.sy = (int)lv.sy[l];
+  G.sx = (int)lv.sx[l];
+  G.scs = (int)lv.sc[l];
   // sample positions (sampling ratio 2: the reference's "/ 2" is an exact halving)
   auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
   auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
@@ -527,77 +505,78 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
   }
   const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
   const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  const bool active = lane < nbins;
-  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)2 * npairs * nbins * 4);
-  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  const int ostep = nbins * 4;
-  if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: all bins 0
-    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
-    return;
-  }
+  G.empty = !(y1 >= y0 && x1 >= x0);
+  G.y0 = y0;
+  G.x0 = x0;
   const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;
-  const int R = dy ? y1 - y0 + 1 : nly, Cs = dx ? x1 - x0 + 1 : nlx;
-  const int Cs2 = Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
-  const int ncell = R * Cs2;
-  const bool small = ncell <= PairLayout<8, kHalf>::kCells;
+  G.dy = dy;
+  G.dx = dx;
+  G.R = dy ? y1 - y0 + 1 : nly;
+  G.Cs = dx ? x1 - x0 + 1 : nlx;
+  G.Cs2 = G.Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
   // feature byte offsets of slab row / column `lane`
-  const int rsrc = (dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * sy * 4;
-  const int csrc = (dx ? x0 + min(lane, Cs - 1) : (xcol >= 0 ? xcol : x0)) * sx * 4;
-  // this lane's bin: weights (zero for invalid samples) and LDS addresses of its 16 taps
-  const int bin = active ? lane : 0;
+  P.rsrc = (dy ? y0 + min(lane, G.R - 1) : (yrow >= 0 ? yrow : y0)) * G.sy * 4;
+  P.csrc = (dx ? x0 + min(lane, G.Cs - 1) : (xcol >= 0 ? xcol : x0)) * G.sx * 4;
+  // this lane's bin: per-sample factors (zeroed for invalid samples: the same products, or +0)
+  // and tap bases + row / column deltas
+  const int bin = lane < nbins ? lane : 0;
   const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  const uint32_t lbase = sbase;
-  float wt[SR][SR][4];
-  uint32_t ta[SR][SR][4];
 #pragma unroll
   for (int iy = 0; iy < SR; ++iy) {
     const Tap a = make_tap(pos_y(py, iy), H);
+    P.fyh[iy] = a.valid ? a.h : 0.f;
+    P.fyl[iy] = a.valid ? a.l : 0.f;
     const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
+    P.tdr[iy] = 8u * (uint32_t)((r1 - r0) * G.Cs2);
 #pragma unroll
     for (int ix = 0; ix < SR; ++ix) {
       const Tap b = make_tap(pos_x(px, ix), W);
       const int q0 = dx ? b.lo - x0 : 2 * (px * SR + ix), q1 = dx ? b.hi - x0 : 2 * (px * SR + ix) + 1;
-      const bool ok = a.valid && b.valid;
-      wt[iy][ix][0] = ok ? a.h * b.h : 0.f;
-      wt[iy][ix][1] = ok ? a.h * b.l : 0.f;
-      wt[iy][ix][2] = ok ? a.l * b.h : 0.f;
-      wt[iy][ix][3] = ok ? a.l * b.l : 0.f;
-      ta[iy][ix][0] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q0) : 0u);
-      ta[iy][ix][1] = lbase + (ok ? 8u * (uint32_t)(r0 * Cs2 + q1) : 0u);
-      ta[iy][ix][2] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q0) : 0u);
-      ta[iy][ix][3] = lbase + (ok ? 8u * (uint32_t)(r1 * Cs2 + q1) : 0u);
-    }
-  }
-  // kLean: the 16 weights and 16 tap addresses rebuilt per half-row from per-sample factors
-  // (a.h, a.l, b.h, b.l zeroed for invalid samples: the same products, or +0) and
-  // per-sample bases + row / column deltas -- 16 registers instead of 32
-  float fyh[SR], fyl[SR], fxh[SR], fxl[SR];
-  uint32_t tb0[SR][SR], tdq[SR], tdr[SR];
-  if constexpr (kLean) {
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy) {
-      const Tap a = make_tap(pos_y(py, iy), H);
-      fyh[iy] = a.valid ? a.h : 0.f;
-      fyl[iy] = a.valid ? a.l : 0.f;
-      const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
-      tdr[iy] = 8u * (uint32_t)((r1 - r0) * Cs2);
-#pragma unroll
-      for (int ix = 0; ix < SR; ++ix) {
-        const Tap b = make_tap(pos_x(px, ix), W);
-        const int q0 = dx ? b.lo - x0 : 2 * (px * SR + ix), q1 = dx ? b.hi - x0 : 2 * (px * SR + ix) + 1;
-        if (iy == 0) {
-          fxh[ix] = b.valid ? b.h : 0.f;
-          fxl[ix] = b.valid ? b.l : 0.f;
-          tdq[ix] = 8u * (uint32_t)(q1 - q0);
-        }
-        tb0[iy][ix] = lbase + ((a.valid && b.valid) ? 8u * (uint32_t)(r0 * Cs2 + q0) : 0u);
+      if (iy == 0) {
+        P.fxh[ix] = b.valid ? b.h : 0.f;
+        P.fxl[ix] = b.valid ? b.l : 0.f;
+        P.tdq[ix] = 8u * (uint32_t)(q1 - q0);
       }
+      P.tb0[iy][ix] = (a.valid && b.valid) ? 8u * (uint32_t)(r0 * G.Cs2 + q0) : 0u;
     }
   }
-  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
-  const int64_t extent = ((int64_t)(c.C - 1) * scs + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  const uint32_t inv = (65536u + (uint32_t)Cs2 - 1u) / (uint32_t)Cs2;  // e / Cs2 == (e * inv) >> 16 for e < 1024
+  G.base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  G.extent = (uint32_t)(((int64_t)(c.C - 1) * G.scs + (int64_t)(H - 1) * G.sy + (int64_t)(W - 1) * G.sx + 1) * 4);
+  G.inv = (65536u + (uint32_t)G.Cs2 - 1u) / (uint32_t)G.Cs2;
+}
+
+// One item: RoI k, channel chunk `chunk` (16 channels).  kStAux / kLdAux: cache policy
+// of the output stores / staging loads (cdna.h).  kStamp (tools-only timing builds):
+// lane 0 writes 8 int64 per item after the output -- s_memrealtime at start / setup
+// done / first stage landed / end, D, cells, RoI record landed, XCD.
+template <int kStAux, int kLdAux, bool kStamp>
+__device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
+                                          int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
+  constexpr int SR = 2, kPW = kPairWave, kHalf = kPairHalf;
+  int64_t t_setup = 0, t_land = 0, t_fetched = 0;
+  const int cw0 = chunk * 2 * kPW;
+  const int npairs = min(kPW, (c.C - cw0) / 2);  // host: C even
+  const int nbins = c.ph * c.pw;
+  PairGeom G;
+  PairLane P;
+  const RoiRaw raw = roi_fetch(c, k);
+  if (kStamp) t_fetched = (int64_t)__builtin_amdgcn_s_memrealtime();
+  pair_setup(lv, c, raw, lane, G, P);
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)2 * npairs * nbins * 4);
+  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  const int ostep = nbins * 4;
+  if (G.empty) {  // no valid sample: all bins 0
+    for (int ch = 0; ch < 2 * npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
+    return;
+  }
+  const int y0 = G.y0, x0 = G.x0, R = G.R, Cs = G.Cs, Cs2 = G.Cs2, sy = G.sy, sx = G.sx, scs = G.scs;
+  const bool dy = G.dy, dx = G.dx;
+  const int ncell = R * Cs2;
+  const bool small = ncell <= PairLayout<8, kHalf>::kCells;
+  const int rsrc = P.rsrc, csrc = P.csrc;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(G.base, (int64_t)G.extent);
+  const uint32_t inv = G.inv;
   if (kStamp) t_setup = (int64_t)__builtin_amdgcn_s_memrealtime();
   int stamp_d = 0;
 
@@ -613,79 +592,50 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
       return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx + (lane & 1) * scs) * 4
                         : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave) + (lane & 1) * scs * 4;
     };
-    // kDynR with many rounds per pair (the big windows of D <= 2): the per-lane DMA offsets are
-    // recomputed per stage instead of held in RP registers, which would set the register
-    // budget of the whole kernel for a few percent of its items
-    constexpr bool kFly = kDynR && RP > 4;
-    int goff[kFly ? 1 : RP];
-    if constexpr (!kFly) {
+    int goff[RP];
 #pragma unroll
-      for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
-    }
-    const int nr = kDynR ? min(RP, (ncell + 31) >> 5) : RP;  // 32 cells (64 dwords) per round
+    for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
     auto issue = [&](int s) {  // pairs past the last re-read it (their stores are dropped)
-      const uint32_t buf = sbase + 4u * (uint32_t)(kSingle ? 0 : (s & 1) * kHalf);
-      if constexpr (kFly) {
-        for (int j = 0; j < nr; ++j) {
-          const int g = goff_at(j);
-#pragma unroll
-          for (int d = 0; d < D; ++d)
-            lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), g,
-                                  (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4);
-        }
-        return;
-      }
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int soff = (cw0 + 2 * min(s * D + d, npairs - 1)) * scs * 4;
 #pragma unroll
-        for (int j = 0; j < RP; ++j)
-          if (!kDynR || j < nr) lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
+        for (int j = 0; j < RP; ++j) lds_dma_at<4, kLdAux>(fr, sbase + 4u * (uint32_t)(d * RS + j * kWave), goff[j], soff);
       }
     };
-    auto eval = [&](auto bb, int s) {
-      constexpr int kBuf = decltype(bb)::value;
-      // half-rows h = 2 d + iy: 8 tap reads each; reads of h + 1 in flight while h is summed
-      // kRA: the tap reads of half-row h + 1 in flight while h is summed (16 more VGPRs)
-      constexpr int NB = kRA ? 2 : 1;
-      f32x2 v[NB][8];
+    auto eval = [&](int s) {
+      // half-rows h = 2 d + iy: 8 tap reads each; the reads of h + 1 in flight while h is summed
+      f32x2 v[2][8];
       f32x2 acc = {0.0f, 0.0f};
-      // kLean: the factors pass through an opaque copy per stage, so the products and sums
-      // below are computed here and not hoisted out of the stage loop into live registers
+      // the factors pass through an opaque copy per stage, so the products and sums below are
+      // computed here and not hoisted out of the stage loop into live registers
       float ly_h[SR], ly_l[SR], lx_h[SR], lx_l[SR];
       uint32_t lb[SR][SR], ldq[SR], ldr[SR];
-      if constexpr (kLean) {
 #pragma unroll
-        for (int i = 0; i < SR; ++i) {
-          ly_h[i] = fyh[i], ly_l[i] = fyl[i], lx_h[i] = fxh[i], lx_l[i] = fxl[i], ldq[i] = tdq[i], ldr[i] = tdr[i];
-          asm volatile("" : "+v"(ly_h[i]), "+v"(ly_l[i]), "+v"(lx_h[i]), "+v"(lx_l[i]), "+v"(ldq[i]), "+v"(ldr[i]));
+      for (int i = 0; i < SR; ++i) {
+        ly_h[i] = P.fyh[i], ly_l[i] = P.fyl[i], lx_h[i] = P.fxh[i], lx_l[i] = P.fxl[i], ldq[i] = P.tdq[i],
+        ldr[i] = P.tdr[i];
+        asm volatile("" : "+v"(ly_h[i]), "+v"(ly_l[i]), "+v"(lx_h[i]), "+v"(lx_l[i]), "+v"(ldq[i]), "+v"(ldr[i]));
 #pragma unroll
-          for (int j = 0; j < SR; ++j) {
-            lb[i][j] = tb0[i][j];
-            asm volatile("" : "+v"(lb[i][j]));
-          }
+        for (int j = 0; j < SR; ++j) {
+          lb[i][j] = sbase + P.tb0[i][j];
+          asm volatile("" : "+v"(lb[i][j]));
         }
       }
       auto tap = [&](int iy, int ix, int q) -> uint32_t {
-        if constexpr (kLean) return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
-        return ta[iy][ix][q];
+        return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
       };
       auto load = [&](auto hh) {
-        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (kBuf * kHalf + d * RS);
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (d * RS);
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[h % NB][ix * 4 + q] = lds_read_b64<OFF>(tap(iy, ix, q));
+          for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b64<OFF>(tap(iy, ix, q));
       };
-      if constexpr (kRA) load(std::integral_constant<int, 0>{});
+      load(std::integral_constant<int, 0>{});
       static_for<0, 2 * D>([&](auto hh) {
         constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
-        if constexpr (!kRA) {
-          constexpr int OFF = 4 * (kBuf * kHalf + d * RS);
-          const uint32_t a8[8] = {tap(iy, 0, 0), tap(iy, 0, 1), tap(iy, 0, 2), tap(iy, 0, 3),
-                                  tap(iy, 1, 0), tap(iy, 1, 1), tap(iy, 1, 2), tap(iy, 1, 3)};
-          lds_read8_wait<OFF>(v[0], a8);
-        } else if constexpr (h + 1 < 2 * D) {
+        if constexpr (h + 1 < 2 * D) {
           load(std::integral_constant<int, h + 1>{});
           lds_wait<8>(v[h & 1]);
         } else {
@@ -694,100 +644,36 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
         if (iy == 0) acc = f32x2{0.0f, 0.0f};
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix) {
-          float wl[4];
-          if constexpr (kLean) {
-            wl[0] = ly_h[iy] * lx_h[ix];
-            wl[1] = ly_h[iy] * lx_l[ix];
-            wl[2] = ly_l[iy] * lx_h[ix];
-            wl[3] = ly_l[iy] * lx_l[ix];
-          }
-          const float* w = kLean ? wl : wt[iy][ix];
-          const f32x2* x = &v[h % NB][ix * 4];
+          const float w[4] = {ly_h[iy] * lx_h[ix], ly_h[iy] * lx_l[ix], ly_l[iy] * lx_h[ix], ly_l[iy] * lx_l[ix]};
+          const f32x2* x = &v[h & 1][ix * 4];
           const f32x2 val = ((f32x2(w[0]) * x[0] + f32x2(w[1]) * x[1]) + f32x2(w[2]) * x[2]) + f32x2(w[3]) * x[3];
           acc = acc + val;
         }
         if (iy == 1) {
           const f32x2 r = acc * 0.25f;
           const int p = s * D + d;
-          if constexpr (kWideSt) {  // idle lanes write past the block (obase has 64 spare floats)
-            auto* ol = (__attribute__((address_space(3))) float*)(uintptr_t)obase;
-            const int o0 = active ? (2 * d) * nbins + lane : 2 * kPW * kWave + lane;
-            ol[o0] = r.x;
-            ol[o0 + (active ? nbins : 0)] = r.y;
-            asm volatile("" ::: "memory");  // written here: the results do not stay live in registers
-          } else {
-            const int vo = p < npairs ? ovoff : 0x40000000;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
-          }
+          const int vo = p < npairs ? ovoff : 0x40000000;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
         }
       });
-      if constexpr (kWideSt) {  // the stage's [channel][bin] block: 16-B pieces (8-B when not a multiple of 4 floats)
-        const int nd = min(D, npairs - s * D);
-        const int nf = 2 * nd * nbins, base = 2 * s * D * ostep;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if ((nf & 3) == 0 && (base & 15) == 0) {
-          auto* o4 = (__attribute__((address_space(3))) u32x4*)(uintptr_t)obase;
-          for (int q = lane; 4 * q < nf; q += kWave)
-            __builtin_amdgcn_raw_buffer_store_b128(o4[q], orr, 16 * q, base, kStAux);
-        } else {
-          auto* o2 = (__attribute__((address_space(3))) u32x2*)(uintptr_t)obase;
-          for (int q = lane; 2 * q < nf; q += kWave)
-            __builtin_amdgcn_raw_buffer_store_b64(o2[q], orr, 8 * q, base, kStAux);
-        }
-      }
     };
-    auto step = [&](auto bb, int s) {
-      if (s >= nst) return;
-      // retire stage s: younger than its DMAs are stage s-1's 2D stores and stage s+1's DMAs
-      if (s + 1 < nst) {
-        issue(s + 1);
-        if (s == 0)
-          wait_vmcnt<D * RP>();
-        else
-          wait_vmcnt<D * RP + 2 * D>();
-      } else if (s == 0) {
-        wait_vmcnt<0>();
-      } else {
-        wait_vmcnt<2 * D>();
-      }
+    stamp_d = D;
+    for (int s = 0; s < nst; ++s) {
+      issue(s);  // the previous stage's tap reads completed (lds_wait<0> + barrier below)
+      wait_vmcnt<0>();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (kStamp && s == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
-      eval(bb, s);
+      eval(s);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    stamp_d = D;
-    if constexpr (kSingle) {
-      for (int s = 0; s < nst; ++s) {
-        issue(s);  // the previous stage's tap reads completed (lds_wait<0> + barrier in eval / below)
-        wait_vmcnt<0>();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (kStamp && s == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
-        eval(std::integral_constant<int, 0>{}, s);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      return;
-    }
-    issue(0);
-    for (int s = 0; s < nst; s += 2) {
-      step(std::integral_constant<int, 0>{}, s);
-      step(std::integral_constant<int, 1>{}, s + 1);
     }
   };
   if (small)
     run(std::integral_constant<int, 8>{});
-  else if (FRH_ONLY8)
-    return;
   else if (ncell <= PairLayout<4, kHalf>::kCells)
     run(std::integral_constant<int, 4>{});
   else if (ncell <= PairLayout<2, kHalf>::kCells)
@@ -808,307 +694,24 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
   }
 }
 
-// kItems (1 or 2): items per wave.  With 2 the second item's RoI and level are fetched
-// with the first's (one memory round trip for both), so its prologue is ALU and
-// kernel-argument loads only.
-template <int kPW = kPairWave, int kHalf = kPairHalf, int kOrder = 0, int kStAux = 0, int kLdAux = 0,
-          bool kStamp = false, bool kSingle = false, int kMinW = 1, bool kRA = true, int kItems = 1,
-          bool kLean = false>
-__global__ void __launch_bounds__(kWave, kMinW) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  static_assert(kItems == 1 || (kItems == 2 && kOrder == 1), "two items per wave: chunk-major order only");
+// A 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups in which XCD x
+// (= linear id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item list,
+// so each XCD's L2 holds the feature planes of its own channel chunks.  32-bit item
+// arithmetic (host: K * chunks < 2^31).
+template <int kStAux = kCpolNT, bool kStamp = false>
+__global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  __shared__ __attribute__((aligned(16))) float slab[kSingle ? kHalf : 2 * kHalf];
+  __shared__ __attribute__((aligned(16))) float slab[kPairHalf];
   // the slab as an LDS byte address (integer: no generic-pointer casts)
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
-  if (kOrder == 0) {
-    const int64_t k = blockIdx.x;
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k, blockIdx.y,
-                                                                (int64_t)blockIdx.y * gridDim.x + blockIdx.x,
-                                                                roi_fetch(c, k), sbase, t_start, threadIdx.x & (kWave - 1));
-    return;
-  }
-  // 32-bit item arithmetic (host: K * G < 2^31): no 64-bit software division.  XCD x (= linear
-  // id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item list.
-  const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
+  const uint32_t G = (uint32_t)(c.C + kPairChunk - 1) / (uint32_t)kPairChunk, K32 = (uint32_t)c.K;
   const uint32_t total = K32 * G, per = (total + 7u) / 8u;
-  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3) * (uint32_t)kItems;
+  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
   const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
   if (w >= wend) return;
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
-  if constexpr (kItems == 1) {
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k0, ch0, w, roi_fetch(c, k0), sbase,
-                                                                t_start, threadIdx.x & (kWave - 1));
-  } else {
-    const bool two = w + 1 < wend;
-    const uint32_t w1 = two ? w + 1 : w;
-    const int ch1 = (int)(w1 / K32);
-    const int64_t k1 = (int64_t)(w1 - (uint32_t)ch1 * K32);
-    RoiRaw r0, r1;
-    roi_fetch2(c, k0, k1, &r0, &r1);
-    pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k0, ch0, w, r0, sbase, t_start,
-                                                                threadIdx.x & (kWave - 1));
-    if (two) {
-      // the slab is reused: the first item's tap reads are complete (lds_wait<0> + barrier)
-      pair_item<kPW, kHalf, kStAux, kLdAux, kStamp, kSingle, kRA, kLean>(lv, c, out, k1, ch1, w1, r1, sbase, t_start,
-                                                                  threadIdx.x & (kWave - 1));
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent pipelined channel-pair forward.  Each wave walks a static list of items
-// (RoI, 16 channels) and treats their stages (D channel pairs of one item, the slab
-// layout of pair_item) as one stream: while it evaluates stage k from one slab buffer,
-// the DMA of stage k+1 -- the same item's next pairs or the next item's first -- is
-// landing in the other.  The next RoI's record and window are loaded / computed while
-// the current stage's copies are in flight, so the per-item prologue (RoI load, window,
-// DMA issue) leaves the critical path that bounds the one-item-per-wave kernel (DESIGN
-// §4).  DMA rounds are issued only as far as the window needs (ceil(cells / 32)) and
-// their per-lane offsets computed per round.  Two kHalf-dword buffers per wave.  Same
-// taps, weights and operation order as pair_item: bit-identical.
-struct PipeItem {
-  int k, chunk, empty, l, b, H, W, sy, sx, scs;
-  int y0, x0, Cs, Cs2, ncell, dense, dy, dx;
-  int D, RS, nr, nst, npairs, cw0;
-  uint32_t inv;
-  float start_h, start_w, bin_h, bin_w;
-  int rsrc, csrc;  // per lane: feature byte offsets of slab row / column `lane` (sparse windows)
-};
-
-template <int kPW, int kHalf>
-__device__ __forceinline__ PipeItem pipe_prep(const RoiLevels& lv, const RoiCfg& c, int64_t k, int chunk, int lane) {
-  constexpr int SR = 2;
-  PipeItem it;
-  const RoiGeom g = roi_geom_raw(c, lv, roi_fetch(c, k));
-  it.k = (int)k;
-  it.chunk = chunk;
-  it.l = g.lvl;
-  it.b = g.b;
-  it.H = lv.h[it.l];
-  it.W = lv.w[it.l];
-  it.sy = (int)lv.sy[it.l];
-  it.sx = (int)lv.sx[it.l];
-  it.scs = (int)lv.sc[it.l];
-  it.start_h = g.start_h;
-  it.start_w = g.start_w;
-  it.bin_h = g.bin_h;
-  it.bin_w = g.bin_w;
-  it.cw0 = chunk * 2 * kPW;
-  it.npairs = min(kPW, (c.C - it.cw0) / 2);
-  auto pos_y = [&](int p, int i) { return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f; };
-  auto pos_x = [&](int p, int i) { return g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f; };
-  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
-  int yrow = -1, xcol = -1, ylo = 1 << 30, yhi = -1, xlo = 1 << 30, xhi = -1;
-  if (lane < nly) {
-    const int s = lane >> 1;
-    const Tap t = make_tap(pos_y(s >> 1, s & 1), it.H);
-    if (t.valid) yrow = (lane & 1) ? t.hi : t.lo, ylo = t.lo, yhi = t.hi;
-  }
-  if (lane < nlx) {
-    const int s = lane >> 1;
-    const Tap t = make_tap(pos_x(s >> 1, s & 1), it.W);
-    if (t.valid) xcol = (lane & 1) ? t.hi : t.lo, xlo = t.lo, xhi = t.hi;
-  }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(ylo)), y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(yhi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(xlo)), x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(xhi));
-  it.empty = !(y1 >= y0 && x1 >= x0);
-  it.y0 = y0;
-  it.x0 = x0;
-  it.dy = y1 - y0 + 1 <= nly;
-  it.dx = x1 - x0 + 1 <= nlx;
-  it.dense = it.dy && it.dx;
-  const int R = it.dy ? y1 - y0 + 1 : nly;
-  it.Cs = it.dx ? x1 - x0 + 1 : nlx;
-  it.Cs2 = it.Cs | 1;
-  it.ncell = it.empty ? 0 : R * it.Cs2;
-  it.rsrc = (it.dy ? y0 + min(lane, R - 1) : (yrow >= 0 ? yrow : y0)) * it.sy * 4;
-  it.csrc = (it.dx ? x0 + min(lane, it.Cs - 1) : (xcol >= 0 ? xcol : x0)) * it.sx * 4;
-  it.D = it.ncell <= PairLayout<8, kHalf>::kCells ? 8
-       : it.ncell <= PairLayout<4, kHalf>::kCells ? 4
-       : it.ncell <= PairLayout<2, kHalf>::kCells ? 2 : 1;
-  it.RS = (kHalf / it.D) / kWave * kWave;
-  it.nr = it.empty ? 0 : min(it.RS / kWave, (it.ncell + 31) >> 5);
-  it.nst = it.empty ? 1 : (it.npairs + it.D - 1) / it.D;
-  it.inv = (65536u + (uint32_t)it.Cs2 - 1u) / (uint32_t)it.Cs2;
-  return it;
-}
-
-// issue the DMA rounds of stage s of `it` into the buffer at LDS byte address buf;
-// returns the number of vector-memory operations issued (wave-uniform)
-template <int kLdAux>
-__device__ __forceinline__ int pipe_issue(const RoiLevels& lv, const RoiCfg& c, const PipeItem& it, int s,
-                                          uint32_t buf, int lane) {
-  if (it.empty) return 0;
-  const float* base = lv.feat[it.l] + (int64_t)it.b * lv.sb[it.l];
-  const int64_t extent = ((int64_t)(c.C - 1) * it.scs + (int64_t)(it.H - 1) * it.sy + (int64_t)(it.W - 1) * it.sx + 1) * 4;
-  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(base, extent);
-  for (int j = 0; j < it.nr; ++j) {
-    int e = (j * kWave + lane) >> 1;
-    e = e < it.ncell ? e : 0;
-    const int r = (int)(((uint32_t)e * it.inv) >> 16), col = min(e - r * it.Cs2, it.Cs - 1);
-    const int goff = it.dense ? ((it.y0 + r) * it.sy + (it.x0 + col) * it.sx + (lane & 1) * it.scs) * 4
-                              : __shfl(it.rsrc, r, kWave) + __shfl(it.csrc, col, kWave) + (lane & 1) * it.scs * 4;
-    for (int d = 0; d < it.D; ++d)
-      lds_dma_at<4, kLdAux>(fr, buf + 4u * (uint32_t)(d * it.RS + j * kWave), goff,
-                            (it.cw0 + 2 * min(s * it.D + d, it.npairs - 1)) * it.scs * 4);
-  }
-  return it.nr * it.D;
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n < 32
-__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
-  switch (n) {
-#define FRH_VM(i) \
-  case i:         \
-    wait_vmcnt<i>(); \
-    break;
-    FRH_VM(0) FRH_VM(1) FRH_VM(2) FRH_VM(3) FRH_VM(4) FRH_VM(5) FRH_VM(6) FRH_VM(7) FRH_VM(8) FRH_VM(9) FRH_VM(10)
-    FRH_VM(11) FRH_VM(12) FRH_VM(13) FRH_VM(14) FRH_VM(15) FRH_VM(16) FRH_VM(17) FRH_VM(18) FRH_VM(19) FRH_VM(20)
-    FRH_VM(21) FRH_VM(22) FRH_VM(23) FRH_VM(24) FRH_VM(25) FRH_VM(26) FRH_VM(27) FRH_VM(28) FRH_VM(29) FRH_VM(30)
-    FRH_VM(31)
-#undef FRH_VM
-    default:
-      wait_vmcnt<0>();
-  }
-}
-
-// evaluate stage s of `it` (D pairs from the buffer at `buf`) and store its outputs
-template <int D, int kPW, int kHalf, int kStAux>
-__device__ __forceinline__ void pipe_eval(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out,
-                                          const PipeItem& it, int s, uint32_t buf, int lane) {
-  constexpr int SR = 2, RS = PairLayout<D, kHalf>::RS;
-  const int nbins = c.ph * c.pw;
-  const bool active = lane < nbins;
-  const __amdgpu_buffer_rsrc_t orr =
-      uniform_rsrc(out + ((int64_t)it.k * c.C + it.cw0) * nbins, (int64_t)2 * it.npairs * nbins * 4);
-  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
-  const int ostep = nbins * 4;
-  if (it.empty) {
-    for (int ch = 0; ch < 2 * it.npairs; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
-    return;
-  }
-  auto pos_y = [&](int p, int i) { return it.start_h + (float)p * it.bin_h + ((float)i + 0.5f) * it.bin_h * 0.5f; };
-  auto pos_x = [&](int p, int i) { return it.start_w + (float)p * it.bin_w + ((float)i + 0.5f) * it.bin_w * 0.5f; };
-  const int bin = active ? lane : 0;
-  const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
-  // lean tap state (pair_item kLean): per-sample factors (zero for invalid samples) and bases
-  float fyh[SR], fyl[SR], fxh[SR], fxl[SR];
-  uint32_t tb0[SR][SR], tdq[SR], tdr[SR];
-#pragma unroll
-  for (int iy = 0; iy < SR; ++iy) {
-    const Tap a = make_tap(pos_y(py, iy), it.H);
-    fyh[iy] = a.valid ? a.h : 0.f;
-    fyl[iy] = a.valid ? a.l : 0.f;
-    const int r0 = it.dy ? a.lo - it.y0 : 2 * (py * SR + iy), r1 = it.dy ? a.hi - it.y0 : 2 * (py * SR + iy) + 1;
-    tdr[iy] = 8u * (uint32_t)((r1 - r0) * it.Cs2);
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      const Tap b = make_tap(pos_x(px, ix), it.W);
-      const int q0 = it.dx ? b.lo - it.x0 : 2 * (px * SR + ix), q1 = it.dx ? b.hi - it.x0 : 2 * (px * SR + ix) + 1;
-      if (iy == 0) {
-        fxh[ix] = b.valid ? b.h : 0.f;
-        fxl[ix] = b.valid ? b.l : 0.f;
-        tdq[ix] = 8u * (uint32_t)(q1 - q0);
-      }
-      tb0[iy][ix] = buf + ((a.valid && b.valid) ? 8u * (uint32_t)(r0 * it.Cs2 + q0) : 0u);
-    }
-  }
-  f32x2 v[2][8];
-  f32x2 acc = {0.0f, 0.0f};
-  auto tap = [&](int iy, int ix, int q) -> uint32_t {
-    return tb0[iy][ix] + ((q & 1) ? tdq[ix] : 0u) + ((q & 2) ? tdr[iy] : 0u);
-  };
-  auto load = [&](auto hh) {
-    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * d * RS;
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[h % 2][ix * 4 + q] = lds_read_b64<OFF>(tap(iy, ix, q));
-  };
-  load(std::integral_constant<int, 0>{});
-  static_for<0, 2 * D>([&](auto hh) {
-    constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
-    if constexpr (h + 1 < 2 * D) {
-      load(std::integral_constant<int, h + 1>{});
-      lds_wait<8>(v[h & 1]);
-    } else {
-      lds_wait<0>(v[h & 1]);
-    }
-    if (iy == 0) acc = f32x2{0.0f, 0.0f};
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-      float wl[4];
-      wl[0] = fyh[iy] * fxh[ix];
-      wl[1] = fyh[iy] * fxl[ix];
-      wl[2] = fyl[iy] * fxh[ix];
-      wl[3] = fyl[iy] * fxl[ix];
-      const f32x2* x = &v[h % 2][ix * 4];
-      const f32x2 val = ((f32x2(wl[0]) * x[0] + f32x2(wl[1]) * x[1]) + f32x2(wl[2]) * x[2]) + f32x2(wl[3]) * x[3];
-      acc = acc + val;
-    }
-    if (iy == 1) {
-      const f32x2 r = acc * 0.25f;
-      const int p = s * D + d;
-      const int vo = p < it.npairs ? ovoff : 0x40000000;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, 2 * p * ostep, kStAux);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (2 * p + 1) * ostep, kStAux);
-    }
-  });
-}
-
-// The wave's items: XCD x (= workgroup id % 8) walks the x-th eighth of the chunk-major
-// (chunk, RoI) list; the Q waves of an XCD interleave over it (wave q: items q, q + Q, ...).
-template <int kPW = kPairWave, int kHalf = kPairHalf, int kStAux = kCpolNT, int kLdAux = 0>
-__global__ void __launch_bounds__(kWave) roi_align_fwd_pipe_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float slab[2 * kHalf];
-  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t G = (uint32_t)(c.C + 2 * kPW - 1) / (uint32_t)(2 * kPW), K32 = (uint32_t)c.K;
-  const uint32_t total = K32 * G, per = (total + 7u) / 8u, Q = gridDim.x >> 3;
-  const uint32_t lo = (blockIdx.x & 7u) * per, hi = min(lo + per, total);
-  uint32_t w = lo + (blockIdx.x >> 3);
-  if (w >= hi) return;
-  auto prep = [&](uint32_t item) {
-    const int ch = (int)(item / K32);
-    return pipe_prep<kPW, kHalf>(lv, c, (int64_t)(item - (uint32_t)ch * K32), ch, lane);
-  };
-  PipeItem cur = prep(w);
-  int cs = 0, buf = 0;
-  pipe_issue<kLdAux>(lv, c, cur, 0, sbase, lane);
-  for (;;) {
-    // the next stage: the current item's, or the next item's first
-    PipeItem nxt = cur;
-    int ns = cs + 1;
-    bool have = true;
-    if (ns >= cur.nst) {
-      w += Q;
-      have = w < hi;
-      if (have) nxt = prep(w);  // the RoI record loads while the current stage's copies land
-      ns = 0;
-    }
-    const uint32_t nb = sbase + 4u * (uint32_t)((buf ^ 1) * kHalf);
-    const int nvm = have ? pipe_issue<kLdAux>(lv, c, nxt, ns, nb, lane) : 0;
-    wait_vmcnt_dyn(nvm);  // the current stage landed (older: its copies, the previous stage's stores)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t cb = sbase + 4u * (uint32_t)(buf * kHalf);
-    switch (cur.D) {
-      case 8: pipe_eval<8, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
-      case 4: pipe_eval<4, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
-      case 2: pipe_eval<2, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
-      default: pipe_eval<1, kPW, kHalf, kStAux>(lv, c, out, cur, cs, cb, lane); break;
-    }
-    // every tap read of this buffer completed (lds_wait<0> in the evaluation) before it is refilled
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!have) break;
-    cur = nxt;
-    cs = ns;
-    buf ^= 1;
-  }
+  pair_item<kStAux, 0, kStamp>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1));
 }
 
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,

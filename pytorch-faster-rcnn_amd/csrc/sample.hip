@@ -226,14 +226,14 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
   const int kp = npos < pos_num ? npos : pos_num;
   const int slots = max_num - kp;
   const int k = (v & 1) ? (nneg < slots ? nneg : slots) : kp;
-  uint32_t hsum = 0u;  // bin t (kSampBins == kTkThreads); 8 chunk loads in flight per step
+  uint32_t hsum = 0u;  // bin t (kSampBins == kTkThreads); 32 chunk loads in flight per step
   const uint32_t* ph = sb.part_hist + (int64_t)v * sb.nchunk * kSampBins + t;
-  for (int c0 = 0; c0 < nch; c0 += 8) {
-    uint32_t x[8];
+  for (int c0 = 0; c0 < nch; c0 += 32) {
+    uint32_t x[32];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) x[c] = c0 + c < nch ? ph[(int64_t)(c0 + c) * kSampBins] : 0u;
+    for (int c = 0; c < 32; ++c) x[c] = c0 + c < nch ? ph[(int64_t)(c0 + c) * kSampBins] : 0u;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) hsum += x[c];
+    for (int c = 0; c < 32; ++c) hsum += x[c];
   }
   sm.h1[t] = hsum;
   __syncthreads();

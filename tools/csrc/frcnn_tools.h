@@ -1,6 +1,6 @@
 // TOOLS-ONLY entry points (tools/lib/libfrcnn_tools.so; never linked into the product
-// library).  RoIAlign forward laboratory: the product default kernel, a per-wave
-// timestamped build of it, and candidate kernels under measurement (tools/bench_roi_align.py).
+// library).  RoIAlign forward laboratory: the product's forward kernel and a per-wave
+// timestamped build of it (tools/bench_roi_align.py).
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -9,10 +9,9 @@
 extern "C" {
 #endif
 
-/* variant 0: the product default (frh_roi_align_fwd_strided's pair kernel);
- * 1: the same kernel with per-item stamps (8 int64 per item after the output);
- * >= 10: candidates (tools/csrc/roi_lab.hip).  Arguments as frh_roi_align_fwd_strided,
- * plus a workspace for variants that need one. */
+/* variant 0: frh_roi_align_fwd_strided's pair kernel; 1: the same with per-item stamps (8
+ * int64 per item after the output).  Arguments as frh_roi_align_fwd_strided, plus a
+ * workspace of frh_roi_align_workspace bytes (unused by these two). */
 int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
                                   const int32_t* feat_hw, const int64_t* strides, const float* scales,
                                   int32_t batch, int32_t channels, const float* rois, const int64_t* roi_levels,

@@ -13,8 +13,8 @@ python tools/step_breakdown.py $OUT/stats --warmup 3 --steps 10 > $OUT/step_brea
 rm -f $OUT/stats/run_kernel_trace.csv  # large; the summary and the breakdown are kept
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 47 > $OUT/pmc_calib.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 47 > $OUT/pmc_calib_small.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 0 > $OUT/pmc_calib.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 0 > $OUT/pmc_calib_small.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc OccupancyPercent MeanOccupancyPerCU --kernel-trace -d $OUT/pmc_occ -o run --output-format csv -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline > $OUT/pmc_occ.log 2>&1
 python tools/pmc_summary.py --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel roi_align_fwd_pair_kernel \
   --calib-fetch $OUT/pmc_calib $OUT/pmc_calib_small --calib-bytes 220463104 150994944 --out $OUT/roi_align_pmc.json
