@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # in-step kernel groups of the detection path (substrings of the dispatched kernel names)
 KERNEL_GROUPS = [
-    ('roi_align_fwd', ('roi_align_fwd', 'roi_align_pair_desc')),
+    ('roi_align_fwd', ('roi_align_fwd',)),
     ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
     ('proposals', ('rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
@@ -477,14 +477,9 @@ def main():
         nrecs = list(ops.NMS_PROFILE['records'])
         per_group, det_us, group_names, det_kernels = (summarise_trace(trace, steps_traced) if trace else
                                                         ({}, None, {}, {}))
-        # one forward call = the descriptor launch (frh_roi_align_fwd_ws) + the pair kernel
         roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]
-        roi_desc = [us for n, us in (trace or []) if 'roi_align_pair_desc' in n]
-        roi_in_step = (float(np.sum([us for _, us in roi_launches]) + np.sum(roi_desc)) / len(roi_launches)
-                       if roi_launches else None)
+        roi_in_step = float(np.mean([us for _, us in roi_launches])) if roi_launches else None
         roi_kernel = kernel_short(roi_launches[0][0]) if roi_launches else None
-        if roi_kernel and roi_desc:
-            roi_kernel = 'frh::roi_align_pair_desc_kernel + ' + roi_kernel
         warm, cold = roi_align_replays(recs, dev)
         avg_bytes = float(np.mean([roi_align_bytes(r) for r in recs])) if recs else None
         us_for_frac = roi_in_step if roi_in_step else warm
@@ -528,8 +523,7 @@ def main():
                 'avg_launch_us_in_step': roi_in_step, 'avg_launch_us_replay_warm': warm,
                 'avg_launch_us_replay_cold': cold,
                 'timing': ('in-step device durations from the ROCm kernel tracer (torch.profiler) over {} steps '
-                           'after the timed region, per forward call (descriptor launch + pair kernel)'.format(
-                               steps_traced) if roi_in_step else
+                           'after the timed region'.format(steps_traced) if roi_in_step else
                            'kernel tracer unavailable ({}): back-to-back replay, warm caches'.format(trace_err)) +
                           '; replay_warm = the same launches back to back, replay_cold = each after a 768 MB read '
                           '(L2 + Infinity Cache evicted); traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '

@@ -278,18 +278,89 @@ struct MergeArgs {
 // Cross-level top-k as a merge: each level's survivors are already in
 // (score desc) order, so the rank of survivor j of level l among all levels
 // (score desc, concatenation order on ties) is j + sum over other levels of
-// a binary search (upper bound for earlier levels, lower bound for later).
-// Grid: (survivor chunks of 256, level, image); no sort.  kLds: the image's
-// survivor scores of every level are gathered into LDS first (L * P floats,
-// two memory round trips), so the searches are LDS reads instead of chains of
-// dependent global loads.
+// a binary search (upper bound for earlier levels, lower bound for later).  No sort.
 __device__ __forceinline__ float kept_score(const MergeArgs& p, int seg, int j) {
   return p.sel_scores[(int64_t)seg * p.P + p.keep[(int64_t)seg * p.P + j]];
 }
 
-template <bool kLds>
+__device__ __forceinline__ void merge_write(const MergeArgs& p, int b, int seg, int pos, int rank, float s) {
+  float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + pos];
+  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
+  ob[rank] = bx.x;
+  ob[p.out_cap + rank] = bx.y;
+  ob[2 * p.out_cap + rank] = bx.z;
+  ob[3 * p.out_cap + rank] = bx.w;
+  p.out_scores[(int64_t)b * p.out_cap + rank] = s;
+}
+
+// One 1024-thread workgroup per (level, image): the image's survivor scores of every
+// level are gathered into LDS first (L * P floats; each thread's keep-index loads in
+// flight together, then its score gathers), so the searches are LDS reads, not chains
+// of dependent global loads.
+constexpr int kMergeThreads = 1024;
+constexpr int kMergePer = 16;  // gathered scores per thread and batch
+
+static __global__ void __launch_bounds__(kMergeThreads) rpn_merge_lds_kernel(MergeArgs p) {
+  extern __shared__ float ms[];  // [L][P] survivor scores of image b
+  __shared__ int cnt_s[FRH_MAX_LEVELS + 1];
+  const int l = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (t < p.L) cnt_s[t] = p.keep_count[b * p.L + t];
+  __syncthreads();
+  int total = 0, base = 0;
+  for (int q = 0; q < p.L; ++q) {
+    base += q < l ? cnt_s[q] : 0;
+    total += cnt_s[q];
+  }
+  const bool cut = p.max_num > 0 && total > p.max_num;
+  if (l == 0 && t == 0) p.out_counts[b] = cut ? p.max_num : total;
+  if (cut) {
+    // flat index e over (level, survivor), e = q * P + i
+    for (int e0 = 0; e0 < p.L * p.P; e0 += kMergeThreads * kMergePer) {
+      int kidx[kMergePer];
+#pragma unroll
+      for (int u = 0; u < kMergePer; ++u) {
+        const int e = e0 + u * kMergeThreads + t, q = e / p.P, i = e - q * p.P;
+        kidx[u] = (q < p.L && i < cnt_s[q]) ? p.keep[(int64_t)(b * p.L + q) * p.P + i] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kMergePer; ++u) {
+        const int e = e0 + u * kMergeThreads + t, q = e / p.P;
+        if (kidx[u] >= 0) ms[e] = p.sel_scores[(int64_t)(b * p.L + q) * p.P + kidx[u]];
+      }
+    }
+    __syncthreads();
+  }
+  const int seg = b * p.L + l;
+  for (int j = t; j < cnt_s[l]; j += kMergeThreads) {
+    const int pos = p.keep[(int64_t)seg * p.P + j];
+    const float s = cut ? ms[l * p.P + j] : p.sel_scores[(int64_t)seg * p.P + pos];
+    int rank = base + j;
+    if (cut) {
+      rank = j;
+      for (int q = 0; q < p.L; ++q) {
+        if (q == l) continue;
+        int lo = 0, hi = cnt_s[q];
+        // count of survivors of level q ordered before (s, this level)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const float o = ms[q * p.P + mid];
+          const bool before = q < l ? (o >= s) : (o > s);
+          if (before)
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank >= p.max_num) continue;
+    }
+    merge_write(p, b, seg, pos, rank, s);
+  }
+}
+
+// The same with the searches in global memory (levels x survivors beyond the LDS):
+// grid (survivor chunks of 256, level, image).
 static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
-  extern __shared__ float ms[];  // kLds: [L][P] survivor scores of image b
   const int b = blockIdx.z, l = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int seg = b * p.L + l;
@@ -302,14 +373,6 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
   }
   const bool cut = p.max_num > 0 && total > p.max_num;
   if (blockIdx.x == 0 && threadIdx.x == 0 && l == 0) p.out_counts[b] = cut ? p.max_num : total;
-  if (kLds && cut) {
-    for (int q = 0; q < p.L; ++q) {
-      const int oseg = b * p.L + q, c = p.keep_count[oseg];
-      for (int i = threadIdx.x; i < c; i += blockDim.x)
-        ms[q * p.P + i] = p.sel_scores[(int64_t)oseg * p.P + p.keep[(int64_t)oseg * p.P + i]];
-    }
-    __syncthreads();
-  }
   if (j >= cnt) return;
   const int pos = p.keep[(int64_t)seg * p.P + j];
   const float s = p.sel_scores[(int64_t)seg * p.P + pos];
@@ -320,10 +383,9 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
       if (q == l) continue;
       const int oseg = b * p.L + q;
       int lo = 0, hi = p.keep_count[oseg];
-      // count of survivors of level q ordered before (s, this level)
       while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        float o = kLds ? ms[q * p.P + mid] : kept_score(p, oseg, mid);
+        float o = kept_score(p, oseg, mid);
         bool before = q < l ? (o >= s) : (o > s);
         if (before)
           lo = mid + 1;
@@ -334,13 +396,7 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
     }
     if (rank >= p.max_num) return;
   }
-  float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + pos];
-  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
-  ob[rank] = bx.x;
-  ob[p.out_cap + rank] = bx.y;
-  ob[2 * p.out_cap + rank] = bx.z;
-  ob[3 * p.out_cap + rank] = bx.w;
-  p.out_scores[(int64_t)b * p.out_cap + rank] = s;
+  merge_write(p, b, seg, pos, rank, s);
 }
 
 static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -493,11 +549,13 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   if (r) return r;
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};
-  dim3 mg((unsigned)((post + 255) / 256), (unsigned)num_levels, (unsigned)num_imgs);
   const size_t merge_lds = (size_t)num_levels * z.P * sizeof(float);
-  if (merge_lds <= 65536)
-    hipLaunchKernelGGL(rpn_merge_kernel<true>, mg, dim3(256), merge_lds, st, mp);
-  else
-    hipLaunchKernelGGL(rpn_merge_kernel<false>, mg, dim3(256), 0, st, mp);
+  if (merge_lds <= 65536 - 256) {  // + the kernel's static counts
+    hipLaunchKernelGGL(rpn_merge_lds_kernel, dim3((unsigned)num_levels, (unsigned)num_imgs), dim3(kMergeThreads),
+                       merge_lds, st, mp);
+  } else {
+    dim3 mg((unsigned)((post + 255) / 256), (unsigned)num_levels, (unsigned)num_imgs);
+    hipLaunchKernelGGL(rpn_merge_kernel, mg, dim3(256), 0, st, mp);
+  }
   return check_launch("rpn_merge");
 }

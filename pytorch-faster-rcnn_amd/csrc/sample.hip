@@ -139,11 +139,16 @@ struct SampBufs {
   int32_t* sel_cnt;      // [V] how many
 };
 
-static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const int64_t* lab_in, int64_t lstride,
+// 1024 threads x 4 boxes per 4096-box chunk (the collect launch's chunk): four times
+// the waves of a 256-thread chunk for the same histogram layout.
+constexpr int kSkThreads = 1024;
+constexpr int kSkPer = kTkChunk / kSkThreads;
+
+static __global__ void __launch_bounds__(kSkThreads) sampler_keys_kernel(const int64_t* lab_in, int64_t lstride,
                                                                          const int32_t* num, uint64_t seed,
                                                                          SampBufs sb, int64_t* lab_out) {
   __shared__ uint32_t h[2][kSampBins];
-  __shared__ int scratch[kTkThreads / kWave];
+  __shared__ int scratch[kSkThreads / kWave];
   const TkBufs& b = sb.tk;
   const int s = blockIdx.y, c = blockIdx.x;
   const int64_t n = num[s];
@@ -153,15 +158,15 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const i
   uint32_t* kp = const_cast<uint32_t*>(b.keys) + (int64_t)(2 * s) * b.ld;
   uint32_t* kn = kp + b.ld;
   int cp = 0, cn = 0;
-  int64_t lab[kTkPerThread];  // every label load in flight at once
+  int64_t lab[kSkPer];  // every label load in flight at once
 #pragma unroll
-  for (int r = 0; r < kTkPerThread; ++r) {
-    const int64_t i = base + r * kTkThreads + threadIdx.x;
+  for (int r = 0; r < kSkPer; ++r) {
+    const int64_t i = base + r * kSkThreads + threadIdx.x;
     lab[r] = i < n ? lab_in[(int64_t)s * lstride + i] : -1;
   }
 #pragma unroll
-  for (int r = 0; r < kTkPerThread; ++r) {
-    const int64_t i = base + r * kTkThreads + threadIdx.x;
+  for (int r = 0; r < kSkPer; ++r) {
+    const int64_t i = base + r * kSkThreads + threadIdx.x;
     const bool pos = lab[r] > 0, neg = lab[r] == 0;
     if (lab_out && i < n) lab_out[(int64_t)s * lstride + i] = -1;
     const uint32_t keyp = pos ? ((~hash_u32(seed, 2 * s, (uint32_t)i)) | 1u) : 0u;
@@ -182,7 +187,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_keys_kernel(const i
     sb.part_count[(int64_t)(2 * s + 1) * sb.nchunk + c] = cn;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * kSampBins; i += kTkThreads) {
+  for (int i = threadIdx.x; i < 2 * kSampBins; i += kSkThreads) {
     const int w = i / kSampBins;
     sb.part_hist[((int64_t)(2 * s + w) * sb.nchunk + c) * kSampBins + (i % kSampBins)] = h[w][i % kSampBins];
   }
@@ -352,7 +357,7 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
                      reinterpret_cast<int32_t*>(ws + z.state), reinterpret_cast<uint64_t*>(ws + z.cand)},
               reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
               sel, (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
-  hipLaunchKernelGGL(sampler_keys_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
+  hipLaunchKernelGGL(sampler_keys_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kSkThreads), 0, st,
                      labels_in, label_seg_stride, num_boxes, seed, sb, labels_out);
   hipLaunchKernelGGL(sampler_collect_kernel, dim3((unsigned)z.nchunk, (unsigned)V), dim3(kTkThreads), 0, st,
                      labels_in, label_seg_stride, num_boxes, max_num, pos_num, sb, labels_out);

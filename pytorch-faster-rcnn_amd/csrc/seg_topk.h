@@ -121,6 +121,42 @@ __device__ __forceinline__ int block_reserve(int cnt, int* counter, int* part, i
   return sh[0] + pre + incl - cnt;  // sh[0] = the workgroup's first slot, sh[1] = its count
 }
 
+// The same for two lists whose counters are adjacent words (c[0]: selections,
+// c[1]: candidates; 8-byte aligned): one packed scan and ONE 64-bit atomic.  Per
+// workgroup each count is < 65536.  Returns this thread's first (selection,
+// candidate) slots; sh[0] / sh[1] = the workgroup's first selection slot /
+// selection count, *cb = its first candidate slot.
+__device__ __forceinline__ int2 block_reserve2(int nsel, int ncand, int* c, int* part, int* sh, int* cb) {
+  const int t = threadIdx.x, w = t / kWave;
+  __syncthreads();  // part / sh free
+  const int cnt = nsel | (ncand << 16);
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if (lane_id() >= o) incl += x;
+  }
+  if (lane_id() == kWave - 1) part[w] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int i = 0; i < (int)blockDim.x / kWave; ++i) {
+    const int v = part[i];
+    pre += i < w ? v : 0;
+    tot += v;
+  }
+  if (t == 0) {
+    const uint32_t ts = (uint32_t)tot & 0xffffu, tc = (uint32_t)tot >> 16;
+    const unsigned long long old =
+        tot ? atomicAdd(reinterpret_cast<unsigned long long*>(c), ((unsigned long long)tc << 32) | ts) : 0ull;
+    sh[0] = (int)(uint32_t)old;
+    sh[1] = (int)ts;
+    *cb = (int)(uint32_t)(old >> 32);
+  }
+  __syncthreads();
+  const int ex = pre + incl - cnt;
+  return make_int2(sh[0] + (ex & 0xffff), *cb + (ex >> 16));
+}
+
 // --------------------------------------------- first-level histogram (keys)
 // The key kernels build it per chunk: clear, add, flush (block-uniform calls).
 __device__ __forceinline__ void tk_hist1_clear(uint32_t* h, int bins) {
@@ -148,6 +184,7 @@ struct TkSmem {
   int part[kTkThreads / kWave];
   int last, bin, above, tot, ncand;
   int base, tot_sel;  // block_reserve's (first slot, count); adjacent
+  int cbase;          // block_reserve2's first candidate slot
 };
 
 // Suffix search over 2^hb bins (highest first), 256 threads: sm.bin / sm.above
@@ -312,15 +349,18 @@ __device__ void tk_collect_chunk(const TkBufs& b, int v, int n, const TkPlan& pl
       sel |= (key[r] != 0u && (all || pre > P)) ? 1u << r : 0u;
       eq |= (key[r] != 0u && !all && pre == P) ? 1u << r : 0u;
     }
+    // one reservation for both lists (TK_OUT, TK_CAND adjacent)
+    static_assert(TK_CAND == TK_OUT + 1 && TK_OUT % 2 == 0, "adjacent, 8-byte aligned counters");
+    const int2 slots = block_reserve2(__popc(sel), __popc(eq), &st[TK_OUT], sm.part, &sm.base, &sm.cbase);
     // candidates: straight to the segment's list (no dependent loads)
-    int c = block_reserve(__popc(eq), &st[TK_CAND], sm.part, &sm.base);
+    int c = slots.y;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r)
       if (eq & (1u << r))
         xwg_store(cand + c++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)(base + r * kTkThreads + t));
     // selections: staged in LDS, then handed to the policy one per thread per
     // round, so the policy's loads for a round are in flight together
-    int s = block_reserve(__popc(sel), &st[TK_OUT], sm.part, &sm.base);
+    int s = slots.x;
     const int gbase = sm.base, nsel = sm.tot_sel;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r)

@@ -265,6 +265,47 @@ def test_device_sampler_properties(dev, max_num, pos_num):
     assert not np.array_equal(out, out2)
 
 
+def _hash_u32(seed, a, b):
+    """block_ops.h hash_u32 (splitmix64 finaliser of seed ^ (a << 32 | b)), vectorised over b."""
+    m = np.uint64(0xFFFFFFFFFFFFFFFF)
+    z = np.uint64(seed) ^ ((np.uint64(a) << np.uint64(32)) | b.astype(np.uint64))
+    with np.errstate(over='ignore'):
+        z = z + np.uint64(0x9e3779b97f4a7c15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    z = (z ^ (z >> np.uint64(31))) & m
+    return (z >> np.uint64(32)).astype(np.uint32)
+
+
+def test_device_sampler_selects_top_hash_keys(dev):
+    """The device sampler's selection is exactly its definition: per image, the kp = min(npos,
+    pos_num) positives and kn = min(nneg, max_num - kp) negatives with the largest keys
+    (~hash(seed, 2s (+1), box) | 1), ties by box index -- recomputed here in numpy."""
+    from frcnn_amd import ops
+    rng = np.random.default_rng(21)
+    S, n, max_num, pos_num = 3, 200003, 256, 128
+    lab = rng.choice([-1, 0, 1], size=(S, n), p=[0.4, 0.59, 0.01]).astype(np.int64)
+    lab[1, :] = np.where(lab[1] > 0, -1, lab[1])  # no positives
+    num = torch.tensor([n, n - 11, 70000], dtype=torch.int32, device=dev)
+    ops.set_sampler_mode('device', seed=5)
+    out = ops.sample_labels(T(lab, dev), num, n, max_num, pos_num, mode='device').cpu().numpy()
+    seed = (ops._SAMPLER['seed'] * 0x9E3779B97F4A7C15 + ops._SAMPLER['calls']) & 0xFFFFFFFFFFFFFFFF
+    ops.set_sampler_mode('numpy')
+    for s in range(S):
+        ns = int(num[s])
+        idx = np.arange(ns, dtype=np.uint32)
+        src = lab[s, :ns]
+        want = np.full(ns, -1, np.int64)
+        pos, neg = np.nonzero(src > 0)[0], np.nonzero(src == 0)[0]
+        kp = min(len(pos), pos_num)
+        kn = min(len(neg), max_num - kp)
+        for cand, v, k in ((pos, 2 * s, kp), (neg, 2 * s + 1, kn)):
+            key = (~_hash_u32(seed, v, idx[cand])) | np.uint32(1)
+            order = np.lexsort((cand, -key.astype(np.int64)))  # key desc, index asc
+            want[cand[order[:k]]] = src[cand[order[:k]]]
+        np.testing.assert_array_equal(out[s, :ns], want)
+
+
 @pytest.mark.parametrize('max_num,pos_num', [(256, 128), (512, 128)])
 def test_device_sampler_lists_feed_targets(dev, max_num, pos_num):
     """The device sampler's selection lists (frh_sample_random sel / sel_counts) fed straight
