@@ -253,6 +253,30 @@ __device__ __forceinline__ int lds_poll(int* p) {
   asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
   return __builtin_amdgcn_readfirstlane(v);
 }
+// The resolver's reads for one block in ONE asm statement: the block's ready flag first,
+// then its partial word and three staged tiles, one wait.  One CU serves LDS requests in
+// order, so if the flag read returns the block as ready, the reads issued after it see
+// the data its loader stored (or whose LDS-DMA it waited for) before publishing.
+__device__ __forceinline__ int lds_block_reads(const int* flag, const uint64_t* pa, const uint64_t* t1a,
+                                               const uint64_t* t2a, const uint64_t* da, uint64_t& pw, uint64_t& t1,
+                                               uint64_t& t2, uint64_t& d) {
+  auto la = [](const void* q) {
+    return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)q);
+  };
+  int f;
+  asm volatile(
+      "ds_read_b32 %0, %5\n\t"
+      "ds_read_b64 %1, %6\n\t"
+      "ds_read_b64 %2, %7\n\t"
+      "ds_read_b64 %3, %8\n\t"
+      "ds_read_b64 %4, %9\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(f), "=&v"(pw), "=&v"(t1), "=&v"(t2), "=&v"(d)
+      : "v"(la(flag)), "v"(la(pa)), "v"(la(t1a)), "v"(la(t2a)), "v"(la(da))
+      : "memory");
+  return __builtin_amdgcn_readfirstlane(f);
+}
+
 __device__ __forceinline__ int lds_acquire(int* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -312,17 +336,22 @@ __device__ __forceinline__ void lds_flag(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// kStamp (tools-only timing build): per (segment, block) 8 int64 of s_memrealtime at
+// stamps + (s * nbw + b) * 8: [0] resolver starts waiting, [1] block ready seen, [2]
+// resolved and published, [3] loader published the fold, [4] loader issued the copies.
+template <bool kStamp>
 __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restrict__ mask,
                                                        const int32_t* __restrict__ counts, int nbw, int span,
                                                        int max_keep, int32_t* __restrict__ keep, int64_t kstride,
                                                        int32_t* __restrict__ kcounts,
-                                                       const int64_t* __restrict__ seg_base) {
+                                                       const int64_t* __restrict__ seg_base, int64_t* stamps) {
   extern __shared__ __attribute__((aligned(16))) uint64_t nms_lds[];
   __shared__ uint64_t kept[kMaxNmsWords];
   __shared__ uint64_t partial[kNmsRing][kWave];
   __shared__ int ready[kNmsRing];
   __shared__ int s_resolved, s_stop;
-  const int s = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid & (kWave - 1);
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);  // uniform: the copies' offsets stay scalar
   const int n = counts[s];
   const int nb = (n + 63) >> 6;
   if (tid < kNmsRing) ready[tid] = 0;
@@ -333,21 +362,32 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   __syncthreads();
   const int slot_words = ((span + 1) & ~1) * 64;  // whole 1 KB copies: an even number of tiles
   const int64_t base = seg_tile_base(seg_base, s, nbw);
-  auto tile = [&](const uint64_t* slot, int j0, int j, int b) {
-    return j >= j0 ? slot[(j - j0) * 64 + lane] : mask[tile_word(base, j, b) + lane];
-  };
   if (wave == 0) {
     int32_t* K = keep + (int64_t)s * kstride;
     int nk = 0;
     uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
+    auto stamp = [&](int b, int i) {
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + b) * 8 + i] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    };
     for (int b = 0; b < nb; ++b) {
-      while (lds_poll(&ready[b % kNmsRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
+      stamp(b, 0);
       const uint64_t* slot = nms_lds + (b % kNmsRing) * slot_words;
       const int j0 = max(0, b - span + 1);
-      uint64_t acc = partial[b % kNmsRing][lane];
-      if (b >= 1) acc |= tile(slot, j0, b - 1, b) & kb1;
-      if (b >= 2) acc |= tile(slot, j0, b - 2, b) & kb2;
-      const uint64_t d = slot[(b - j0) * 64 + lane];
+      // tiles b-1 and b-2 are always staged (span >= min(nbw, 3)); before block 2 the reads
+      // are clamped into the slot and masked by the empty kept sets kb1 / kb2.  The block's
+      // data is read together with its ready flag (the loaders are normally ahead); if it
+      // was not ready, poll, then read again.
+      const uint64_t* pa = &partial[b % kNmsRing][lane];
+      const uint64_t* t1a = slot + max(b - 1 - j0, 0) * 64 + lane;
+      const uint64_t* t2a = slot + max(b - 2 - j0, 0) * 64 + lane;
+      const uint64_t* da = slot + (b - j0) * 64 + lane;
+      uint64_t pw, t1, t2, d;
+      if (lds_block_reads(&ready[b % kNmsRing], pa, t1a, t2a, da, pw, t1, t2, d) != b + 1) {
+        while (lds_poll(&ready[b % kNmsRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
+        lds_block_reads(&ready[b % kNmsRing], pa, t1a, t2a, da, pw, t1, t2, d);
+      }
+      stamp(b, 1);
+      const uint64_t acc = pw | (t1 & kb1) | (t2 & kb2);
       uint64_t r = __ballot(acc != 0ull);
       const int valid = n - b * 64;
       if (valid < 64) r |= (~0ull) << valid;
@@ -369,11 +409,14 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       nk += __popcll(kb);
       kb2 = kb1;
       kb1 = kb;
-      if (lane == 0) {
+      if (lane == 0) {  // in-order LDS: the loaders see kept[b] / s_stop once they see the flag
         kept[b] = kb;
         if (stop) s_stop = b;
-        lds_flag(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1);
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(&s_resolved, stop ? nb + kNmsRing + 1 : b + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      stamp(b, 2);
       if (stop) break;
     }
     if (lane == 0) kcounts[s] = nk;
@@ -404,6 +447,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       for (; j < p - 2; ++j) acc |= slot[(j - j0) * 64 + lane] & kept[j];
       partial[p % kNmsRing][lane] = acc;
       if (lane == 0) lds_flag(&ready[p % kNmsRing], p + 1);
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
     };
     int prev = -1;
     for (int b = wave - 1; b < nb; b += kNmsLoaders) {
@@ -414,6 +458,7 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
       const uint32_t dst = lds0 + (uint32_t)((b % kNmsRing) * slot_words * 8);
       const int src = (int)((tile_word(0, j0, b)) * 8);
       for (int k = 0; k < ninst; ++k) lds_dma_at<16>(mr, dst + (uint32_t)k * 1024u, lane * 16, src + k * 1024);
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + b) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (prev >= 0) {
         wait_vmcnt_atmost(ninst);  // prev's copies are older than these ninst
         asm volatile("" ::: "memory");
@@ -437,7 +482,9 @@ static int32_t nms_scan_attr() {
   FRH_HIP(hipGetDevice(&dev));
   const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
   if (bit && (g_scan_attr_devices.load(std::memory_order_acquire) & bit)) return FRH_OK;
-  FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel),
+  FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kNmsRing * kNmsSpan * 64 * 8));
+  FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(nms_scan_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kNmsRing * kNmsSpan * 64 * 8));
   g_scan_attr_devices.fetch_or(bit, std::memory_order_acq_rel);
   return FRH_OK;
@@ -445,7 +492,7 @@ static int32_t nms_scan_attr() {
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, const int64_t* seg_base, hipStream_t st) {
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps) {
   const int nbw = (n_max + 63) / 64;
   FRH_REQUIRE(nbw <= kMaxNmsWords, "n_max %d exceeds %d", n_max, 64 * kMaxNmsWords);
   const int32_t r = nms_scan_attr();
@@ -455,8 +502,12 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
                      seg_base);
   const int span = std::min(nbw, kNmsSpan);
   const size_t lds = (size_t)kNmsRing * ((span + 1) & ~1) * 64 * sizeof(uint64_t);
-  hipLaunchKernelGGL(nms_scan_kernel, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep, kstride,
-                     kcounts, seg_base);
+  if (stamps)
+    hipLaunchKernelGGL(nms_scan_kernel<true>, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep,
+                       kstride, kcounts, seg_base, stamps);
+  else
+    hipLaunchKernelGGL(nms_scan_kernel<false>, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep,
+                       kstride, kcounts, seg_base, nullptr);
   return check_launch("nms");
 }
 
@@ -486,5 +537,5 @@ extern "C" int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t 
     return FRH_OK;
   }
   return launch_nms_sorted(num_segs, boxes, seg_stride, counts, n_max, iou_thr, max_keep, keep, keep_seg_stride,
-                           keep_counts, reinterpret_cast<uint64_t*>(workspace), nullptr, as_stream(stream));
+                           keep_counts, reinterpret_cast<uint64_t*>(workspace), nullptr, as_stream(stream), nullptr);
 }

@@ -16,7 +16,7 @@ namespace frh {
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, const int64_t* seg_base, hipStream_t st);
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps = nullptr);
 size_t nms_mask_bytes(int32_t S, int32_t n_max);
 
 constexpr int kPropThreads = 1024;
@@ -331,30 +331,33 @@ static __global__ void __launch_bounds__(kMergeThreads) rpn_merge_lds_kernel(Mer
     __syncthreads();
   }
   const int seg = b * p.L + l;
+  if (!cut) {  // everything fits: rank = concatenation position (a separate loop: no pointer select)
+    for (int j = t; j < cnt_s[l]; j += kMergeThreads) {
+      const int pos = p.keep[(int64_t)seg * p.P + j];
+      merge_write(p, b, seg, pos, base + j, p.sel_scores[(int64_t)seg * p.P + pos]);
+    }
+    return;
+  }
   for (int j = t; j < cnt_s[l]; j += kMergeThreads) {
     const int pos = p.keep[(int64_t)seg * p.P + j];
-    const float s = cut ? ms[l * p.P + j] : p.sel_scores[(int64_t)seg * p.P + pos];
-    int rank = base + j;
-    if (cut) {
-      rank = j;
-      for (int q = 0; q < p.L; ++q) {
-        if (q == l) continue;
-        int lo = 0, hi = cnt_s[q];
-        // count of survivors of level q ordered before (s, this level)
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          const float o = ms[q * p.P + mid];
-          const bool before = q < l ? (o >= s) : (o > s);
-          if (before)
-            lo = mid + 1;
-          else
-            hi = mid;
-        }
-        rank += lo;
+    const float s = ms[l * p.P + j];
+    int rank = j;
+    for (int q = 0; q < p.L; ++q) {
+      if (q == l) continue;
+      int lo = 0, hi = cnt_s[q];
+      // count of survivors of level q ordered before (s, this level)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const float o = ms[q * p.P + mid];
+        const bool before = q < l ? (o >= s) : (o > s);
+        if (before)
+          lo = mid + 1;
+        else
+          hi = mid;
       }
-      if (rank >= p.max_num) continue;
+      rank += lo;
     }
-    merge_write(p, b, seg, pos, rank, s);
+    if (rank < p.max_num) merge_write(p, b, seg, pos, rank, s);
   }
 }
 

@@ -1,6 +1,7 @@
 // TOOLS-ONLY entry points (tools/lib/libfrcnn_tools.so; never linked into the product
 // library).  RoIAlign forward laboratory: the product's forward kernel and a per-wave
-// timestamped build of it (tools/bench_roi_align.py).
+// timestamped build of it (tools/bench_roi_align.py); the NMS scan's stamped build
+// (tools/bench_nms.py).
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -19,6 +20,14 @@ int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const flo
                                   int32_t aligned, float* out, void* workspace, size_t ws_bytes, void* stream);
 /* workspace bytes of frh_roi_align_fwd_variant for num_rois RoIs */
 size_t frh_roi_align_workspace(int64_t num_rois);
+
+/* frh_nms_sorted with the stamped scan build: per (segment, column block) 8 int64 of
+ * s_memrealtime (100 MHz) at stamps + (s * ceil(n_max / 64) + b) * 8 -- resolver starts
+ * waiting, block ready seen, block resolved, loader fold published, loader copies issued. */
+int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
+                               int32_t n_max, double iou_thr, int32_t max_keep, int32_t* keep,
+                               int64_t keep_seg_stride, int32_t* keep_counts, void* workspace, size_t ws_bytes,
+                               int64_t* stamps, void* stream);
 
 #ifdef __cplusplus
 }

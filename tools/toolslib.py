@@ -1,6 +1,6 @@
 """ctypes loader of the TOOLS-ONLY library tools/lib/libfrcnn_tools.so (see
 tools/build_tools.py): the product ABI (frcnn_amd._lib.SIGNATURES) plus the RoIAlign
-laboratory entry points of tools/csrc/frcnn_tools.h.  Used by tools/bench_roi_align.py and
+laboratory entry points of tools/csrc/frcnn_tools.h.  Used by tools/bench_roi_align.py, tools/bench_nms.py and
 tests/test_abi.py only; never by the product."""
 import ctypes
 import os
@@ -16,6 +16,8 @@ _RA = [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp, c
 TOOL_SIGNATURES = {
     'frh_roi_align_fwd_variant': (c_i32, [c_i32] + _RA + [c_vp, c_vp, c_size, c_vp]),
     'frh_roi_align_workspace': (c_size, [c_i64]),
+    'frh_nms_sorted_stamped': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, ctypes.c_double, c_i32, c_vp, c_i64, c_vp,
+                                       c_vp, c_size, c_vp, c_vp]),
 }
 _lib_t = None
 
