@@ -248,6 +248,154 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
   tk_collect_chunk(sb.tk, v, n, plan, pol, sm);
 }
 
+// Small images (num_boxes <= kSsMax, e.g. the RCNN stage's ~2000 proposal rows): the whole
+// sampler of an image in ONE 1024-thread workgroup -- the same keys (hash of (seed, 2s or
+// 2s + 1, box)), the same selection (the k largest keys, equal keys by ascending box), by
+// an exact radix select over the keys held in registers: per 8-bit digit, an LDS
+// histogram of the keys still tied with the threshold prefix, the digit holding the k-th
+// key found by one wave, until the tied bucket is taken whole or the full key is fixed.
+// No global round trips between the label loads and the outputs.
+constexpr int kSsThreads = 1024;
+constexpr int kSsPer = 16;
+constexpr int kSsMax = kSsThreads * kSsPer;
+
+struct SsPlan {
+  uint32_t P;  // threshold prefix (pb bits)
+  int pb;      // prefix bits fixed (0, 8, .., 32)
+  int k;       // keys with prefix == P still to take
+  int all;     // every key with prefix == P is taken
+};
+
+// Exact top-k plan over the nonzero keys key[r] of the workgroup (k >= 1, k < #nonzero).
+// Block-uniform call.
+__device__ SsPlan ss_plan(const uint32_t (&key)[kSsPer], int k, uint32_t* h, int* sh) {
+  const int t = threadIdx.x;
+  uint32_t P = 0u;
+  int pb = 0;
+  for (;;) {
+    for (int i = t; i < 256; i += kSsThreads) h[i] = 0u;
+    __syncthreads();
+    const int sh_digit = 24 - pb;
+#pragma unroll
+    for (int r = 0; r < kSsPer; ++r) {
+      const bool in = key[r] != 0u && (pb == 0 || (key[r] >> (32 - pb)) == P);
+      if (in) atomicAdd(&h[(key[r] >> sh_digit) & 255u], 1u);
+    }
+    __syncthreads();
+    if (t < kWave) {  // wave 0: lane l holds digits 255 - 4l .. 252 - 4l (descending)
+      uint32_t c[4], sum = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sum += (c[q] = h[255 - 4 * t - q]);
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o, kWave);
+        if (t >= o) incl += x;
+      }
+      uint32_t run = incl - sum;  // keys with a larger digit than this lane's first
+      if (run < (uint32_t)k && incl >= (uint32_t)k) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (run + c[q] >= (uint32_t)k) {
+            sh[0] = 255 - 4 * t - q;  // the digit holding the k-th key
+            sh[1] = (int)run;         // keys above it
+            sh[2] = (int)c[q];        // keys in it
+            break;
+          }
+          run += c[q];
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t d = (uint32_t)sh[0];
+    const int above = sh[1], inb = sh[2];
+    __syncthreads();  // sh reused by the next level
+    P = (P << 8) | d;
+    pb += 8;
+    k -= above;
+    if (inb == k || pb == 32) return SsPlan{P, pb, k, inb == k};
+  }
+}
+
+// grid (2, images): workgroup (w, s) selects image s's positives (w = 0) or negatives
+// (w = 1), so only its own class's keys are hashed; both count both classes (kn depends on
+// kp).  Box labels: the positives' workgroup writes positives and ignored boxes, the
+// negatives' workgroup negatives.
+__global__ void __launch_bounds__(kSsThreads) sampler_small_kernel(const int64_t* lab_in, int64_t lstride,
+                                                                   const int32_t* num, int max_num, int pos_num,
+                                                                   uint64_t seed, int64_t* lab_out, int32_t* sel,
+                                                                   int64_t sel_ld, int32_t* sel_cnt) {
+  __shared__ uint32_t h[256];
+  __shared__ int scratch[kSsThreads / kWave];
+  __shared__ int sh[4];
+  __shared__ int slot;
+  __shared__ int part[kSsThreads / kWave];
+  const int w = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
+  const int v = 2 * s + w;
+  const int n = num[s];
+  int64_t lab[kSsPer];
+  uint32_t key[kSsPer];
+  int cnt[2] = {0, 0};
+#pragma unroll
+  for (int r = 0; r < kSsPer; ++r) {
+    const int i = r * kSsThreads + t;
+    lab[r] = i < n ? lab_in[(int64_t)s * lstride + i] : -1;
+  }
+#pragma unroll
+  for (int r = 0; r < kSsPer; ++r) {
+    const int i = r * kSsThreads + t;
+    const bool pos = lab[r] > 0, neg = lab[r] == 0;
+    cnt[0] += pos;
+    cnt[1] += neg;
+    key[r] = (w == 0 ? pos : neg) ? ((~hash_u32(seed, (uint32_t)v, (uint32_t)i)) | 1u) : 0u;
+  }
+  const int npos = block_sum(cnt[0], scratch), nneg = block_sum(cnt[1], scratch);
+  const int kp = npos < pos_num ? npos : pos_num;
+  const int kn = nneg < max_num - kp ? nneg : max_num - kp;
+  const int k = w == 0 ? kp : kn, c = w == 0 ? npos : nneg;
+  uint32_t take = 0u;  // bit r: element r taken
+  if (k > 0 && k >= c) {  // every candidate
+#pragma unroll
+    for (int r = 0; r < kSsPer; ++r) take |= key[r] != 0u ? 1u << r : 0u;
+  } else if (k > 0) {
+    const SsPlan pl = ss_plan(key, k, h, sh);
+    const int sh_p = 32 - pl.pb;
+    uint32_t tie = 0u;
+#pragma unroll
+    for (int r = 0; r < kSsPer; ++r) {
+      const uint32_t pre = key[r] >> sh_p;
+      if (key[r] != 0u && pre > pl.P) take |= 1u << r;
+      if (key[r] != 0u && pre == pl.P) tie |= 1u << r;
+    }
+    if (pl.all) {
+      take |= tie;
+    } else {  // the first pl.k tied keys by ascending box (box = r * kSsThreads + t)
+      int before = 0;
+      for (int r = 0; r < kSsPer; ++r) {
+        int tot;
+        const bool f = (tie >> r) & 1u;
+        const int rk = block_rank(f, part, &tot);
+        if (f && before + rk < pl.k) take |= 1u << r;
+        before += tot;
+      }
+    }
+  }
+  if (t == 0) slot = 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSsPer; ++r) {
+    const int i = r * kSsThreads + t;
+    const bool tk = (take >> r) & 1u;
+    const bool mine = w == 0 ? lab[r] != 0 : lab[r] == 0;  // positives + ignored, or negatives
+    if (lab_out && i < n && mine) lab_out[(int64_t)s * lstride + i] = tk ? lab[r] : -1;
+    if (sel) {
+      const int sp = wave_append(tk, &slot);
+      if (tk) sel[(int64_t)v * sel_ld + sp] = i;
+    }
+  }
+  if (sel && t == 0) sel_cnt[v] = k > 0 ? k : 0;
+}
+
 int32_t launch_compact_lists(int32_t S, const int64_t* labels, int64_t label_seg_stride,
                              const int32_t* num, int64_t max_n, int npred, const int* preds,
                              int32_t** lists, int64_t list_seg_stride, int32_t* counts,
@@ -350,6 +498,12 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
   FRH_REQUIRE(max_boxes <= INT32_MAX, "max_boxes must fit in int32");
   static_assert(kSampBins == kTkThreads, "sampler_collect_kernel sums one bin per thread");
   hipStream_t st = as_stream(stream);
+  if (max_boxes <= kSsMax) {  // one workgroup per image, one launch
+    hipLaunchKernelGGL(sampler_small_kernel, dim3(2u, (unsigned)num_segs), dim3(kSsThreads), 0, st, labels_in,
+                       label_seg_stride, num_boxes, max_num, pos_num, seed, labels_out, sel,
+                       (int64_t)(max_num > 0 ? max_num : 1), sel_counts);
+    return check_launch("frh_sample_random");
+  }
   char* ws = reinterpret_cast<char*>(workspace);
   SampLayout z = samp_layout(num_segs, max_boxes);
   const int V = 2 * num_segs;

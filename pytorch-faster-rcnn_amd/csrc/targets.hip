@@ -148,11 +148,11 @@ __global__ void anchor_target_kernel(AnchorTargetArgs p) {
 // box order: each item's output position is the number of listed boxes below it (rank by
 // counting over the list staged in LDS) -- the reference's nonzero(labels >= 0) order
 // (anchor.py:49-50, bbox.py:52-58) without a compaction pass over every box.
-// Dynamic LDS: 2 * sel_ld int32.
+// Dynamic LDS: 2 * sel_ld + 4 int32.
 template <class F>
 __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32_t* sel_cnt, int64_t sel_ld, int S,
                                                  int32_t* out_counts, F&& item) {
-  extern __shared__ int32_t su[];
+  extern __shared__ __attribute__((aligned(16))) int32_t su[];
   const int s = blockIdx.y;
   const int np = sel_cnt[2 * s], cnt = np + sel_cnt[2 * s + 1];
   int64_t off = 0;
@@ -164,13 +164,18 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
   if ((int64_t)blockIdx.x * blockDim.x >= cnt) return;  // uniform per workgroup
   const int32_t* pos = sel + (int64_t)(2 * s) * sel_ld;
   const int32_t* neg = pos + sel_ld;
-  for (int q = threadIdx.x; q < cnt; q += blockDim.x) su[q] = q < np ? pos[q] : neg[q - np];
+  const int cnt4 = (cnt + 3) & ~3;  // padded with INT32_MAX (never below an index): 16-B LDS reads
+  for (int q = threadIdx.x; q < cnt4; q += blockDim.x) su[q] = q < np ? pos[q] : (q < cnt ? neg[q - np] : INT32_MAX);
   __syncthreads();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= cnt) return;
   const int32_t x = su[j];
   int rank = 0;
-  for (int q = 0; q < cnt; ++q) rank += su[q] < x;
+  const int4* s4 = reinterpret_cast<const int4*>(su);
+  for (int q = 0; q < cnt4 / 4; ++q) {
+    const int4 v = s4[q];
+    rank += (v.x < x) + (v.y < x) + (v.z < x) + (v.w < x);
+  }
   item(s, (int64_t)x, off + rank);
 }
 
@@ -386,13 +391,13 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
   hipStream_t st = as_stream(stream);
   unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
   if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
-    FRH_REQUIRE(2 * max_out_per_seg * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
+    FRH_REQUIRE((2 * max_out_per_seg + 4) * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
     AnchorTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, anchors, anchor_ld, anchor_seg_stride,
                        gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                        max_out_per_seg, chosen_idx, seg_of, tar_labels, tar_anchors, tar_bbox, tar_param, out_ld,
                        out_counts, num_segs, sel, sel_counts, max_out_per_seg};
     hipLaunchKernelGGL(anchor_target_sel_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256),
-                       2 * max_out_per_seg * sizeof(int32_t), st, p);
+                       (2 * max_out_per_seg + 4) * sizeof(int32_t), st, p);
     return check_launch("frh_anchor_target");
   }
   FRH_REQUIRE(workspace && ws_bytes >= frh_anchor_target_workspace(num_segs, max_boxes), "workspace too small");
@@ -495,13 +500,13 @@ extern "C" int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int6
   hipStream_t st = as_stream(stream);
   unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
   if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
-    FRH_REQUIRE(2 * max_out_per_seg * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
+    FRH_REQUIRE((2 * max_out_per_seg + 4) * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
     BBoxTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, num_gts, props, prop_ld, prop_seg_stride,
                      gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                      max_out_per_seg, tar_props, tar_bbox, tar_param, tar_label, tar_is_gt, out_ld, out_counts,
                      num_segs, sel, sel_counts, max_out_per_seg};
     hipLaunchKernelGGL(bbox_target_sel_kernel, dim3(gx > 0 ? gx : 1, (unsigned)num_segs), dim3(256),
-                       2 * max_out_per_seg * sizeof(int32_t), st, p);
+                       (2 * max_out_per_seg + 4) * sizeof(int32_t), st, p);
     return check_launch("frh_bbox_target");
   }
   FRH_REQUIRE(workspace && ws_bytes >= frh_bbox_target_workspace(num_segs, max_rows), "workspace too small");

@@ -277,16 +277,20 @@ def _hash_u32(seed, a, b):
     return (z >> np.uint64(32)).astype(np.uint32)
 
 
-def test_device_sampler_selects_top_hash_keys(dev):
+@pytest.mark.parametrize('n,max_num,pos_num', [(200003, 256, 128), (2050, 512, 128), (16384, 512, 128),
+                                               (3000, 4000, 1000)])
+def test_device_sampler_selects_top_hash_keys(dev, n, max_num, pos_num):
     """The device sampler's selection is exactly its definition: per image, the kp = min(npos,
     pos_num) positives and kn = min(nneg, max_num - kp) negatives with the largest keys
-    (~hash(seed, 2s (+1), box) | 1), ties by box index -- recomputed here in numpy."""
+    (~hash(seed, 2s (+1), box) | 1), ties by box index -- recomputed here in numpy.  Images
+    up to 16384 boxes take the one-workgroup radix select, larger ones the two-launch
+    segmented top-k."""
     from frcnn_amd import ops
     rng = np.random.default_rng(21)
-    S, n, max_num, pos_num = 3, 200003, 256, 128
-    lab = rng.choice([-1, 0, 1], size=(S, n), p=[0.4, 0.59, 0.01]).astype(np.int64)
+    S = 3
+    lab = rng.choice([-1, 0, 1], size=(S, n), p=[0.4, 0.5, 0.1] if n < 20000 else [0.4, 0.59, 0.01]).astype(np.int64)
     lab[1, :] = np.where(lab[1] > 0, -1, lab[1])  # no positives
-    num = torch.tensor([n, n - 11, 70000], dtype=torch.int32, device=dev)
+    num = torch.tensor([n, n - 11, n // 3], dtype=torch.int32, device=dev)
     ops.set_sampler_mode('device', seed=5)
     out = ops.sample_labels(T(lab, dev), num, n, max_num, pos_num, mode='device').cpu().numpy()
     seed = (ops._SAMPLER['seed'] * 0x9E3779B97F4A7C15 + ops._SAMPLER['calls']) & 0xFFFFFFFFFFFFFFFF
@@ -306,15 +310,15 @@ def test_device_sampler_selects_top_hash_keys(dev):
         np.testing.assert_array_equal(out[s, :ns], want)
 
 
-@pytest.mark.parametrize('max_num,pos_num', [(256, 128), (512, 128)])
-def test_device_sampler_lists_feed_targets(dev, max_num, pos_num):
+@pytest.mark.parametrize('max_num,pos_num,n', [(256, 128, 20000), (512, 128, 20000), (512, 128, 3000)])
+def test_device_sampler_lists_feed_targets(dev, max_num, pos_num, n):
     """The device sampler's selection lists (frh_sample_random sel / sel_counts) fed straight
     into the target gathers (rank-by-counting into ascending box order, no compaction pass)
     give exactly the targets of the sampled-labels path (labels >= 0 compacted in order), for
     the same draw; also for an image with fewer candidates than slots and an empty one."""
     from frcnn_amd import ops
     rng = np.random.default_rng(8)
-    S, n = 4, 20000
+    S = 4
     lab = rng.choice([-1, 0, 1, 2, 3], size=(S, n), p=[0.3, 0.6, 0.04, 0.03, 0.03]).astype(np.int64)
     lab[3, :] = np.where(lab[3] >= 0, -1, lab[3])
     lab[3, :40] = 0  # 40 candidates for max_num slots
