@@ -296,9 +296,12 @@ __device__ __forceinline__ void merge_write(const MergeArgs& p, int b, int seg, 
 // One 1024-thread workgroup per (level, image): the image's survivor scores of every
 // level are gathered into LDS first (L * P floats; each thread's keep-index loads in
 // flight together, then its score gathers), so the searches are LDS reads, not chains
-// of dependent global loads.
+// of dependent global loads.  The workgroup's own survivors (j = t, t + 1024) are loaded
+// by the threads that rank them -- keep index, then score and box together -- so their
+// outputs need no further loads.
 constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;  // gathered scores per thread and batch
+constexpr int kMergeOwn = 2;   // own survivors per thread (post_nms <= 2048)
 
 static __global__ void __launch_bounds__(kMergeThreads) rpn_merge_lds_kernel(MergeArgs p) {
   extern __shared__ float ms[];  // [L][P] survivor scores of image b
@@ -313,6 +316,23 @@ static __global__ void __launch_bounds__(kMergeThreads) rpn_merge_lds_kernel(Mer
   }
   const bool cut = p.max_num > 0 && total > p.max_num;
   if (l == 0 && t == 0) p.out_counts[b] = cut ? p.max_num : total;
+  const int seg = b * p.L + l, cnt = cnt_s[l];
+  // own survivors: keep index, then score + box (in flight with the staging gathers below)
+  int own_pos[kMergeOwn];
+#pragma unroll
+  for (int u = 0; u < kMergeOwn; ++u) {
+    const int j = t + u * kMergeThreads;
+    own_pos[u] = j < cnt ? p.keep[(int64_t)seg * p.P + j] : -1;
+  }
+  float own_s[kMergeOwn];
+  float4 own_bx[kMergeOwn];
+#pragma unroll
+  for (int u = 0; u < kMergeOwn; ++u) {
+    if (own_pos[u] >= 0) {
+      own_s[u] = p.sel_scores[(int64_t)seg * p.P + own_pos[u]];
+      own_bx[u] = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + own_pos[u]];
+    }
+  }
   if (cut) {
     // flat index e over (level, survivor), e = q * P + i
     for (int e0 = 0; e0 < p.L * p.P; e0 += kMergeThreads * kMergePer) {
@@ -330,34 +350,37 @@ static __global__ void __launch_bounds__(kMergeThreads) rpn_merge_lds_kernel(Mer
     }
     __syncthreads();
   }
-  const int seg = b * p.L + l;
-  if (!cut) {  // everything fits: rank = concatenation position (a separate loop: no pointer select)
-    for (int j = t; j < cnt_s[l]; j += kMergeThreads) {
-      const int pos = p.keep[(int64_t)seg * p.P + j];
-      merge_write(p, b, seg, pos, base + j, p.sel_scores[(int64_t)seg * p.P + pos]);
-    }
-    return;
-  }
-  for (int j = t; j < cnt_s[l]; j += kMergeThreads) {
-    const int pos = p.keep[(int64_t)seg * p.P + j];
-    const float s = ms[l * p.P + j];
-    int rank = j;
-    for (int q = 0; q < p.L; ++q) {
-      if (q == l) continue;
-      int lo = 0, hi = cnt_s[q];
-      // count of survivors of level q ordered before (s, this level)
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const float o = ms[q * p.P + mid];
-        const bool before = q < l ? (o >= s) : (o > s);
-        if (before)
-          lo = mid + 1;
-        else
-          hi = mid;
+  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
+#pragma unroll
+  for (int u = 0; u < kMergeOwn; ++u) {
+    const int j = t + u * kMergeThreads;
+    if (own_pos[u] < 0) continue;
+    const float s = own_s[u];
+    int rank = base + j;
+    if (cut) {
+      rank = j;
+      for (int q = 0; q < p.L; ++q) {
+        if (q == l) continue;
+        int lo = 0, hi = cnt_s[q];
+        // count of survivors of level q ordered before (s, this level)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const float o = ms[q * p.P + mid];
+          const bool before = q < l ? (o >= s) : (o > s);
+          if (before)
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        rank += lo;
       }
-      rank += lo;
+      if (rank >= p.max_num) continue;
     }
-    if (rank < p.max_num) merge_write(p, b, seg, pos, rank, s);
+    ob[rank] = own_bx[u].x;
+    ob[p.out_cap + rank] = own_bx[u].y;
+    ob[2 * p.out_cap + rank] = own_bx[u].z;
+    ob[3 * p.out_cap + rank] = own_bx[u].w;
+    p.out_scores[(int64_t)b * p.out_cap + rank] = s;
   }
 }
 
@@ -553,7 +576,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};
   const size_t merge_lds = (size_t)num_levels * z.P * sizeof(float);
-  if (merge_lds <= 65536 - 256) {  // + the kernel's static counts
+  if (merge_lds <= 65536 - 256 && z.P <= kMergeThreads * kMergeOwn) {  // + the kernel's static counts
     hipLaunchKernelGGL(rpn_merge_lds_kernel, dim3((unsigned)num_levels, (unsigned)num_imgs), dim3(kMergeThreads),
                        merge_lds, st, mp);
   } else {
