@@ -411,6 +411,20 @@ int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
                           int64_t n, int64_t m, int64_t n_sel, float beta,
                           const float* grad_out, float* grad_x, int64_t gs_i, int64_t gs_j,
                           int64_t gs_l, void* stream);
+/* One head's two losses in ONE launch, scaled as the heads scale them: out[0] =
+ * (cls_sum * cls_weight) / cls_div, out[1] = (reg_sum * reg_weight) / reg_div (f32), cls_sum
+ * as frh_cls_loss_fwd, reg_sum as frh_smooth_l1_fwd (both sums bit-identical to theirs).
+ * Replaces `loss_cls(...) / avg_factor` and `loss_bbox.masked / class_selected(...) /
+ * avg_factor` of AnchorHead.calc_loss (anchor_head.py:113-139) and BBoxHead.calc_loss
+ * (bbox_head.py:56-87) with a sampler (avg_factor = the sample count, a host value).
+ * Workspace as frh_cls_loss_fwd.  Backward: frh_cls_loss_bwd / frh_smooth_l1_bwd. */
+int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr, int64_t sc,
+                         const void* target, int32_t target_is_float, float alpha, float gamma,
+                         float cls_weight, float cls_div, const float* rx, int64_t xs_i,
+                         int64_t xs_j, int64_t xs_l, const float* ry, int64_t ys_i, int64_t ys_j,
+                         const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel, float beta,
+                         float reg_weight, float reg_div, float* out, void* workspace,
+                         size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- f4: image pipeline
  * The train/test pipelines of configs/faster_rcnn_r50_fpn.py:120-139 (mmdet v1: Resize

@@ -34,6 +34,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace frh {
 namespace {
 
@@ -276,6 +278,104 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_bwd_kernel(L1Args a, c
   }
 }
 
+// Classification + regression loss of one head in ONE launch (AnchorHead / BBoxHead
+// calc_loss with a sampler: anchor_head.py:113-139, bbox_head.py:56-87).  Workgroup b
+// takes the cls elements of workgroup b of cls_loss_fwd_kernel's grid (b < nbc) and the
+// smooth-L1 elements of workgroup b of smooth_l1_fwd_kernel's grid (b < nbr); the last
+// workgroup to arrive sums each loss's partials in the fixed order of fan_in_finalize,
+// so both sums equal the separate launches' bit for bit, and applies the heads' scaling
+// as torch does it: loss = (sum * loss_weight) / avg_factor in f32.
+struct DetScale {
+  float wc, dc, wr, dr;
+  float* out;  // [2]: cls, reg
+};
+
+__device__ void det_fan_in(float pc, float pr, uint32_t* counter, float* partial, int nbc, int nbr,
+                           const DetScale& o) {
+  __shared__ double s[kLossThreads];
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partial + kMaxPartials + blockIdx.x, pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  float res[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int nb = q ? nbr : nbc;
+    const float* p = partial + q * kMaxPartials;
+    double v = 0.0;
+    for (int j = threadIdx.x; j < nb; j += kLossThreads)
+      v += (double)__hip_atomic_load(const_cast<float*>(p + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = kLossThreads / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+      __syncthreads();
+    }
+    res[q] = (float)s[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    o.out[0] = (res[0] * o.wc) / o.dc;
+    o.out[1] = (res[1] * o.wr) / o.dr;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int kKind>
+__global__ void __launch_bounds__(kLossThreads) det_loss_fwd_kernel(ClsArgs a, int nbc, L1Args r, int nbr,
+                                                                    uint32_t* counter, float* partial, DetScale o) {
+  __shared__ float scratch[kLossThreads / kWave];
+  float acc = 0.0f;
+  if ((int)blockIdx.x < nbc) {
+    if constexpr (kKind == kSoftmaxCe) {
+      for (int64_t i = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; i < a.n; i += (int64_t)nbc * kLossThreads) {
+        const float* row = a.x + i * a.sr;
+        float m = -INFINITY;
+        for (int64_t k = 0; k < a.c; ++k) m = fmaxf(m, row[k * a.sc]);
+        float sm = 0.0f;
+        for (int64_t k = 0; k < a.c; ++k) sm += expf(row[k * a.sc] - m);
+        int64_t l = label_at(a, i);
+        float xl = (l >= 0 && l < a.c) ? row[l * a.sc] : NAN;
+        acc += (logf(sm) + m) - xl;
+      }
+    } else {
+      const int64_t total = a.n * a.c;
+      for (int64_t e = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; e < total;
+           e += (int64_t)nbc * kLossThreads) {
+        int64_t i, k;
+        elem_index(a, e, &i, &k);
+        float x = a.x[i * a.sr + k * a.sc];
+        float t = elem_target(a, i, k);
+        acc += kKind == kFocal ? focal_elem(x, t, a.alpha, a.gamma, nullptr) : bce_logits(x, t);
+      }
+    }
+  }
+  float accr = 0.0f;
+  if ((int)blockIdx.x < nbr) {
+    const int64_t total = r.n * r.m;
+    for (int64_t e = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; e < total; e += (int64_t)nbr * kLossThreads) {
+      int64_t i = e / r.m, j = e - i * r.m, off;
+      if (!l1_row(r, i, &off)) continue;
+      if (r.xs_l && (r.label[i] >= r.n_sel)) {
+        accr += NAN;
+        continue;
+      }
+      float d = fabsf(r.x[off + j * r.xs_j] - r.y[i * r.ys_i + j * r.ys_j]);
+      accr += d < r.beta ? (d * d) / (2.0f * r.beta) : d - 0.5f * r.beta;
+    }
+  }
+  const float pc = block_sum_f(acc, scratch);
+  __syncthreads();
+  const float pr = block_sum_f(accr, scratch);
+  det_fan_in(pc, pr, counter, partial, nbc, nbr, o);
+}
+
 
 int grid_for(int64_t work) {
   int64_t b = (work + kLossThreads - 1) / kLossThreads;
@@ -343,7 +443,7 @@ using namespace frh;
 
 extern "C" {
 
-size_t frh_loss_workspace(void) { return kCounterBytes + kMaxPartials * sizeof(float); }
+size_t frh_loss_workspace(void) { return kCounterBytes + 2 * kMaxPartials * sizeof(float); }
 
 static FanIn fan_in(void* workspace, float* out) {
   char* w = static_cast<char*>(workspace);
@@ -403,6 +503,38 @@ int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
   hipLaunchKernelGGL(smooth_l1_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, as_stream(stream), a,
                      fan_in(workspace, out));
   return check_launch("frh_smooth_l1_fwd");
+}
+
+int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr, int64_t sc,
+                         const void* target, int32_t target_is_float, float alpha, float gamma, float cls_weight,
+                         float cls_div, const float* rx, int64_t xs_i, int64_t xs_j, int64_t xs_l, const float* ry,
+                         int64_t ys_i, int64_t ys_j, const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel,
+                         float beta, float reg_weight, float reg_div, float* out, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  ClsArgs a = make_cls(x, n, c, sr, sc, target, target_is_float, alpha, gamma);
+  int32_t st = check_cls(kind, a);
+  if (st != FRH_OK) return st;
+  L1Args r = make_l1(rx, xs_i, xs_j, xs_l, ry, ys_i, ys_j, label, rn, rm, n_sel, beta);
+  st = check_l1(r);
+  if (st != FRH_OK) return st;
+  FRH_REQUIRE(out, "det loss: null output");
+  FRH_REQUIRE(workspace && ws_bytes >= frh_loss_workspace(), "det loss: workspace too small");
+  const int nbc = grid_for(kind == kSoftmaxCe ? n : n * c), nbr = grid_for(rn * rm);
+  char* w = static_cast<char*>(workspace);
+  uint32_t* counter = reinterpret_cast<uint32_t*>(w);
+  float* partial = reinterpret_cast<float*>(w + kCounterBytes);
+  const DetScale o{cls_weight, cls_div, reg_weight, reg_div, out};
+  const dim3 g((unsigned)std::max(nbc, nbr));
+  hipStream_t s = as_stream(stream);
+  if (kind == kFocal)
+    hipLaunchKernelGGL(det_loss_fwd_kernel<kFocal>, g, dim3(kLossThreads), 0, s, a, nbc, r, nbr, counter, partial, o);
+  else if (kind == kSigmoidBce)
+    hipLaunchKernelGGL(det_loss_fwd_kernel<kSigmoidBce>, g, dim3(kLossThreads), 0, s, a, nbc, r, nbr, counter, partial,
+                       o);
+  else
+    hipLaunchKernelGGL(det_loss_fwd_kernel<kSoftmaxCe>, g, dim3(kLossThreads), 0, s, a, nbc, r, nbr, counter, partial,
+                       o);
+  return check_launch("frh_det_loss_fwd");
 }
 
 int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l, const float* y, int64_t ys_i,

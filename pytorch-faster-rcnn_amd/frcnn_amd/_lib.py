@@ -94,6 +94,9 @@ SIGNATURES = {
                                   c_vp, c_vp, c_size, c_vp]),
     'frh_smooth_l1_bwd': (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
                                   c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    'frh_det_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32,
+                                 c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
+                                 c_f32, c_f32, c_vp, c_vp, c_size, c_vp]),
     'frh_atss_assign': (c_i32, [c_i32, c_i32, P(c_i32), P(c_f32), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32,
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }

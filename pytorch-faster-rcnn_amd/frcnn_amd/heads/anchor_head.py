@@ -126,6 +126,11 @@ class AnchorHead(nn.Module):
         sampling = 'sampler' in train_cfg
         avg_factor = len(tar_labels) if sampling else (tar_labels > 0).sum()
         if tar_labels.numel() != 0:
+            # both losses and their scaling in one launch (HIP losses, sampled avg_factor)
+            fused = losses.head_losses(self.loss_cls, self.loss_bbox, tar_cls_out.t(), tar_labels,
+                                       lambda: ops._l1_args(tar_reg_out, tar_param, tar_labels, 1), avg_factor)
+            if fused is not None:
+                return fused
             cls_loss = self.loss_cls(tar_cls_out.t(), tar_labels) / avg_factor
             if isinstance(self.loss_bbox, losses.SmoothL1Loss):
                 # fused masked smooth-L1 over the positive columns of [4, S] (one kernel, no sync)

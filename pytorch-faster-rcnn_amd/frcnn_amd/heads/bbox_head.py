@@ -40,6 +40,14 @@ class BBoxHead(nn.Module):
             logging.warning('return zero loss due to zero avg_factor')
             return cls_loss, reg_loss
         if tar_label.numel() != 0:
+            # both losses and their scaling in one launch (HIP losses, sampled avg_factor)
+            if self.reg_class_agnostic:
+                l1 = lambda: ops._l1_args(reg_out, tar_param.t(), tar_label, 0)  # noqa: E731
+            else:
+                l1 = lambda: ops._l1_class_select_args(reg_out, self.num_classes, tar_param.t(), tar_label)  # noqa: E731
+            fused = losses.head_losses(self.loss_cls, self.loss_bbox, cls_out, tar_label, l1, avg_factor)
+            if fused is not None:
+                return fused
             cls_loss = self.loss_cls(cls_out, tar_label) / avg_factor
             if isinstance(self.loss_bbox, losses.SmoothL1Loss):
                 # fused class selection + positive-row mask + smooth-L1 (one kernel each way)

@@ -119,6 +119,24 @@ class CrossEntropyLoss(nn.Module):
         return F.cross_entropy(pred, label, reduction='none').sum() * self.loss_weight
 
 
+def head_losses(loss_cls, loss_bbox, cls_x, cls_label, l1_args, avg_factor):
+    """(loss_cls(cls_x, cls_label) / avg_factor, loss_bbox.<masked | class_selected>(...) /
+    avg_factor) as ONE HIP launch (ops.det_losses) when both modules are the HIP-backed
+    kinds, the tensors are on the GPU and avg_factor is a host number (the sampled count);
+    l1_args() builds the regression loss's arguments.  None when it does not apply (the
+    caller then runs the modules one by one)."""
+    if not (cls_x.is_cuda and isinstance(loss_bbox, SmoothL1Loss)) or isinstance(avg_factor, torch.Tensor):
+        return None
+    if isinstance(loss_cls, FocalLoss):
+        kind, alpha, gamma = ops.CLS_FOCAL, loss_cls.alpha, loss_cls.gamma
+    elif isinstance(loss_cls, CrossEntropyLoss):
+        kind, alpha, gamma = (ops.CLS_SIGMOID_BCE if loss_cls.use_sigmoid else ops.CLS_SOFTMAX_CE), 0.25, 2.0
+    else:
+        return None
+    return ops.det_losses(cls_x, cls_label.reshape(-1), kind, alpha, gamma, loss_cls.loss_weight, l1_args(),
+                          loss_bbox.beta, loss_bbox.loss_weight, avg_factor)
+
+
 class GIoULoss(nn.Module):
     def __init__(self, loss_weight=1.0):
         super().__init__()

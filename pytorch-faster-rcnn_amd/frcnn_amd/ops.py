@@ -864,9 +864,8 @@ class _SmoothL1(torch.autograd.Function):
         return gx, None, None, None, None, None, None, None, None
 
 
-def smooth_l1_loss(x, y, beta, label=None, rows_dim=0):
-    """Summed smooth_l1_loss_v2 of x and y (same shape, 2-D, rows along `rows_dim`),
-    counting only rows whose label is > 0 when `label` is given (frh_smooth_l1_fwd/bwd)."""
+def _l1_args(x, y, label, rows_dim):
+    """(x, y, label, x strides, y strides, n, m, n_sel) of a masked smooth-L1 sum."""
     _need_cuda(x, y, label)
     if x.shape != y.shape or x.dim() != 2:
         raise AssertionError('smooth_l1_loss: x and y must be equal 2-D shapes')
@@ -878,13 +877,16 @@ def smooth_l1_loss(x, y, beta, label=None, rows_dim=0):
     if label is not None and label.numel() != n:
         raise AssertionError('smooth_l1_loss: one label per row expected')
     lab = label.contiguous().long() if label is not None else None
-    return _SmoothL1.apply(x, y, lab, (x.stride(rows_dim), x.stride(cd), 0), (y.stride(rows_dim), y.stride(cd)), n, m,
-                           1, beta)
+    return x, y, lab, (x.stride(rows_dim), x.stride(cd), 0), (y.stride(rows_dim), y.stride(cd)), n, m, 1
 
 
-def smooth_l1_class_select(reg_out, num_classes, target, label, beta):
-    """BBoxHead's regression loss: reg_out [n, 4*C] viewed [n, 4, C], the labelled class's
-    deltas of the positive rows against target [n, 4] (any strides), summed."""
+def smooth_l1_loss(x, y, beta, label=None, rows_dim=0):
+    """Summed smooth_l1_loss_v2 of x and y (same shape, 2-D, rows along `rows_dim`),
+    counting only rows whose label is > 0 when `label` is given (frh_smooth_l1_fwd/bwd)."""
+    return _SmoothL1.apply(*_l1_args(x, y, label, rows_dim), beta)
+
+
+def _l1_class_select_args(reg_out, num_classes, target, label):
     _need_cuda(reg_out, target, label)
     n = reg_out.shape[0]
     if reg_out.dim() != 2 or reg_out.shape[1] != 4 * num_classes or target.shape != (n, 4) or label.numel() != n:
@@ -893,5 +895,60 @@ def smooth_l1_class_select(reg_out, num_classes, target, label, beta):
     if reg_out.stride(1) != 1:
         reg_out = reg_out.contiguous()
     xs = (reg_out.stride(0), num_classes, 1)
-    return _SmoothL1.apply(reg_out, target, label.contiguous().long(), xs, (target.stride(0), target.stride(1)), n, 4,
-                           num_classes, beta)
+    return reg_out, target, label.contiguous().long(), xs, (target.stride(0), target.stride(1)), n, 4, num_classes
+
+
+def smooth_l1_class_select(reg_out, num_classes, target, label, beta):
+    """BBoxHead's regression loss: reg_out [n, 4*C] viewed [n, 4, C], the labelled class's
+    deltas of the positive rows against target [n, 4] (any strides), summed."""
+    return _SmoothL1.apply(*_l1_class_select_args(reg_out, num_classes, target, label), beta)
+
+
+class _DetLoss(torch.autograd.Function):
+    """A head's classification and regression losses in one launch (frh_det_loss_fwd),
+    each scaled as the heads scale it: (sum * weight) / avg_factor."""
+
+    @staticmethod
+    def forward(ctx, x, target, kind, alpha, gamma, wc, rx, ry, rlabel, xs, ys, rn, rm, n_sel, beta, wr, div):
+        n, c = x.shape
+        tfloat = int(target.dtype == torch.float32)
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        ws = _loss_workspace(x)
+        call('frh_det_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
+             float(gamma), float(wc), float(div), ptr(rx), xs[0], xs[1], xs[2], ptr(ry), ys[0], ys[1], ptr(rlabel), rn,
+             rm, n_sel, float(beta), float(wr), float(div), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+        ctx.save_for_backward(x, target, rx, ry, rlabel)
+        ctx.cfg = (kind, tfloat, alpha, gamma, wc, xs, ys, rn, rm, n_sel, beta, wr, div)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, gc, gr):
+        x, target, rx, ry, rlabel = ctx.saved_tensors
+        kind, tfloat, alpha, gamma, wc, xs, ys, rn, rm, n_sel, beta, wr, div = ctx.cfg
+        gx = grx = None
+        if gc is not None and ctx.needs_input_grad[0]:
+            g = _f32((gc / div) * wc).contiguous()  # the reference's Div then Mul backward
+            n, c = x.shape
+            gx = torch.empty_like(x)
+            call('frh_cls_loss_bwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
+                 float(gamma), ptr(g), ptr(gx), gx.stride(0), gx.stride(1), stream_of(x))
+        if gr is not None and ctx.needs_input_grad[6]:
+            g = _f32((gr / div) * wr).contiguous()
+            grx = torch.zeros_like(rx)
+            if grx.stride() != rx.stride():
+                raise AssertionError('det loss: gradient layout differs from the input')
+            call('frh_smooth_l1_bwd', ptr(rx), xs[0], xs[1], xs[2], ptr(ry), ys[0], ys[1], ptr(rlabel), rn, rm, n_sel,
+                 float(beta), ptr(g), ptr(grx), xs[0], xs[1], xs[2], stream_of(rx))
+        return gx, None, None, None, None, None, grx, None, None, None, None, None, None, None, None, None, None
+
+
+def det_losses(x, target, kind, alpha, gamma, cls_weight, l1_args, beta, reg_weight, avg_factor):
+    """(cls, reg) = (cls_loss(x, target, kind) * cls_weight / avg_factor,
+    smooth-L1(*l1_args) * reg_weight / avg_factor) in one launch; l1_args from _l1_args /
+    _l1_class_select_args.  avg_factor is a host number (the sampled count)."""
+    _need_cuda(x, target)
+    if target.dtype != torch.int64:
+        target = target.long()
+    rx, ry, rlabel, xs, ys, rn, rm, n_sel = l1_args
+    return _DetLoss.apply(_f32(x), target.contiguous(), int(kind), alpha, gamma, cls_weight, rx, ry, rlabel, xs, ys,
+                          rn, rm, n_sel, beta, reg_weight, float(avg_factor))

@@ -132,3 +132,54 @@ def test_bad_label_gives_nan():
     x = torch.randn(8, 5, device=DEV)
     lab = torch.tensor([0, 1, 2, 3, 4, 5, 0, 1], device=DEV)
     assert torch.isnan(ops.cls_loss(x, lab, ops.CLS_SOFTMAX_CE))
+
+
+@pytest.mark.parametrize('case', ['rpn_sigmoid', 'rpn_focal', 'rcnn_softmax_class_select', 'rcnn_agnostic'])
+def test_det_losses_one_launch_equal_separate(case):
+    """losses.head_losses (frh_det_loss_fwd: both losses of a head and their scaling in one
+    launch) must equal the separate modules divided by avg_factor BIT FOR BIT (same
+    partitioned sums, same f32 scaling), and give the same gradients (the reference's
+    Div-then-Mul backward)."""
+    g = torch.Generator().manual_seed(11)
+    beta = 1.0 / 9.0
+    if case.startswith('rpn'):
+        S = 512
+        c = 1 if case == 'rpn_sigmoid' else 20
+        lab = _labels(S, c, 0.25, g).to(DEV)
+        cls0 = (torch.randn(c, S, generator=g) * 2).to(DEV)       # AnchorHead: tar_cls_out [C, S]
+        reg0 = torch.randn(4, S, generator=g).to(DEV)             # tar_reg_out [4, S]
+        tgt = torch.randn(4, S, generator=g).to(DEV)
+        loss_cls = (losses.CrossEntropyLoss(use_sigmoid=True) if c == 1 else losses.FocalLoss())
+        l1 = lambda r: ops._l1_args(r, tgt, lab, 1)  # noqa: E731
+        sep_reg = lambda r: losses.SmoothL1Loss(beta).masked(r, tgt, lab, rows_dim=1)  # noqa: E731
+        cls_in = lambda x: x.t()  # noqa: E731
+    else:
+        n, C = 1024, 21
+        lab = _labels(n, C - 1, 0.25, g).to(DEV)
+        cls0 = torch.randn(n, C, generator=g).to(DEV)
+        loss_cls = losses.CrossEntropyLoss()
+        tgt = torch.randn(4, n, generator=g).to(DEV)              # tar_param [4, n]
+        if case == 'rcnn_agnostic':
+            reg0 = torch.randn(n, 4, generator=g).to(DEV)
+            l1 = lambda r: ops._l1_args(r, tgt.t(), lab, 0)  # noqa: E731
+            sep_reg = lambda r: losses.SmoothL1Loss(1.0).masked(r, tgt.t(), lab, rows_dim=0)  # noqa: E731
+        else:
+            reg0 = torch.randn(n, 4 * C, generator=g).to(DEV)
+            l1 = lambda r: ops._l1_class_select_args(r, C, tgt.t(), lab)  # noqa: E731
+            sep_reg = lambda r: losses.SmoothL1Loss(1.0).class_selected(r, C, tgt.t(), lab)  # noqa: E731
+        beta = 1.0
+        cls_in = lambda x: x  # noqa: E731
+    loss_bbox = losses.SmoothL1Loss(beta)
+    avg = lab.numel()
+    xa, xb = cls0.clone().requires_grad_(True), cls0.clone().requires_grad_(True)
+    ra, rb = reg0.clone().requires_grad_(True), reg0.clone().requires_grad_(True)
+    fa = losses.head_losses(loss_cls, loss_bbox, cls_in(xa), lab, lambda: l1(ra), avg)
+    assert fa is not None
+    ca, qa = fa
+    cb = loss_cls(cls_in(xb), lab) / avg
+    qb = sep_reg(rb) / avg
+    assert torch.equal(ca, cb) and torch.equal(qa, qb), (ca.item(), cb.item(), qa.item(), qb.item())
+    (ca * 0.7 + qa * 1.3).backward()
+    (cb * 0.7 + qb * 1.3).backward()
+    assert torch.equal(xa.grad, xb.grad)
+    assert torch.equal(ra.grad, rb.grad)

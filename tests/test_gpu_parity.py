@@ -568,6 +568,32 @@ def test_nms_empty_and_batched(dev):
     np.testing.assert_array_equal(ks.cpu().numpy(), scores[k])
 
 
+@pytest.mark.parametrize('S,max_keep', [(12, -1), (12, 1), (12, 37), (12, 500), (150, 20)])
+def test_nms_sorted_segments_max_keep(dev, S, max_keep):
+    """frh_nms_sorted over S pre-sorted segments of ragged counts (0, 1, 63, 64, 65, ...,
+    2500), with the RPN's max_keep stop: S <= 128 takes the fused mask + scan launch
+    (column counters, the scan consuming column blocks as the mask waves publish them),
+    S = 150 the separate launches.  Each segment's keep list equals the oracle's greedy
+    NMS cut at max_keep."""
+    from frcnn_amd import ops
+    rng = np.random.default_rng(S * 1000 + max_keep)
+    base = [0, 1, 63, 64, 65, 300, 1000, 2000, 2500, 129, 7, 1999]
+    counts = np.array([base[i % len(base)] for i in range(S)], np.int32)
+    n_max = int(counts.max())
+    rows = np.zeros((S, n_max, 4), np.float32)
+    for i in range(S):
+        if counts[i]:
+            rows[i, :counts[i]] = inputs.random_boxes(i + 1, int(counts[i]), min_wh=5, max_wh=150).T
+    keep, kc = ops.nms_sorted(T(rows, dev), T(counts, dev), n_max, 0.6, max_keep)
+    keep, kc = keep.cpu().numpy(), kc.cpu().numpy()
+    for i in range(S):
+        n = int(counts[i])
+        want = oracle.nms(rows[i, :n], np.linspace(1.0, 0.0, max(n, 1), dtype=np.float32)[:n], 0.6, max_keep) \
+            if n else np.zeros(0, np.int64)
+        assert kc[i] == len(want), (i, n, kc[i], len(want))
+        np.testing.assert_array_equal(keep[i, :kc[i]], want)
+
+
 @pytest.mark.parametrize('n', [16385, 20000])
 def test_nms_above_16384_boxes(dev, n):
     """torchvision.ops.nms takes any n; the reference's offset-trick batched_nms
