@@ -54,7 +54,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # in-step kernel groups of the detection path (substrings of the dispatched kernel names)
 KERNEL_GROUPS = [
     ('roi_align_fwd', ('roi_align_fwd',)),
-    ('nms', ('nms_mask_kernel', 'nms_scan_kernel', 'nms_fused_kernel')),
+    ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
     ('proposals', ('rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
     ('sampler', ('sampler_', 'chunk_count', 'chunk_write_lists')),

@@ -40,13 +40,15 @@
 // array (row * classes + class official, row strict): ties order exactly as
 // its stable sort does, also when rows the reference drops before the call
 // (row_valid = 0) are kept in place here.
-#include "nms.h"
 #include <algorithm>
 
 #include "block_ops.h"
 
 namespace frh {
 
+int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
+                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps = nullptr);
 
 constexpr int kMcMaxSeg = 65536;    // per-segment candidates (the NMS limit)
 constexpr int kMcSortChunk = 16384; // records sorted per workgroup in LDS (128 KB)

@@ -28,27 +28,10 @@
 
 #include "block_ops.h"
 #include "cdna.h"
-#include "nms.h"
-
-#ifndef FRH_FUSE_THREADS
-#define FRH_FUSE_THREADS 512
-#endif
-#ifndef FRH_FUSE_LDS
-#define FRH_FUSE_LDS 1
-#endif
 
 namespace frh {
 
 constexpr int kMaxNmsWords = 1024;  // n <= 65536 boxes per segment
-
-// agent-scope relaxed loads (sc1: the reader's L1 is bypassed) of words another
-// workgroup of the same launch stored write-through (fused mask + scan below)
-__device__ __forceinline__ uint64_t xwg_load(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t xwg_load(const int32_t* p) {
-  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // The suppression test IoU > thr without the division.  v = RN(inter / union) is
 // a float, so v > thr (double) <=> v >= t_up, the smallest float above thr, <=>
@@ -149,18 +132,24 @@ __device__ __forceinline__ int64_t seg_tile_base(const int64_t* seg_base, int s,
   return seg_base ? seg_base[s] : (int64_t)s * tri_tiles(nbw);
 }
 
-// One tile (rb, cb) of segment s by one wave, staging the tile's 64 ROW boxes in LDS
-// (rb_box / rb_area: this wave's 64 slots); lane = column.  Lane j sweeps the rows and
-// sets bit i of its column word when row i suppresses box j.  IoU is symmetric bit for
-// bit (min / max and the area sum (area_i + area_j) - inter commute exactly), so this is
-// the reference's test of the kept box i against candidate j.  Returns false (nothing
-// stored) when the tile lies past the segment's count.  kXwg: the column words are stored
-// write-through (agent scope) for a consumer in another workgroup of the same launch.
-template <bool kXwg>
-__device__ __forceinline__ bool mask_tile(const float* __restrict__ boxes, int64_t seg_stride,
-                                          const int32_t* __restrict__ counts, int n_max, int nbw, const NmsThr& T,
-                                          uint64_t* __restrict__ mask, const int64_t* __restrict__ seg_base, int s,
-                                          int rb, int cb, float4* rb_box, float* rb_area, int t) {
+// Four tiles per 256-thread workgroup, each wave staging its tile's 64 ROW boxes in
+// LDS; lane = column.  Lane j sweeps the rows and sets bit i of its column word when
+// row i suppresses box j.  IoU is symmetric bit for bit (min / max and the area sum
+// (area_i + area_j) - inter commute exactly), so this is the reference's test of the
+// kept box i against candidate j.
+__global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
+                                                       const int32_t* __restrict__ counts, int n_max, int nbw,
+                                                       NmsThr T, uint64_t* __restrict__ mask,
+                                                       const int64_t* __restrict__ seg_base) {
+  __shared__ float4 rb_box_all[4][64];
+  __shared__ float rb_area_all[4][64];
+  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
+  if (tile >= nbw * (nbw + 1) / 2) return;
+  int rb, cb;
+  tri_tile(__builtin_amdgcn_readfirstlane(tile), &rb, &cb);
+  rb = __builtin_amdgcn_readfirstlane(rb);
+  cb = __builtin_amdgcn_readfirstlane(cb);
   // the count, the row box and the column box in flight together (indices clamped to
   // the buffer: slots past the count are read, never used)
   const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
@@ -168,7 +157,9 @@ __device__ __forceinline__ bool mask_tile(const float* __restrict__ boxes, int64
   const int n = counts[s];
   const float4 r = bx[min(row, n_max - 1)];
   const float4 a = bx[min(col, n_max - 1)];
-  if (rb * 64 >= n || cb * 64 >= n) return false;
+  if (rb * 64 >= n || cb * 64 >= n) return;
+  float4* rb_box = rb_box_all[wv];
+  float* rb_area = rb_area_all[wv];
   const bool row_nn = row >= n || nn_finite(r);
   rb_box[t] = r;
   rb_area[t] = (r.z - r.x) * (r.w - r.y);
@@ -236,31 +227,7 @@ __device__ __forceinline__ bool mask_tile(const float* __restrict__ boxes, int64
   const int nrows = min(64, n - rb * 64);
   if (nrows < 64) colw &= (1ull << nrows) - 1ull;
   if (cb == rb) colw &= t == 0 ? 0ull : (~0ull >> (64 - t));  // rows before the column only
-  uint64_t* w = mask + tile_word(seg_tile_base(seg_base, s, nbw), rb, cb) + t;
-  const uint64_t v = cvalid ? colw : 0ull;
-  if (kXwg)
-    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *w = v;
-  return true;
-}
-
-// Four tiles per 256-thread workgroup (one per wave), grid.y = segment.
-__global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
-                                                       const int32_t* __restrict__ counts, int n_max, int nbw,
-                                                       NmsThr T, uint64_t* __restrict__ mask,
-                                                       const int64_t* __restrict__ seg_base) {
-  __shared__ float4 rb_box_all[4][64];
-  __shared__ float rb_area_all[4][64];
-  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
-  if (tile >= nbw * (nbw + 1) / 2) return;
-  int rb, cb;
-  tri_tile(__builtin_amdgcn_readfirstlane(tile), &rb, &cb);
-  rb = __builtin_amdgcn_readfirstlane(rb);
-  cb = __builtin_amdgcn_readfirstlane(cb);
-  mask_tile<false>(boxes, seg_stride, counts, n_max, nbw, T, mask, seg_base, s, rb, cb, rb_box_all[wv],
-                   rb_area_all[wv], t);
+  mask[tile_word(seg_tile_base(seg_base, s, nbw), rb, cb) + t] = cvalid ? colw : 0ull;
 }
 
 __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
@@ -505,211 +472,6 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   }
 }
 
-// ---------------------------------------------------------------------------
-// Fused mask + scan: ONE launch of S scan workgroups (ids 0..S-1, dispatched first)
-// followed by the mask workgroups, so each segment's scan runs while the mask of its
-// later column blocks is still being computed.
-//  Mask: one tile per wave, tiles numbered column-group-major over all segments (every
-//   segment's column block 0, then every segment's column block 1, ...: the columns the
-//   scans need first are computed first).  A wave stores its tile's column words
-//   write-through (agent scope), waits for them (vmcnt(0)) and adds 1 to its (segment,
-//   column block) counter (agent-scope atomic); column block b of a segment is complete
-//   when its counter reaches b + 1 (tiles (0..b, b)) (MI355X_MICROARCH.md hand-off table,
-//   row 1: signal after every storing wave's vmcnt(0), stores and loads agent scope).
-//  Scan: wave 0 resolves exactly as nms_scan_kernel's resolver; waves 1..7 load (the
-//   other waves of the 1024-thread workgroup leave after the LDS set-up).  The
-//   loader of block b waits for its ring slot (resolver at b - kFuseRing + 1) and for
-//   column b's counter, reads its lane's column words of tiles (j, b), j <= b, with
-//   agent-scope loads (kFuseBatch in flight), keeps tiles b-2, b-1, b in the slot for the
-//   resolver, folds the kept rows of blocks j <= b - 3 (kept[j], published by the
-//   resolver before s_resolved passes j) into the slot's partial word and publishes
-//   ready[slot] = b + 1 -- the LDS protocol of nms_scan_kernel.
-//  Progress: mask waves wait for nothing.  The scan workgroups have the lowest ids, so
-//   they are resident before any mask workgroup is dispatched, and the host takes this
-//   path only for S <= kFuseMaxSegs (half of the 256 CUs, one workgroup each), so mask
-//   workgroups always find room.  A loader waits on s_resolved (as in nms_scan_kernel)
-//   and on mask counters, which always complete.
-//  The counters ([S][nbw] int32) must be zero at launch (the callers' memset regions).
-constexpr int kFuseThreads = FRH_FUSE_THREADS, kFuseWaves = kFuseThreads / kWave, kFuseLoaders = 7;
-constexpr int kFuseRing = 8, kFuseBatch = 16, kFuseMaxSegs = 128;
-constexpr int kFuseLdsBytes = FRH_FUSE_LDS * 1024;
-#ifndef FRH_FUSE_EARLY
-#define FRH_FUSE_EARLY 8
-#endif
-constexpr int kFuseEarlyCols = FRH_FUSE_EARLY;
-
-struct FuseScanLds {
-  uint64_t kept[kMaxNmsWords];
-  int nkpre[kMaxNmsWords];  // kept before block b
-  uint64_t slot[kFuseRing][4][kWave];  // partial word, tiles b-2, b-1, b
-  int ready[kFuseRing];
-  int resolved, stop;
-};
-struct FuseMaskLds {
-  float4 box[kFuseWaves][kWave];
-  float area[kFuseWaves][kWave];
-};
-
-template <bool kStamp>
-__global__ void __launch_bounds__(kFuseThreads) nms_fused_kernel(const float* __restrict__ boxes, int64_t seg_stride,
-                                                                 const int32_t* __restrict__ counts, int S, int n_max,
-                                                                 int nbw, NmsThr T, uint64_t* __restrict__ mask,
-                                                                 const int64_t* __restrict__ seg_base,
-                                                                 int32_t* __restrict__ colcnt, int max_keep,
-                                                                 int32_t* __restrict__ keep, int64_t kstride,
-                                                                 int32_t* __restrict__ kcounts, int64_t* stamps) {
-  // Each workgroup owns its CU (LDS sized past half of it): a scan's resolver never shares
-  // its SIMD or its CU's LDS queue with mask waves (both measured to triple its per-block
-  // latency), and the mask workgroups run 16 waves per CU.
-  __shared__ union {
-    FuseScanLds sc;
-    FuseMaskLds mk;
-    char own_cu[kFuseLdsBytes];
-  } L;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  if ((int)blockIdx.x >= S) {
-    // ---- mask: one tile per wave; column group c holds S (c + 1) tiles from S c (c + 1) / 2
-    const int64_t tt = ((int64_t)blockIdx.x - S) * kFuseWaves + wave;
-    int c = (int)((sqrt(8.0 * ((double)tt / (double)S) + 1.0) - 1.0) * 0.5);
-    c = max(c, 0);
-    while (c > 0 && (int64_t)S * c * (c + 1) / 2 > tt) --c;
-    while ((int64_t)S * (c + 1) * (c + 2) / 2 <= tt) ++c;
-    c = __builtin_amdgcn_readfirstlane(c);
-    if (c >= nbw) return;
-    const int64_t u = tt - (int64_t)S * c * (c + 1) / 2;
-    const int sg = __builtin_amdgcn_readfirstlane((int)(u / (c + 1)));
-    const int rb = __builtin_amdgcn_readfirstlane((int)(u - (int64_t)sg * (c + 1)));
-    // the first column blocks start every scan: their tiles issue ahead of the others
-    if (c < kFuseEarlyCols) __builtin_amdgcn_s_setprio(2);
-    const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-    if (mask_tile<true>(boxes, seg_stride, counts, n_max, nbw, T, mask, seg_base, sg, rb, c, L.mk.box[wave],
-                        L.mk.area[wave], lane)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        const int old =
-            __hip_atomic_fetch_add(colcnt + (int64_t)sg * nbw + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (kStamp && old == c) {  // the column's last tile: [5] its wave's start, [6] the column complete
-          stamps[((int64_t)sg * nbw + c) * 8 + 5] = t_start;
-          stamps[((int64_t)sg * nbw + c) * 8 + 6] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        }
-      }
-    }
-    return;
-  }
-  // ---- scan of segment s
-  FuseScanLds& sm = L.sc;
-  const int s = blockIdx.x;
-  const int n = counts[s];
-  const int nb = (n + 63) >> 6;
-  if (tid < kFuseRing) sm.ready[tid] = 0;
-  if (tid == 0) {
-    sm.resolved = 0;
-    sm.stop = nb;
-  }
-  __syncthreads();
-  const int64_t base = seg_tile_base(seg_base, s, nbw);
-  auto stamp = [&](int b, int i) {
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + b) * 8 + i] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  };
-  if (wave == 0) {
-    // the resolve chain is the launch's critical path: it issues ahead of the loaders and of
-    // the mask waves that share its CU
-    __builtin_amdgcn_s_setprio(3);
-    int nk = 0;
-    uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
-    for (int b = 0; b < nb; ++b) {
-      stamp(b, 0);
-      const int sl = b % kFuseRing;
-      // before block 2 the tile words b-1 / b-2 are not written; the empty kept sets mask them
-      uint64_t pw, t1, t2, d;
-      if (lds_block_reads(&sm.ready[sl], &sm.slot[sl][0][lane], &sm.slot[sl][2][lane], &sm.slot[sl][1][lane],
-                          &sm.slot[sl][3][lane], pw, t1, t2, d) != b + 1) {
-        while (lds_poll(&sm.ready[sl]) != b + 1) __builtin_amdgcn_s_sleep(1);
-        lds_block_reads(&sm.ready[sl], &sm.slot[sl][0][lane], &sm.slot[sl][2][lane], &sm.slot[sl][1][lane],
-                        &sm.slot[sl][3][lane], pw, t1, t2, d);
-      }
-      stamp(b, 1);
-      const uint64_t acc = pw | (t1 & kb1) | (t2 & kb2);
-      uint64_t r = __ballot(acc != 0ull);
-      const int valid = n - b * 64;
-      if (valid < 64) r |= (~0ull) << valid;
-      uint64_t kb = 0, und = ~r;
-      while (und) {
-        const uint64_t sup = __ballot((d & und) != 0ull);
-        const uint64_t nkp = und & ~sup;
-        kb |= nkp;
-        const uint64_t vic = __ballot((d & nkp) != 0ull);
-        und &= ~(nkp | vic);
-      }
-      bool stop = false;
-      if (max_keep >= 0) {
-        const int room = max_keep - nk;
-        while (__popcll(kb) > room) kb &= ~(1ull << (63 - __clzll(kb)));  // drop lowest-score extras
-        stop = nk + __popcll(kb) >= max_keep;
-      }
-      // no global store in this loop (a store's pending data registers make the compiler
-      // drain vmcnt before the next block's reads): the loaders write the keep indices
-      if (lane == 0) sm.nkpre[b] = nk;
-      nk += __popcll(kb);
-      kb2 = kb1;
-      kb1 = kb;
-      if (lane == 0) {  // in-order LDS: the loaders see kept[b] / stop once they see the flag
-        sm.kept[b] = kb;
-        if (stop) sm.stop = b;
-        asm volatile("" ::: "memory");
-        __hip_atomic_store(&sm.resolved, stop ? nb + kFuseRing + 1 : b + 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      stamp(b, 2);
-      if (stop) break;
-    }
-    if (lane == 0) kcounts[s] = nk;
-    return;
-  }
-  __builtin_amdgcn_s_setprio(2);  // loaders ahead of the mask waves on this CU
-  if (wave > kFuseLoaders) return;
-  const int32_t* cc = colcnt + (int64_t)s * nbw;
-  for (int b = wave - 1; b < nb; b += kFuseLoaders) {
-    while (lds_poll(&sm.resolved) < b - kFuseRing + 1) __builtin_amdgcn_s_sleep(1);
-    if (sm.stop < b) break;
-    while (__builtin_amdgcn_readfirstlane(xwg_load(cc + b)) < b + 1) __builtin_amdgcn_s_sleep(1);
-    stamp(b, 4);
-    uint64_t(*slot)[kWave] = sm.slot[b % kFuseRing];
-    uint64_t acc = 0;
-    for (int j0 = 0; j0 <= b; j0 += kFuseBatch) {
-      const int cnt = min(kFuseBatch, b + 1 - j0);
-      uint64_t t[kFuseBatch];
-#pragma unroll
-      for (int u = 0; u < kFuseBatch; ++u)
-        t[u] = u < cnt ? xwg_load(mask + tile_word(base, j0 + u, b) + lane) : 0ull;
-      const int jf = min(j0 + cnt, b - 2);  // this batch folds rows of blocks [j0, jf)
-      if (jf > j0)
-        while (lds_poll(&sm.resolved) < jf) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int u = 0; u < kFuseBatch; ++u) {
-        const int j = j0 + u;
-        if (j < jf)
-          acc |= t[u] & sm.kept[j];
-        else if (u < cnt)
-          slot[1 + j - (b - 2)][lane] = t[u];  // j in [b - 2, b]
-      }
-    }
-    slot[0][lane] = acc;
-    if (lane == 0) lds_flag(&sm.ready[b % kFuseRing], b + 1);
-    stamp(b, 3);
-  }
-  // keep indices of the resolved blocks, once the resolver is done (s_resolved >= nb; a
-  // max_keep stop pushes it past nb with s_stop = the last resolved block)
-  while (lds_poll(&sm.resolved) < nb) __builtin_amdgcn_s_sleep(1);
-  const int nres = min(nb, sm.stop + 1);
-  int32_t* K = keep + (int64_t)s * kstride;
-  for (int b = wave - 1; b < nres; b += kFuseLoaders) {
-    const uint64_t kb = sm.kept[b];
-    if ((kb >> lane) & 1ull) K[sm.nkpre[b] + __popcll(kb & lanemask_lt())] = b * 64 + lane;
-  }
-}
-
 // The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
 // set for every device the first time a launch runs on it (one bit per device id;
 // setting it twice from racing threads is harmless).
@@ -730,23 +492,9 @@ static int32_t nms_scan_attr() {
 
 int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps, int32_t* colcnt) {
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps) {
   const int nbw = (n_max + 63) / 64;
   FRH_REQUIRE(nbw <= kMaxNmsWords, "n_max %d exceeds %d", n_max, 64 * kMaxNmsWords);
-  if (colcnt && S <= kFuseMaxSegs) {  // one launch: zeroed column counters given
-    const int64_t tiles = (int64_t)S * tri_tiles(nbw);
-    const int64_t grid = S + (tiles + kFuseWaves - 1) / kFuseWaves;
-    FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many NMS tiles");
-    if (stamps)
-      hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFuseThreads), 0, st, boxes, seg_stride,
-                         counts, S, n_max, nbw, nms_thr(thr), mask, seg_base, colcnt, max_keep, keep, kstride, kcounts,
-                         stamps);
-    else
-      hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFuseThreads), 0, st, boxes, seg_stride,
-                         counts, S, n_max, nbw, nms_thr(thr), mask, seg_base, colcnt, max_keep, keep, kstride, kcounts,
-                         nullptr);
-    return check_launch("nms");
-  }
   const int32_t r = nms_scan_attr();
   if (r) return r;
   dim3 g((unsigned)((tri_tiles(nbw) + 3) / 4), S);
@@ -771,11 +519,8 @@ size_t nms_mask_bytes(int32_t S, int32_t n_max) {  // S triangles of the n_max s
 
 using namespace frh;
 
-static inline size_t nms_al(size_t x) { return (x + 255) & ~(size_t)255; }
-
-extern "C" size_t frh_nms_workspace(int32_t num_segs, int32_t n_max) {  // mask + column counters
-  const int32_t n = n_max > 0 ? n_max : 1;
-  return nms_al(nms_mask_bytes(num_segs, n)) + nms_colcnt_bytes(num_segs, n);
+extern "C" size_t frh_nms_workspace(int32_t num_segs, int32_t n_max) {
+  return nms_mask_bytes(num_segs, n_max > 0 ? n_max : 1);
 }
 
 extern "C" int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
@@ -791,9 +536,6 @@ extern "C" int32_t frh_nms_sorted(int32_t num_segs, const float* boxes, int64_t 
     FRH_HIP(hipMemsetAsync(keep_counts, 0, sizeof(int32_t) * num_segs, as_stream(stream)));
     return FRH_OK;
   }
-  int32_t* colcnt = reinterpret_cast<int32_t*>(static_cast<char*>(workspace) + nms_al(nms_mask_bytes(num_segs, n_max)));
-  FRH_HIP(hipMemsetAsync(colcnt, 0, nms_colcnt_bytes(num_segs, n_max), as_stream(stream)));
   return launch_nms_sorted(num_segs, boxes, seg_stride, counts, n_max, iou_thr, max_keep, keep, keep_seg_stride,
-                           keep_counts, reinterpret_cast<uint64_t*>(workspace), nullptr, as_stream(stream), nullptr,
-                           colcnt);
+                           keep_counts, reinterpret_cast<uint64_t*>(workspace), nullptr, as_stream(stream), nullptr);
 }

@@ -10,11 +10,14 @@
 //  2. NMS mask + scan over all segments (nms.hip), keep <= post_nms.
 //  3. merge   (1 block per image): concatenate the levels' survivors and, if
 //     more than max_num, keep the best max_num by (score desc, concat order).
-#include "nms.h"
 #include "seg_topk.h"
 
 namespace frh {
 
+int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
+                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps = nullptr);
+size_t nms_mask_bytes(int32_t S, int32_t n_max);
 
 constexpr int kPropThreads = 1024;
 constexpr int kMaxSort = 16384;
@@ -426,7 +429,7 @@ static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, colcnt, total;
+  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, total;
   int64_t nmax, kld;
 };
 
@@ -458,8 +461,7 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
   z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
   z.mem = z.keys + al(S * (size_t)z.kld * sizeof(uint32_t));
   z.zero = z.mem + al(S * (size_t)z.kld * sizeof(uint64_t));
-  z.colcnt = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));  // NMS column counters (fused launch)
-  z.total = z.colcnt + al(nms_colcnt_bytes((int32_t)S, P));
+  z.total = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
   return z;
 }
 
@@ -549,7 +551,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
             reinterpret_cast<uint32_t*>(zb + (size_t)S * (1 << kRpnHistBits) * sizeof(uint32_t)),
             reinterpret_cast<int32_t*>(zb + (size_t)S * ((1 << kRpnHistBits) + kTkBins2) * sizeof(uint32_t)),
             reinterpret_cast<uint64_t*>(ws + z.mem)};
-  FRH_HIP(hipMemsetAsync(zb, 0, (z.colcnt - z.zero) + nms_colcnt_bytes(S, z.P), st));  // + the NMS counters
+  FRH_HIP(hipMemsetAsync(zb, 0, tk_zero_bytes(S, kRpnHistBits), st));
   const dim3 grid((unsigned)((z.nmax + kTkChunk - 1) / kTkChunk), (unsigned)S);
   hipLaunchKernelGGL(rpn_keys_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
   hipLaunchKernelGGL(rpn_refine_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
@@ -569,8 +571,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);
   int32_t* kcnt = reinterpret_cast<int32_t*>(ws + z.kcnt);
   r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
-                        (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, reinterpret_cast<uint64_t*>(ws + z.mask), nullptr, st,
-                        nullptr, reinterpret_cast<int32_t*>(ws + z.colcnt));
+                        (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, reinterpret_cast<uint64_t*>(ws + z.mask), nullptr, st);
   if (r) return r;
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};

@@ -571,10 +571,9 @@ def test_nms_empty_and_batched(dev):
 @pytest.mark.parametrize('S,max_keep', [(12, -1), (12, 1), (12, 37), (12, 500), (150, 20)])
 def test_nms_sorted_segments_max_keep(dev, S, max_keep):
     """frh_nms_sorted over S pre-sorted segments of ragged counts (0, 1, 63, 64, 65, ...,
-    2500), with the RPN's max_keep stop: S <= 128 takes the fused mask + scan launch
-    (column counters, the scan consuming column blocks as the mask waves publish them),
-    S = 150 the separate launches.  Each segment's keep list equals the oracle's greedy
-    NMS cut at max_keep."""
+    2500) in one call, with the RPN's max_keep stop (the scan's early exit and its loaders'
+    stop protocol).  Each segment's keep list equals the oracle's greedy NMS cut at
+    max_keep."""
     from frcnn_amd import ops
     rng = np.random.default_rng(S * 1000 + max_keep)
     base = [0, 1, 63, 64, 65, 300, 1000, 2000, 2500, 129, 7, 1999]

@@ -67,17 +67,12 @@ def main():
     torch.cuda.synchronize()
     assert torch.equal(kc, ref_kc) and all(torch.equal(keep[s, :int(kc[s])], ref_keep[s, :int(kc[s])]) for s in range(S))
     st = stamps.view(S, nbw, 8).cpu().numpy()
-    fused = bool((st[:, :, 6] > 0).any())  # fused mask + scan launch: column completion stamps
-    t0 = st[:, :, :7][st[:, :, :7] > 0].min()
+    t0 = st[:, :, :5][st[:, :, :5] > 0].min()
     counts = cnt.cpu().tolist()
     for s in range(S):
         nb = (counts[s] + 63) // 64
         x = (st[s, :nb, :5] - t0) / 100.0
         x[st[s, :nb, :5] == 0] = np.nan
-        if fused:
-            col = (st[s, :nb, 6] - t0) / 100.0
-            print('  columns complete (us) first/median/last: {:.2f} {:.2f} {:.2f}'.format(col.min(), np.median(col),
-                                                                                   col.max()))
         print('segment {} ({} boxes, {} kept): resolver done at {:.2f} us'.format(s, counts[s], int(kc[s]),
                                                                                    np.nanmax(x[:, 2])))
         per = np.diff(x[:, 2])
@@ -87,8 +82,7 @@ def main():
         if s == 0:
             for b in range(nb):
                 print('   b={:2d} wait {:6.2f} ready {:6.2f} resolved {:6.2f} | copies {:6.2f} fold {:6.2f}'.format(
-                    b, *x[b, [0, 1, 2, 4, 3]]) + ('' if not fused else ' | column: last tile started {:6.2f} done {:6.2f}'.format(
-                        *((st[s, b, 5:7] - t0) / 100.0))))
+                    b, *x[b, [0, 1, 2, 4, 3]]))
 
 
 if __name__ == '__main__':

@@ -1,8 +1,12 @@
 // TOOLS-ONLY: the product NMS (mask + scan) with the scan's per-block timestamps.
-#include "nms.h"
 #include "frcnn_tools.h"
 #include "common.h"
 
+namespace frh {
+int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
+                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
+                          uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps);
+}  // namespace frh
 
 extern "C" int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride,
                                           const int32_t* counts, int32_t n_max, double iou_thr, int32_t max_keep,
@@ -10,11 +14,7 @@ extern "C" int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, 
                                           void* workspace, size_t ws_bytes, int64_t* stamps, void* stream) {
   FRH_REQUIRE(num_segs > 0 && n_max > 0 && stamps, "bad arguments");
   FRH_REQUIRE(workspace && ws_bytes >= frh_nms_workspace(num_segs, n_max), "workspace too small");
-  // the product's layout (frh_nms_workspace): mask, then the column counters of the fused launch
-  const size_t mb = (frh::nms_mask_bytes(num_segs, n_max) + 255) & ~(size_t)255;
-  int32_t* colcnt = reinterpret_cast<int32_t*>(static_cast<char*>(workspace) + mb);
-  FRH_HIP(hipMemsetAsync(colcnt, 0, frh::nms_colcnt_bytes(num_segs, n_max), frh::as_stream(stream)));
   return frh::launch_nms_sorted(num_segs, boxes, seg_stride, counts, n_max, iou_thr, max_keep, keep, keep_seg_stride,
                                 keep_counts, static_cast<uint64_t*>(workspace), nullptr, frh::as_stream(stream),
-                                stamps, colcnt);
+                                stamps);
 }
