@@ -358,7 +358,7 @@ def main():
     ap.add_argument('--sampler', default='device', choices=['device', 'numpy'])
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--trace-steps', type=int, default=3,
+    ap.add_argument('--trace-steps', type=int, default=6,
                     help='extra steps (after the timed region) run under the kernel tracer for the kernel lines; 0 = off')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='torch.distributed backend for N > 1 (nccl = RCCL; gloo lets several ranks share one GPU)')
@@ -451,12 +451,26 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    # the RoIAlign forward launches of the timed steps carry a pair of HIP events bound to the
+    # kernel's own dispatch (frh_roi_align_fwd_strided_timed): its in-step duration, read after
+    # the timed region; the events are created (recorded once) before it
+    pool = []
+    for _ in range(4 * args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e1.record()
+        pool.append((e0, e1))
+    ops.ROI_ALIGN_PROFILE['event_pool'] = pool
+    ops.ROI_ALIGN_PROFILE['timed'] = timed_roi = []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     barrier()
     elapsed = time.perf_counter() - t0
+    ops.ROI_ALIGN_PROFILE['timed'] = None
+    ops.ROI_ALIGN_PROFILE['event_pool'] = []
+    roi_timed_us = [1e3 * a.elapsed_time(b) for a, b in timed_roi]
     assert torch.isfinite(loss).all()
     t_max = max_over_ranks(elapsed, dev, world)
 
@@ -478,7 +492,10 @@ def main():
         per_group, det_us, group_names, det_kernels = (summarise_trace(trace, steps_traced) if trace else
                                                         ({}, None, {}, {}))
         roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]
-        roi_in_step = float(np.mean([us for _, us in roi_launches])) if roi_launches else None
+        # median over the traced steps' launches (the first traced step carries the tracer's start-up)
+        roi_tracer = float(np.median([us for _, us in roi_launches])) if roi_launches else None
+        roi_in_step = float(np.median(roi_timed_us)) if roi_timed_us else roi_tracer
+        roi_in_step_all = [round(us, 2) for us in roi_timed_us]
         roi_kernel = kernel_short(roi_launches[0][0]) if roi_launches else None
         warm, cold = roi_align_replays(recs, dev)
         avg_bytes = float(np.mean([roi_align_bytes(r) for r in recs])) if recs else None
@@ -520,10 +537,13 @@ def main():
                 'frac': achieved / HBM_PEAK_GBS if achieved else None, 'traffic': traffic,
                 'avg_launch_us': us_for_frac, 'algorithmic_bytes_per_launch': avg_bytes,
                 'launches': len(roi_launches) or len(recs),
-                'avg_launch_us_in_step': roi_in_step, 'avg_launch_us_replay_warm': warm,
+                'avg_launch_us_in_step': roi_in_step, 'in_step_launches_us': roi_in_step_all,
+                'avg_launch_us_kernel_tracer': roi_tracer, 'avg_launch_us_replay_warm': warm,
                 'avg_launch_us_replay_cold': cold,
-                'timing': ('in-step device durations from the ROCm kernel tracer (torch.profiler) over {} steps '
-                           'after the timed region'.format(steps_traced) if roi_in_step else
+                'timing': ('in-step: median over the timed steps of the RoIAlign forward\'s own dispatch '
+                           'timestamps (HIP events bound by hipExtLaunchKernel, frh_roi_align_fwd_strided_timed); '
+                           'kernel_tracer = torch.profiler over {} steps after the timed region'.format(steps_traced)
+                           if roi_in_step else
                            'kernel tracer unavailable ({}): back-to-back replay, warm caches'.format(trace_err)) +
                           '; replay_warm = the same launches back to back, replay_cold = each after a 768 MB read '
                           '(L2 + Infinity Cache evicted); traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per '

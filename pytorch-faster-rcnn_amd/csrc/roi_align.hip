@@ -19,6 +19,7 @@
 // strides: NCHW, channels_last and strided views (FPN P6 = P5[..., ::2, ::2]) all
 // run.  The forward laboratory (stamped builds, candidate kernels) is the tools-only
 // library (tools/csrc/roi_lab.hip).
+#include <hip/hip_ext.h>
 #include "roi_kernels.h"
 
 namespace frh {
@@ -108,11 +109,11 @@ extern "C" int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t bo
   return check_launch("frh_roi_rows");
 }
 
-extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
-                                             const int64_t* strides, const float* scales, int32_t batch,
-                                             int32_t channels, const float* rois, const int64_t* roi_levels,
-                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
-                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
+static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int32_t* feat_hw, const int64_t* strides,
+                       const float* scales, int32_t batch, int32_t channels, const float* rois,
+                       const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                       int32_t sampling_ratio, int32_t aligned, float* out, hipStream_t st, hipEvent_t e0,
+                       hipEvent_t e1) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
   FRH_REQUIRE((feats && out) || num_rois == 0, "null pointer argument");
@@ -122,20 +123,49 @@ extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* co
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+  // e0 / e1 (measurement entry): the kernel's own start / end timestamps (hipExtLaunchKernel
+  // binds them to the dispatch; no extra packets in the stream)
+  auto go = [&](auto kern, dim3 grid, dim3 block) {
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kern, grid, block, 0, st, e0, e1, 0, lv, c, out);
+    else
+      hipLaunchKernelGGL(kern, grid, block, 0, st, lv, c, out);
+  };
   if (pair_ok(f, channels, pooled_h, pooled_w)) {
     // chunk-major XCD order, nt output stores, one 6.5 KB slab per wave, lean tap state
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kCpolNT, false>), dim3((unsigned)(8 * ((total + 7) / 8))),
-                       dim3(kWave), 0, as_stream(stream), lv, c, out);
+    go(roi_align_fwd_pair_kernel<kCpolNT, false>, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave));
   } else if (f.lds) {
-    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    hipLaunchKernelGGL(roi_align_fwd_lds_kernel<256>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    go(roi_align_fwd_lds_kernel<256>, dim3((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk)),
+       dim3(kRoiThreads));
   } else {
-    const dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    hipLaunchKernelGGL(roi_align_fwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, out);
+    go(roi_align_fwd_kernel, dim3((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk)),
+       dim3(kRoiThreads));
   }
   return check_launch("frh_roi_align_fwd");
+}
+
+extern "C" int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
+                                             const int64_t* strides, const float* scales, int32_t batch,
+                                             int32_t channels, const float* rois, const int64_t* roi_levels,
+                                             int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
+                                             int32_t sampling_ratio, int32_t aligned, float* out, void* stream) {
+  return roi_fwd(num_levels, feats, feat_hw, strides, scales, batch, channels, rois, roi_levels, num_rois, pooled_h,
+                 pooled_w, sampling_ratio, aligned, out, as_stream(stream), nullptr, nullptr);
+}
+
+extern "C" int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const float* const* feats,
+                                                   const int32_t* feat_hw, const int64_t* strides,
+                                                   const float* scales, int32_t batch, int32_t channels,
+                                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
+                                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
+                                                   int32_t aligned, float* out, void* start_event, void* stop_event,
+                                                   void* stream) {
+  FRH_REQUIRE(start_event && stop_event, "null event");
+  return roi_fwd(num_levels, feats, feat_hw, strides, scales, batch, channels, rois, roi_levels, num_rois, pooled_h,
+                 pooled_w, sampling_ratio, aligned, out, as_stream(stream), static_cast<hipEvent_t>(start_event),
+                 static_cast<hipEvent_t>(stop_event));
 }
 
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,

@@ -574,7 +574,10 @@ def _feat_desc(feats):
 # feature tensors only to replay the same launch shape for timing; with a graphed
 # trunk they alias the graph's output buffers, so a replay reads the newest step's
 # values -- never use a record's features for their contents.
-ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True}
+ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True, 'timed': None, 'event_pool': []}
+# 'timed': a list -> each forward launch takes a (start, end) pair from 'event_pool' (created
+# beforehand), goes through frh_roi_align_fwd_strided_timed (the events are bound to the
+# kernel's own dispatch timestamps: nothing is added to the stream) and appends the pair.
 
 
 class _RoIAlignMulti(torch.autograd.Function):
@@ -592,9 +595,17 @@ class _RoIAlignMulti(torch.autograd.Function):
         if prof and ROI_ALIGN_PROFILE['events']:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales),
-             feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
-             ptr(out), stream_of(out))
+        timed = ROI_ALIGN_PROFILE['timed']
+        if timed is not None and ROI_ALIGN_PROFILE['event_pool']:
+            ev = ROI_ALIGN_PROFILE['event_pool'].pop()
+            call('frh_roi_align_fwd_strided_timed', len(feats), ptr_array(feats), hw, st, f32_array(scales),
+                 feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
+                 ptr(out), ev[0].cuda_event, ev[1].cuda_event, stream_of(out))
+            timed.append(ev)
+        else:
+            call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales),
+                 feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
+                 ptr(out), stream_of(out))
         if prof:
             if e1 is not None:
                 e1.record()
