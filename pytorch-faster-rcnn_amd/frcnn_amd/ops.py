@@ -633,16 +633,22 @@ class _RoIAlignMulti(torch.autograd.Function):
         return (None, None, None, None, None, None) + tuple(grads)
 
 
-def roi_align_replay(rec, out=None):
+def roi_align_replay(rec, out=None, events=None):
     """Re-issue a recorded RoIAlign forward launch (same features, RoIs and levels) on the
-    current stream; bench.py times back-to-back replays for the per-launch kernel duration."""
+    current stream; bench.py times back-to-back replays for the per-launch kernel duration.
+    events: a (start, end) pair bound to the dispatch (frh_roi_align_fwd_strided_timed)."""
     _, _, rois, levels, shapes, (ph, pw), feats, scales, sr = rec
     K, C = rois.shape[0], shapes[0][1]
     if out is None:
         out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
     hw, st = _feat_desc(feats)
-    call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales), shapes[0][0], C,
-         ptr(rois), ptr(levels), K, ph, pw, int(sr), 0, ptr(out), stream_of(out))
+    if events is not None:
+        call('frh_roi_align_fwd_strided_timed', len(feats), ptr_array(feats), hw, st, f32_array(scales),
+             shapes[0][0], C, ptr(rois), ptr(levels), K, ph, pw, int(sr), 0, ptr(out), events[0].cuda_event,
+             events[1].cuda_event, stream_of(out))
+    else:
+        call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales), shapes[0][0], C,
+             ptr(rois), ptr(levels), K, ph, pw, int(sr), 0, ptr(out), stream_of(out))
     return out
 
 
