@@ -133,7 +133,21 @@ def kernel_trace(step, n, dev):
     ks.sort()
     if not any('frh::' in k[1] for k in ks):
         return None, 'the kernel tracer reported no frcnn_amd kernels ({} device events)'.format(len(ks))
+    # device timeline of the traced steps: span, and the time no kernel was running (host-bound
+    # gaps: launches the host had not issued yet, the per-step host synchronisations)
+    global TRACE_TIMELINE
+    end, idle = None, 0.0
+    for t0, _, us in ks:
+        t0 = float(t0)
+        if end is not None and t0 > end:
+            idle += t0 - end
+        end = max(end, t0 + us) if end is not None else t0 + us
+    TRACE_TIMELINE = {'span_us_per_step': (end - float(ks[0][0])) / n, 'idle_us_per_step': idle / n,
+                      'kernels_per_step': len(ks) / n}
     return [(name, float(us)) for _, name, us in ks], None
+
+
+TRACE_TIMELINE = None
 
 
 def kernel_short(name):
@@ -611,6 +625,7 @@ def main():
                     lines[g] = {'us_per_step': per_group.get(g)}
             lines['roi_align_fwd'] = {'us_per_step': per_group.get('roi_align_fwd')}
             out['kernels'] = {'per_step': lines, 'detection_path_us_per_step': det_us,
+                              'device_timeline': TRACE_TIMELINE,
                               'detection_path_kernels_us_per_step': det_kernels, 'dispatched': group_names,
                               'timing': 'in-step device durations, ROCm kernel tracer, {} steps'.format(steps_traced)}
             if recs and lines.get('nms', {}).get('us_per_step'):
