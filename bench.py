@@ -136,14 +136,19 @@ def kernel_trace(step, n, dev):
     # device timeline of the traced steps: span, and the time no kernel was running (host-bound
     # gaps: launches the host had not issued yet, the per-step host synchronisations)
     global TRACE_TIMELINE
-    end, idle = None, 0.0
-    for t0, _, us in ks:
+    end, idle, prev, gaps = None, 0.0, None, {}
+    for t0, name, us in ks:
         t0 = float(t0)
         if end is not None and t0 > end:
             idle += t0 - end
+            key = '{} -> {}'.format(kernel_short(prev)[-40:], kernel_short(name)[-40:])
+            gaps[key] = gaps.get(key, 0.0) + (t0 - end) / n
         end = max(end, t0 + us) if end is not None else t0 + us
+        prev = name
+    top = sorted(gaps.items(), key=lambda kv: -kv[1])[:12]
     TRACE_TIMELINE = {'span_us_per_step': (end - float(ks[0][0])) / n, 'idle_us_per_step': idle / n,
-                      'kernels_per_step': len(ks) / n}
+                      'kernels_per_step': len(ks) / n,
+                      'largest_idle_us_per_step': {k: round(v, 1) for k, v in top}}
     return [(name, float(us)) for _, name, us in ks], None
 
 
