@@ -135,7 +135,9 @@ int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t la
  * sel / sel_counts (nullable; frh_sample_random's lists, max_num = max_out_per_seg
  * <= 8192): the chosen boxes are those lists (ranked into ascending box order in
  * the gather itself) and `labels` are the assignment labels before sampling; no
- * workspace is needed. */
+ * workspace is needed.  With sel, columns [total, num_segs*max_out_per_seg) are padding
+ * (seg_of -1, tar_labels -1, zero boxes), so a caller may consume the whole capacity
+ * against the device total instead of reading it back. */
 int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                           const int32_t* num_boxes, int64_t max_boxes, const float* anchors,
                           int64_t anchor_ld, int64_t anchor_seg_stride, const float* gts,
@@ -151,7 +153,8 @@ size_t frh_anchor_target_workspace(int32_t num_segs, int64_t max_boxes);
 /* gather of per-level head outputs at chosen anchors (anchor.py:51-56) and its
  * adjoint (autograd backward).  Level l tensor: [B, C*A, H, W] contiguous
  * viewed per image as [C, A*H*W] (anchor_head.py:82); level_off[l] = first
- * flat index of the level.  out: [C, out_ld]. */
+ * flat index of the level.  out: [C, out_ld].  A column with seg_of < 0 (padding) gathers
+ * zeros and scatters nothing. */
 int32_t frh_gather_level_outputs(int32_t num_levels, const float* const* level_ptrs,
                                  const int64_t* level_off, const int64_t* level_hw_a,
                                  int32_t channels, int64_t total, const int64_t* chosen_idx,
@@ -171,7 +174,8 @@ int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
  * gathers the chosen rows (ascending) into concatenated
  * outputs: tar_props/tar_bbox/tar_param [4, out_ld], tar_label (int64, gt
  * class or 0), tar_is_gt (int64 0/1), out_counts[S+1] as in frh_anchor_target;
- * sel / sel_counts as in frh_anchor_target (labels = the prepended rows). */
+ * sel / sel_counts as in frh_anchor_target (labels = the prepended rows; padding columns
+ * past the total: tar_label -1, tar_is_gt 0, zero boxes). */
 int32_t frh_prepend_gt_labels(int32_t num_segs, const int64_t* prop_labels,
                               int64_t prop_label_seg_stride, const int32_t* num_props,
                               const int32_t* num_gts, int64_t max_rows, int64_t* rows_out,
@@ -302,6 +306,13 @@ int32_t frh_roi_level_map(const float* rois, int64_t num_rois, float finest_scal
 int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t box_ld, int64_t box_seg_stride,
                      int32_t flat, const int64_t* seg_offsets, float finest_scale, int32_t num_levels,
                      float* rois, int64_t* levels, void* stream);
+/* frh_roi_rows for rows of a fixed capacity whose per-image counts stay on the device
+ * (seg_counts[b], image b's rows back to back from column 0 of boxes, images in order; rows
+ * past their total are padding rows of image 0): the RCNN targets' buffer consumed without a
+ * host synchronisation on its size (num_rows = the capacity). */
+int32_t frh_roi_rows_dev(int32_t num_segs, const float* boxes, int64_t box_ld, int64_t num_rows,
+                         const int32_t* seg_counts, float finest_scale, int32_t num_levels,
+                         float* rois, int64_t* levels, void* stream);
 int32_t frh_roi_align_fwd(int32_t num_levels, const float* const* feats, const int32_t* feat_hw,
                           const float* scales, int32_t batch, int32_t channels, int32_t layout,
                           const float* rois, const int64_t* roi_levels, int64_t num_rois,
@@ -391,7 +402,8 @@ int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gam
  * value itself, int64 or, with target_is_float, f32), 2 = CrossEntropyLoss softmax
  * (losses.py:151-153, labels in [0, C)).  Logit (i, k) is x[i*sr + k*sc] (any strides,
  * so AnchorHead's [C, S] targets need no transpose copy); out is one f32 on the device.
- * Backward writes grad_x (i, k) at grad_x[i*gsr + k*gsc] = grad_out[0] * dL/dx.
+ * Backward writes grad_x (i, k) at grad_x[i*gsr + k*gsc] = grad_out[0] * dL/dx.  Rows with an
+ * int64 label < 0 (padding rows of a fixed-capacity target buffer) add nothing, gradient 0.
  * Callers: AnchorHead.calc_loss (anchor_head.py:113-139), BBoxHead.calc_loss
  * (bbox_head.py:56-87), FCOSHead losses (fcos_head.py:418-534). */
 /* Forward workspace: frh_loss_workspace() bytes whose first 256 bytes (the arrival counter of
@@ -427,14 +439,16 @@ int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
  * Replaces `loss_cls(...) / avg_factor` and `loss_bbox.masked / class_selected(...) /
  * avg_factor` of AnchorHead.calc_loss (anchor_head.py:113-139) and BBoxHead.calc_loss
  * (bbox_head.py:56-87) with a sampler (avg_factor = the sample count, a host value).
- * Workspace as frh_cls_loss_fwd.  Backward: frh_cls_loss_bwd / frh_smooth_l1_bwd. */
+ * Workspace as frh_cls_loss_fwd.  Backward: frh_cls_loss_bwd / frh_smooth_l1_bwd.
+ * div_count (nullable): both divisors are this device int32 count instead (a fixed-capacity
+ * target buffer consumed without a host sync; 0 gives zero losses, as the heads return). */
 int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr, int64_t sc,
                          const void* target, int32_t target_is_float, float alpha, float gamma,
                          float cls_weight, float cls_div, const float* rx, int64_t xs_i,
                          int64_t xs_j, int64_t xs_l, const float* ry, int64_t ys_i, int64_t ys_j,
                          const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel, float beta,
-                         float reg_weight, float reg_div, float* out, void* workspace,
-                         size_t ws_bytes, void* stream);
+                         float reg_weight, float reg_div, const int32_t* div_count, float* out,
+                         void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- f4: image pipeline
  * The train/test pipelines of configs/faster_rcnn_r50_fpn.py:120-139 (mmdet v1: Resize

@@ -63,6 +63,11 @@ __device__ __forceinline__ int64_t label_at(const ClsArgs& a, int64_t i) {
   return static_cast<const int64_t*>(a.target)[i];
 }
 
+// rows labelled < 0 are padding rows of a fixed-capacity target buffer (frh_anchor_target /
+// frh_bbox_target past their device count): they contribute nothing, forward or backward
+// (the reference's sampled targets never carry such labels)
+__device__ __forceinline__ bool ignored(const ClsArgs& a, int64_t i) { return !a.tfloat && label_at(a, i) < 0; }
+
 // torch: binary_cross_entropy_with_logits = (1 - t) * x - log_sigmoid(x),
 // log_sigmoid(x) = min(x, 0) - log1p(exp(-|x|)).
 __device__ __forceinline__ float bce_logits(float x, float t) {
@@ -162,6 +167,7 @@ __global__ void __launch_bounds__(kLossThreads) cls_loss_fwd_kernel(ClsArgs a, F
   if constexpr (kKind == kSoftmaxCe) {
     for (int64_t i = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * kLossThreads) {
+      if (ignored(a, i)) continue;
       const float* row = a.x + i * a.sr;
       float m = -INFINITY;
       for (int64_t k = 0; k < a.c; ++k) m = fmaxf(m, row[k * a.sc]);
@@ -177,6 +183,7 @@ __global__ void __launch_bounds__(kLossThreads) cls_loss_fwd_kernel(ClsArgs a, F
          e += (int64_t)gridDim.x * kLossThreads) {
       int64_t i, k;
       elem_index(a, e, &i, &k);
+      if (ignored(a, i)) continue;
       float x = a.x[i * a.sr + k * a.sc];
       float t = elem_target(a, i, k);
       acc += kKind == kFocal ? focal_elem(x, t, a.alpha, a.gamma, nullptr) : bce_logits(x, t);
@@ -192,6 +199,10 @@ __global__ void __launch_bounds__(kLossThreads) cls_loss_bwd_kernel(ClsArgs a, c
   if constexpr (kKind == kSoftmaxCe) {
     for (int64_t i = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * kLossThreads) {
+      if (ignored(a, i)) {
+        for (int64_t k = 0; k < a.c; ++k) gx[i * gsr + k * gsc] = 0.0f;
+        continue;
+      }
       const float* row = a.x + i * a.sr;
       float m = -INFINITY;
       for (int64_t k = 0; k < a.c; ++k) m = fmaxf(m, row[k * a.sc]);
@@ -211,6 +222,10 @@ __global__ void __launch_bounds__(kLossThreads) cls_loss_bwd_kernel(ClsArgs a, c
          e += (int64_t)gridDim.x * kLossThreads) {
       int64_t i, k;
       elem_index(a, e, &i, &k);
+      if (ignored(a, i)) {
+        gx[i * gsr + k * gsc] = 0.0f;
+        continue;
+      }
       float x = a.x[i * a.sr + k * a.sc];
       float t = elem_target(a, i, k);
       float d;
@@ -287,7 +302,8 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_bwd_kernel(L1Args a, c
 // as torch does it: loss = (sum * loss_weight) / avg_factor in f32.
 struct DetScale {
   float wc, dc, wr, dr;
-  float* out;  // [2]: cls, reg
+  float* out;           // [2]: cls, reg
+  const int32_t* ndev;  // nullable: avg_factor = this device count for both (0 -> zero losses)
 };
 
 __device__ void det_fan_in(float pc, float pr, uint32_t* counter, float* partial, int nbc, int nbr,
@@ -321,8 +337,15 @@ __device__ void det_fan_in(float pc, float pr, uint32_t* counter, float* partial
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    o.out[0] = (res[0] * o.wc) / o.dc;
-    o.out[1] = (res[1] * o.wr) / o.dr;
+    if (o.ndev) {
+      const int32_t nd = *o.ndev;
+      const float d = (float)nd;
+      o.out[0] = nd ? (res[0] * o.wc) / d : 0.0f;
+      o.out[1] = nd ? (res[1] * o.wr) / d : 0.0f;
+    } else {
+      o.out[0] = (res[0] * o.wc) / o.dc;
+      o.out[1] = (res[1] * o.wr) / o.dr;
+    }
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -335,6 +358,7 @@ __global__ void __launch_bounds__(kLossThreads) det_loss_fwd_kernel(ClsArgs a, i
   if ((int)blockIdx.x < nbc) {
     if constexpr (kKind == kSoftmaxCe) {
       for (int64_t i = blockIdx.x * (int64_t)kLossThreads + threadIdx.x; i < a.n; i += (int64_t)nbc * kLossThreads) {
+        if (ignored(a, i)) continue;
         const float* row = a.x + i * a.sr;
         float m = -INFINITY;
         for (int64_t k = 0; k < a.c; ++k) m = fmaxf(m, row[k * a.sc]);
@@ -350,6 +374,7 @@ __global__ void __launch_bounds__(kLossThreads) det_loss_fwd_kernel(ClsArgs a, i
            e += (int64_t)nbc * kLossThreads) {
         int64_t i, k;
         elem_index(a, e, &i, &k);
+        if (ignored(a, i)) continue;
         float x = a.x[i * a.sr + k * a.sc];
         float t = elem_target(a, i, k);
         acc += kKind == kFocal ? focal_elem(x, t, a.alpha, a.gamma, nullptr) : bce_logits(x, t);
@@ -509,8 +534,8 @@ int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
                          const void* target, int32_t target_is_float, float alpha, float gamma, float cls_weight,
                          float cls_div, const float* rx, int64_t xs_i, int64_t xs_j, int64_t xs_l, const float* ry,
                          int64_t ys_i, int64_t ys_j, const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel,
-                         float beta, float reg_weight, float reg_div, float* out, void* workspace, size_t ws_bytes,
-                         void* stream) {
+                         float beta, float reg_weight, float reg_div, const int32_t* div_count, float* out,
+                         void* workspace, size_t ws_bytes, void* stream) {
   ClsArgs a = make_cls(x, n, c, sr, sc, target, target_is_float, alpha, gamma);
   int32_t st = check_cls(kind, a);
   if (st != FRH_OK) return st;
@@ -523,7 +548,7 @@ int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
   char* w = static_cast<char*>(workspace);
   uint32_t* counter = reinterpret_cast<uint32_t*>(w);
   float* partial = reinterpret_cast<float*>(w + kCounterBytes);
-  const DetScale o{cls_weight, cls_div, reg_weight, reg_div, out};
+  const DetScale o{cls_weight, cls_div, reg_weight, reg_div, out, div_count};
   const dim3 g((unsigned)std::max(nbc, nbr));
   hipStream_t s = as_stream(stream);
   if (kind == kFocal)

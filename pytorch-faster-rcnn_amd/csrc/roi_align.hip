@@ -55,6 +55,7 @@ struct RowsArgs {
   float* rois;
   int64_t* levels;
   int64_t offs[kRowSegs + 1];
+  const int32_t* dev_counts;  // nullable: per-image row counts on the device (flat rows, capacity K)
 };
 
 // RoI rows [K, 5] = (image, x1, y1, x2, y2) of the images' boxes, concatenated in image
@@ -64,7 +65,13 @@ __global__ void roi_rows_kernel(RowsArgs a) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.K) return;
   int b = 0;
-  while (b + 1 < a.S && k >= a.offs[b + 1]) ++b;
+  if (a.dev_counts) {  // rows past the images' total are padding rows: image 0
+    int64_t end = a.dev_counts[0];
+    while (b + 1 < a.S && k >= end) end += a.dev_counts[++b];
+    if (k >= end) b = 0;
+  } else {
+    while (b + 1 < a.S && k >= a.offs[b + 1]) ++b;
+  }
   const int64_t col = a.flat ? k : k - a.offs[b];
   const float* p = a.boxes + (int64_t)b * a.seg_stride + col;
   const float x1 = p[0], y1 = p[a.ld], x2 = p[2 * a.ld], y2 = p[3 * a.ld];
@@ -97,7 +104,7 @@ extern "C" int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t bo
   FRH_REQUIRE(num_segs >= 1 && num_segs <= kRowSegs, "num_segs must be in [1, %d]", kRowSegs);
   FRH_REQUIRE(seg_offsets && num_levels >= 1, "bad arguments");
   RowsArgs a{boxes, box_ld, box_seg_stride, num_segs, flat ? 1 : 0, num_levels, finest_scale, 0, rois,
-             num_levels > 1 ? levels : nullptr, {}};
+             num_levels > 1 ? levels : nullptr, {}, nullptr};
   for (int b = 0; b <= num_segs; ++b) {
     a.offs[b] = seg_offsets[b];
     FRH_REQUIRE(b == 0 ? a.offs[0] == 0 : a.offs[b] >= a.offs[b - 1], "seg_offsets must start at 0 and not decrease");
@@ -107,6 +114,19 @@ extern "C" int32_t frh_roi_rows(int32_t num_segs, const float* boxes, int64_t bo
   FRH_REQUIRE(boxes && rois && (num_levels == 1 || levels), "null pointer argument");
   hipLaunchKernelGGL(roi_rows_kernel, dim3((unsigned)((a.K + 255) / 256)), dim3(256), 0, as_stream(stream), a);
   return check_launch("frh_roi_rows");
+}
+
+extern "C" int32_t frh_roi_rows_dev(int32_t num_segs, const float* boxes, int64_t box_ld, int64_t num_rows,
+                                    const int32_t* seg_counts, float finest_scale, int32_t num_levels, float* rois,
+                                    int64_t* levels, void* stream) {
+  FRH_REQUIRE(num_segs >= 1 && num_segs <= kRowSegs, "num_segs must be in [1, %d]", kRowSegs);
+  FRH_REQUIRE(seg_counts && num_levels >= 1 && num_rows >= 0, "bad arguments");
+  if (num_rows == 0) return FRH_OK;
+  FRH_REQUIRE(boxes && rois && (num_levels == 1 || levels), "null pointer argument");
+  RowsArgs a{boxes, box_ld, 0, num_segs, 1, num_levels, finest_scale, num_rows, rois,
+             num_levels > 1 ? levels : nullptr, {}, seg_counts};
+  hipLaunchKernelGGL(roi_rows_kernel, dim3((unsigned)((num_rows + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+  return check_launch("frh_roi_rows_dev");
 }
 
 static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int32_t* feat_hw, const int64_t* strides,

@@ -149,17 +149,28 @@ __global__ void anchor_target_kernel(AnchorTargetArgs p) {
 // counting over the list staged in LDS) -- the reference's nonzero(labels >= 0) order
 // (anchor.py:49-50, bbox.py:52-58) without a compaction pass over every box.
 // Dynamic LDS: 2 * sel_ld + 4 int32.
-template <class F>
+template <class F, class P>
 __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32_t* sel_cnt, int64_t sel_ld, int S,
-                                                 int32_t* out_counts, F&& item) {
+                                                 int32_t* out_counts, int64_t cap, F&& item, P&& pad) {
   extern __shared__ __attribute__((aligned(16))) int32_t su[];
   const int s = blockIdx.y;
   const int np = sel_cnt[2 * s], cnt = np + sel_cnt[2 * s + 1];
-  int64_t off = 0;
-  for (int q = 0; q < s; ++q) off += sel_cnt[2 * q] + sel_cnt[2 * q + 1];
+  int64_t off = 0, total = 0;
+  for (int q = 0; q < S; ++q) {
+    const int64_t c = sel_cnt[2 * q] + sel_cnt[2 * q + 1];
+    off += q < s ? c : 0;
+    total += c;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     out_counts[s] = cnt;
-    if (s == S - 1) out_counts[S] = (int32_t)(off + cnt);
+    if (s == S - 1) out_counts[S] = (int32_t)total;
+  }
+  // rows [total, S * cap) of the output get neutral values (ignored label), so a caller may
+  // consume the whole capacity with the device count instead of synchronising on it: this
+  // segment writes its cap - cnt share, starting at total + s * cap - off
+  {
+    const int64_t jp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (jp >= cnt && jp < cap) pad(total + (int64_t)s * cap - off + (jp - cnt));
   }
   if ((int64_t)blockIdx.x * blockDim.x >= cnt) return;  // uniform per workgroup
   const int32_t* pos = sel + (int64_t)(2 * s) * sel_ld;
@@ -180,8 +191,16 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
 }
 
 __global__ void anchor_target_sel_kernel(AnchorTargetArgs p) {
-  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts,
-                   [&](int s, int64_t n, int64_t o) { anchor_target_item(p, s, n, o); });
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap,
+                   [&](int s, int64_t n, int64_t o) { anchor_target_item(p, s, n, o); },
+                   [&](int64_t o) {  // padding row: no anchor (seg -1), label -1 (ignored), zero targets
+                     p.chosen_idx[o] = 0;
+                     p.seg_of[o] = -1;
+                     p.tar_labels[o] = -1;
+#pragma unroll
+                     for (int k = 0; k < 4; ++k)
+                       p.tar_anchors[k * p.out_ld + o] = p.tar_bbox[k * p.out_ld + o] = p.tar_param[k * p.out_ld + o] = 0.0f;
+                   });
 }
 
 __device__ void anchor_target_item(const AnchorTargetArgs& p, int s, int64_t n, int64_t o) {
@@ -220,6 +239,10 @@ __global__ void gather_levels_kernel(LevelMap lm, int C, int64_t total, const in
   if (j >= total) return;
   int64_t n = chosen[j];
   int b = seg_of[j];
+  if (b < 0) {  // padding row of a fixed-capacity target buffer
+    for (int c = 0; c < C; ++c) out[c * out_ld + j] = 0.0f;
+    return;
+  }
   int l = 0;
   while (l + 1 < lm.n && n >= lm.off[l + 1]) ++l;
   int64_t loc = n - lm.off[l];
@@ -233,6 +256,7 @@ __global__ void scatter_levels_kernel(LevelMap lm, int C, int64_t total, const i
   if (j >= total) return;
   int64_t n = chosen[j];
   int b = seg_of[j];
+  if (b < 0) return;  // padding row: no gradient (and no read-modify-write race with a real row)
   int l = 0;
   while (l + 1 < lm.n && n >= lm.off[l + 1]) ++l;
   int64_t loc = n - lm.off[l];
@@ -293,8 +317,15 @@ __global__ void bbox_target_kernel(BBoxTargetArgs p) {
 }
 
 __global__ void bbox_target_sel_kernel(BBoxTargetArgs p) {
-  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts,
-                   [&](int s, int64_t row, int64_t o) { bbox_target_item(p, s, row, o); });
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap,
+                   [&](int s, int64_t row, int64_t o) { bbox_target_item(p, s, row, o); },
+                   [&](int64_t o) {  // padding row: zero box, label -1 (ignored), not a gt
+                     p.tar_label[o] = -1;
+                     p.tar_is_gt[o] = 0;
+#pragma unroll
+                     for (int k = 0; k < 4; ++k)
+                       p.tar_props[k * p.out_ld + o] = p.tar_bbox[k * p.out_ld + o] = p.tar_param[k * p.out_ld + o] = 0.0f;
+                   });
 }
 
 __device__ void bbox_target_item(const BBoxTargetArgs& p, int s, int64_t row, int64_t o) {

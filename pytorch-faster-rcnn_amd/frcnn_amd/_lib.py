@@ -69,6 +69,7 @@ SIGNATURES = {
                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_size, c_vp, c_size, c_vp]),
     'frh_roi_level_map': (c_i32, [c_vp, c_i64, c_f32, c_i32, c_vp, c_vp]),
     'frh_roi_rows': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i32, P(c_i64), c_f32, c_i32, c_vp, c_vp, c_vp]),
+    'frh_roi_rows_dev': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_vp, c_f32, c_i32, c_vp, c_vp, c_vp]),
     'frh_roi_align_fwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,
                                   c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_align_bwd': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_f32), c_i32, c_i32, c_i32, c_vp, c_vp, c_i64,
@@ -98,7 +99,7 @@ SIGNATURES = {
                                   c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     'frh_det_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32,
                                  c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
-                                 c_f32, c_f32, c_vp, c_vp, c_size, c_vp]),
+                                 c_f32, c_f32, c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_atss_assign': (c_i32, [c_i32, c_i32, P(c_i32), P(c_f32), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32,
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }

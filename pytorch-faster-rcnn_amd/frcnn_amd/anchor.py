@@ -61,7 +61,7 @@ def in_grid_sizes(img_size, grid_sizes, strides):
     return out
 
 
-def anchor_targets_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, sampler, means, stds):
+def anchor_targets_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, sampler, means, stds, sync=True):
     """Sample (optional) + gather/encode for all images: the per-image anchor_target
     results concatenated in image order (anchor_head.py:177-192)."""
     if sampler is not None:  # device mode: the sampler's lists feed the gather (no compaction pass)
@@ -70,7 +70,8 @@ def anchor_targets_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels
         cap = sampler.max_num
     else:
         cap = max_boxes
-    return ops.anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, cap)
+    return ops.anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, cap,
+                                     sync=sync)
 
 
 def anchor_target(cls_out, reg_out, cls_channels, in_anchors, in_mask, gt_bbox, gt_label=None, assigner=None,

@@ -37,7 +37,10 @@ def _as_batch(props_list, dev):
 
 
 def bbox_targets_batched(props_list, gt_bboxes, gt_labels, assigner, sampler, target_means=None,
-                         target_stds=None):
+                         target_stds=None, sync=True):
+    """sync=False (device sampler mode): the flat full-capacity buffers of
+    ops.bbox_target_batched(sync=False) -- padding columns past the device total, no
+    per-image split -- with no host synchronisation on their size."""
     from .builder import build_module
     if isinstance(assigner, dict):
         assigner = build_module(assigner)
@@ -55,7 +58,9 @@ def bbox_targets_batched(props_list, gt_bboxes, gt_labels, assigner, sampler, ta
     rows = ops.sample_labels(rows, num_rows, max_rows, sampler.max_num, sampler.pos_num,
                              lists=ops.sampler_mode() == 'device')
     r = ops.bbox_target_batched(rows, num_rows, gcnt, max_rows, props, pstride, gts, glab,
-                                target_means, target_stds, sampler.max_num)
+                                target_means, target_stds, sampler.max_num, sync=sync)
+    if not sync:
+        return r
     out = {k: FlatList(r[k]) for k in ('tar_bbox', 'tar_label', 'tar_param', 'tar_is_gt')}
     out['tar_props'] = PropBatch()
     out['tar_props'].flat_buffer = r['tar_props']  # [4, n]: the images' rows back to back

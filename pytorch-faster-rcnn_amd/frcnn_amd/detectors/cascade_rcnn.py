@@ -5,6 +5,7 @@ import torch
 from torch import nn
 
 from .. import utils
+from ..region import RoiBatch
 
 
 class CascadeRCNN(nn.Module):
@@ -53,6 +54,15 @@ class CascadeRCNN(nn.Module):
         if self.with_shared_head:
             self.shared_head.init_weights()
 
+    def _sync_free_rcnn(self, feats):
+        """Faster R-CNN (one stage) with the device sampler, RoIAlign extraction and the fused
+        HIP head losses: the RCNN stage needs no host synchronisation on the sampled sizes."""
+        if self.num_stages != 1 or self.with_shared_head:
+            return False
+        head, extractor = self.rcnn_head[0], self.roi_extractors[0]
+        return (getattr(extractor, 'forward_flat', None) is not None and extractor._fusable() and
+                getattr(head, 'sync_free', None) is not None and head.sync_free(self.train_cfg.rcnn[0], feats[0].device))
+
     def extract_feat(self, x):
         x = self.backbone(x)
         return self.neck(x) if self.with_neck else x
@@ -71,6 +81,19 @@ class CascadeRCNN(nn.Module):
         l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
         losses['rpn_cls_loss'] = l_cls
         losses['rpn_reg_loss'] = l_reg
+        if self._sync_free_rcnn(feats):
+            # one stage, device sampler: padded targets, all rows through RoIAlign and the head,
+            # the loss divides by the device count -- no host synchronisation in the RCNN stage
+            head, extractor, scfg = self.rcnn_head[0], self.roi_extractors[0], cfg.rcnn[0]
+            r = head.bbox_targets_flat(props, gt_bboxes, gt_labels, scfg)
+            roi_out = extractor.forward_flat(feats, r['tar_props'], r['counts_dev'])
+            rois = RoiBatch([roi_out])
+            rois.flat = roi_out
+            cls_out, reg_out = head(rois)[0].flat
+            c_loss, r_loss = head.calc_loss_dev(cls_out, reg_out, r['tar_label'], r['tar_param'], r['n_dev'])
+            losses['rcnn_0_cls_loss'] = c_loss * cfg.stage_loss_weight[0]
+            losses['rcnn_0_reg_loss'] = r_loss * cfg.stage_loss_weight[0]
+            return losses
         for i in range(self.num_stages):
             head, extractor, scfg = self.rcnn_head[i], self.roi_extractors[i], cfg.rcnn[i]
             tar_props, tar_bboxes, tar_labels, tar_params, tar_is_gts = head.bbox_targets(

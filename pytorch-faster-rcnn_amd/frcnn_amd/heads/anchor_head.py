@@ -83,6 +83,17 @@ class AnchorHead(nn.Module):
     # ------------------------------------------------------------ targets
     def targets_batched(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg):
         """(tar_cls_out [C, T], tar_reg_out [4, T], tar_labels [T], tar_param [4, T]) for the batch."""
+        return self._targets(cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg)[:4]
+
+    def sync_free(self, train_cfg, device):
+        """Whether the loss can consume the targets without reading their size back to the
+        host: the device sampler's lists, fixed capacity S * max_num with padding columns,
+        and the fused head losses dividing by the device count (= len(tar_labels), the
+        reference's sampled avg_factor, anchor_head.py:123-126)."""
+        return (device.type == 'cuda' and train_cfg.get('sampler', None) is not None and
+                ops.sampler_mode() == 'device' and losses.fused_kinds(self.loss_cls, self.loss_bbox))
+
+    def _targets(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg, sync=True):
         dev = cls_outs[0].device
         grid_sizes = [tuple(c.shape[-2:]) for c in cls_outs]
         anchors = self._flat_anchors(grid_sizes, dev)
@@ -105,10 +116,10 @@ class AnchorHead(nn.Module):
         labels, _ = ops.maxiou_assign(anchors, 0, num, N, gts, gcnt, gmax, assigner.pos_iou, assigner.neg_iou,
                                       assigner.min_pos_iou, valid=masks, valid_seg_stride=masks.stride(0))
         r = anchor_targets_batched(labels, num, N, anchors, gts, glab, sampler, self.target_means,
-                                   self.target_stds)
+                                   self.target_stds, sync=sync)
         tar_cls = ops.gather_level_outputs(cls_outs, r['chosen_idx'], r['seg_of'], self.cls_channels)
         tar_reg = ops.gather_level_outputs(reg_outs, r['chosen_idx'], r['seg_of'], 4)
-        return tar_cls, tar_reg, r['tar_labels'], r['tar_param']
+        return tar_cls, tar_reg, r['tar_labels'], r['tar_param'], r.get('n_dev')
 
     def single_image_targets(self, level_cls_outs, level_reg_outs, gt_bbox, gt_label, level_anchors, input_size,
                              grid_sizes, img_meta, train_cfg):
@@ -144,6 +155,12 @@ class AnchorHead(nn.Module):
         return cls_loss, reg_loss
 
     def loss(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg):
+        if self.sync_free(train_cfg, cls_outs[0].device):
+            # padded targets + device count: no host synchronisation between the sampler and the loss
+            tc, tr, tl, tp, n_dev = self._targets(cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg,
+                                                  sync=False)
+            return losses.head_losses(self.loss_cls, self.loss_bbox, tc.t(), tl,
+                                      lambda: ops._l1_args(tr, tp, tl, 1), None, div_count=n_dev)
         tc, tr, tl, tp = self.targets_batched(cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg)
         return self.calc_loss(tc, tr, tl, tp, train_cfg)
 

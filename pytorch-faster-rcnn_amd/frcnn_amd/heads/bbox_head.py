@@ -30,6 +30,26 @@ class BBoxHead(nn.Module):
                                  tuple(self.target_means), tuple(self.target_stds))
         return r['tar_props'], r['tar_bbox'], r['tar_label'], r['tar_param'], r['tar_is_gt']
 
+    def sync_free(self, train_cfg, device):
+        """Whether this head's targets and loss can run without reading the sampled row
+        count back (see AnchorHead.sync_free): device sampler lists, fused HIP losses."""
+        return (device.type == 'cuda' and train_cfg.get('sampler', None) is not None and
+                ops.sampler_mode() == 'device' and losses.fused_kinds(self.loss_cls, self.loss_bbox))
+
+    def bbox_targets_flat(self, img_props, gt_bboxes, gt_labels, train_cfg):
+        """bbox_targets for the sync-free path: the flat padded buffers and the device counts."""
+        return bbox_targets_batched(img_props, gt_bboxes, gt_labels, train_cfg.assigner, train_cfg.sampler,
+                                    tuple(self.target_means), tuple(self.target_stds), sync=False)
+
+    def calc_loss_dev(self, cls_out, reg_out, tar_label, tar_param, n_dev):
+        """calc_loss_all over padded targets (label -1 rows ignored) with the sampled
+        avg_factor as the device count n_dev (bbox_head.py:56-80; 0 rows -> zero losses)."""
+        if self.reg_class_agnostic:
+            l1 = lambda: ops._l1_args(reg_out, tar_param.t(), tar_label, 0)  # noqa: E731
+        else:
+            l1 = lambda: ops._l1_class_select_args(reg_out, self.num_classes, tar_param.t(), tar_label)  # noqa: E731
+        return losses.head_losses(self.loss_cls, self.loss_bbox, cls_out, tar_label, l1, None, div_count=n_dev)
+
     def calc_loss_all(self, cls_out, reg_out, tar_label, tar_param, train_cfg):
         """bbox_head.py:56-80."""
         dev = cls_out.device

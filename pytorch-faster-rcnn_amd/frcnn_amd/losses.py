@@ -119,13 +119,23 @@ class CrossEntropyLoss(nn.Module):
         return F.cross_entropy(pred, label, reduction='none').sum() * self.loss_weight
 
 
-def head_losses(loss_cls, loss_bbox, cls_x, cls_label, l1_args, avg_factor):
+def fused_kinds(loss_cls, loss_bbox):
+    """True when head_losses can run this pair of loss modules as one launch."""
+    return isinstance(loss_bbox, SmoothL1Loss) and isinstance(loss_cls, (FocalLoss, CrossEntropyLoss))
+
+
+def head_losses(loss_cls, loss_bbox, cls_x, cls_label, l1_args, avg_factor, div_count=None):
     """(loss_cls(cls_x, cls_label) / avg_factor, loss_bbox.<masked | class_selected>(...) /
     avg_factor) as ONE HIP launch (ops.det_losses) when both modules are the HIP-backed
     kinds, the tensors are on the GPU and avg_factor is a host number (the sampled count);
     l1_args() builds the regression loss's arguments.  None when it does not apply (the
-    caller then runs the modules one by one)."""
-    if not (cls_x.is_cuda and isinstance(loss_bbox, SmoothL1Loss)) or isinstance(avg_factor, torch.Tensor):
+    caller then runs the modules one by one).  div_count (device int32 [1]) replaces
+    avg_factor for sync-free targets: padding rows (label -1) are ignored."""
+    if div_count is not None:
+        if not (cls_x.is_cuda and fused_kinds(loss_cls, loss_bbox)):
+            raise AssertionError('sync-free targets need the fused HIP head losses')
+        avg_factor = div_count
+    elif not (cls_x.is_cuda and isinstance(loss_bbox, SmoothL1Loss)) or isinstance(avg_factor, torch.Tensor):
         return None
     if isinstance(loss_cls, FocalLoss):
         kind, alpha, gamma = ops.CLS_FOCAL, loss_cls.alpha, loss_cls.gamma

@@ -252,8 +252,15 @@ def _numpy_keep(n, cap):
 
 
 # ---------------------------------------------------------------- target gathers (a6/a12)
-def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, max_out_per_seg):
-    """labels: the sampled labels [S, n] (chosen = label >= 0) or a SampleLists."""
+def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels, means, stds, max_out_per_seg,
+                          sync=True):
+    """labels: the sampled labels [S, n] (chosen = label >= 0) or a SampleLists.
+    sync=False (SampleLists only): no read-back of the output size -- every output keeps
+    its full capacity S * max_out_per_seg, the columns past the device total being padding
+    (seg_of -1, label -1, zero boxes: the gathers and losses ignore them), and 'n_dev' is
+    the total as a device int32 [1] (the heads' avg_factor)."""
+    if not sync and not isinstance(labels, SampleLists):
+        raise AssertionError('sync-free targets need the device sampler lists')
     sl = labels if isinstance(labels, SampleLists) else None
     if sl is not None:
         labels = sl.labels
@@ -277,6 +284,9 @@ def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels,
          ptr(sl.sel_counts if sl else None), ptr(chosen_idx), ptr(seg_of), ptr(tar_labels), ptr(tars[0]),
          ptr(tars[1]), ptr(tars[2]), T, ptr(counts), ptr(ws), ws.numel() if ws is not None else 0,
          stream_of(labels))
+    if not sync:
+        return dict(chosen_idx=chosen_idx, seg_of=seg_of, tar_labels=tar_labels, tar_anchors=tars[0],
+                    tar_bbox=tars[1], tar_param=tars[2], counts=None, counts_dev=counts[:S], n_dev=counts[S:])
     cnt = counts.cpu().tolist()  # output sizes are data dependent: one sync per batch
     n = cnt[S]
     return dict(chosen_idx=chosen_idx[:n], seg_of=seg_of[:n], tar_labels=tar_labels[:n],
@@ -338,8 +348,12 @@ def prepend_gt_labels(prop_labels, num_props, num_gts, max_rows):
 
 
 def bbox_target_batched(rows, num_rows, num_gts, max_rows, props, prop_seg_stride, gts, gt_labels, means, stds,
-                        max_out_per_seg):
-    """rows: the sampled prepended rows [S, n] (chosen = label >= 0) or a SampleLists."""
+                        max_out_per_seg, sync=True):
+    """rows: the sampled prepended rows [S, n] (chosen = label >= 0) or a SampleLists.
+    sync=False: full-capacity outputs with padding columns and device counts, as
+    anchor_target_batched."""
+    if not sync and not isinstance(rows, SampleLists):
+        raise AssertionError('sync-free targets need the device sampler lists')
     sl = rows if isinstance(rows, SampleLists) else None
     if sl is not None:
         rows = sl.labels
@@ -360,6 +374,9 @@ def bbox_target_batched(rows, num_rows, num_gts, max_rows, props, prop_seg_strid
          gt_labels.stride(0), m, sd, cap, ptr(sl.sel if sl else None), ptr(sl.sel_counts if sl else None),
          ptr(tars[0]), ptr(tars[1]), ptr(lab[0]), ptr(tars[2]), ptr(lab[1]), T, ptr(counts), ptr(ws),
          ws.numel() if ws is not None else 0, stream_of(rows))
+    if not sync:
+        return dict(tar_props=tars[0], tar_bbox=tars[1], tar_label=lab[0], tar_param=tars[2], tar_is_gt=lab[1],
+                    counts=None, counts_dev=counts[:S], n_dev=counts[S:])
     cnt = counts.cpu().tolist()
     n = cnt[S]
     return dict(tar_props=tars[0][:, :n], tar_bbox=tars[1][:, :n], tar_label=lab[0][:n], tar_param=tars[2][:, :n],
@@ -550,6 +567,19 @@ def roi_rows(boxes, counts, finest_scale, num_levels, seg_stride=0, flat=True):
     for c in counts:
         offs.append(offs[-1] + int(c))
     call('frh_roi_rows', len(counts), ptr(boxes), boxes.stride(-2), seg_stride, int(bool(flat)), i64_array(offs),
+         float(finest_scale), int(num_levels), ptr(rois), ptr(lv), stream_of(boxes))
+    return rois, lv
+
+
+def roi_rows_dev(boxes, counts_dev, finest_scale, num_levels):
+    """roi_rows for a fixed-capacity flat buffer [4, K] whose per-image counts stay on the
+    device (frh_roi_rows_dev): all K rows, those past the total being padding rows."""
+    _need_cuda(boxes, counts_dev)
+    K = boxes.shape[1]
+    dev = boxes.device
+    rois = torch.empty(K, 5, dtype=torch.float32, device=dev)
+    lv = torch.empty(K, dtype=torch.int64, device=dev) if num_levels > 1 else None
+    call('frh_roi_rows_dev', counts_dev.numel(), ptr(boxes), boxes.stride(-2), K, ptr(counts_dev),
          float(finest_scale), int(num_levels), ptr(rois), ptr(lv), stream_of(boxes))
     return rois, lv
 
@@ -931,9 +961,14 @@ class _DetLoss(torch.autograd.Function):
         tfloat = int(target.dtype == torch.float32)
         out = torch.empty(2, dtype=torch.float32, device=x.device)
         ws = _loss_workspace(x)
+        dcount = div if isinstance(div, torch.Tensor) else None  # device int32 count (sync-free targets)
+        hdiv = 1.0 if dcount is not None else float(div)
         call('frh_det_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
-             float(gamma), float(wc), float(div), ptr(rx), xs[0], xs[1], xs[2], ptr(ry), ys[0], ys[1], ptr(rlabel), rn,
-             rm, n_sel, float(beta), float(wr), float(div), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+             float(gamma), float(wc), hdiv, ptr(rx), xs[0], xs[1], xs[2], ptr(ry), ys[0], ys[1], ptr(rlabel), rn,
+             rm, n_sel, float(beta), float(wr), hdiv, ptr(dcount), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+        if dcount is not None:
+            # backward divides by the count as f32 (count 0: every row is padding, gradients 0)
+            div = dcount.float()
         ctx.save_for_backward(x, target, rx, ry, rlabel)
         ctx.cfg = (kind, tfloat, alpha, gamma, wc, xs, ys, rn, rm, n_sel, beta, wr, div)
         return out[0], out[1]
@@ -962,10 +997,17 @@ class _DetLoss(torch.autograd.Function):
 def det_losses(x, target, kind, alpha, gamma, cls_weight, l1_args, beta, reg_weight, avg_factor):
     """(cls, reg) = (cls_loss(x, target, kind) * cls_weight / avg_factor,
     smooth-L1(*l1_args) * reg_weight / avg_factor) in one launch; l1_args from _l1_args /
-    _l1_class_select_args.  avg_factor is a host number (the sampled count)."""
+    _l1_class_select_args.  avg_factor is a host number (the sampled count) or a device
+    int32 [1] count (sync-free targets: rows labelled < 0 are padding and ignored, a count
+    of 0 gives zero losses)."""
     _need_cuda(x, target)
     if target.dtype != torch.int64:
         target = target.long()
     rx, ry, rlabel, xs, ys, rn, rm, n_sel = l1_args
+    if isinstance(avg_factor, torch.Tensor):
+        if avg_factor.dtype != torch.int32 or avg_factor.numel() != 1 or not avg_factor.is_cuda:
+            raise AssertionError('a device avg_factor is an int32 [1] count')
+    else:
+        avg_factor = float(avg_factor)
     return _DetLoss.apply(_f32(x), target.contiguous(), int(kind), alpha, gamma, cls_weight, rx, ry, rlabel, xs, ys,
-                          rn, rm, n_sel, beta, reg_weight, float(avg_factor))
+                          rn, rm, n_sel, beta, reg_weight, avg_factor)

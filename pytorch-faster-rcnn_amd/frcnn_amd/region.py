@@ -139,6 +139,21 @@ class BasicRoIExtractor(nn.Module):
         res.flat = out
         return res
 
+    def forward_flat(self, level_feats, boxes, counts_dev):
+        """forward over a fixed-capacity flat box buffer [4, K] whose per-image counts stay
+        on the device (the sync-free RCNN targets): [K, C, ph, pw] for all K rows, the rows
+        past the total being padding (image 0, zero box)."""
+        n_lvls = len(self.roi_layers)
+        if not (0 < n_lvls <= len(level_feats)) or not self._fusable():
+            raise AssertionError('forward_flat needs RoIAlign layers of one configuration')
+        if not 0 < counts_dev.numel() <= 64:
+            raise AssertionError('forward_flat takes 1..64 images')
+        rois, levels = ops.roi_rows_dev(boxes, counts_dev, self.finest_scale, n_lvls)
+        first = self.roi_layers[0]
+        return ops.roi_align_multilevel(list(level_feats[:n_lvls]), rois, levels,
+                                        [l.spatial_scale for l in self.roi_layers], first.output_size,
+                                        first.sampling_ratio, first.aligned)
+
     def _rows(self, rois_list, counts, n_lvls, dev):
         """(image, box) rows + levels in one kernel (frh_roi_rows), reading the RCNN targets'
         flat buffer or the RPN's batched proposal buffer in place when the list carries one."""

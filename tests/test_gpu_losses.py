@@ -183,3 +183,77 @@ def test_det_losses_one_launch_equal_separate(case):
     (cb * 0.7 + qb * 1.3).backward()
     assert torch.equal(xa.grad, xb.grad)
     assert torch.equal(ra.grad, rb.grad)
+
+
+@pytest.mark.parametrize('case', ['rpn_sigmoid', 'rcnn_softmax_class_select', 'empty'])
+def test_det_losses_padded_rows_device_count(case):
+    """Sync-free targets: the fixed-capacity buffers carry padding rows (label -1) past the
+    sampled total and the divisor is that total as a device int32 count.  The losses equal the
+    unpadded ones with the host count (rtol 2e-5: the padded launch may partition the sum
+    differently), the real rows' gradients are bit-identical and the padding rows' are 0; a
+    count of 0 (every row padding) gives zero losses and zero gradients."""
+    g = torch.Generator().manual_seed(5)
+    n = 0 if case == 'empty' else 300
+    pad = 212
+    if case.startswith('rcnn'):
+        C = 21
+        lab = torch.cat([_labels(n, C - 1, 0.25, g), torch.full((pad,), -1, dtype=torch.int64)]).to(DEV)
+        cls0 = torch.randn(n + pad, C, generator=g).to(DEV)
+        reg0 = torch.randn(n + pad, 4 * C, generator=g).to(DEV)
+        tgt = torch.randn(4, n + pad, generator=g).to(DEV)
+        loss_cls, beta = losses.CrossEntropyLoss(), 1.0
+        l1 = lambda r, k: ops._l1_class_select_args(r[:k], C, tgt.t()[:k], lab[:k])  # noqa: E731
+        cls_in = lambda x, k: x[:k]  # noqa: E731
+    else:
+        lab = torch.cat([_labels(n, 1, 0.25, g), torch.full((pad,), -1, dtype=torch.int64)]).to(DEV)
+        cls0 = (torch.randn(1, n + pad, generator=g) * 2).to(DEV)
+        reg0 = torch.randn(4, n + pad, generator=g).to(DEV)
+        tgt = torch.randn(4, n + pad, generator=g).to(DEV)
+        loss_cls, beta = losses.CrossEntropyLoss(use_sigmoid=True), 1.0 / 9.0
+        l1 = lambda r, k: ops._l1_args(r[:, :k], tgt[:, :k], lab[:k], 1)  # noqa: E731
+        cls_in = lambda x, k: x[:, :k].t()  # noqa: E731
+    loss_bbox = losses.SmoothL1Loss(beta)
+    T = n + pad
+    cnt = torch.tensor([n], dtype=torch.int32, device=DEV)
+    xa, xb = cls0.clone().requires_grad_(True), cls0.clone().requires_grad_(True)
+    ra, rb = reg0.clone().requires_grad_(True), reg0.clone().requires_grad_(True)
+    ca, qa = losses.head_losses(loss_cls, loss_bbox, cls_in(xa, T), lab, lambda: l1(ra, T), None, div_count=cnt)
+    if n == 0:
+        assert float(ca) == 0.0 and float(qa) == 0.0
+        (ca + qa).backward()
+        assert not xa.grad.any() and not ra.grad.any()
+        return
+    cb, qb = losses.head_losses(loss_cls, loss_bbox, cls_in(xb, n), lab[:n], lambda: l1(rb, n), n)
+    torch.testing.assert_close(ca.view(()), cb.view(()), rtol=2e-5, atol=0)
+    torch.testing.assert_close(qa.view(()), qb.view(()), rtol=2e-5, atol=0)
+    (ca * 0.7 + qa * 1.3).sum().backward()
+    (cb * 0.7 + qb * 1.3).backward()
+    real = (slice(None, n),) if case.startswith('rcnn') else (slice(None), slice(None, n))
+    padr = (slice(n, None),) if case.startswith('rcnn') else (slice(None), slice(n, None))
+    assert torch.equal(xa.grad[real], xb.grad[real]) and torch.equal(ra.grad[real], rb.grad[real])
+    assert not xa.grad[padr].any() and not ra.grad[padr].any()
+
+
+def test_level_gather_skips_padding_columns():
+    """frh_gather_level_outputs / frh_scatter_level_grads: a column with seg_of -1 (a padding
+    column of the sync-free anchor targets) gathers zeros and scatters nothing, even where a
+    real column names the same location (no lost read-modify-write)."""
+    g = torch.Generator().manual_seed(2)
+    lv = [torch.randn(2, 3, 4, 5, generator=g).to(DEV).requires_grad_(True),
+          torch.randn(2, 3, 2, 3, generator=g).to(DEV).requires_grad_(True)]
+    idx = torch.tensor([0, 7, 25, 0, 0, 3], dtype=torch.int64, device=DEV)
+    seg = torch.tensor([0, 1, 0, -1, -1, 1], dtype=torch.int32, device=DEV)
+    out = ops.gather_level_outputs(lv, idx, seg, 3)
+    flat = [torch.cat([l[b].reshape(3, -1) for l in lv], 1) for b in range(2)]
+    want = torch.stack([flat[int(s)][:, int(i)] if s >= 0 else torch.zeros(3, device=DEV)
+                        for i, s in zip(idx.tolist(), seg.tolist())], 1)
+    assert torch.equal(out, want)
+    gout = torch.randn(3, 6, generator=g).to(DEV)
+    out.backward(gout)
+    ref = [torch.zeros_like(l) for l in lv]
+    rflat = [torch.cat([r[b].reshape(3, -1) for r in ref], 1) for b in range(2)]
+    for j, (i, s) in enumerate(zip(idx.tolist(), seg.tolist())):
+        if s >= 0:
+            rflat[s][:, i] += gout[:, j]
+    got = [torch.cat([l.grad[b].reshape(3, -1) for l in lv], 1) for b in range(2)]
+    assert torch.equal(got[0], rflat[0]) and torch.equal(got[1], rflat[1])

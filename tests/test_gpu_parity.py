@@ -1420,3 +1420,55 @@ def test_forward_train_loss_dict_vs_reference(dev):
     assert set(losses) == set(ref['losses'])
     for k, v in ref['losses'].items():
         assert float(losses[k]) == pytest.approx(v, rel=1e-4), (k, float(losses[k]), v)
+
+
+@pytest.mark.parametrize('max_props', [None, 100])
+def test_sync_free_targets_match_synced(dev, max_props):
+    """cfg2 forward_train with the device sampler: the sync-free RPN loss and RCNN stage
+    (padded fixed-capacity targets, frh_roi_rows_dev, device avg_factor) against the synced
+    path (read-back sizes, per-image split) on the same sampler stream and the same trunk
+    outputs (held fixed: MIOpen may pick another conv solver from one call to the next, see
+    test_graphed_trunk_matches_eager) -- same losses, and the same gradients w.r.t. the
+    features, the RPN outputs and the RCNN head parameters.  max_props=100 caps the proposals
+    so the RCNN buffer really carries padding rows (100 + gts < 512 per image).  Tolerances:
+    the padded launches may partition the f32 sums differently (losses rtol 1e-5), the FC
+    GEMMs run over more rows and RoIAlign backward accumulates with atomics."""
+    import bench
+    from frcnn_amd import set_sampler_mode
+    model, _ = bench.make_model(dev, seed=0)
+    if max_props is not None:
+        model.train_cfg.rpn_proposal.max_num = max_props
+    imgs, boxes, labels, metas = bench.make_batch(dev, 2, seed=1)
+    with torch.no_grad():
+        feats = [f.detach().clone().requires_grad_(True) for f in model.extract_feat(imgs)]
+        rc, rr = model.rpn_head(feats)
+    rc = [c.detach().clone().requires_grad_(True) for c in rc]
+    rr = [r.detach().clone().requires_grad_(True) for r in rr]
+    model.extract_feat = lambda x: feats
+    model.rpn_head.forward = lambda xs: (rc, rr)
+    leaves = feats + rc + rr + [p for p in model.rcnn_head.parameters() if p.requires_grad]
+    calls = []
+    ff = model.roi_extractors[0].forward_flat
+    model.roi_extractors[0].forward_flat = lambda *a: calls.append(1) or ff(*a)
+
+    def run():
+        set_sampler_mode('device', seed=21)
+        ls = model.forward_train(imgs, boxes, labels, metas)
+        gr = torch.autograd.grad(sum(ls.values()), leaves, allow_unused=True)
+        return {k: v.detach().clone() for k, v in ls.items()}, gr
+
+    la, ga = run()
+    assert calls, 'the sync-free RCNN stage did not run'
+    model.rpn_head.sync_free = lambda *a: False
+    model._sync_free_rcnn = lambda *a: False
+    lb, gb = run()
+    assert len(calls) == 1
+    assert la.keys() == lb.keys()
+    for k in la:
+        a, b = float(la[k]), float(lb[k])
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-7), (k, a, b)
+    for a, b in zip(ga, gb):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * float(b.abs().max()) + 1e-12)
