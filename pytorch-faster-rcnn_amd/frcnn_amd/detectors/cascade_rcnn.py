@@ -43,8 +43,9 @@ class CascadeRCNN(nn.Module):
         self.test_cfg = test_cfg
         # optional hipGraph of backbone + neck + RPN head convs (frcnn_amd.graphs.capture_trunk)
         self.graphed_trunk = None
-        # proposals on a second stream, concurrent with the RPN targets / loss (forward_train)
-        self.overlap_proposals = True
+        # proposals on a second stream, concurrent with the RPN targets / loss (forward_train);
+        # opt-in until its GPU measurement lands (the in-line order is the measured default)
+        self.overlap_proposals = False
         self._streams = {}
 
     def init_weights(self):
