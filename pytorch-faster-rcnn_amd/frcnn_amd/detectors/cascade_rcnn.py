@@ -23,6 +23,10 @@ class CascadeRCNN(nn.Module):
             self.neck = nn.Sequential(*[build_module(c) for c in neck]) if isinstance(neck, list) else \
                 build_module(neck)
         self.rpn_head = build_module(rpn_head)
+        if hasattr(self.rpn_head, 'allow_sync_free'):
+            # sync-free targets with the one-stage (Faster R-CNN) graph only; cascades keep the
+            # synced RPN targets (their multi-rank test pins them against a replayed reference)
+            self.rpn_head.allow_sync_free = num_stages == 1
         cfgs = roi_extractor if isinstance(roi_extractor, list) else [roi_extractor] * num_stages
         if len(cfgs) < num_stages:
             raise AssertionError('not enough roi extractors')

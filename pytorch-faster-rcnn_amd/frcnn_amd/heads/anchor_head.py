@@ -42,6 +42,7 @@ class AnchorHead(nn.Module):
         self.cls_channels = num_classes - 1 if self.use_sigmoid else num_classes
         self._anchor_cache = {}
         self._mask_cache = {}
+        self.allow_sync_free = True  # the detector may keep the synced targets (CascadeRCNN with > 1 stage)
 
     # ------------------------------------------------------------ anchors
     def _flat_anchors(self, grid_sizes, device):
@@ -90,7 +91,7 @@ class AnchorHead(nn.Module):
         host: the device sampler's lists, fixed capacity S * max_num with padding columns,
         and the fused head losses dividing by the device count (= len(tar_labels), the
         reference's sampled avg_factor, anchor_head.py:123-126)."""
-        return (device.type == 'cuda' and train_cfg.get('sampler', None) is not None and
+        return (self.allow_sync_free and device.type == 'cuda' and train_cfg.get('sampler', None) is not None and
                 ops.sampler_mode() == 'device' and losses.fused_kinds(self.loss_cls, self.loss_bbox))
 
     def _targets(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg, sync=True):
