@@ -4,7 +4,7 @@ every detection primitive underneath runs batched on the HIP kernels."""
 import torch
 from torch import nn
 
-from .. import utils
+from .. import ops, utils
 from ..heads.rpn_head import RPNHead
 from ..region import RoiBatch
 
@@ -23,10 +23,6 @@ class CascadeRCNN(nn.Module):
             self.neck = nn.Sequential(*[build_module(c) for c in neck]) if isinstance(neck, list) else \
                 build_module(neck)
         self.rpn_head = build_module(rpn_head)
-        if hasattr(self.rpn_head, 'allow_sync_free'):
-            # sync-free targets with the one-stage (Faster R-CNN) graph only; cascades keep the
-            # synced RPN targets (their multi-rank test pins them against a replayed reference)
-            self.rpn_head.allow_sync_free = num_stages == 1
         cfgs = roi_extractor if isinstance(roi_extractor, list) else [roi_extractor] * num_stages
         if len(cfgs) < num_stages:
             raise AssertionError('not enough roi extractors')
@@ -89,6 +85,12 @@ class CascadeRCNN(nn.Module):
 
     def forward_train(self, img_data, gt_bboxes, gt_labels, img_metas):
         """cascade_rcnn.py:90-154."""
+        try:
+            return self._forward_train(img_data, gt_bboxes, gt_labels, img_metas)
+        finally:
+            ops.release_packs()  # the batch's gt packs are shared by the RPN and every stage only
+
+    def _forward_train(self, img_data, gt_bboxes, gt_labels, img_metas):
         losses = {}
         if self.graphed_trunk is not None and self.graphed_trunk.matches(img_data):
             feats, rpn_cls, rpn_reg = self.graphed_trunk(img_data)

@@ -10,6 +10,7 @@ gather.  Results equal the reference's per-image targets concatenated in
 image order.
 """
 import logging
+from collections import OrderedDict
 
 import torch
 from torch import nn
@@ -41,8 +42,8 @@ class AnchorHead(nn.Module):
         self.use_sigmoid = self.loss_cls.use_sigmoid
         self.cls_channels = num_classes - 1 if self.use_sigmoid else num_classes
         self._anchor_cache = {}
-        self._mask_cache = {}
-        self.allow_sync_free = True  # the detector may keep the synced targets (CascadeRCNN with > 1 stage)
+        self._mask_cache = OrderedDict()  # LRU: keep-ratio resizing makes many image shapes
+        self.allow_sync_free = True  # False: keep the synced (read-back) targets even with the device sampler
 
     # ------------------------------------------------------------ anchors
     def _flat_anchors(self, grid_sizes, device):
@@ -66,20 +67,30 @@ class AnchorHead(nn.Module):
             off += n
         return out
 
+    MASK_CACHE_MAX = 64  # per-image masks, batch stacks and count tensors (LRU)
+
+    def _cached(self, key, make):
+        c = self._mask_cache
+        v = c.get(key)
+        if v is None:
+            v = c[key] = make()
+            while len(c) > self.MASK_CACHE_MAX:
+                c.popitem(last=False)
+        else:
+            c.move_to_end(key)
+        return v
+
     def _valid_masks(self, anchors, grid_sizes, img_metas, allowed_border):
-        keys = []
+        grids = tuple((int(h), int(w)) for h, w in grid_sizes)
+        masks = []
         for m in img_metas:
             img = tuple(int(v) for v in m['img_shape'][:2])
-            key = (tuple((int(h), int(w)) for h, w in grid_sizes), img, int(allowed_border), anchors.data_ptr())
-            if key not in self._mask_cache:
-                ins = in_grid_sizes(img, grid_sizes, self.anchor_strides)
-                self._mask_cache[key] = ops.inside_mask(anchors, grid_sizes, ins, self.num_anchors, img[0], img[1],
-                                                        allowed_border)
-            keys.append(key)
-        bkey = ('batch',) + tuple(keys)  # the [B, N] stack of a batch of image shapes, cached as well
-        if bkey not in self._mask_cache:
-            self._mask_cache[bkey] = torch.stack([self._mask_cache[k] for k in keys])
-        return self._mask_cache[bkey]
+            key = (grids, img, int(allowed_border), anchors.data_ptr())
+            masks.append((key, self._cached(key, lambda: ops.inside_mask(
+                anchors, grid_sizes, in_grid_sizes(img, grid_sizes, self.anchor_strides), self.num_anchors, img[0],
+                img[1], allowed_border))))
+        # the [B, N] stack of the batch's image shapes (cached too: a fixed-shape batch repeats it)
+        return self._cached(('batch',) + tuple(k for k, _ in masks), lambda: torch.stack([v for _, v in masks]))
 
     # ------------------------------------------------------------ targets
     def targets_batched(self, cls_outs, reg_outs, gt_bboxes, gt_labels, img_metas, train_cfg):
@@ -110,10 +121,7 @@ class AnchorHead(nn.Module):
             sampler = build_module(sampler)
         gts, gcnt, gmax = ops.pack_boxes([g.float() for g in gt_bboxes], dev)
         glab = ops.pack_labels(gt_labels, gmax, dev) if gt_labels is not None else None
-        nkey = ('num', B, N, dev)
-        if nkey not in self._mask_cache:
-            self._mask_cache[nkey] = torch.full((B,), N, dtype=torch.int32, device=dev)
-        num = self._mask_cache[nkey]
+        num = self._cached(('num', B, N, dev), lambda: torch.full((B,), N, dtype=torch.int32, device=dev))
         labels, _ = ops.maxiou_assign(anchors, 0, num, N, gts, gcnt, gmax, assigner.pos_iou, assigner.neg_iou,
                                       assigner.min_pos_iou, valid=masks, valid_seg_stride=masks.stride(0))
         r = anchor_targets_batched(labels, num, N, anchors, gts, glab, sampler, self.target_means,

@@ -90,7 +90,12 @@ _PACKED = []  # (inputs, their versions, key, result): the packs of the last few
 def _memo(inputs, key, make):
     """A batch's gt boxes / labels are packed once and reused by the RPN and every RCNN stage:
     hit only for the same tensor objects (held by the entry, so their storage cannot be
-    reused) with unchanged version counters."""
+    reused) with unchanged version counters, on the same stream (a pack is made on the
+    current stream and read in stream order).  Detectors drop the entries at the end of
+    each forward_train (release_packs)."""
+    dev = key[1]
+    if isinstance(dev, torch.device) and dev.type == 'cuda':
+        key = key + (torch.cuda.current_stream(dev).cuda_stream,)
     vers = tuple(t._version for t in inputs)
     for ent in _PACKED:
         if ent[2] == key and len(ent[0]) == len(inputs) and all(a is b for a, b in zip(ent[0], inputs)) \
@@ -100,6 +105,11 @@ def _memo(inputs, key, make):
     _PACKED.insert(0, (tuple(inputs), vers, key, res))
     del _PACKED[8:]
     return res
+
+
+def release_packs():
+    """Forget the memoised gt packs (end of a forward_train)."""
+    del _PACKED[:]
 
 
 def pack_boxes(box_list, device, min_cols=1):

@@ -63,8 +63,19 @@ def install_shims():
             return torch.from_numpy(out)
 
     class RoIPool(torch.nn.Module):
-        def __init__(self, output_size, spatial_scale):
+        """torchvision's legacy RoIPool as the oracle restates it.  Accepts and ignores
+        `sampling_ratio`, which the reference's cfg1 passes (configs/faster_rcnn_r50.py:26)
+        and torchvision itself rejects."""
+
+        def __init__(self, output_size, spatial_scale, sampling_ratio=None):
             super().__init__()
+            self.output_size = output_size if isinstance(output_size, tuple) else (output_size, output_size)
+            self.spatial_scale = spatial_scale
+
+        def forward(self, x, rois):
+            out, _ = oracle.roi_pool(x.detach().numpy(), rois.detach().numpy(), self.output_size,
+                                     self.spatial_scale)
+            return torch.from_numpy(out)
 
     ops.nms, ops.RoIAlign, ops.RoIPool = nms, RoIAlign, RoIPool
     ops.roi_align = ops.roi_pool = None
@@ -253,6 +264,23 @@ def gen_rpn(lib_anchor, rpn_head_mod):
             cls, reg = inputs.head_outputs(500 + i, inputs.FPN_GRIDS, 3, 1, reg_scale=0.5)
             b, s, _ = head.predict_single_image([torch.from_numpy(c[0]) for c in cls],
                                                 [torch.from_numpy(r[0]) for r in reg], anchors, inputs.img_meta(),
+                                                cd(cfg))
+            res['{}_{}_boxes'.format(tag, i)] = b.numpy()
+            res['{}_{}_scores'.format(tag, i)] = s.numpy()
+    # cfg1 (configs/faster_rcnn_r50.py:14-20,60-66): ONE stride-16 level of 12 anchors on the
+    # C4 grid (29 184 anchors), pre_nms 12 000 -> one 12 000-box NMS -> 2 000, min size 16
+    # (x scale_factor 1.6); the n_lvls == 1 path of rpn_head.py:68-120
+    c4 = [lib_anchor.AnchorCreator(base=16, scales=[4, 8, 16, 32], aspect_ratios=[0.5, 1.0, 2.0])(16, g)
+          for g in inputs.C4_GRIDS]
+    head = rpn_head_mod.RPNHead(1024, 256, anchor_scales=[4, 8, 16, 32], anchor_strides=[16],
+                                loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True),
+                                loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0))
+    for tag, cfg in (('c4train', dict(pre_nms=12000, post_nms=2000, max_num=2000, nms_iou=0.7, min_bbox_size=16)),
+                     ('c4test', dict(pre_nms=6000, post_nms=300, max_num=300, nms_iou=0.7, min_bbox_size=0.0))):
+        for i in range(2):
+            cls, reg = inputs.head_outputs(550 + i, inputs.C4_GRIDS, 12, 1, reg_scale=0.5)
+            b, s, _ = head.predict_single_image([torch.from_numpy(c[0]) for c in cls],
+                                                [torch.from_numpy(r[0]) for r in reg], c4, inputs.img_meta(),
                                                 cd(cfg))
             res['{}_{}_boxes'.format(tag, i)] = b.numpy()
             res['{}_{}_scores'.format(tag, i)] = s.numpy()
@@ -475,7 +503,7 @@ def _topk_by_center_floor(fcos_head_mod):
     fcos_head_mod.topk_by_center = topk_by_center
 
 
-def gen_whole_detectors():
+def gen_whole_detectors(only=None):
     """forward_train loss dict AND forward_test detections of the reference's own detector for
     each BASELINE config in inputs.WHOLE_DETECTORS (lib/builder.py; CascadeRCNN
     lib/detectors/cascade_rcnn.py:90-203, RetinaNet retinanet.py:43-59, FCOS fcos.py:42-57) on
@@ -488,6 +516,8 @@ def gen_whole_detectors():
     import lib.heads.fcos_head as fcos_head_mod
     _topk_by_center_floor(fcos_head_mod)
     for tag, fname, over, shape in inputs.WHOLE_DETECTORS:
+        if only and tag not in only:
+            continue
         img, boxes, labels, metas = inputs.ftrain_case(shape)
         cfg = Config.fromfile(os.path.join(REF, 'configs', fname))
         cfg.model.backbone.pretrained = False
@@ -544,8 +574,11 @@ def main():
     if '--only-ftrain' in sys.argv:
         gen_forward_train()
         return 0
-    if '--only-whole' in sys.argv:
-        gen_whole_detectors()
+    if '--only-whole' in sys.argv:  # optionally followed by config tags (cfg1 cfg2 ...)
+        gen_whole_detectors([a for a in sys.argv if a.startswith('cfg')])
+        return 0
+    if '--only-rpn' in sys.argv:
+        gen_rpn(lib_anchor, rpn_head_mod)
         return 0
     if '--only-new' in sys.argv:
         import lib.heads.retina_head as retina_mod

@@ -221,9 +221,11 @@ def ftrain_case(shape=FTRAIN_SHAPE):
 # test_cfg overrides, image shape).  The two-stage configs' RCNN classifiers are N(0, 0.01^2)
 # under seeded_state, so every softmax score sits near 1/21 < 0.05: their fixtures lower
 # min_score to 0 (every (proposal, class) pair is a multiclass-NMS candidate: one offset NMS
-# over up to 20 000 boxes).  cfg5 runs on 384x640: the reference's ATSS top-9 per level needs
+# over up to 20 000 boxes).  cfg1 is the C4 graph: one stride-16 level, RoIPool (its
+# sampling_ratio accepted and ignored), pre_nms 12 000.  cfg5 runs on 384x640: the reference's ATSS top-9 per level needs
 # 9 cells on P7 (stride 128).
-WHOLE_DETECTORS = [('cfg2', 'faster_rcnn_r50_fpn.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
+WHOLE_DETECTORS = [('cfg1', 'faster_rcnn_r50.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
+                   ('cfg2', 'faster_rcnn_r50_fpn.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
                    ('cfg3', 'retinanet_r50_fpn.py', {}, FTRAIN_SHAPE),
                    ('cfg4', 'cascade_rcnn_r50_fpn.py', {'rcnn': {'min_score': 0.0}}, FTRAIN_SHAPE),
                    ('cfg5', 'fcos_r50_fpn_atss.py', {}, (384, 640))]

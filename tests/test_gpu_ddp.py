@@ -1,15 +1,35 @@
-"""Data-parallel training of the REAL detector on the HIP path: two `gloo` ranks share
+"""Data-parallel training of the REAL detectors on the HIP path: two `gloo` ranks share
 cuda:0 (a one-GPU box cannot run two RCCL ranks), each running frcnn_amd.train.TrainStep
-(DistributedDataParallel, bucketed gradient all-reduce) on the cfg4 Cascade R-CNN
-(configs/cascade_rcnn_r50_fpn.py: 3 RCNN stages, refine, per-stage stds) with its own
-2-image shard, for two iterations (a parameter DDP never saw a gradient for would fail
-the second iteration's reduction).  Both ranks must hold identical parameters after each
-iteration, and the first iteration's update must equal (to float-atomic tolerance: the
-RoIAlign backward and MIOpen's backward convolutions sum in run-dependent order) one
-single-process iteration on the rank-averaged gradient -- the reference's train_one_iter
-(lib/trainer/trainer.py:100-127, hooks.py:55-59) with DDP averaging.  (Later iterations
-are not compared with the reference: a last-bit difference in the updated weights can
-flip the RPN's near-tied random-init scores, i.e. which proposals are selected.)"""
+(DistributedDataParallel, bucketed gradient all-reduce) on its own 2-image shard for two
+iterations (a parameter DDP never saw a gradient for fails the second iteration's
+reduction), for
+  * cfg4 Cascade R-CNN (configs/cascade_rcnn_r50_fpn.py: 3 RCNN stages, refine, per-stage
+    stds; reference lib/detectors/cascade_rcnn.py:90-154), and
+  * cfg5 ATSS (configs/fcos_r50_fpn_atss.py: FCOSHead with centerness, trainable level
+    coefficients, GIoU; reference lib/detectors/fcos.py:42-57, lib/heads/fcos_head.py:525-568).
+
+The reference iteration is computed IN EACH WORKER PROCESS, before its DDP step, on a deep
+copy of the same model: the plain (non-DDP) forward_train + backward of the rank's shard on
+the same device-sampler stream, the gradients averaged over ranks with one all-reduce of
+their concatenation, then clip_grad_norm_ and SGD -- the reference's train_one_iter
+(lib/trainer/trainer.py:100-127, hooks.py:55-59) on the rank-averaged gradient.  Checks:
+  * each rank's DDP loss equals its own reference loss (the forward is the same
+    computation in the same process);
+  * after the first iteration every parameter equals the reference update to
+    float-atomic tolerance (the RoIAlign backward and MIOpen's backward convolutions sum
+    in run-dependent order);
+  * the ranks hold identical parameters after every iteration.
+
+Why the reference runs in the worker and not in the test process: a second process is
+not guaranteed the same convolution solutions (MIOpen's immediate mode reads a find
+database that other processes may have updated), and a last-bit difference in the trunk's
+outputs can flip which of the near-tied random-init RPN scores are selected -- round 3's
+version of this test, which replayed both ranks in the pytest process, saw rank 1's loss
+1.2e-3 away from the replay with the synced and the sync-free RPN targets alike, while
+in-process replays of the same calls are bit-identical under poisoned workspaces
+(tests/test_gpu_state.py, tools/diag_state.py)."""
+import copy
+import hashlib
 import os
 import socket
 
@@ -19,7 +39,6 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-CONFIG = 'cascade_rcnn_r50_fpn'
 STEPS = 2
 WORLD = 2
 
@@ -32,15 +51,34 @@ def _port():
     return p
 
 
-def _setup(dev):
-    import bench
-    torch.backends.cudnn.benchmark = False
-    torch.backends.cudnn.deterministic = True
-    model, cfg = bench.make_model(dev, seed=0, config=os.path.join(bench.CONFIG_DIR, CONFIG + '.py'))
-    return model, cfg
+def _reference_step(model, cfg, batch, world, seed):
+    """One plain iteration on a copy of `model`: returns (loss, updated trainable params)."""
+    import torch.distributed as dist
+    from frcnn_amd import set_sampler_mode
+    from frcnn_amd.train import build_optimizer
+    ref = copy.deepcopy(model)
+    params = [p for p in ref.parameters() if p.requires_grad]
+    opt = build_optimizer(params, cfg.optimizer)
+    set_sampler_mode('device', seed=seed)
+    loss = sum(ref.forward_train(*batch).values())
+    loss.backward()
+    grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+    flat = torch.cat([g.reshape(-1) for g in grads]).cpu()
+    dist.all_reduce(flat)
+    flat /= world
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.grad = flat[off:off + n].view_as(p).to(p.device)
+        off += n
+    clip = cfg.optimizer_config.get('grad_clip')
+    if clip:
+        torch.nn.utils.clip_grad_norm_(params, clip['max_norm'], clip.get('norm_type', 2))
+    opt.step()
+    return float(loss), [p.detach().cpu().numpy() for p in ref.parameters()]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, config):
     try:
         import sys
         repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -49,101 +87,67 @@ def _worker(rank, world, port, q):
         os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         dist.init_process_group('gloo', rank=rank, world_size=world)
         import bench
-        import frcnn_amd
+        from frcnn_amd import set_sampler_mode
         from frcnn_amd.train import TrainStep
         dev = torch.device('cuda', 0)
         torch.cuda.set_device(dev)
-        frcnn_amd.set_sampler_mode('device', seed=1234 + rank)
-        model, cfg = _setup(dev)
+        torch.backends.cudnn.benchmark = False
+        torch.backends.cudnn.deterministic = True
+        model, cfg = bench.make_model(dev, seed=0, config=os.path.join(bench.CONFIG_DIR, config + '.py'))
         batch = bench.make_batch(dev, 2, seed=0, rank=rank)
+        init = [p.detach().cpu().numpy() for p in model.parameters()]
+        ref_loss, ref_params = _reference_step(model, cfg, batch, world, 1234 + rank)
+        set_sampler_mode('device', seed=1234 + rank)  # the same sampler stream for the DDP step
         step = TrainStep(model, cfg.optimizer, cfg.optimizer_config.get('grad_clip'), world, dev, bucket_mb=25)
-        import hashlib
-        losses, snaps = [], []
-        for it in range(STEPS):  # the first iteration's parameters in full, later ones as digests
+        losses, digests, first = [], [], None
+        for it in range(STEPS):
             losses.append(float(step(*batch)))
             ps = [p.detach().cpu().numpy() for p in model.parameters()]
-            snaps.append(ps if it == 0 else [hashlib.sha256(x.tobytes()).hexdigest() for x in ps])
+            digests.append([hashlib.sha256(x.tobytes()).hexdigest() for x in ps])
+            if it == 0:
+                first = ps
         torch.cuda.synchronize()
-        q.put((rank, losses, snaps))
+        # first update vs the reference update (float-atomic summation noise)
+        worst, moved = 0.0, 0
+        for a, r, i in zip(first, ref_params, init):
+            d, dr = a - i, r - i
+            scale = max(float(np.abs(dr).max()), 1e-12)
+            worst = max(worst, (float(np.abs(d - dr).max()) - 1e-9) / scale)
+            moved += int(np.abs(dr).max() > 0)
+        q.put((rank, dict(losses=losses, ref_loss=ref_loss, digests=digests, worst=worst, moved=moved,
+                          nparams=len(first))))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent on the queue
         import traceback
-        q.put((rank, None, traceback.format_exc()[-3000:] + repr(e)))
+        q.put((rank, traceback.format_exc()[-3000:] + repr(e)))
 
 
-def _reference(dev):
-    """One iteration in one process on the rank-averaged gradient; each rank's device
-    sampler stream is replayed (seed 1234 + rank, its own call counter)."""
-    import bench
-    from frcnn_amd import ops
-    from frcnn_amd.train import build_optimizer
-    model, cfg = _setup(dev)
-    params = [p for p in model.parameters() if p.requires_grad]
-    opt = build_optimizer(params, cfg.optimizer)
-    clip = cfg.optimizer_config.get('grad_clip')
-    batches = [bench.make_batch(dev, 2, seed=0, rank=r) for r in range(WORLD)]
-    samplers = [{'mode': 'device', 'seed': 1234 + r, 'calls': 0} for r in range(WORLD)]
-    saved = dict(ops._SAMPLER)
-    losses = [[] for _ in range(WORLD)]
-    try:
-        for _ in range(1):
-            opt.zero_grad(set_to_none=True)
-            for r in range(WORLD):
-                ops._SAMPLER.clear()
-                ops._SAMPLER.update(samplers[r])
-                loss = sum(model.forward_train(*batches[r]).values())
-                (loss / WORLD).backward()
-                samplers[r] = dict(ops._SAMPLER)
-                losses[r].append(float(loss))
-            if clip:
-                torch.nn.utils.clip_grad_norm_(params, clip['max_norm'], clip.get('norm_type', 2))
-            opt.step()
-    finally:
-        ops._SAMPLER.clear()
-        ops._SAMPLER.update(saved)
-    torch.cuda.synchronize()
-    return losses, [p.detach().cpu().numpy() for p in model.parameters()]
-
-
-def test_cascade_ddp_two_gloo_ranks_on_one_gpu(dev):
+@pytest.mark.parametrize('config', ['cascade_rcnn_r50_fpn', 'fcos_r50_fpn_atss'])
+def test_ddp_two_gloo_ranks_on_one_gpu(dev, config):
     import torch.multiprocessing as mp
-    flags = (torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, config)) for r in range(WORLD)]
     for p in procs:
         p.start()
     try:
-        out = sorted((q.get(timeout=240) for _ in procs), key=lambda x: x[0])
+        out = sorted((q.get(timeout=300) for _ in procs), key=lambda x: x[0])
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for rank, losses, snaps in out:
-        assert losses is not None, 'rank {} failed:\n{}'.format(rank, snaps)
+    for rank, res in out:
+        assert isinstance(res, dict), 'rank {} failed:\n{}'.format(rank, res)
     for p in procs:
         assert p.exitcode == 0
-    (_, l0, s0), (_, l1, s1) = out
-    try:
-        ref_losses, ref = _reference(dev)
-        init, _ = _setup(dev)
-        init = [p.detach().cpu().numpy() for p in init.parameters()]
-    finally:
-        torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = flags
-    assert all(np.isfinite(l0)) and all(np.isfinite(l1)) and l0[0] != l1[0]  # each rank's own shard
-    np.testing.assert_allclose([l0[0], l1[0]], [ref_losses[0][0], ref_losses[1][0]], rtol=1e-4)
-    for it in range(STEPS):
-        for a, b in zip(s0[it], s1[it]):
-            if it == 0:
-                np.testing.assert_array_equal(a, b)  # one all-reduced gradient: ranks stay in lock step
-            else:
-                assert a == b
-    moved = 0
-    for a, r, i in zip(s0[0], ref, init):
-        d, dr = a - i, r - i  # the first update agrees to float-atomic summation noise
-        scale = max(float(np.abs(dr).max()), 1e-12)
-        assert float(np.abs(d - dr).max()) <= 1e-2 * scale + 1e-9, (float(np.abs(d - dr).max()), scale)
-        moved += int(np.abs(dr).max() > 0)
-    assert moved > len(ref) // 2
+    r0, r1 = out[0][1], out[1][1]
+    assert all(np.isfinite(r0['losses'])) and all(np.isfinite(r1['losses']))
+    assert r0['losses'][0] != r1['losses'][0]  # each rank's own shard
+    for r in (r0, r1):
+        np.testing.assert_allclose(r['losses'][0], r['ref_loss'], rtol=1e-6)
+        assert r['worst'] <= 1e-2, r['worst']  # |update - reference update| <= 1e-2 x its scale
+        assert r['moved'] > r['nparams'] // 2
+    for it in range(STEPS):  # one all-reduced gradient: the ranks stay in lock step
+        assert r0['digests'][it] == r1['digests'][it], it

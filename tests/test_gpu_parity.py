@@ -448,6 +448,31 @@ def test_rpn_proposals_vs_reference(dev, golden, tag, cfg):
         np.testing.assert_allclose(canon_ties(b, s), canon_ties(rb, rs), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize('tag,cfg', [('c4train', (12000, 2000, 2000, 0.7, 16.0)), ('c4test', (6000, 300, 300, 0.7, 0.0))])
+def test_rpn_proposals_c4_vs_reference(dev, golden, tag, cfg):
+    """cfg1's single-level RPN (configs/faster_rcnn_r50.py:14-20,60-66): 12 anchors per cell on the
+    38x64 stride-16 grid (29 184), pre_nms 12 000 -> one 12 000-box NMS -> 2 000 with min size
+    16 x 1.6, against the reference's own RPNHead.predict_single_image (gen_golden.gen_rpn)."""
+    from frcnn_amd.config import wrap
+    from frcnn_amd.heads.rpn_head import RPNHead
+    g = golden('rpn.npz')
+    pre, post, mx, thr, minb = cfg
+    head = RPNHead(1024, 256, anchor_scales=[4, 8, 16, 32], anchor_strides=[16],
+                   loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True),
+                   loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0)).to(dev)
+    tcfg = wrap(dict(pre_nms=pre, post_nms=post, max_num=mx, nms_iou=thr, min_bbox_size=minb))
+    outs = [inputs.head_outputs(550 + i, inputs.C4_GRIDS, 12, 1, reg_scale=0.5) for i in range(2)]
+    cls_b = [T(np.concatenate([outs[0][0][0], outs[1][0][0]], 0), dev)]
+    reg_b = [T(np.concatenate([outs[0][1][0], outs[1][1][0]], 0), dev)]
+    props, scores, _ = head.predict_bboxes_from_output(cls_b, reg_b, [inputs.img_meta()] * 2, tcfg)
+    for i in range(2):
+        rb, rs = g['{}_{}_boxes'.format(tag, i)], g['{}_{}_scores'.format(tag, i)]
+        b, s = props[i].cpu().numpy(), scores[i].cpu().numpy()
+        assert b.shape == rb.shape, (b.shape, rb.shape)
+        np.testing.assert_allclose(s, rs, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(canon_ties(b, s), canon_ties(rb, rs), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize('n,thr', [(2000, 0.7), (1000, 0.5), (5000, 0.3), (12000, 0.7), (1, 0.5), (63, 0.5),
                                    (64, 0.5), (65, 0.5)])
 def test_nms_keep_bit_exact(dev, n, thr):

@@ -179,6 +179,22 @@ def test_rpn_proposals(golden, tag, cfg):
         np.testing.assert_allclose(b, rb, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize('tag,cfg', [('c4train', (12000, 2000, 2000, 0.7, 16.0)), ('c4test', (6000, 300, 300, 0.7, 0.0))])
+def test_rpn_proposals_c4(golden, tag, cfg):
+    """cfg1's single stride-16 level (12 anchors per cell, pre_nms 12 000: one 12 000-box NMS)."""
+    g = golden('rpn.npz')
+    pre, post, mx, thr, minb = cfg
+    anchors = [oracle.anchor_grid(16, [4, 8, 16, 32], [0.5, 1.0, 2.0], 16, gr) for gr in inputs.C4_GRIDS]
+    for i in range(2):
+        cls, reg = inputs.head_outputs(550 + i, inputs.C4_GRIDS, 12, 1, reg_scale=0.5)
+        b, s = oracle.rpn_predict_single_image([c[0] for c in cls], [r[0] for r in reg], anchors, inputs.IMG_SHAPE,
+                                               1.6 * minb, pre, post, mx, thr)
+        rb, rs = g['{}_{}_boxes'.format(tag, i)], g['{}_{}_scores'.format(tag, i)]
+        assert b.shape == rb.shape
+        np.testing.assert_allclose(s, rs, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(canon_ties(b, s), canon_ties(rb, rs), rtol=1e-5, atol=1e-3)
+
+
 # ----------------------------------------------------------------- a16 ATSS / LTRB
 def atss_anchors():
     return [oracle.anchor_grid(s, [8], [1.0], s, g).reshape(4, -1)
