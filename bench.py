@@ -24,8 +24,9 @@ After the timed region (never inside it):
   * `cpu_baseline`: the same forward+loss on the host (torch CPU convs + the
     oracle's C restatement of the hot path), bounded 1-image sample, img/s.
   * `cpu_baseline_hot_path`: the oracle's C assign / anchor_target /
-    proposals+NMS / RoIAlign timed on this run's own inputs on one host core,
-    beside the GPU µs of the same functions.
+    proposals+NMS / RoIAlign timed on this run's own inputs on the host's threads
+    (OpenMP; `cores`) and on one thread, with the CPU model, beside the GPU µs of
+    the same functions.
 """
 import argparse
 import json
@@ -311,8 +312,9 @@ def cpu_baseline(seed, max_s):
 
 def hot_path_cpu_baseline(model, cfg, batch, roi_rec, dev, gpu_us, batch_size):
     """The oracle's C restatement of the hot-path functions on THIS run's inputs (the
-    trunk's RPN outputs, the VOC gts, the timed step's RoIs and features), one host core,
-    each function on every image of the batch; GPU µs of the same functions beside."""
+    trunk's RPN outputs, the VOC gts, the timed step's RoIs and features), on the host's
+    threads and on one thread, each function on every image of the batch; GPU µs of the
+    same functions beside."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import oracle  # oracle/oracle.py (test infrastructure: the timed CPU baseline)
     imgs, gts, gt_labels, metas = batch
@@ -331,43 +333,79 @@ def hot_path_cpu_baseline(model, cfg, batch, roi_rec, dev, gpu_us, batch_size):
     mk = masks.cpu().numpy().astype(bool)
     cls_np = [c.cpu().numpy() for c in cls_outs]
     reg_np = [r.cpu().numpy() for r in reg_outs]
-    t = {'assign': 0.0, 'anchor_target': 0.0, 'proposals_nms': 0.0, 'roi_align': 0.0}
     B = imgs.shape[0]
     rc = cfg.train_cfg.rpn
     pc = cfg.train_cfg.rpn_proposal
-    for i in range(B):
-        gt = gts[i].cpu().numpy()
-        in_anc = np.ascontiguousarray(anc[:, mk[i]])
-        t0 = time.perf_counter()
-        oracle.maxiou_assign(in_anc, gt, rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou)
-        t['assign'] += time.perf_counter() - t0
-        co = np.concatenate([c[i].reshape(1, -1) for c in cls_np], 1)
-        ro = np.concatenate([r[i].reshape(4, -1) for r in reg_np], 1)
-        t0 = time.perf_counter()
-        oracle.anchor_target(co, ro, 1, in_anc, mk[i], gt, None,
-                             (rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou),
-                             (rc.sampler.max_num, rc.sampler.pos_num), None, None)
-        t['anchor_target'] += time.perf_counter() - t0
-        t0 = time.perf_counter()
-        oracle.rpn_predict_single_image([c[i] for c in cls_np], [r[i] for r in reg_np], lv_anc, IMG_SHAPE,
-                                        float(pc.min_bbox_size), pc.pre_nms, pc.post_nms, pc.max_num, pc.nms_iou)
-        t['proposals_nms'] += time.perf_counter() - t0
+    roi_in = None
     if roi_rec is not None:
         _, _, rois, levels, shapes, (ph, pw) = roi_rec[:6]
-        scales = roi_rec[7]
-        fnp = [f.cpu().numpy() for f in feats[:len(shapes)]]
-        t0 = time.perf_counter()
-        oracle.roi_align(fnp, rois.cpu().numpy(), levels.cpu().numpy(), scales, (ph, pw), 2)
-        t['roi_align'] = time.perf_counter() - t0
-    per_img = {k: v * 1e3 / B for k, v in t.items()}
-    out = {'unit': 'ms per image', 'cores': 1, 'kind': 'port',
-           'sample': 'oracle C restatement on this run\'s {} images: trunk RPN outputs, VOC gts, the timed step\'s '
-                     'RoIs + P2-P5 features'.format(B),
-           'cpu_ms_per_image': per_img, 'gpu_us_per_image': {k: (v / batch_size if v is not None else None)
-                                                              for k, v in gpu_us.items()}}
-    out['speedup'] = {k: (per_img[k] * 1e3 / out['gpu_us_per_image'][k]) if out['gpu_us_per_image'].get(k) else None
-                      for k in per_img}
+        roi_in = ([f.cpu().numpy() for f in feats[:len(shapes)]], rois.cpu().numpy(), levels.cpu().numpy(),
+                  roi_rec[7], (ph, pw))
+
+    def timed(threads):
+        oracle.set_threads(threads)
+        t = {'assign': 0.0, 'anchor_target': 0.0, 'proposals_nms': 0.0, 'roi_align': 0.0}
+        for i in range(B):
+            gt = gts[i].cpu().numpy()
+            in_anc = np.ascontiguousarray(anc[:, mk[i]])
+            t0 = time.perf_counter()
+            oracle.maxiou_assign(in_anc, gt, rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou)
+            t['assign'] += time.perf_counter() - t0
+            co = np.concatenate([c[i].reshape(1, -1) for c in cls_np], 1)
+            ro = np.concatenate([r[i].reshape(4, -1) for r in reg_np], 1)
+            t0 = time.perf_counter()
+            oracle.anchor_target(co, ro, 1, in_anc, mk[i], gt, None,
+                                 (rc.assigner.pos_iou, rc.assigner.neg_iou, rc.assigner.min_pos_iou),
+                                 (rc.sampler.max_num, rc.sampler.pos_num), None, None)
+            t['anchor_target'] += time.perf_counter() - t0
+            t0 = time.perf_counter()
+            oracle.rpn_predict_single_image([c[i] for c in cls_np], [r[i] for r in reg_np], lv_anc, IMG_SHAPE,
+                                            float(pc.min_bbox_size), pc.pre_nms, pc.post_nms, pc.max_num, pc.nms_iou)
+            t['proposals_nms'] += time.perf_counter() - t0
+        if roi_in is not None:
+            fnp, r5, lvs, scales, osz = roi_in
+            t0 = time.perf_counter()
+            oracle.roi_align(fnp, r5, lvs, scales, osz, 2)
+            t['roi_align'] = time.perf_counter() - t0
+        return {k: v * 1e3 / B for k, v in t.items()}
+
+    threads = host_threads()
+    per_img_1 = timed(1)
+    per_img = timed(threads)
+    oracle.set_threads(1)
+    gpu = {k: (v / batch_size if v is not None else None) for k, v in gpu_us.items()}
+    out = {'unit': 'ms per image', 'cores': threads, 'kind': 'port',
+           'sample': 'oracle C restatement (OpenMP over the IoU table, assignment, NMS mask and RoIAlign RoIs) '
+                     'on this run\'s {} images: trunk RPN outputs, VOC gts, the timed step\'s RoIs + P2-P5 '
+                     'features'.format(B),
+           'host': host_info(), 'cpu_ms_per_image': per_img, 'cpu_ms_per_image_1_thread': per_img_1,
+           'gpu_us_per_image': gpu}
+    out['speedup'] = {k: (per_img[k] * 1e3 / gpu[k]) if gpu.get(k) else None for k in per_img}
+    out['speedup_vs_1_thread'] = {k: (per_img_1[k] * 1e3 / gpu[k]) if gpu.get(k) else None for k in per_img_1}
     return out
+
+
+def host_threads():
+    """The host threads this process may use: OMP_NUM_THREADS when set (the GPU box sets
+    it to its CPU share), else the CPUs of the affinity mask."""
+    v = os.environ.get('OMP_NUM_THREADS')
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    return len(os.sched_getaffinity(0))
+
+
+def host_info():
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for ln in f:
+                if ln.startswith('model name'):
+                    model = ln.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'cpu_model': model, 'nproc': os.cpu_count(), 'affinity_cpus': len(os.sched_getaffinity(0)),
+            'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
 
 
 def max_over_ranks(elapsed, dev, world):

@@ -165,6 +165,22 @@ int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
                                 int32_t channels, int64_t total, const int64_t* chosen_idx,
                                 const int32_t* seg_of, const float* grad, int64_t grad_ld,
                                 void* stream);
+/* The same for head outputs of any layout (NCHW or channels-last): level l is
+ * [B, C*A, H_l, W_l] with element strides level_strides[4l..4l+3] = (b, c, y, x),
+ * level_hw[2l..2l+1] = (H_l, W_l), A = num_anchors; anchor index a*H*W + y*W + x of the
+ * reference's [C, A*H*W] view reads tensor channel c*A + a. */
+int32_t frh_gather_level_outputs_strided(int32_t num_levels, const float* const* level_ptrs,
+                                         const int64_t* level_off, const int32_t* level_hw,
+                                         const int64_t* level_strides, int32_t num_anchors,
+                                         int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                         const int32_t* seg_of, float* out, int64_t out_ld,
+                                         void* stream);
+int32_t frh_scatter_level_grads_strided(int32_t num_levels, float* const* level_grads,
+                                        const int64_t* level_off, const int32_t* level_hw,
+                                        const int64_t* level_strides, int32_t num_anchors,
+                                        int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                        const int32_t* seg_of, const float* grad, int64_t grad_ld,
+                                        void* stream);
 
 /* ---- a12: bbox_target (lib/bbox.py:6-82) ------------------------------------
  * frh_prepend_gt_labels builds the reference's candidate list
@@ -227,6 +243,20 @@ int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* con
                           int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
                           float* out_scores, int32_t* out_counts, void* workspace,
                           size_t ws_bytes, void* stream);
+
+/* The same for head outputs of any layout (NCHW or the channels-last outputs of an NHWC
+ * RPN head): cls_strides / reg_strides [L][4] element strides (b, c, y, x) of each level;
+ * anchor a*H*W + y*W + x reads channel c*A + a (cls) / coord*A + a (reg), as the
+ * reference's views (anchor_head.py:82, rpn_head.py:72). */
+int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                                  const float* const* reg_ptrs, const int64_t* cls_strides,
+                                  const int64_t* reg_strides, const int32_t* grid_hw,
+                                  int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                                  int64_t anchor_ld, const float* means, const float* stds,
+                                  const float* img_hw, const float* min_size, int32_t pre_nms,
+                                  int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                                  float* out_scores, int32_t* out_counts, void* workspace,
+                                  size_t ws_bytes, void* stream);
 
 /* Measurement hook: byte offsets in the frh_rpn_proposals workspace of its per-level
  * NMS input (out[0] boxes [S, P, 4] in descending-score order, out[1] counts [S]
@@ -394,6 +424,16 @@ int32_t frh_atss_assign(int32_t batch, int32_t num_levels, const int32_t* grid_h
 int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gamma,
                    const float* beta, const float* mean, const float* var, float eps,
                    int64_t n, int32_t c, int64_t hw, int32_t relu, void* stream);
+
+/* FPN top-down merge into channels-last levels (lib/necks.py:72-84):
+ * out[b, y, x, c] = lat[b, c, y, x] + up[b, iy, ix, c] with torch's nearest rule
+ * (iy = min(floor(y * (float)up_h / height), up_h - 1); y / 2 when height == 2 * up_h);
+ * lat: any strides (lat_strides = element strides b, c, y, x); up: NHWC contiguous
+ * [batch, up_h, up_w, channels] or NULL (the top level: a transpose); out: NHWC
+ * contiguous [batch, height, width, channels].  One f32 add per element. */
+int32_t frh_fpn_merge_nhwc(const float* lat, const int64_t* lat_strides, const float* up, int32_t up_h,
+                           int32_t up_w, float* out, int32_t batch, int32_t channels, int32_t height,
+                           int32_t width, void* stream);
 
 /* ---------------------------------------------------------------- f1: fused losses
  * Classification losses of lib/losses.py on the head outputs, summed (the reference's

@@ -21,12 +21,32 @@
  *   atss targets        lib/heads/fcos_head.py:51-116,283-368
  * torchvision is not vendored in the reference and not installed here: the
  * nms / roi_align / roi_pool rows are "parity unpinned" (SURVEY §8c).
+ *
+ * OpenMP (bench.py's host-core CPU baseline): the IoU table, the assignment,
+ * the NMS suppression mask and RoIAlign run over the host's threads
+ * (orc_set_threads); every output element is computed by one thread in the same
+ * operation order, so results do not depend on the thread count.
  */
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* thread count of the parallel loops (1 = the scalar baseline); returns the previous */
+int orc_set_threads(int n) {
+#ifdef _OPENMP
+  int prev = omp_get_max_threads();
+  omp_set_num_threads(n > 0 ? n : 1);
+  return prev;
+#else
+  (void)n;
+  return 1;
+#endif
+}
 
 static float iou_p1(const float* a, int64_t lda, int64_t i, const float* b, int64_t ldb, int64_t j) {
   float ax1 = a[i], ay1 = a[lda + i], ax2 = a[2 * lda + i], ay2 = a[3 * lda + i];
@@ -42,6 +62,7 @@ static float iou_p1(const float* a, int64_t lda, int64_t i, const float* b, int6
 
 /* calc_iou: out[n*k] row-major */
 void orc_iou_table(const float* a, int64_t lda, int64_t n, const float* b, int64_t ldb, int64_t k, float* out) {
+#pragma omp parallel for schedule(static) if (n * k > 65536)
   for (int64_t i = 0; i < n; ++i)
     for (int64_t j = 0; j < k; ++j) out[i * k + j] = iou_p1(a, lda, i, b, ldb, j);
 }
@@ -70,10 +91,31 @@ int orc_maxiou_assign(const float* boxes, int64_t ld, int64_t n, const float* gt
   float* colmax = (float*)malloc(sizeof(float) * (size_t)g);
   if (!tab || !colmax) return -2;
   orc_iou_table(boxes, ld, n, gts, gld, g, tab);
-  for (int64_t j = 0; j < g; ++j) {
-    int64_t dummy;
-    if (n > 0) row_max(tab + j, n, g, &colmax[j], &dummy);
+  /* per-gt max over the boxes (torch.max over dim 0: NaN wins): chunk maxima in
+   * parallel, combined in chunk order with the same rule -- the same value */
+  enum { kCh = 64 };
+  float* part = (float*)malloc(sizeof(float) * (size_t)g * kCh);
+  int64_t per = (n + kCh - 1) / kCh;
+#pragma omp parallel for schedule(static) if (n > 65536)
+  for (int q = 0; q < kCh; ++q) {
+    int64_t lo = (int64_t)q * per, hi = lo + per < n ? lo + per : n;
+    for (int64_t j = 0; j < g; ++j) {
+      int64_t dummy;
+      float m = NAN;
+      if (hi > lo) row_max(tab + lo * g + j, hi - lo, g, &m, &dummy);
+      part[(size_t)j * kCh + q] = hi > lo ? m : -INFINITY;
+    }
   }
+  for (int64_t j = 0; j < g; ++j) {
+    float mx = part[(size_t)j * kCh];
+    for (int q = 1; q < kCh && !isnan(mx); ++q) {
+      float x = part[(size_t)j * kCh + q];
+      if (!(x <= mx)) mx = x;
+    }
+    colmax[j] = mx;
+  }
+  free(part);
+#pragma omp parallel for schedule(static) if (n > 65536)
   for (int64_t i = 0; i < n; ++i) {
     float m;
     int64_t arg;
@@ -183,28 +225,57 @@ void orc_roi_level_map(const float* rois, int64_t k, float finest, int L, int64_
 
 /* torchvision nms on boxes [n,4] already sorted by descending score;
  * keep = positions; returns count */
+static int nms_above(const float* b, const float* area, int64_t i, int64_t j, double thr) {
+  float xx1 = b[4 * i] > b[4 * j] ? b[4 * i] : b[4 * j];
+  float yy1 = b[4 * i + 1] > b[4 * j + 1] ? b[4 * i + 1] : b[4 * j + 1];
+  float xx2 = b[4 * i + 2] < b[4 * j + 2] ? b[4 * i + 2] : b[4 * j + 2];
+  float yy2 = b[4 * i + 3] < b[4 * j + 3] ? b[4 * i + 3] : b[4 * j + 3];
+  float w = xx2 - xx1, h = yy2 - yy1;
+  w = w > 0.0f ? w : 0.0f;
+  h = h > 0.0f ? h : 0.0f;
+  float inter = w * h;
+  float ovr = inter / ((area[i] + area[j]) - inter);
+  return (double)ovr > thr;
+}
+
+/* torchvision nms on boxes [n,4] already sorted by descending score;
+ * keep = positions; returns count.  Several threads: the upper-triangle
+ * suppression bit mask in parallel (rows over threads), then the greedy scan
+ * over it -- the same keep list as the sequential loop below. */
 int64_t orc_nms_sorted(const float* b, int64_t n, double thr, int64_t max_keep, int64_t* keep) {
-  unsigned char* sup = (unsigned char*)calloc((size_t)(n > 0 ? n : 1), 1);
   float* area = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
   for (int64_t i = 0; i < n; ++i) area[i] = (b[4 * i + 2] - b[4 * i]) * (b[4 * i + 3] - b[4 * i + 1]);
   int64_t nk = 0;
+  int threads = 1;
+#ifdef _OPENMP
+  threads = omp_get_max_threads();
+#endif
+  if (threads > 1 && n >= 512) {
+    const int64_t nw = (n + 63) / 64;
+    uint64_t* mask = (uint64_t*)calloc((size_t)n * (size_t)nw, sizeof(uint64_t));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t j = i + 1; j < n; ++j)
+        if (nms_above(b, area, i, j, thr)) mask[i * nw + j / 64] |= 1ull << (j % 64);
+    uint64_t* removed = (uint64_t*)calloc((size_t)nw, sizeof(uint64_t));
+    for (int64_t i = 0; i < n; ++i) {
+      if (removed[i / 64] >> (i % 64) & 1ull) continue;
+      if (max_keep >= 0 && nk >= max_keep) break;
+      keep[nk++] = i;
+      for (int64_t w = i / 64; w < nw; ++w) removed[w] |= mask[i * nw + w];
+    }
+    free(removed);
+    free(mask);
+    free(area);
+    return nk;
+  }
+  unsigned char* sup = (unsigned char*)calloc((size_t)(n > 0 ? n : 1), 1);
   for (int64_t i = 0; i < n; ++i) {
     if (sup[i]) continue;
     if (max_keep >= 0 && nk >= max_keep) break;
     keep[nk++] = i;
-    for (int64_t j = i + 1; j < n; ++j) {
-      if (sup[j]) continue;
-      float xx1 = b[4 * i] > b[4 * j] ? b[4 * i] : b[4 * j];
-      float yy1 = b[4 * i + 1] > b[4 * j + 1] ? b[4 * i + 1] : b[4 * j + 1];
-      float xx2 = b[4 * i + 2] < b[4 * j + 2] ? b[4 * i + 2] : b[4 * j + 2];
-      float yy2 = b[4 * i + 3] < b[4 * j + 3] ? b[4 * i + 3] : b[4 * j + 3];
-      float w = xx2 - xx1, h = yy2 - yy1;
-      w = w > 0.0f ? w : 0.0f;
-      h = h > 0.0f ? h : 0.0f;
-      float inter = w * h;
-      float ovr = inter / ((area[i] + area[j]) - inter);
-      if ((double)ovr > thr) sup[j] = 1;
-    }
+    for (int64_t j = i + 1; j < n; ++j)
+      if (!sup[j] && nms_above(b, area, i, j, thr)) sup[j] = 1;
   }
   free(sup);
   free(area);
@@ -242,6 +313,10 @@ static tap_t mk_tap(float v, int size) {
 void orc_roi_align_fwd(int L, const float* const* feats, const int32_t* hw, const int64_t* st, const float* scales,
                        int C, const float* rois, const int64_t* levels, int64_t K, int ph, int pw, int sampling,
                        int aligned, float* out) {
+  (void)L;
+  /* torchvision's CPU kernel: the bilinear taps / weights of every sample of a RoI are
+   * computed once (pre_calc) and reused by all channels; RoIs over the threads */
+#pragma omp parallel for schedule(dynamic, 4)
   for (int64_t k = 0; k < K; ++k) {
     const float* r = rois + k * 5;
     int b = (int)r[0];
@@ -258,29 +333,45 @@ void orc_roi_align_fwd(int L, const float* const* feats, const int32_t* hw, cons
     int gh = sampling > 0 ? sampling : (int)ceilf(rh / (float)ph);
     int gw = sampling > 0 ? sampling : (int)ceilf(rw / (float)pw);
     float cnt = (float)(gh * gw > 1 ? gh * gw : 1);
+    int64_t sy = st[4 * l + 2], sx = st[4 * l + 3];
+    const int ns = ph * pw * gh * gw;
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * 4 * (size_t)ns);
+    float* wt = (float*)malloc(sizeof(float) * 4 * (size_t)ns);
+    unsigned char* ok = (unsigned char*)malloc((size_t)ns);
+    int e = 0;
+    for (int py = 0; py < ph; ++py)
+      for (int px = 0; px < pw; ++px)
+        for (int iy = 0; iy < gh; ++iy) {
+          tap_t ty = mk_tap(sh + (float)py * bh + ((float)iy + 0.5f) * bh / (float)gh, H);
+          for (int ix = 0; ix < gw; ++ix, ++e) {
+            tap_t tx = mk_tap(sw + (float)px * bw + ((float)ix + 0.5f) * bw / (float)gw, W);
+            ok[e] = (unsigned char)(ty.valid && tx.valid);
+            wt[4 * e] = ty.h * tx.h, wt[4 * e + 1] = ty.h * tx.l, wt[4 * e + 2] = ty.l * tx.h, wt[4 * e + 3] = ty.l * tx.l;
+            pos[4 * e] = ty.lo * sy + tx.lo * sx, pos[4 * e + 1] = ty.lo * sy + tx.hi * sx;
+            pos[4 * e + 2] = ty.hi * sy + tx.lo * sx, pos[4 * e + 3] = ty.hi * sy + tx.hi * sx;
+          }
+        }
     for (int c = 0; c < C; ++c) {
       const float* f = feats[l] + b * st[4 * l] + c * st[4 * l + 1];
-      int64_t sy = st[4 * l + 2], sx = st[4 * l + 3];
-      for (int py = 0; py < ph; ++py)
-        for (int px = 0; px < pw; ++px) {
-          float acc = 0.0f;
-          for (int iy = 0; iy < gh; ++iy) {
-            tap_t ty = mk_tap(sh + (float)py * bh + ((float)iy + 0.5f) * bh / (float)gh, H);
-            for (int ix = 0; ix < gw; ++ix) {
-              tap_t tx = mk_tap(sw + (float)px * bw + ((float)ix + 0.5f) * bw / (float)gw, W);
-              float val = 0.0f;
-              if (ty.valid && tx.valid) {
-                float w1 = ty.h * tx.h, w2 = ty.h * tx.l, w3 = ty.l * tx.h, w4 = ty.l * tx.l;
-                float v1 = f[ty.lo * sy + tx.lo * sx], v2 = f[ty.lo * sy + tx.hi * sx];
-                float v3 = f[ty.hi * sy + tx.lo * sx], v4 = f[ty.hi * sy + tx.hi * sx];
-                val = ((w1 * v1 + w2 * v2) + w3 * v3) + w4 * v4;
-              }
-              acc = acc + val;
-            }
+      const float* w4 = wt;
+      const int64_t* p4 = pos;
+      for (int bin = 0, q = 0; bin < ph * pw; ++bin) {
+        float acc = 0.0f;
+        for (int s = 0; s < gh * gw; ++s, ++q) {
+          float val = 0.0f;
+          if (ok[q]) {
+            const float* w = w4 + 4 * q;
+            const int64_t* p = p4 + 4 * q;
+            val = ((w[0] * f[p[0]] + w[1] * f[p[1]]) + w[2] * f[p[2]]) + w[3] * f[p[3]];
           }
-          out[((k * C + c) * ph + py) * pw + px] = acc / cnt;
+          acc = acc + val;
         }
+        out[(k * C + c) * ph * pw + bin] = acc / cnt;
+      }
     }
+    free(pos);
+    free(wt);
+    free(ok);
   }
 }
 

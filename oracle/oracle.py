@@ -44,7 +44,14 @@ def lib():
         _c = ctypes.CDLL(LIB)
         _c.orc_nms_sorted.restype = ctypes.c_int64
         _c.orc_maxiou_assign.restype = ctypes.c_int
+        _c.orc_set_threads.restype = ctypes.c_int
     return _c
+
+
+def set_threads(n):
+    """Thread count of the C restatement's parallel loops (OpenMP); returns the previous one.
+    Results do not depend on it (every output element is one thread's, in reference order)."""
+    return int(lib().orc_set_threads(int(n)))
 
 
 def _f(a):

@@ -25,6 +25,8 @@ constexpr int kMaxSort = 16384;
 struct PropArgs {
   const float* cls[FRH_MAX_LEVELS];
   const float* reg[FRH_MAX_LEVELS];
+  int64_t cst[FRH_MAX_LEVELS][4], rst[FRH_MAX_LEVELS][4];  // element strides (b, c, y, x)
+  int nchw;  // every level contiguous [B, C*A, H, W]: flat indexing
   int32_t h[FRH_MAX_LEVELS], w[FRH_MAX_LEVELS];
   int64_t off[FRH_MAX_LEVELS];
   int L, A, C;  // levels, anchors per location, cls channels (1 sigmoid, 2 softmax)
@@ -54,6 +56,15 @@ __device__ __forceinline__ float score_of2(float x0, float x1, int C) {
   return e1 / (e0 + e1);
 }
 
+// element (image b, row c, level-local anchor i = a*H*W + y*W + x) of a [B, R*A, H, W]
+// head output viewed per image as [R, A*H*W] (anchor_head.py:82; rpn_head.py:72): tensor
+// channel c*A + a, whatever the strides (NCHW or channels-last)
+__device__ __forceinline__ int64_t rpn_elem(const int64_t (&st)[4], int A, int H, int W, int b, int c, int64_t i) {
+  const uint32_t hw = (uint32_t)H * (uint32_t)W, u = (uint32_t)i, a = u / hw, sp = u - a * hw;
+  const uint32_t y = sp / (uint32_t)W, x = sp - y * (uint32_t)W;
+  return (int64_t)b * st[0] + (int64_t)(c * A + (int)a) * st[1] + (int64_t)y * st[2] + (int64_t)x * st[3];
+}
+
 constexpr int kRpnHistBits = 12;
 constexpr int kRpnSelFused = 2048;  // selections decoded at selection time, ordered by rpn_rank_kernel
 
@@ -73,14 +84,24 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_keys_kernel(PropArgs p,
   }
   if (base >= hwa) return;
   tk_hist1_clear(h, 1 << kRpnHistBits);
-  const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
   uint32_t* kk = const_cast<uint32_t*>(b.keys) + (int64_t)seg * b.ld;
   float x0[kTkPerThread], x1[kTkPerThread];  // every logit load in flight at once
+  if (p.nchw) {
+    const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
 #pragma unroll
-  for (int r = 0; r < kTkPerThread; ++r) {
-    const int64_t i = base + r * kTkThreads + threadIdx.x;
-    x0[r] = i < hwa ? cls[i] : 0.0f;
-    x1[r] = (p.C == 2 && i < hwa) ? cls[hwa + i] : 0.0f;
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int64_t i = base + r * kTkThreads + threadIdx.x;
+      x0[r] = i < hwa ? cls[i] : 0.0f;
+      x1[r] = (p.C == 2 && i < hwa) ? cls[hwa + i] : 0.0f;
+    }
+  } else {
+    const float* cls = p.cls[l];
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int64_t i = base + r * kTkThreads + threadIdx.x;
+      x0[r] = i < hwa ? cls[rpn_elem(p.cst[l], p.A, p.h[l], p.w[l], bi, 0, i)] : 0.0f;
+      x1[r] = (p.C == 2 && i < hwa) ? cls[rpn_elem(p.cst[l], p.A, p.h[l], p.w[l], bi, 1, i)] : 0.0f;
+    }
   }
 #pragma unroll
   for (int r = 0; r < kTkPerThread; ++r) {
@@ -99,16 +120,24 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_keys_kernel(PropArgs p,
 __device__ __forceinline__ float4 rpn_decode_one(const PropArgs& p, const ImgArgs& ia, int seg, int i) {
   const int b = seg / p.L, l = seg % p.L;
   const int64_t hwa = (int64_t)p.A * p.h[l] * p.w[l];
-  const float* reg = p.reg[l] + (int64_t)b * 4 * hwa;
   const float img_h = ia.hw[2 * b], img_w = ia.hw[2 * b + 1];
   const int64_t ai = p.off[l] + i;
   const float* an = p.anchors;
   const int64_t ld = p.anchor_ld;
   float ax1 = an[ai], ay1 = an[ld + ai], ax2 = an[2 * ld + ai], ay2 = an[3 * ld + ai];
-  float tx = reg[i] * p.sd[0] + p.m[0];
-  float ty = reg[hwa + i] * p.sd[1] + p.m[1];
-  float tw = reg[2 * hwa + i] * p.sd[2] + p.m[2];
-  float th = reg[3 * hwa + i] * p.sd[3] + p.m[3];
+  float d[4];
+  if (p.nchw) {
+    const float* reg = p.reg[l] + (int64_t)b * 4 * hwa;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = reg[q * hwa + i];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = p.reg[l][rpn_elem(p.rst[l], p.A, p.h[l], p.w[l], b, q, i)];
+  }
+  float tx = d[0] * p.sd[0] + p.m[0];
+  float ty = d[1] * p.sd[1] + p.m[1];
+  float tw = d[2] * p.sd[2] + p.m[2];
+  float th = d[3] * p.sd[3] + p.m[3];
   float bw = (ax2 - ax1) + 1.0f, bh = (ay2 - ay1) + 1.0f;
   float bcx = (ax2 + ax1) / 2.0f, bcy = (ay2 + ay1) / 2.0f;
   float cx = tx * bw + bcx, cy = ty * bh + bcy;
@@ -489,6 +518,16 @@ extern "C" int32_t frh_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_leve
   return FRH_OK;
 }
 
+extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                                             const float* const* reg_ptrs, const int64_t* cls_strides,
+                                             const int64_t* reg_strides, const int32_t* grid_hw,
+                                             int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                                             int64_t anchor_ld, const float* means, const float* stds,
+                                             const float* img_hw, const float* min_size, int32_t pre_nms,
+                                             int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                                             float* out_scores, int32_t* out_counts, void* workspace,
+                                             size_t ws_bytes, void* stream);
+
 extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                      const float* const* reg_ptrs, const int32_t* grid_hw, int32_t num_anchors,
                                      int32_t cls_channels, const float* anchors, int64_t anchor_ld,
@@ -496,6 +535,29 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
                                      const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num,
                                      double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
                                      void* workspace, size_t ws_bytes, void* stream) {
+  FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS && grid_hw, "bad level count %d", num_levels);
+  int64_t cs[4 * FRH_MAX_LEVELS], rs[4 * FRH_MAX_LEVELS];
+  for (int l = 0; l < num_levels; ++l) {  // contiguous [B, R*A, H, W]
+    const int64_t hw = (int64_t)grid_hw[2 * l] * grid_hw[2 * l + 1];
+    cs[4 * l] = (int64_t)cls_channels * num_anchors * hw, cs[4 * l + 1] = hw, cs[4 * l + 2] = grid_hw[2 * l + 1],
+    cs[4 * l + 3] = 1;
+    rs[4 * l] = (int64_t)4 * num_anchors * hw, rs[4 * l + 1] = hw, rs[4 * l + 2] = grid_hw[2 * l + 1], rs[4 * l + 3] = 1;
+  }
+  return frh_rpn_proposals_strided(num_imgs, num_levels, cls_ptrs, reg_ptrs, cs, rs, grid_hw, num_anchors,
+                                   cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms, post_nms,
+                                   max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes, stream);
+}
+
+extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                                             const float* const* reg_ptrs, const int64_t* cls_strides,
+                                             const int64_t* reg_strides, const int32_t* grid_hw,
+                                             int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                                             int64_t anchor_ld, const float* means, const float* stds,
+                                             const float* img_hw, const float* min_size, int32_t pre_nms,
+                                             int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                                             float* out_scores, int32_t* out_counts, void* workspace,
+                                             size_t ws_bytes, void* stream) {
+  FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
   FRH_REQUIRE(cls_channels == 1 || cls_channels == 2, "cls_channels must be 1 (sigmoid) or 2 (softmax)");
@@ -511,13 +573,19 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   char* ws = reinterpret_cast<char*>(workspace);
   PropArgs p{};
   int64_t off = 0;
+  p.nchw = 1;
   for (int l = 0; l < num_levels; ++l) {
     p.cls[l] = cls_ptrs[l];
     p.reg[l] = reg_ptrs[l];
     p.h[l] = grid_hw[2 * l];
     p.w[l] = grid_hw[2 * l + 1];
     p.off[l] = off;
-    off += (int64_t)num_anchors * p.h[l] * p.w[l];
+    const int64_t hw = (int64_t)p.h[l] * p.w[l];
+    off += (int64_t)num_anchors * hw;
+    for (int q = 0; q < 4; ++q) p.cst[l][q] = cls_strides[4 * l + q], p.rst[l][q] = reg_strides[4 * l + q];
+    p.nchw = p.nchw && p.cst[l][0] == (int64_t)cls_channels * num_anchors * hw && p.cst[l][1] == hw &&
+             p.cst[l][2] == p.w[l] && p.cst[l][3] == 1 && p.rst[l][0] == (int64_t)4 * num_anchors * hw &&
+             p.rst[l][1] == hw && p.rst[l][2] == p.w[l] && p.rst[l][3] == 1;
   }
   FRH_REQUIRE(anchor_ld >= off, "anchor_ld smaller than the total anchor count");
   p.L = num_levels;

@@ -6,6 +6,9 @@
 //
 // Forward (all bit-identical: -ffp-contract=off, reference op order; kernels in
 // roi_kernels.h):
+//  * roi_align_fwd_quad_kernel -- channels-last features (unit channel stride, C % 4
+//    == 0, sampling 2, up to 8x8 bins): the pair kernel's structure with channel quads:
+//    16-B LDS-DMA staging (lane = cell), one ds_read_b128 per tap for 4 channels.
 //  * roi_align_fwd_pair_kernel -- the default (sampling 2, up to 8x8 bins, even C):
 //    one wave per (RoI, 16 channels); the RoI's tap window staged by LDS-DMA with
 //    channel pairs interleaved into one slab buffer per wave, packed-f32 bilinear sums.
@@ -151,7 +154,12 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     else
       hipLaunchKernelGGL(kern, grid, block, 0, st, lv, c, out);
   };
-  if (pair_ok(f, channels, pooled_h, pooled_w)) {
+  if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
+    // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels), 16-B DMA
+    const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
+    FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
+    go(roi_align_fwd_quad_kernel<kCpolNT, false, 3>, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave));
+  } else if (pair_ok(f, channels, pooled_h, pooled_w)) {
     // chunk-major XCD order, nt output stores, one 6.5 KB slab per wave, lean tap state
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");

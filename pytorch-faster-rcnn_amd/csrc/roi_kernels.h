@@ -478,6 +478,8 @@ struct PairLane {
   uint32_t tb0[2][2], tdq[2], tdr[2];
 };
 
+// kUnit: bytes of one cell's entry in a slab region (8: a channel pair; 16: a quad)
+template <int kUnit = 8>
 __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c, const RoiRaw& raw, int lane,
                                            PairGeom& G, PairLane& P) {
   constexpr int SR = 2;
@@ -527,7 +529,7 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
     P.fyh[iy] = a.valid ? a.h : 0.f;
     P.fyl[iy] = a.valid ? a.l : 0.f;
     const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
-    P.tdr[iy] = 8u * (uint32_t)((r1 - r0) * G.Cs2);
+    P.tdr[iy] = (uint32_t)kUnit * (uint32_t)((r1 - r0) * G.Cs2);
 #pragma unroll
     for (int ix = 0; ix < SR; ++ix) {
       const Tap b = make_tap(pos_x(px, ix), W);
@@ -535,9 +537,9 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
       if (iy == 0) {
         P.fxh[ix] = b.valid ? b.h : 0.f;
         P.fxl[ix] = b.valid ? b.l : 0.f;
-        P.tdq[ix] = 8u * (uint32_t)(q1 - q0);
+        P.tdq[ix] = (uint32_t)kUnit * (uint32_t)(q1 - q0);
       }
-      P.tb0[iy][ix] = (a.valid && b.valid) ? 8u * (uint32_t)(r0 * G.Cs2 + q0) : 0u;
+      P.tb0[iy][ix] = (a.valid && b.valid) ? (uint32_t)kUnit * (uint32_t)(r0 * G.Cs2 + q0) : 0u;
     }
   }
   G.base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
@@ -712,6 +714,266 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
   pair_item<kStAux, 0, kStamp>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1));
+}
+
+
+// ---------------------------------------------------------------------------
+// Channel-quad forward for channels-last features (unit channel stride: the FPN's NHWC
+// outputs).  The pair kernel's structure -- one wave per (RoI, 16 channels), lane = bin,
+// per-bin tap state computed once per item, the RoI's tap cells staged in LDS, packed-f32
+// bilinear sums -- with the staging matched to NHWC: slab region d holds channel quad d
+// (4 channels = 16 B) of every staged cell, filled by 16-B LDS-DMA (lane = cell: one
+// instruction stages 64 cells of a quad; the 4 quads of an item read each cell's 64
+// contiguous bytes), and every tap is ONE ds_read_b128 giving 4 channels.  A stage holds
+// the D quads (D = 4, 2, 1) whose regions fit the 8-KB slab; windows of more cells than
+// D = 1 holds are gathered per lane from global memory.  Same operation order:
+// bit-identical to the other kernels.
+constexpr int kQuadWave = 4;     // channel quads per wave (= workgroup): 16 channels
+constexpr int kQuadSlab = 2048;  // dwords per slab (8 KB)
+constexpr int kQuadChunk = 4 * kQuadWave;
+
+template <int D>
+struct QuadLayout {
+  static constexpr int RS = (kQuadSlab / D) / 256 * 256;  // dwords per quad region: whole 64-cell DMA rounds
+  static constexpr int RP = RS / 256;                      // DMA rounds per region
+  static constexpr int kCells = RS / 4;
+  static_assert(D * RP < 64, "vmcnt is 6 bits");
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait4(f32x4 (&v)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+               : "i"(N)
+               : "memory");
+}
+
+// torchvision's per-sample sum for 4 channels: ((w1 v1 + w2 v2) + w3 v3) + w4 v4, as two
+// packed halves
+__device__ __forceinline__ f32x4 quad_val(const float (&w)[4], const f32x4* x) {
+  f32x2 lo = ((f32x2(w[0]) * x[0].xy + f32x2(w[1]) * x[1].xy) + f32x2(w[2]) * x[2].xy) + f32x2(w[3]) * x[3].xy;
+  f32x2 hi = ((f32x2(w[0]) * x[0].zw + f32x2(w[1]) * x[1].zw) + f32x2(w[2]) * x[2].zw) + f32x2(w[3]) * x[3].zw;
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+
+// kQW: channel quads per item (4: 16 channels).  kOut: 0 = per-channel 4-B stores of the
+// bin row (lane = bin), 1 = [channel][bin] staged in LDS (obuf), then 16-B stores of the
+// item's contiguous output block, 2 = no stores (tools-only diagnostic).
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0>
+__device__ __forceinline__ void quad_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
+                                          int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane,
+                                          float* obuf = nullptr) {
+  constexpr int SR = 2;
+  int64_t t_setup = 0, t_land = 0;
+  const int cw0 = chunk * 4 * kQW;
+  const int nquads = min(kQW, (c.C - cw0) / 4);  // host: C % 4 == 0
+  const int nbins = c.ph * c.pw;
+  PairGeom G;
+  PairLane P;
+  const RoiRaw raw = roi_fetch(c, k);
+  pair_setup<16>(lv, c, raw, lane, G, P);
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)4 * nquads * nbins * 4);
+  const int ovoff = active ? lane * 4 : 0x40000000;  // idle lanes: dropped by the range check
+  const int ostep = nbins * 4;
+  if (G.empty) {  // no valid sample: all bins 0
+    for (int ch = 0; ch < 4 * nquads; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, ovoff, ch * ostep, kStAux);
+    return;
+  }
+  const int y0 = G.y0, x0 = G.x0, Cs = G.Cs, Cs2 = G.Cs2, sy = G.sy, sx = G.sx;
+  const bool dy = G.dy, dx = G.dx;
+  const int ncell = G.R * Cs2;
+  const int rsrc = P.rsrc, csrc = P.csrc;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(G.base, (int64_t)G.extent);
+  const uint32_t inv = G.inv;
+  if (kStamp) t_setup = (int64_t)__builtin_amdgcn_s_memrealtime();
+  int stamp_d = 0;
+  auto store4 = [&](int q, f32x4 r) {
+    if constexpr (kOut == 2) {
+      if (r.x == 1234.5f) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, ovoff, 0, kStAux);
+      return;
+    }
+    if constexpr (kOut == 1) {
+      if (q < nquads && active) {
+        obuf[(4 * q) * nbins + lane] = r.x;
+        obuf[(4 * q + 1) * nbins + lane] = r.y;
+        obuf[(4 * q + 2) * nbins + lane] = r.z;
+        obuf[(4 * q + 3) * nbins + lane] = r.w;
+      }
+      return;
+    }
+    const int vo = q < nquads ? ovoff : 0x40000000;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x), orr, vo, (4 * q) * ostep, kStAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y), orr, vo, (4 * q + 1) * ostep, kStAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.z), orr, vo, (4 * q + 2) * ostep, kStAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.w), orr, vo, (4 * q + 3) * ostep, kStAux);
+  };
+  auto run = [&](auto dd) {
+    constexpr int D = decltype(dd)::value, RS = QuadLayout<D>::RS, RP = QuadLayout<D>::RP;
+    const int nst = (nquads + D - 1) / D;
+    // region 16-B unit j * 64 + lane of every quad  <-  that quad of cell j * 64 + lane
+    auto goff_at = [&](int j) {
+      int e = j * kWave + lane;
+      e = e < ncell ? e : 0;
+      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
+      return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave);
+    };
+    int goff[RP];
+#pragma unroll
+    for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
+    auto issue = [&](int s) {  // quads past the last re-read it (their stores are dropped)
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int soff = (cw0 + 4 * min(s * D + d, nquads - 1)) * 4;
+#pragma unroll
+        for (int j = 0; j < RP; ++j) lds_dma_at<16, 0>(fr, sbase + 4u * (uint32_t)(d * RS + j * 256), goff[j], soff);
+      }
+    };
+    auto eval = [&](int s) {
+      f32x4 v[2][8];
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      float ly_h[SR], ly_l[SR], lx_h[SR], lx_l[SR];
+      uint32_t lb[SR][SR], ldq[SR], ldr[SR];
+#pragma unroll
+      for (int i = 0; i < SR; ++i) {
+        ly_h[i] = P.fyh[i], ly_l[i] = P.fyl[i], lx_h[i] = P.fxh[i], lx_l[i] = P.fxl[i], ldq[i] = P.tdq[i],
+        ldr[i] = P.tdr[i];
+        asm volatile("" : "+v"(ly_h[i]), "+v"(ly_l[i]), "+v"(lx_h[i]), "+v"(lx_l[i]), "+v"(ldq[i]), "+v"(ldr[i]));
+#pragma unroll
+        for (int j = 0; j < SR; ++j) {
+          lb[i][j] = sbase + P.tb0[i][j];
+          asm volatile("" : "+v"(lb[i][j]));
+        }
+      }
+      auto tap = [&](int iy, int ix, int q) -> uint32_t {
+        return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
+      };
+      auto load = [&](auto hh) {
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1, OFF = 4 * (d * RS);
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[h & 1][ix * 4 + q] = lds_read_b128<OFF>(tap(iy, ix, q));
+      };
+      load(std::integral_constant<int, 0>{});
+      static_for<0, 2 * D>([&](auto hh) {
+        constexpr int h = decltype(hh)::value, d = h >> 1, iy = h & 1;
+        if constexpr (h + 1 < 2 * D) {
+          load(std::integral_constant<int, h + 1>{});
+          lds_wait4<8>(v[h & 1]);
+        } else {
+          lds_wait4<0>(v[h & 1]);
+        }
+        if (iy == 0) acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const float w[4] = {ly_h[iy] * lx_h[ix], ly_h[iy] * lx_l[ix], ly_l[iy] * lx_h[ix], ly_l[iy] * lx_l[ix]};
+          acc = acc + quad_val(w, &v[h & 1][ix * 4]);
+        }
+        if (iy == 1) store4(s * D + d, acc * 0.25f);  // count 4: / 4 == * 0.25
+      });
+    };
+    stamp_d = D;
+    for (int s = 0; s < nst; ++s) {
+      issue(s);  // the previous stage's tap reads completed (lds_wait4<0> + barrier below)
+      wait_vmcnt<0>();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (kStamp && s == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
+      eval(s);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  };
+  if (ncell <= QuadLayout<4>::kCells) {
+    run(std::integral_constant<int, 4>{});
+  } else if (ncell <= QuadLayout<2>::kCells) {
+    run(std::integral_constant<int, 2>{});
+  } else if (ncell <= QuadLayout<1>::kCells) {
+    run(std::integral_constant<int, 1>{});
+  } else {
+    // more tap cells than the slab holds (tap lists of a RoI wider than 28 cells on both
+    // axes): lane = bin gathers its taps from global memory, 4 channels per load
+    for (int q = 0; q < nquads; ++q) {
+      const int soff = (cw0 + 4 * q) * 4;
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          // slab offsets -> feature offsets: slab cell (r, col) = tap-list / window entry
+          const uint32_t t0 = P.tb0[iy][ix] / 16u;
+          const int r0 = (int)(t0 / (uint32_t)Cs2), c0 = (int)(t0 - (uint32_t)r0 * (uint32_t)Cs2);
+          const int r1 = r0 + (int)(P.tdr[iy] / 16u / (uint32_t)Cs2), c1 = c0 + (int)(P.tdq[ix] / 16u);
+          const int ro0 = __shfl(rsrc, r0, kWave), ro1 = __shfl(rsrc, r1, kWave);
+          const int co0 = __shfl(csrc, c0, kWave), co1 = __shfl(csrc, c1, kWave);
+          f32x4 x[4];
+          const int offs[4] = {ro0 + co0, ro0 + co1, ro1 + co0, ro1 + co1};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(fr, offs[t], soff, 0);
+            x[t] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+          }
+          const float w[4] = {P.fyh[iy] * P.fxh[ix], P.fyh[iy] * P.fxl[ix], P.fyl[iy] * P.fxh[ix],
+                              P.fyl[iy] * P.fxl[ix]};
+          acc = acc + quad_val(w, x);
+        }
+      store4(q, acc * 0.25f);
+    }
+  }
+  if constexpr (kOut == 1) {  // the item's [channel][bin] block: contiguous, 16-B stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n4 = 4 * nquads * nbins / 4;
+    const float4* o4 = reinterpret_cast<const float4*>(obuf);
+    for (int e = lane; e < n4; e += kWave) {
+      const float4 q = o4[e];
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(q.x), __float_as_uint(q.y), __float_as_uint(q.z), __float_as_uint(q.w)}, orr, e * 16,
+          0, kStAux);
+    }
+  }
+  if (kStamp && lane == 0) {
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + item * 8;
+    const int64_t t_end = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[0] = t_start;
+    st[1] = t_setup;
+    st[2] = t_land;
+    st[3] = t_end;
+    st[4] = stamp_d;
+    st[5] = ncell;
+    st[6] = t_setup;
+    st[7] = blockIdx.x & 7;
+  }
+}
+
+// 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups, chunk-major per XCD (as the
+// pair kernel: the two 16-channel chunks of a 128-B line share an XCD)
+template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 4, int kQW = kQuadWave, int kOut = 0>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe))) roi_align_fwd_quad_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) float slab[kQuadSlab];
+  __shared__ __attribute__((aligned(16))) float obuf[kOut == 1 ? 4 * kQW * kWave : 4];  // [channel][bin], <= 64 bins
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const uint32_t G = (uint32_t)(c.C + 4 * kQW - 1) / (uint32_t)(4 * kQW), K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
+  if (w >= wend) return;
+  const int ch0 = (int)(w / K32);
+  const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
+  quad_item<kStAux, kStamp, kQW, kOut>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
 }
 
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
@@ -1028,6 +1290,197 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(R
   }
 }
 
+// ---------------------------------------------------------------------------
+// Channels-last forward (features with unit channel stride: the FPN's NHWC outputs).
+// One wave per (RoI, 64 channels), lane = channel: every tap is wave-uniform, so the
+// sample geometry is computed once per wave (14 y- and 14 x-samples, one lane each,
+// broadcast by v_readlane) and every feature access is a 256-B run of one cell's
+// channels.  The RoI's tap cells (the dense window [y0, y1] x [x0, x1], or per axis the
+// 2 * 2 * P (lo, hi) tap list when the window is wider -- as the pair kernel) are staged
+// into the wave's LDS slab by 16-B LDS-DMA, one 1-KB instruction per 4 cells (full
+// 128-B lines); a window with more than kCells cells is staged in bands of slab rows,
+// each band holding whole sample rows.  Each sample's four taps are ds_read_b32 of
+// consecutive channels (conflict-free); the bilinear sums run per lane in torchvision's
+// operation order, so the result is bit-identical to the other kernels.  The 7 x 7
+// outputs of the lane's channel collect in VGPRs and leave through the slab, transposed
+// to [channel][bin], as 16-B stores of one contiguous 12.5-KB block.
+constexpr int kNhwcGroup = 64;  // channels per wave
+
+// kRegOut: the outputs stay in VGPRs until the end (LDS = the slab only) instead of a
+// separate [channel][bin] LDS buffer.  kStamp (tools-only timing builds): lane 0 writes 8
+// int64 per item after the output -- s_memrealtime at start / prologue done / first band
+// landed / eval done / end, bands staged, cells of the first band, XCD.
+template <int PH, int PW, int kCells, int kStAux, bool kRegOut = true, bool kStamp = false>
+__global__ void __launch_bounds__(kWave) roi_align_fwd_nhwc_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  int64_t t_pro = 0, t_land = 0, t_eval = 0;
+  int n_bands = 0, first_cells = 0;
+  static_assert(2 * PH <= 32 && 2 * PW <= 32 && kCells % 4 == 0 && kCells >= 2 * 4 * PW, "tap lanes / DMA rounds");
+  static_assert(!kRegOut || kCells >= PH * PW, "the outputs leave through the slab");
+  constexpr int NLY = 4 * PH, NLX = 4 * PW;  // tap-list lengths
+  constexpr int NB = PH * PW;
+  __shared__ __attribute__((aligned(16))) float slab[kCells * kNhwcGroup];
+  __shared__ __attribute__((aligned(16))) float obuf[kRegOut ? 4 : kNhwcGroup * NB];  // [channel][bin]
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const int lane = threadIdx.x;
+  // XCD x (= workgroup id mod 8) walks the x-th eighth of the group-major (group, RoI) list
+  const uint32_t G = (uint32_t)c.C / kNhwcGroup, K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (w >= min((blockIdx.x & 7u) * per + per, total)) return;
+  const int grp = (int)(w / K32);
+  const int64_t k = (int64_t)(w - (uint32_t)grp * K32);
+  const RoiRaw raw = roi_fetch(c, k);
+  const RoiGeom g = roi_geom_raw(c, lv, raw);
+  const int l = g.lvl, H = lv.h[l], W = lv.w[l];
+  // lane s < 2 PH: y sample s (bin s / 2, sub-sample s % 2); lane 32 + s < 32 + 2 PW: x sample s
+  const bool isy = lane < 2 * PH, isx = lane >= 32 && lane < 32 + 2 * PW;
+  const int s = isy ? lane : lane - 32;
+  Tap t{0, 0, 0.f, 0.f, 0};
+  if (isy || isx) {
+    const float st = isy ? g.start_h : g.start_w, bn = isy ? g.bin_h : g.bin_w;
+    t = make_tap(st + (float)(s >> 1) * bn + ((float)(s & 1) + 0.5f) * bn * 0.5f, isy ? H : W);
+  }
+  const bool tv = (isy || isx) && t.valid;
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(isy && tv ? t.lo : 1 << 30));
+  const int y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(isy && tv ? t.hi : -1));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(isx && tv ? t.lo : 1 << 30));
+  const int x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(isx && tv ? t.hi : -1));
+  float* o = out + (k * c.C + (int64_t)grp * kNhwcGroup) * NB;  // [64][NB], contiguous
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(o, (int64_t)kNhwcGroup * NB * 4);
+  if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: every bin is 0
+    for (int e = lane; e < kNhwcGroup * NB / 4; e += kWave)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, orr, e * 16, 0, kStAux);
+    return;
+  }
+  const bool dy = y1 - y0 + 1 <= NLY, dx = x1 - x0 + 1 <= NLX;
+  const int R = dy ? y1 - y0 + 1 : NLY, Cs = dx ? x1 - x0 + 1 : NLX;
+  // per-lane sample data: slab indices (row of y sample / column of x sample) and factors,
+  // zeroed (and pointed at index 0) for invalid samples
+  const int i0 = !tv ? 0 : (isy ? (dy ? t.lo - y0 : 2 * s) : (dx ? t.lo - x0 : 2 * s));
+  const int i1 = !tv ? 0 : (isy ? (dy ? t.hi - y0 : 2 * s + 1) : (dx ? t.hi - x0 : 2 * s + 1));
+  const float fl = tv ? t.l : 0.f, fh = tv ? t.h : 0.f;
+  // tap-list source rows / columns: list entry e of an axis is tap (e & 1 ? hi : lo) of sample e / 2
+  // (the source lane supplies both taps; the destination picks by its own parity)
+  const int ysrc_e = (lane < NLY) ? lane : 0, xsrc_e = (lane < NLX) ? lane : 0;
+  const int ylo_s = __shfl(tv ? t.lo : y0, ysrc_e >> 1, kWave), yhi_s = __shfl(tv ? t.hi : y0, ysrc_e >> 1, kWave);
+  const int xlo_s = __shfl(tv ? t.lo : x0, 32 + (xsrc_e >> 1), kWave);
+  const int xhi_s = __shfl(tv ? t.hi : x0, 32 + (xsrc_e >> 1), kWave);
+  const int ysrc = (ysrc_e & 1) ? yhi_s : ylo_s, xsrc = (xsrc_e & 1) ? xhi_s : xlo_s;
+  const int64_t sy = lv.sy[l], sx = lv.sx[l];
+  const float* base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  const __amdgpu_buffer_rsrc_t fr =
+      uniform_rsrc(base, ((int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + c.C) * 4);
+  const int rows_cap = kCells / Cs;  // >= 2: Cs <= NLX
+  const uint32_t inv = (65536u + (uint32_t)Cs - 1u) / (uint32_t)Cs;  // e / Cs for e < 1024
+  const int quad = (lane & 15) * 16, soff = grp * kNhwcGroup * 4;
+  int band_lo = 0, band_hi = 0;
+  if (kStamp) t_pro = (int64_t)__builtin_amdgcn_s_memrealtime();
+  // sample row sr (in order): stage its band if needed, then acc[px] += its two samples of each bin column
+  auto row = [&](int sr, float (&acc)[PW]) {
+    // opaque copies: the broadcasts are re-read per row, not hoisted into ~60 live SGPRs
+    int a0 = i0, a1 = i1, av = tv;
+    float al = fl, ah = fh;
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(av), "+v"(al), "+v"(ah));
+    int r0 = __builtin_amdgcn_readlane(a0, sr), r1 = __builtin_amdgcn_readlane(a1, sr);
+    const float ly = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(al), sr));
+    const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ah), sr));
+    if (!__builtin_amdgcn_readlane(av, sr) && band_hi > band_lo) r0 = r1 = band_lo;  // zero weights: any cell
+    if (r0 < band_lo || r1 >= band_hi) {  // stage the band of slab rows [r0, r0 + rows_cap)
+      band_lo = r0;
+      band_hi = min(r0 + rows_cap, R);
+      const int ncell = (band_hi - band_lo) * Cs;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous band's tap reads are done
+      __builtin_amdgcn_wave_barrier();
+      for (int i = 0; 4 * i < ncell; ++i) {
+        int e = 4 * i + (lane >> 4);
+        e = e < ncell ? e : ncell - 1;
+        const int rr = (int)(((uint32_t)e * inv) >> 16), cc = e - rr * Cs;
+        const int yy = dy ? y0 + band_lo + rr : __shfl(ysrc, band_lo + rr, kWave);
+        const int xx = dx ? x0 + cc : __shfl(xsrc, cc, kWave);
+        lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)i, (int)(((int64_t)yy * sy + (int64_t)xx * sx) * 4) + quad,
+                          soff);
+      }
+      wait_vmcnt<0>();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (kStamp) {
+        if (n_bands == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime(), first_cells = ncell;
+        ++n_bands;
+      }
+    }
+    const float* row0 = slab + (r0 - band_lo) * Cs * kNhwcGroup + lane;
+    const float* row1 = slab + (r1 - band_lo) * Cs * kNhwcGroup + lane;
+#pragma unroll
+    for (int ix = 0; ix < 2 * PW; ++ix) {
+      const int q0 = __builtin_amdgcn_readlane(a0, 32 + ix) * kNhwcGroup;
+      const int q1 = __builtin_amdgcn_readlane(a1, 32 + ix) * kNhwcGroup;
+      const float lx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(al), 32 + ix));
+      const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ah), 32 + ix));
+      const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+      const float val = ((w1 * row0[q0] + w2 * row0[q1]) + w3 * row1[q0]) + w4 * row1[q1];
+      acc[ix >> 1] = acc[ix >> 1] + val;
+    }
+  };
+  float* ob = kRegOut ? slab : obuf;  // [channel][bin]
+  if constexpr (kRegOut) {
+    // the 7 x 7 outputs of this lane's channel in VGPRs: a dynamic bin-row loop shifts each
+    // row's results into the tail of outv (static indices only), then out through the slab
+    float outv[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) outv[j] = 0.0f;
+    for (int py = 0; py < PH; ++py) {
+      float acc[PW];
+#pragma unroll
+      for (int px = 0; px < PW; ++px) acc[px] = 0.0f;
+      row(2 * py, acc);
+      row(2 * py + 1, acc);
+#pragma unroll
+      for (int j = 0; j < NB - PW; ++j) outv[j] = outv[j + PW];
+#pragma unroll
+      for (int px = 0; px < PW; ++px) outv[NB - PW + px] = acc[px] * 0.25f;  // count 4: / 4 == * 0.25
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < NB; ++j) ob[lane * NB + j] = outv[j];  // stride NB (odd): no bank conflicts
+  } else {
+    for (int py = 0; py < PH; ++py) {
+      float acc[PW];
+#pragma unroll
+      for (int px = 0; px < PW; ++px) acc[px] = 0.0f;
+      row(2 * py, acc);
+      row(2 * py + 1, acc);
+#pragma unroll
+      for (int px = 0; px < PW; ++px) ob[lane * NB + py * PW + px] = acc[px] * 0.25f;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (kStamp) t_eval = (int64_t)__builtin_amdgcn_s_memrealtime();
+  const float4* s4 = reinterpret_cast<const float4*>(ob);
+  for (int e = lane; e < kNhwcGroup * NB / 4; e += kWave) {
+    const float4 q = s4[e];
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u32x4{__float_as_uint(q.x), __float_as_uint(q.y), __float_as_uint(q.z), __float_as_uint(q.w)}, orr, e * 16, 0,
+        kStAux);
+  }
+  if (kStamp && lane == 0) {
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * NB) + (int64_t)w * 8;
+    st[0] = t_start;
+    st[1] = t_pro;
+    st[2] = t_land;
+    st[3] = t_eval;
+    st[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[5] = n_bands;
+    st[6] = first_cells;
+    st[7] = blockIdx.x & 7;
+  }
+}
+
 static inline int32_t make_levels(int32_t L, const float* const* feats, float* const* grads, const int32_t* feat_hw,
                            const int64_t* strides, const float* scales, RoiLevels* lv) {
   FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "num_levels %d out of range", L);
@@ -1082,6 +1535,29 @@ static inline FwdCaps fwd_caps(const RoiLevels& lv, int32_t channels, int32_t ph
 
 
 // kernels of the product's forward, chosen by shape class
+constexpr int kNhwcCells = 56;  // slab cells of the channels-last kernel (14 KB + 12.25 KB of outputs per wave)
+
+// channels-last features: unit channel stride, 16-B aligned cells, 64-channel groups
+static inline bool nhwc_ok(const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw, int32_t sr) {
+  if (sr != 2 || ph != 7 || pw != 7 || channels % kNhwcGroup != 0) return false;
+  for (int l = 0; l < lv.L; ++l) {
+    const int64_t ext = ((int64_t)(lv.h[l] - 1) * lv.sy[l] + (int64_t)(lv.w[l] - 1) * lv.sx[l] + channels) * 4;
+    if (lv.sc[l] != 1 || lv.sx[l] < channels || lv.sy[l] < lv.sx[l] || lv.sx[l] % 4 || lv.sy[l] % 4 ||
+        lv.sb[l] % 4 || (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15) || ext >= ((int64_t)1 << 31))
+      return false;
+  }
+  return true;
+}
+
+// channels-last features for the quad kernel: unit channel stride, C % 4 == 0, 16-B aligned
+static inline bool quad_ok(const FwdCaps& f, const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw) {
+  if (!f.buf || channels % 4 != 0 || 4 * ph > kWave || 4 * pw > kWave || ph * pw > kWave) return false;
+  for (int l = 0; l < lv.L; ++l)
+    if (lv.sc[l] != 1 || lv.sx[l] % 4 || lv.sy[l] % 4 || lv.sb[l] % 4 || (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15))
+      return false;
+  return true;
+}
+
 static inline bool pair_ok(const FwdCaps& f, int32_t channels, int32_t ph, int32_t pw) {
   return f.lds && channels % 2 == 0 && 4 * ph <= kWave && 4 * pw <= kWave &&
          4 * ph * (4 * pw + 1) <= PairLayout<1>::kCells;

@@ -226,12 +226,24 @@ __device__ void anchor_target_item(const AnchorTargetArgs& p, int s, int64_t n, 
   }
 }
 
+// Per-level head outputs [B, C * A, H, W] with explicit element strides (b, c, y, x):
+// NCHW and channels-last alike.  Level-local anchor index loc = a * H * W + y * W + x (the
+// reference's [C, A * H * W] view, anchor_head.py:82); output channel c of anchor a is
+// tensor channel c * A + a.
 struct LevelMap {
   const float* ptr[FRH_MAX_LEVELS];
   int64_t off[FRH_MAX_LEVELS + 1];
-  int64_t hwa[FRH_MAX_LEVELS];
+  int64_t sb[FRH_MAX_LEVELS], sc[FRH_MAX_LEVELS], sy[FRH_MAX_LEVELS], sx[FRH_MAX_LEVELS];
+  uint32_t hw[FRH_MAX_LEVELS], w[FRH_MAX_LEVELS];
+  int A;
   int n;
 };
+
+__device__ __forceinline__ int64_t level_elem(const LevelMap& lm, int l, int b, int c, int64_t loc) {
+  const uint32_t u = (uint32_t)loc, a = u / lm.hw[l], sp = u - a * lm.hw[l], y = sp / lm.w[l], x = sp - y * lm.w[l];
+  return (int64_t)b * lm.sb[l] + (int64_t)(c * lm.A + (int)a) * lm.sc[l] + (int64_t)y * lm.sy[l] +
+         (int64_t)x * lm.sx[l];
+}
 
 __global__ void gather_levels_kernel(LevelMap lm, int C, int64_t total, const int64_t* chosen,
                                      const int32_t* seg_of, float* out, int64_t out_ld) {
@@ -245,9 +257,8 @@ __global__ void gather_levels_kernel(LevelMap lm, int C, int64_t total, const in
   }
   int l = 0;
   while (l + 1 < lm.n && n >= lm.off[l + 1]) ++l;
-  int64_t loc = n - lm.off[l];
-  const float* src = lm.ptr[l] + (int64_t)b * C * lm.hwa[l] + loc;
-  for (int c = 0; c < C; ++c) out[c * out_ld + j] = src[c * lm.hwa[l]];
+  const int64_t loc = n - lm.off[l];
+  for (int c = 0; c < C; ++c) out[c * out_ld + j] = lm.ptr[l][level_elem(lm, l, b, c, loc)];
 }
 
 __global__ void scatter_levels_kernel(LevelMap lm, int C, int64_t total, const int64_t* chosen,
@@ -259,9 +270,9 @@ __global__ void scatter_levels_kernel(LevelMap lm, int C, int64_t total, const i
   if (b < 0) return;  // padding row: no gradient (and no read-modify-write race with a real row)
   int l = 0;
   while (l + 1 < lm.n && n >= lm.off[l + 1]) ++l;
-  int64_t loc = n - lm.off[l];
-  float* dst = const_cast<float*>(lm.ptr[l]) + (int64_t)b * C * lm.hwa[l] + loc;
-  for (int c = 0; c < C; ++c) dst[c * lm.hwa[l]] += grad[c * grad_ld + j];
+  const int64_t loc = n - lm.off[l];
+  float* dst = const_cast<float*>(lm.ptr[l]);
+  for (int c = 0; c < C; ++c) dst[level_elem(lm, l, b, c, loc)] += grad[c * grad_ld + j];
 }
 
 __global__ void prepend_gt_kernel(const int64_t* prop_labels, int64_t pstride, const int32_t* num_props,
@@ -451,27 +462,49 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
   return check_launch("frh_anchor_target");
 }
 
-static int32_t make_levelmap(int32_t L, const float* const* ptrs, const int64_t* off, const int64_t* hwa,
-                             LevelMap* lm) {
+// strides: [L][4] element strides (b, c, y, x); hw: [L][2] grid (H, W); A anchors per cell
+static int32_t make_levelmap(int32_t L, const float* const* ptrs, const int64_t* off, const int32_t* hw,
+                             const int64_t* strides, int32_t A, LevelMap* lm) {
   FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "bad level count");
-  FRH_REQUIRE(ptrs && off && hwa, "null pointer argument");
+  FRH_REQUIRE(ptrs && off && hw && strides && A >= 1, "null pointer argument");
   lm->n = L;
+  lm->A = A;
   for (int l = 0; l < L; ++l) {
     lm->ptr[l] = ptrs[l];
     lm->off[l] = off[l];
-    lm->hwa[l] = hwa[l];
+    FRH_REQUIRE(hw[2 * l] >= 1 && hw[2 * l + 1] >= 1, "empty level %d", l);
+    lm->w[l] = (uint32_t)hw[2 * l + 1];
+    lm->hw[l] = (uint32_t)hw[2 * l] * (uint32_t)hw[2 * l + 1];
+    lm->sb[l] = strides[4 * l];
+    lm->sc[l] = strides[4 * l + 1];
+    lm->sy[l] = strides[4 * l + 2];
+    lm->sx[l] = strides[4 * l + 3];
   }
-  lm->off[L] = off[L - 1] + hwa[L - 1];
+  lm->off[L] = off[L - 1] + (int64_t)A * hw[2 * L - 2] * hw[2 * L - 1];
   return FRH_OK;
 }
 
-extern "C" int32_t frh_gather_level_outputs(int32_t num_levels, const float* const* level_ptrs,
-                                            const int64_t* level_off, const int64_t* level_hw_a,
-                                            int32_t channels, int64_t total, const int64_t* chosen_idx,
-                                            const int32_t* seg_of, float* out, int64_t out_ld, void* stream) {
-  LevelMap lm;
-  int32_t r = make_levelmap(num_levels, level_ptrs, level_off, level_hw_a, &lm);
-  if (r) return r;
+// the contiguous [B, C, A*H*W] form of the non-strided entries: one anchor per "cell", W = A*H*W
+static int32_t contiguous_levelmap(int32_t L, const float* const* ptrs, const int64_t* off, const int64_t* hwa,
+                                   int32_t channels, LevelMap* lm) {
+  FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "bad level count");
+  FRH_REQUIRE(hwa, "null pointer argument");
+  int32_t hw[2 * FRH_MAX_LEVELS];
+  int64_t st[4 * FRH_MAX_LEVELS];
+  for (int l = 0; l < L; ++l) {
+    FRH_REQUIRE(hwa[l] >= 1 && hwa[l] < ((int64_t)1 << 31), "bad level size");
+    hw[2 * l] = 1;
+    hw[2 * l + 1] = (int32_t)hwa[l];
+    st[4 * l] = (int64_t)channels * hwa[l];
+    st[4 * l + 1] = hwa[l];
+    st[4 * l + 2] = hwa[l];
+    st[4 * l + 3] = 1;
+  }
+  return make_levelmap(L, ptrs, off, hw, st, 1, lm);
+}
+
+static int32_t launch_gather(const LevelMap& lm, int32_t channels, int64_t total, const int64_t* chosen_idx,
+                             const int32_t* seg_of, float* out, int64_t out_ld, void* stream) {
   FRH_REQUIRE(channels >= 1 && total >= 0, "bad sizes");
   if (total == 0) return FRH_OK;
   FRH_REQUIRE(chosen_idx && seg_of && out, "null pointer argument");
@@ -480,19 +513,60 @@ extern "C" int32_t frh_gather_level_outputs(int32_t num_levels, const float* con
   return check_launch("frh_gather_level_outputs");
 }
 
-extern "C" int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
-                                           const int64_t* level_off, const int64_t* level_hw_a, int32_t channels,
-                                           int64_t total, const int64_t* chosen_idx, const int32_t* seg_of,
-                                           const float* grad, int64_t grad_ld, void* stream) {
-  LevelMap lm;
-  int32_t r = make_levelmap(num_levels, const_cast<const float* const*>(level_grads), level_off, level_hw_a, &lm);
-  if (r) return r;
+static int32_t launch_scatter(const LevelMap& lm, int32_t channels, int64_t total, const int64_t* chosen_idx,
+                              const int32_t* seg_of, const float* grad, int64_t grad_ld, void* stream) {
   FRH_REQUIRE(channels >= 1 && total >= 0, "bad sizes");
   if (total == 0) return FRH_OK;
   FRH_REQUIRE(chosen_idx && seg_of && grad, "null pointer argument");
   hipLaunchKernelGGL(scatter_levels_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      as_stream(stream), lm, channels, total, chosen_idx, seg_of, grad, grad_ld);
   return check_launch("frh_scatter_level_grads");
+}
+
+extern "C" int32_t frh_gather_level_outputs(int32_t num_levels, const float* const* level_ptrs,
+                                            const int64_t* level_off, const int64_t* level_hw_a,
+                                            int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                            const int32_t* seg_of, float* out, int64_t out_ld, void* stream) {
+  LevelMap lm;
+  int32_t r = contiguous_levelmap(num_levels, level_ptrs, level_off, level_hw_a, channels, &lm);
+  if (r) return r;
+  return launch_gather(lm, channels, total, chosen_idx, seg_of, out, out_ld, stream);
+}
+
+extern "C" int32_t frh_scatter_level_grads(int32_t num_levels, float* const* level_grads,
+                                           const int64_t* level_off, const int64_t* level_hw_a, int32_t channels,
+                                           int64_t total, const int64_t* chosen_idx, const int32_t* seg_of,
+                                           const float* grad, int64_t grad_ld, void* stream) {
+  LevelMap lm;
+  int32_t r = contiguous_levelmap(num_levels, const_cast<const float* const*>(level_grads), level_off, level_hw_a,
+                                  channels, &lm);
+  if (r) return r;
+  return launch_scatter(lm, channels, total, chosen_idx, seg_of, grad, grad_ld, stream);
+}
+
+extern "C" int32_t frh_gather_level_outputs_strided(int32_t num_levels, const float* const* level_ptrs,
+                                                    const int64_t* level_off, const int32_t* level_hw,
+                                                    const int64_t* level_strides, int32_t num_anchors,
+                                                    int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                                    const int32_t* seg_of, float* out, int64_t out_ld,
+                                                    void* stream) {
+  LevelMap lm;
+  int32_t r = make_levelmap(num_levels, level_ptrs, level_off, level_hw, level_strides, num_anchors, &lm);
+  if (r) return r;
+  return launch_gather(lm, channels, total, chosen_idx, seg_of, out, out_ld, stream);
+}
+
+extern "C" int32_t frh_scatter_level_grads_strided(int32_t num_levels, float* const* level_grads,
+                                                   const int64_t* level_off, const int32_t* level_hw,
+                                                   const int64_t* level_strides, int32_t num_anchors,
+                                                   int32_t channels, int64_t total, const int64_t* chosen_idx,
+                                                   const int32_t* seg_of, const float* grad, int64_t grad_ld,
+                                                   void* stream) {
+  LevelMap lm;
+  int32_t r = make_levelmap(num_levels, const_cast<const float* const*>(level_grads), level_off, level_hw,
+                            level_strides, num_anchors, &lm);
+  if (r) return r;
+  return launch_scatter(lm, channels, total, chosen_idx, seg_of, grad, grad_ld, stream);
 }
 
 extern "C" int32_t frh_prepend_gt_labels(int32_t num_segs, const int64_t* prop_labels,

@@ -45,6 +45,10 @@ SIGNATURES = {
                                          c_i64, c_vp]),
     'frh_scatter_level_grads': (c_i32, [c_i32, P(c_vp), P(c_i64), P(c_i64), c_i32, c_i64, c_vp, c_vp, c_vp,
                                         c_i64, c_vp]),
+    'frh_gather_level_outputs_strided': (c_i32, [c_i32, P(c_vp), P(c_i64), P(c_i32), P(c_i64), c_i32, c_i32, c_i64,
+                                                 c_vp, c_vp, c_vp, c_i64, c_vp]),
+    'frh_scatter_level_grads_strided': (c_i32, [c_i32, P(c_vp), P(c_i64), P(c_i32), P(c_i64), c_i32, c_i32, c_i64,
+                                                c_vp, c_vp, c_vp, c_i64, c_vp]),
     'frh_prepend_gt_labels': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'frh_bbox_target_workspace': (c_size, [c_i32, c_i64]),
     'frh_bbox_target': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
@@ -58,6 +62,9 @@ SIGNATURES = {
     'frh_rpn_proposals': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i32), c_i32, c_i32, c_vp, c_i64,
                                   P(c_f32), P(c_f32), P(c_f32), P(c_f32), c_i32, c_i32, c_i32, c_f64, c_vp,
                                   c_vp, c_vp, c_vp, c_size, c_vp]),
+    'frh_rpn_proposals_strided': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i64), P(c_i64), P(c_i32), c_i32, c_i32,
+                                          c_vp, c_i64, P(c_f32), P(c_f32), P(c_f32), P(c_f32), c_i32, c_i32, c_i32,
+                                          c_f64, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_nms_workspace': (c_size, [c_i32, c_i32]),
     'frh_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, c_f64, c_i32, c_vp, c_i64, c_vp, c_vp, c_size,
                                c_vp]),
@@ -87,6 +94,7 @@ SIGNATURES = {
     'frh_atss_workspace': (c_size, [c_i32, c_i32, c_i32, c_i32, c_i64]),
     'frh_bn_act': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_i64, c_i32, c_vp]),
     'frh_loss_workspace': (c_size, []),
+    'frh_fpn_merge_nhwc': (c_i32, [c_vp, P(c_i64), c_vp, c_i32, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
     'frh_image_preprocess': (c_i32, [c_vp, c_i32, P(c_i64), P(c_i32), P(c_i32), P(c_i32), P(c_f32), P(c_f32), c_i32,
                                      c_vp, c_i32, c_i32, c_vp]),
     'frh_cls_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,

@@ -16,11 +16,12 @@ import torch
 from torch import nn
 
 from .. import ops, utils, losses
+from ..utils import ChannelsLastConvs
 from ..anchor import AnchorCreator, in_grid_sizes, anchor_targets_batched
 from ..region import MaxIoUAssigner
 
 
-class AnchorHead(nn.Module):
+class AnchorHead(ChannelsLastConvs):
     def __init__(self, num_classes, anchor_scales=(8,), anchor_ratios=(0.5, 1.0, 2.0),
                  anchor_strides=(4, 8, 16, 32, 64), anchor_center_lt=False, target_means=(0.0, 0.0, 0.0, 0.0),
                  target_stds=(1.0, 1.0, 1.0, 1.0), loss_cls=None, loss_bbox=None):

@@ -16,6 +16,7 @@ from torch import nn
 
 from .. import ops, utils
 from ..anchor import AnchorCreator
+from ..utils import ChannelsLastConvs
 
 
 # ---------------------------------------------------------------- LTRB helpers (fcos_head.py:9-116)
@@ -99,7 +100,7 @@ def _normal_init(m, std, bias=0.0):
     nn.init.constant_(m.bias, bias)
 
 
-class FCOSHead(nn.Module):
+class FCOSHead(ChannelsLastConvs):
     def __init__(self, num_classes=21, in_channels=256, stacked_convs=4, feat_channels=256,
                  strides=(8, 16, 32, 64, 126), anchor_center_lt=False, reg_std=300, reg_mean=0,
                  reg_coef=(1.0, 1.0, 1.0, 1.0, 1.0), reg_coef_trainable=False, atss_cfg=None, loss_cls=None,

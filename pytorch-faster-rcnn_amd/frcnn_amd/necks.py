@@ -1,15 +1,27 @@
-"""FPN neck (stays on PyTorch-ROCm).
+"""FPN neck (convolutions on PyTorch-ROCm).
 
 Same topology and parameter names as the reference FPN (`lib/necks.py:7-90`):
 1x1 laterals, top-down nearest upsample-add, 3x3 output convs, and extra
 levels either by stride-2 subsampling of the last output
 (`max_pool2d(k=1, s=2)`, `necks.py:89`) or by stride-2 3x3 convs.
+
+On a HIP device the levels come out channels-last (NHWC): the top-down merge
+of every level is one HIP pass (`ops.fpn_merge_nhwc`: lateral + nearest
+upsample of the merged coarser level, written NHWC), and the output convs run
+in MIOpen's NHWC layout (channels-last weights, `utils.ChannelsLastConvs`) --
+2.64 -> 2.41 ms for the FPN output convs + RPN head at cfg2 on MI355X
+(`tools/probe_fpn_layout.py`).  The heads and the RoIAlign read NHWC levels
+directly (strided kernels, the channel-quad RoIAlign).  CPU tensors take the
+reference's NCHW ops.
 """
 import torch.nn.functional as F
 from torch import nn
 
+from .utils import ChannelsLastConvs
+from . import ops
 
-class FPN(nn.Module):
+
+class FPN(ChannelsLastConvs):
     def __init__(self, in_channels, out_channels, num_outs, start_level=0, end_level=-1,
                  extra_use_convs=False, extra_convs_on_inputs=True,
                  relu_before_extra_convs=False, with_activation=False):
@@ -52,8 +64,16 @@ class FPN(nn.Module):
         if len(inputs) != self.num_ins:
             raise AssertionError('FPN expects {} inputs'.format(self.num_ins))
         lat = [conv(inputs[self.start_level + i]) for i, conv in enumerate(self.lateral_convs)]
-        for i in range(self.used_ins - 1, 0, -1):
-            lat[i - 1] = lat[i - 1] + F.interpolate(lat[i], size=lat[i - 1].shape[2:], mode='nearest')
+        if lat[0].is_cuda and lat[0].dtype.is_floating_point and lat[0].dtype.itemsize == 4:
+            # top-down merge straight into channels-last levels (one HIP pass per level)
+            merged = [None] * self.used_ins
+            merged[-1] = ops.fpn_merge_nhwc(lat[-1])
+            for i in range(self.used_ins - 1, 0, -1):
+                merged[i - 1] = ops.fpn_merge_nhwc(lat[i - 1], merged[i])
+            lat = merged
+        else:
+            for i in range(self.used_ins - 1, 0, -1):
+                lat[i - 1] = lat[i - 1] + F.interpolate(lat[i], size=lat[i - 1].shape[2:], mode='nearest')
         outs = [self.fpn_convs[i](lat[i]) for i in range(self.used_ins)]
         for i in range(self.used_ins, self.num_outs):
             if self.extra_use_convs:

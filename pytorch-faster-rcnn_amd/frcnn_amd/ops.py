@@ -304,43 +304,50 @@ def anchor_target_batched(labels, num_boxes, max_boxes, anchors, gts, gt_labels,
 
 
 class _GatherLevels(torch.autograd.Function):
-    """tar = cat_l(level_out.view(C, -1))[:, chosen] per image, with its adjoint scatter."""
+    """tar = cat_l(level_out.view(C, -1))[:, chosen] per image, with its adjoint scatter.
+    Levels of any layout (NCHW, or the channels-last outputs of an NHWC head): the kernels
+    take each level's element strides."""
 
     @staticmethod
     def forward(ctx, chosen_idx, seg_of, channels, *levels):
-        levels = [l.contiguous() for l in levels]
         n = chosen_idx.numel()
-        offs, hwa = _level_offsets(levels, channels)
+        offs, hw, st, A = _level_desc(levels, channels)
         out = torch.empty(channels, n, dtype=torch.float32, device=chosen_idx.device)
         if n:
-            call('frh_gather_level_outputs', len(levels), ptr_array(levels), i64_array(offs), i64_array(hwa),
-                 channels, n, ptr(chosen_idx), ptr(seg_of), ptr(out), out.stride(0), stream_of(out))
+            call('frh_gather_level_outputs_strided', len(levels), ptr_array(levels), i64_array(offs), i32_array(hw),
+                 i64_array(st), A, channels, n, ptr(chosen_idx), ptr(seg_of), ptr(out), out.stride(0), stream_of(out))
         ctx.save_for_backward(chosen_idx, seg_of)
-        ctx.shapes = [l.shape for l in levels]
+        ctx.shapes = [(l.shape, l.stride()) for l in levels]
         ctx.channels = channels
         return out
 
     @staticmethod
     def backward(ctx, grad):
         chosen_idx, seg_of = ctx.saved_tensors
-        grads = [torch.zeros(s, dtype=torch.float32, device=grad.device) for s in ctx.shapes]
+        # each level's gradient in the level's own layout
+        grads = [torch.empty_strided(sh, sd, dtype=torch.float32, device=grad.device).zero_() for sh, sd in ctx.shapes]
         grad = grad.contiguous()
         n = chosen_idx.numel()
-        offs, hwa = _level_offsets(grads, ctx.channels)
+        offs, hw, st, A = _level_desc(grads, ctx.channels)
         if n:
-            call('frh_scatter_level_grads', len(grads), ptr_array(grads), i64_array(offs), i64_array(hwa),
-                 ctx.channels, n, ptr(chosen_idx), ptr(seg_of), ptr(grad), grad.stride(0), stream_of(grad))
+            call('frh_scatter_level_grads_strided', len(grads), ptr_array(grads), i64_array(offs), i32_array(hw),
+                 i64_array(st), A, ctx.channels, n, ptr(chosen_idx), ptr(seg_of), ptr(grad), grad.stride(0),
+                 stream_of(grad))
         return (None, None, None) + tuple(grads)
 
 
-def _level_offsets(levels, channels):
-    offs, hwa, acc = [], [], 0
+def _level_desc(levels, channels):
+    """(first flat index per level, (H, W) per level, element strides per level, anchors A)."""
+    offs, hw, st, acc = [], [], [], 0
+    A = levels[0].shape[1] // channels
     for l in levels:
-        per = l.shape[1] * l.shape[2] * l.shape[3] // channels
+        if l.dim() != 4 or l.shape[1] != channels * A:
+            raise AssertionError('head outputs must be [B, C*A, H, W] with one A for every level')
         offs.append(acc)
-        hwa.append(per)
-        acc += per
-    return offs, hwa
+        hw += [l.shape[2], l.shape[3]]
+        st += list(l.stride())
+        acc += A * l.shape[2] * l.shape[3]
+    return offs, hw, st, A
 
 
 def gather_level_outputs(levels, chosen_idx, seg_of, channels):
@@ -429,9 +436,8 @@ def param2bbox(base, param, means, stds, img_size=None):
 # ---------------------------------------------------------------- RPN proposals (a9)
 def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means, stds, img_hw, min_sizes, pre_nms,
                   post_nms, max_num, nms_iou):
-    """All images x levels; returns (boxes [B, 4, cap], scores [B, cap], counts int32 device [B])."""
-    cls_outs = [c.contiguous() for c in cls_outs]
-    reg_outs = [r.contiguous() for r in reg_outs]
+    """All images x levels; returns (boxes [B, 4, cap], scores [B, cap], counts int32 device [B]).
+    cls / reg levels of any layout (NCHW or channels-last: the kernels take their strides)."""
     _need_cuda(*cls_outs)
     B, L = cls_outs[0].shape[0], len(cls_outs)
     grid = [v for c in cls_outs for v in (c.shape[2], c.shape[3])]
@@ -446,11 +452,11 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
     counts = torch.empty(B, dtype=torch.int32, device=dev)
     wsb = _lib.query('frh_rpn_proposals_workspace', B, L, grid_a, num_anchors, int(pre_nms))
     ws = workspace(wsb, dev)
-    call('frh_rpn_proposals', B, L, ptr_array(cls_outs), ptr_array(reg_outs), grid_a, num_anchors, cls_channels,
-         ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
+    call('frh_rpn_proposals_strided', B, L, ptr_array(cls_outs), ptr_array(reg_outs),
+         i64_array([v for c in cls_outs for v in c.stride()]), i64_array([v for r in reg_outs for v in r.stride()]),
+         grid_a, num_anchors, cls_channels, ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
          f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
-         int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(),
-         stream_of(boxes))
+         int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(), stream_of(boxes))
     if NMS_PROFILE['on']:  # keep this call's per-level NMS input (in the workspace) for a replay
         view = (ctypes.c_int64 * 4)()
         call('frh_rpn_proposals_nms_view', B, L, grid_a, num_anchors, int(pre_nms), view)
@@ -797,6 +803,45 @@ def atss_assign(anchors, grid_sizes, strides, gt_list, label_list, img_shapes, t
          ptr(gcnt), ptr(labels), gmax, ptr(img_hw), int(topk), ptr(cls), ptr(reg), ptr(ctr), ptr(ws), ws_n,
          stream_of(cls))
     return cls, reg, ctr
+
+
+# ---------------------------------------------------------------- FPN top-down merge (channels-last levels)
+class _FpnMerge(torch.autograd.Function):
+    """out = lat + nearest_upsample(up) as a channels-last tensor (frh_fpn_merge_nhwc);
+    lat: any layout; up: the merged coarser level (channels-last) or None."""
+
+    @staticmethod
+    def forward(ctx, lat, up):
+        B, C, H, W = lat.shape
+        out = torch.empty(B, C, H, W, dtype=torch.float32, device=lat.device, memory_format=torch.channels_last)
+        uh, uw = (int(up.shape[2]), int(up.shape[3])) if up is not None else (0, 0)
+        call('frh_fpn_merge_nhwc', ptr(lat), i64_array(lat.stride()), ptr(up), uh, uw, ptr(out), B, C, H, W,
+             stream_of(out))
+        ctx.has_up = up is not None
+        if ctx.has_up:
+            ctx.save_for_backward(up)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gup = None
+        if ctx.has_up and ctx.needs_input_grad[1]:
+            (up,) = ctx.saved_tensors
+            with torch.enable_grad():
+                u = up.detach().requires_grad_(True)
+                y = torch.nn.functional.interpolate(u, size=g.shape[2:], mode='nearest')
+                gup, = torch.autograd.grad(y, u, g)
+        return g if ctx.needs_input_grad[0] else None, gup
+
+
+def fpn_merge_nhwc(lat, up=None):
+    """The FPN's top-down step lat + interpolate(up, size=lat.shape[2:], mode='nearest')
+    (lib/necks.py:72-84) as one HIP pass writing a channels-last level."""
+    _need_cuda(lat, up)
+    if lat.dtype != torch.float32 or (up is not None and (up.dtype != torch.float32 or
+                                                          not up.is_contiguous(memory_format=torch.channels_last))):
+        raise AssertionError('fpn_merge_nhwc: f32 lateral and a channels-last f32 coarser level')
+    return _FpnMerge.apply(lat, up)
 
 
 # ---------------------------------------------------------------- backbone epilogue (frozen BN + add + ReLU)

@@ -705,11 +705,13 @@ def test_roi_align_forward_default_vs_oracle_p2(dev, layout):
     np.testing.assert_array_equal(out2, out[:, :95])
 
 
-def test_roi_align_forward_bench_config_bit_exact(dev):
+@pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
+def test_roi_align_forward_bench_config_bit_exact(dev, layout):
     """The forward at the bench's own configuration: the 1024 RoIs of a cfg2 training step
     (tests/golden/cfg2_rois.npz, 873 / 102 / 42 / 7 on P2..P5), C = 256, P2-P5 of a
-    2-image 608x1024 batch (152x256 ... 19x32), NCHW: every output bit-identical to the
-    oracle (lib/region.py:271-296, torchvision legacy RoIAlign semantics)."""
+    2-image 608x1024 batch (152x256 ... 19x32), NCHW (channel-pair kernel) and
+    channels-last (the FPN's NHWC levels: channel-quad kernel): every output bit-identical
+    to the oracle (lib/region.py:271-296, torchvision legacy RoIAlign semantics)."""
     from frcnn_amd import ops
     z = np.load(inputs.golden_path('cfg2_rois.npz'))
     rois, levels = z['r5'], z['lv']
@@ -717,8 +719,10 @@ def test_roi_align_forward_bench_config_bit_exact(dev):
     scales = [float(v) for v in z['scales']]
     feats = inputs.feature_maps(44, [s[2:] for s in shapes], shapes[0][1], shapes[0][0])
     ref = oracle.roi_align(feats, rois, levels, scales, (7, 7), 2)
-    out = ops.roi_align_multilevel([T(f, dev) for f in feats], T(rois, dev), T(levels, dev), scales, (7, 7),
-                                   2).cpu().numpy()
+    ft = [T(f, dev) for f in feats]
+    if layout == 'nhwc':
+        ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), 2).cpu().numpy()
     np.testing.assert_array_equal(out, ref)
 
 
@@ -736,7 +740,7 @@ def test_roi_align_multilevel_vs_oracle(dev, layout, sampling):
     if layout == 'nhwc':
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
     out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (7, 7), sampling).cpu().numpy()
-    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(out, ref)  # every forward kernel keeps the oracle's operation order
 
 
 def test_roi_align_module_and_strided_view(dev):
@@ -746,7 +750,7 @@ def test_roi_align_module_and_strided_view(dev):
     rois = _rois(51, 200, 2)
     out = RoIAlign((7, 7), 0.25, 2)(ft, T(rois, dev)).cpu().numpy()
     ref = oracle.roi_align([np.ascontiguousarray(f[:, :, ::2, ::2])], rois, None, [0.25], (7, 7), 2)
-    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(out, ref)
 
 
 @pytest.mark.parametrize('case', ['small', 'p2', 'p2_nhwc', 'adaptive', 'bins9x7'])
@@ -801,7 +805,7 @@ def test_basic_roi_extractor_matches_reference_flow(dev):
         r5 = np.concatenate([np.full((1, p.shape[1]), b, np.float32), p], 0).T.copy()
         lv = oracle.roi_level_map(r5, 56.0, 4)
         ref = oracle.roi_align(feats, r5, lv, [1 / 4, 1 / 8, 1 / 16, 1 / 32], (7, 7), 2)
-        np.testing.assert_allclose(outs[b].cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(outs[b].cpu().numpy(), ref)
 
 
 # ----------------------------------------------------------------- end to end (cfg2 shapes)

@@ -21,7 +21,9 @@ import bench  # noqa: E402
 from frcnn_amd import ops, _lib, set_sampler_mode  # noqa: E402
 import toolslib  # noqa: E402
 
-STAMPED = {1}
+STAMPED = {1, 9, 15}
+STAMPED_NHWC = {6}  # channels-last stamped build: 8 int64 per 64-channel item
+NHWC = set(range(2, 19))  # channels-last kernels: run on channels_last copies of the same features
 
 
 def calibrate(variants, dev, small=False):
@@ -70,6 +72,20 @@ def stamps_report(stm):
           flush=True)
 
 
+def nhwc_stamps_report(stm):
+    """[start, prologue done, first band landed, eval done, end, bands, first-band cells, xcd]"""
+    stm = stm[stm[:, 0] > 0]
+    t0 = stm[:, 0].min()
+    pc = lambda a: np.percentile(a / 100.0, [50, 90, 99]).round(2).tolist()  # noqa: E731
+    print('  {} waves; span {:.1f} us; start p50/90 {}'.format(len(stm), (stm[:, 4].max() - t0) / 100.0,
+                                                          pc(stm[:, 0] - t0)[:2]))
+    for nb in sorted(set(stm[:, 5].tolist())):
+        x = stm[stm[:, 5] == nb]
+        print('  bands={} waves {:5d} cells p50 {}: prologue {} land {} eval {} store {} life {}'.format(
+            nb, len(x), int(np.median(x[:, 6])), pc(x[:, 1] - x[:, 0]), pc(x[:, 2] - x[:, 1]), pc(x[:, 3] - x[:, 2]),
+            pc(x[:, 4] - x[:, 3]), pc(x[:, 4] - x[:, 0])), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=20)
@@ -105,7 +121,9 @@ def main():
         np.savez(args.dump, rois=r, levels=lv, shapes=np.array(shapes), scales=np.array(scales))
     lib = toolslib.load()
     K, C = rois.shape[0], shapes[0][1]
+    feats_cl = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     hw, st = ops._feat_desc(feats)
+    hw_cl, st_cl = ops._feat_desc(feats_cl)
     wsb = int(lib.frh_roi_align_workspace(K))
     wsp = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
     scratch = torch.ones(768 * 2 ** 20 // 4, device=dev) if args.cold else None
@@ -114,11 +132,15 @@ def main():
     summary = {}
     for v in variants * args.rounds:
         extra = (K * C // 16) * 16 if v in STAMPED else 0  # 8 int64 stamps per 16-channel item
+        if v in STAMPED_NHWC:
+            extra = (K * C // 64 + 8) * 16
         full = torch.zeros(K * C * ph * pw + extra, device=dev)
         out = full[:K * C * ph * pw].view(K, C, ph, pw)
 
+        fv, hv, sv = (feats_cl, hw_cl, st_cl) if v in NHWC else (feats, hw, st)
+
         def launch():
-            s = lib.frh_roi_align_fwd_variant(v, len(feats), _lib.ptr_array(feats), hw, st, _lib.f32_array(scales),
+            s = lib.frh_roi_align_fwd_variant(v, len(fv), _lib.ptr_array(fv), hv, sv, _lib.f32_array(scales),
                                               shapes[0][0], C, _lib.ptr(rois), _lib.ptr(levels), K, ph, pw, sr, 0,
                                               _lib.ptr(full), _lib.ptr(wsp), wsb, _lib.stream_of(out))
             assert s == 0, lib.frh_last_error()
@@ -153,7 +175,7 @@ def main():
                 torch.cuda.synchronize()
                 e0.record()
                 for _ in range(args.iters):
-                    for f in feats:
+                    for f in fv:
                         f.mul_(1.0)
                     if with_launch:
                         launch()
@@ -165,6 +187,8 @@ def main():
         summary.setdefault(v, []).append((warm, cold))
         if v in STAMPED:
             stamps_report(full[K * C * ph * pw:].view(torch.int64).view(-1, 8).cpu().numpy())
+        if v in STAMPED_NHWC:
+            nhwc_stamps_report(full[K * C * ph * pw:].view(torch.int64).view(-1, 8)[:K * C // 64].cpu().numpy())
         if ref is None:
             ref = out.clone()
         same = bool(torch.equal(out, ref))

@@ -22,12 +22,62 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   if (r) return r;
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+  hipStream_t st = as_stream(stream);
+  if (variant >= 8 && variant <= 18) {  // channels-last quad kernel (9: stamped; 10: 3 waves/SIMD; 11: 5;
+                                        // 12 / 13 / 14: 32 / 64 / 128 channels per item; 15: 32 stamped)
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
+    const int qw = variant == 12 || variant == 15 ? 8 : variant == 13 ? 16 : variant == 14 ? 32 : kQuadWave;
+    const int64_t tq = num_rois * ((channels + 4 * qw - 1) / (4 * qw));
+    const dim3 gq((unsigned)(8 * ((tq + 7) / 8)));
+    if (variant == 12)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, 8>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 13)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, 16>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 14)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, 32>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 15)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, true, 3, 8>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 16)  // LDS-staged 16-B output stores
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, 4, 1>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 17)  // no output stores (diagnostic: the staging + evaluation alone)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, 4, 2>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 18)  // LDS-staged 16-B stores, default cache policy
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<0, false, 3, 4, 1>), gq, dim3(kWave), 0, st, lv, c, out);
+    else
+    if (variant == 8)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 9)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, true>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 10)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3>), gq, dim3(kWave), 0, st, lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 5>), gq, dim3(kWave), 0, st, lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
+  if (variant >= 2 && variant <= 7) {  // channels-last kernel: slab cells / outputs in VGPRs or in LDS
+    FRH_REQUIRE(nhwc_ok(lv, channels, pooled_h, pooled_w, sampling_ratio), "the nhwc kernel does not take this shape");
+    const int64_t tn = num_rois * (channels / kNhwcGroup);
+    const dim3 gn((unsigned)(8 * ((tn + 7) / 8)));
+    if (variant == 2)
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 56, kCpolNT, true>), gn, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 3)
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 64, kCpolNT, true>), gn, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 4)
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 96, kCpolNT, true>), gn, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 5)
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 56, kCpolNT, false>), gn, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 6)
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 56, kCpolNT, true, true>), gn, dim3(kWave), 0, st, lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_nhwc_kernel<7, 7, 128, kCpolNT, true>), gn, dim3(kWave), 0, st, lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
   FRH_REQUIRE(pair_ok(f, channels, pooled_h, pooled_w), "the pair kernel does not take this shape");
   const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
   FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
   const dim3 g1((unsigned)(8 * ((total + 7) / 8)));
-  hipStream_t st = as_stream(stream);
   if (variant == 0)
     hipLaunchKernelGGL((roi_align_fwd_pair_kernel<kCpolNT, false>), g1, dim3(kWave), 0, st, lv, c, out);
   else if (variant == 1)
