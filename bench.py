@@ -192,6 +192,7 @@ def summarise_trace(trace, steps):
 
 # ------------------------------------------------------------------ RoIAlign replays
 ROI_EVENT_REPLAY_US = None  # median dispatch-bound event duration of the warm replays
+ROI_SPAN_REPLAY_US = {}  # median in-kernel spans of the warm / cold per-launch replays
 
 
 def roi_align_replays(recs, dev, rounds=3):
@@ -213,25 +214,41 @@ def roi_align_replays(recs, dev, rounds=3):
     warm = e0.elapsed_time(e1) * 1e3 / len(recs)
     # the same back-to-back launches, each with its dispatch-bound event pair: the per-launch
     # event duration minus the amortised duration is what the event pair adds to one launch
-    pairs = []
-    for _ in range(3 * len(recs)):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        b.record()
-        pairs.append((a, b))
-    torch.cuda.synchronize(dev)
+    def triples(n):
+        spans = torch.tensor([[-1, 0]] * n, dtype=torch.int64, device=dev)
+        out = []
+        for i in range(n):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            b.record()
+            out.append((a, b, spans[i]))
+        torch.cuda.synchronize(dev)
+        return out
+
+    def span_us(p):
+        return (int(p[2][1]) - int(p[2][0])) * 1e-2
+
+    pairs = triples(3 * len(recs))
     for i, p in enumerate(pairs):
         ops.roi_align_replay(recs[i % len(recs)], events=p)
     torch.cuda.synchronize(dev)
-    ev = float(np.median([1e3 * a.elapsed_time(b) for a, b in pairs]))
-    global ROI_EVENT_REPLAY_US
+    ev = float(np.median([1e3 * p[0].elapsed_time(p[1]) for p in pairs]))
+    global ROI_EVENT_REPLAY_US, ROI_SPAN_REPLAY_US
     ROI_EVENT_REPLAY_US = ev  # agrees with the amortised figure: no per-launch overhead off the step
+    ROI_SPAN_REPLAY_US['warm'] = float(np.median([span_us(p) for p in pairs]))
     scratch = torch.ones(768 * 2 ** 20 // 4, dtype=torch.float32, device=dev)
     sink = torch.empty((), dtype=torch.float32, device=dev)
 
     def evict():
         torch.sum(scratch, dim=0, out=sink)  # reads only: no dirty lines for the launch to write back
 
+    cold_p = triples(len(recs))
+    for r, p in zip(recs, cold_p):
+        evict()
+        ops.roi_align_replay(r, events=p)
+    torch.cuda.synchronize(dev)
+    ROI_SPAN_REPLAY_US['cold'] = float(np.median([span_us(p) for p in cold_p]))
+    ROI_SPAN_REPLAY_US['cold_event'] = float(np.median([1e3 * p[0].elapsed_time(p[1]) for p in cold_p]))
     evict()
     colds = []
     for _ in range(rounds):
@@ -529,12 +546,14 @@ def main():
     # the RoIAlign forward launches of the timed steps carry a pair of HIP events bound to the
     # kernel's own dispatch (frh_roi_align_fwd_strided_timed): its in-step duration, read after
     # the timed region; the events are created (recorded once) before it
+    # plus a span slot each: the kernel's own first-wave-start / last-wave-end (100 MHz clock)
     pool = []
-    for _ in range(4 * args.steps):
+    spans = torch.tensor([[-1, 0]] * (4 * args.steps), dtype=torch.int64, device=dev)  # -1 = UINT64_MAX
+    for i in range(4 * args.steps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         e1.record()
-        pool.append((e0, e1))
+        pool.append((e0, e1, spans[i]))
     ops.ROI_ALIGN_PROFILE['event_pool'] = pool
     ops.ROI_ALIGN_PROFILE['timed'] = timed_roi = []
     barrier()
@@ -545,7 +564,8 @@ def main():
     elapsed = time.perf_counter() - t0
     ops.ROI_ALIGN_PROFILE['timed'] = None
     ops.ROI_ALIGN_PROFILE['event_pool'] = []
-    roi_timed_us = [1e3 * a.elapsed_time(b) for a, b in timed_roi]
+    roi_timed_us = [1e3 * e[0].elapsed_time(e[1]) for e in timed_roi]
+    roi_span_us = [(int(e[2][1]) - int(e[2][0])) * 1e-2 for e in timed_roi]  # 10 ns ticks
     assert torch.isfinite(loss).all()
     t_max = max_over_ranks(elapsed, dev, world)
 
@@ -571,6 +591,7 @@ def main():
         roi_tracer = float(np.median([us for _, us in roi_launches])) if roi_launches else None
         roi_events = float(np.median(roi_timed_us)) if roi_timed_us else None
         roi_in_step_all = [round(us, 2) for us in roi_timed_us]
+        roi_span = float(np.median(roi_span_us)) if roi_span_us else None
         roi_kernel = kernel_short(roi_launches[0][0]) if roi_launches else None
         warm, cold = roi_align_replays(recs, dev)
         # in-step kernel duration = the timed steps' dispatch-bound event durations minus what an
@@ -622,7 +643,13 @@ def main():
                 'avg_launch_us': us_for_frac, 'algorithmic_bytes_per_launch': avg_bytes,
                 'launches': len(recs),
                 'in_step_event_us_median': roi_events, 'in_step_event_us': roi_in_step_all,
+                'in_step_span_us_median': roi_span, 'in_step_span_us': [round(us, 2) for us in roi_span_us],
+                'achieved_in_step': avg_bytes / (roi_span * 1e-6) / 1e9 if roi_span else None,
+                'frac_in_step': avg_bytes / (roi_span * 1e-6) / 1e9 / HBM_PEAK_GBS if roi_span else None,
                 'replay_event_us_median': ROI_EVENT_REPLAY_US,
+                'replay_span_us_median_warm': ROI_SPAN_REPLAY_US.get('warm'),
+                'replay_span_us_median_cold': ROI_SPAN_REPLAY_US.get('cold'),
+                'replay_event_us_median_cold': ROI_SPAN_REPLAY_US.get('cold_event'),
                 'avg_launch_us_kernel_tracer': roi_tracer, 'avg_launch_us_replay_warm': warm,
                 'avg_launch_us_replay_cold': cold,
                 'timing': ('avg_launch_us = the RoIAlign forward launches of the steps after the timed region '
@@ -631,7 +658,10 @@ def main():
                            'matches rocprofv3\'s kernel trace of the timed steps within a few % (DESIGN 7); '
                            'in_step_event_us = the timed launches\' own dispatch-bound event pairs '
                            '(frh_roi_align_fwd_strided_timed) and kernel_tracer = torch.profiler over {} steps: '
-                           'per-launch timestamps, 7-12 us above rocprofv3 for the same launches; replay_cold = '
+                           'per-launch timestamps, 7-12 us above rocprofv3 for the same launches; '
+                           'in_step_span = the timed launches\' own first-wave start to last-wave end on the '
+                           'GPU 100 MHz clock (s_memrealtime, recorded by the kernel) -- frac_in_step prices it; '
+                           'replay_cold = '
                            'each launch after a 768 MB read (L2 + Infinity Cache evicted)'.format(steps_traced)) +
                           '; traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per launch, '
                           'profiles/roi_align_pmc.json'}

@@ -364,14 +364,18 @@ int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
                                   int32_t aligned, float* out, void* stream);
 /* Measurement entry (bench.py's roofline line): frh_roi_align_fwd_strided with the forward
  * kernel launched through hipExtLaunchKernel, which binds the two caller-created hipEvent_t
- * to the dispatch's own start and end timestamps (no extra stream packets). */
+ * to the dispatch's own start and end timestamps (no extra stream packets).  span (nullable,
+ * device, 2 x u64, initialised to {UINT64_MAX, 0}): the kernel's own span on the GPU's
+ * 100 MHz s_memrealtime clock -- the earliest wave start and the latest wave end (one lane
+ * per wave records both with memory-side atomic min / max). */
 int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const float* const* feats,
                                         const int32_t* feat_hw, const int64_t* strides,
                                         const float* scales, int32_t batch, int32_t channels,
                                         const float* rois, const int64_t* roi_levels,
                                         int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
                                         int32_t sampling_ratio, int32_t aligned, float* out,
-                                        void* start_event, void* stop_event, void* stream);
+                                        void* start_event, void* stop_event, uint64_t* span,
+                                        void* stream);
 /* Backward of the strided forward: grad_feats (same strides) must be cleared by the
  * caller; contributions are added with float atomics (sampling 2, up to 8x8 bins:
  * one atomic per row run of a RoI's taps), so the summation order -- and the last

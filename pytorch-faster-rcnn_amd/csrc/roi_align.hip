@@ -136,7 +136,7 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
                        const float* scales, int32_t batch, int32_t channels, const float* rois,
                        const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h, int32_t pooled_w,
                        int32_t sampling_ratio, int32_t aligned, float* out, hipStream_t st, hipEvent_t e0,
-                       hipEvent_t e1) {
+                       hipEvent_t e1, unsigned long long* span = nullptr) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
   FRH_REQUIRE((feats && out) || num_rois == 0, "null pointer argument");
@@ -144,7 +144,7 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
   r = make_levels(num_levels, feats, nullptr, feat_hw, strides, scales, &lv);
   if (r) return r;
   if (num_rois == 0) return FRH_OK;
-  RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+  RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned, span};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
   // e0 / e1 (measurement entry): the kernel's own start / end timestamps (hipExtLaunchKernel
   // binds them to the dispatch; no extra packets in the stream)
@@ -158,12 +158,20 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels), 16-B DMA
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    go(roi_align_fwd_quad_kernel<kCpolNT, false, 3>, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave));
+    const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
+    if (span)
+      go(roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, true>, grid, dim3(kWave));
+    else
+      go(roi_align_fwd_quad_kernel<kCpolNT, false, 3>, grid, dim3(kWave));
   } else if (pair_ok(f, channels, pooled_h, pooled_w)) {
     // chunk-major XCD order, nt output stores, one 6.5 KB slab per wave, lean tap state
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
-    go(roi_align_fwd_pair_kernel<kCpolNT, false>, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(kWave));
+    const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
+    if (span)
+      go(roi_align_fwd_pair_kernel<kCpolNT, false, true>, grid, dim3(kWave));
+    else
+      go(roi_align_fwd_pair_kernel<kCpolNT, false>, grid, dim3(kWave));
   } else if (f.lds) {
     go(roi_align_fwd_lds_kernel<256>, dim3((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk)),
        dim3(kRoiThreads));
@@ -189,11 +197,11 @@ extern "C" int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const flo
                                                    const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                                    int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                                    int32_t aligned, float* out, void* start_event, void* stop_event,
-                                                   void* stream) {
+                                                   uint64_t* span, void* stream) {
   FRH_REQUIRE(start_event && stop_event, "null event");
   return roi_fwd(num_levels, feats, feat_hw, strides, scales, batch, channels, rois, roi_levels, num_rois, pooled_h,
                  pooled_w, sampling_ratio, aligned, out, as_stream(stream), static_cast<hipEvent_t>(start_event),
-                 static_cast<hipEvent_t>(stop_event));
+                 static_cast<hipEvent_t>(stop_event), reinterpret_cast<unsigned long long*>(span));
 }
 
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,

@@ -21,7 +21,15 @@ struct RoiCfg {
   const int64_t* levels;     // [K] or nullptr
   int64_t K;
   int C, ph, pw, sampling, aligned;
+  unsigned long long* span;  // measurement builds (kSpan): {min wave start, max wave end}, s_memrealtime
 };
+
+// kSpan kernels: the launch's span on the 100 MHz clock, first wave start to last wave end
+// (one lane per wave: two memory-side atomics)
+__device__ __forceinline__ void record_span(const RoiCfg& c, int64_t t_start) {
+  atomicMin(&c.span[0], (unsigned long long)t_start);
+  atomicMax(&c.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
 
 struct Tap {
   int lo, hi;

@@ -700,9 +700,9 @@ __device__ __forceinline__ void pair_item(const RoiLevels& lv, const RoiCfg& c, 
 // (= linear id % 8) takes the x-th eighth of the chunk-major (chunk, RoI) item list,
 // so each XCD's L2 holds the feature planes of its own channel chunks.  32-bit item
 // arithmetic (host: K * chunks < 2^31).
-template <int kStAux = kCpolNT, bool kStamp = false>
+template <int kStAux = kCpolNT, bool kStamp = false, bool kSpan = false>
 __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   __shared__ __attribute__((aligned(16))) float slab[kPairHalf];
   // the slab as an LDS byte address (integer: no generic-pointer casts)
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
@@ -714,6 +714,7 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
   pair_item<kStAux, 0, kStamp>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1));
+  if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 
 
@@ -960,9 +961,10 @@ __device__ __forceinline__ void quad_item(const RoiLevels& lv, const RoiCfg& c, 
 
 // 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups, chunk-major per XCD (as the
 // pair kernel: the two 16-channel chunks of a 128-B line share an XCD)
-template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 4, int kQW = kQuadWave, int kOut = 0>
+template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 4, int kQW = kQuadWave, int kOut = 0,
+          bool kSpan = false>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe))) roi_align_fwd_quad_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  const int64_t t_start = kStamp ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   __shared__ __attribute__((aligned(16))) float slab[kQuadSlab];
   __shared__ __attribute__((aligned(16))) float obuf[kOut == 1 ? 4 * kQW * kWave : 4];  // [channel][bin], <= 64 bins
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
@@ -974,6 +976,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
   quad_item<kStAux, kStamp, kQW, kOut>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
+  if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,

@@ -84,7 +84,8 @@ SIGNATURES = {
     'frh_roi_align_fwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_align_fwd_strided_timed': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
-                                                c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+                                                c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                                c_vp]),
     'frh_roi_align_bwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_pool_fwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp,

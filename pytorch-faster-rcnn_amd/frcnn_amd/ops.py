@@ -621,9 +621,11 @@ def _feat_desc(feats):
 # trunk they alias the graph's output buffers, so a replay reads the newest step's
 # values -- never use a record's features for their contents.
 ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True, 'timed': None, 'event_pool': []}
-# 'timed': a list -> each forward launch takes a (start, end) pair from 'event_pool' (created
-# beforehand), goes through frh_roi_align_fwd_strided_timed (the events are bound to the
-# kernel's own dispatch timestamps: nothing is added to the stream) and appends the pair.
+# 'timed': a list -> each forward launch takes a (start, end, span) triple from 'event_pool'
+# (created beforehand; span = a device u64[2] set to {UINT64_MAX, 0}), goes through
+# frh_roi_align_fwd_strided_timed (the events are bound to the kernel's own dispatch
+# timestamps, the span is the kernel's own first-wave-start / last-wave-end on the 100 MHz
+# GPU clock: nothing is added to the stream) and appends the triple.
 
 
 class _RoIAlignMulti(torch.autograd.Function):
@@ -646,7 +648,7 @@ class _RoIAlignMulti(torch.autograd.Function):
             ev = ROI_ALIGN_PROFILE['event_pool'].pop()
             call('frh_roi_align_fwd_strided_timed', len(feats), ptr_array(feats), hw, st, f32_array(scales),
                  feats[0].shape[0], C, ptr(rois), ptr(levels), K, ph, pw, int(sampling_ratio), int(bool(aligned)),
-                 ptr(out), ev[0].cuda_event, ev[1].cuda_event, stream_of(out))
+                 ptr(out), ev[0].cuda_event, ev[1].cuda_event, ptr(ev[2]) if len(ev) > 2 else None, stream_of(out))
             timed.append(ev)
         else:
             call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales),
@@ -691,7 +693,7 @@ def roi_align_replay(rec, out=None, events=None):
     if events is not None:
         call('frh_roi_align_fwd_strided_timed', len(feats), ptr_array(feats), hw, st, f32_array(scales),
              shapes[0][0], C, ptr(rois), ptr(levels), K, ph, pw, int(sr), 0, ptr(out), events[0].cuda_event,
-             events[1].cuda_event, stream_of(out))
+             events[1].cuda_event, ptr(events[2]) if len(events) > 2 else None, stream_of(out))
     else:
         call('frh_roi_align_fwd_strided', len(feats), ptr_array(feats), hw, st, f32_array(scales), shapes[0][0], C,
              ptr(rois), ptr(levels), K, ph, pw, int(sr), 0, ptr(out), stream_of(out))
