@@ -109,6 +109,13 @@ int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
  *      sel_counts [S][2] -- the form frh_anchor_target / frh_bbox_target take
  *      without a compaction pass over every box. */
 size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes);
+/* frh_sample_random's workspace contract: its leading frh_sample_zero_bytes(num_segs) bytes
+ * are zero before the call and every call leaves them zero (images above 16 384 boxes take
+ * a one-launch sampler whose per-image counters and histograms live there and are reset by
+ * the launch's last workgroup), so a caller zero-fills the buffer once and reuses it for
+ * calls ordered on one stream.  A word in it that stays nonzero after a call flags a
+ * workgroup that waited out its bounded in-launch barrier (never seen). */
+size_t frh_sample_zero_bytes(int32_t num_segs);
 int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                               const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
                               int32_t* neg_list, int64_t list_seg_stride, int32_t* counts,

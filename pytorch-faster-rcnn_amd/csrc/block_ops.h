@@ -52,19 +52,12 @@ struct TopkSmem {
   int cnt_gt;
 };
 
-// Select the k largest u32 keys among indices [0, n) (ties: lowest index
-// first).  Writes the selected indices (unordered) to out_idx and returns
-// min(n, k).  key_of(i) is evaluated several times per element (one radix
-// pass per byte), so it must be pure.
+// The threshold of block_topk_select's selection (n > k > 0): T = the k-th largest key and
+// krem = how many keys equal to T are taken (the lowest indices among them); every key > T
+// is taken.  key_of(i) must be pure (one radix pass per byte).
 template <class KeyF>
-__device__ int block_topk_select(KeyF key_of, int n, int k, int* out_idx, TopkSmem& sm) {
+__device__ uint2 block_topk_threshold(KeyF key_of, int n, int k, TopkSmem& sm) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (k <= 0 || n <= 0) return 0;
-  if (n <= k) {
-    for (int i = tid; i < n; i += nt) out_idx[i] = i;
-    __syncthreads();
-    return n;
-  }
   uint32_t prefix = 0, pmask = 0;
   int krem = k;
   for (int shift = 24; shift >= 0; shift -= 8) {
@@ -99,7 +92,25 @@ __device__ int block_topk_select(KeyF key_of, int n, int k, int* out_idx, TopkSm
     pmask |= 255u << shift;
     __syncthreads();
   }
-  const uint32_t T = prefix;
+  return make_uint2(prefix, (uint32_t)krem);
+}
+
+// Select the k largest u32 keys among indices [0, n) (ties: lowest index
+// first).  Writes the selected indices (unordered) to out_idx and returns
+// min(n, k).  key_of(i) is evaluated several times per element (one radix
+// pass per byte), so it must be pure.
+template <class KeyF>
+__device__ int block_topk_select(KeyF key_of, int n, int k, int* out_idx, TopkSmem& sm) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (k <= 0 || n <= 0) return 0;
+  if (n <= k) {
+    for (int i = tid; i < n; i += nt) out_idx[i] = i;
+    __syncthreads();
+    return n;
+  }
+  const uint2 th = block_topk_threshold(key_of, n, k, sm);
+  const uint32_t T = th.x;
+  const int krem = (int)th.y;
   const int n_gt = k - krem;  // keys strictly greater than T
   if (tid == 0) sm.cnt_gt = 0;
   __syncthreads();

@@ -256,6 +256,222 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_collect_kernel(PropArgs
   tk_collect_chunk(b, seg, n, tk_plan_refined(b, seg), pol, sm);
 }
 
+// ---------------------------------------------------------------------------
+// Fused selection: keys -> two-level histogram -> collect + decode -> order, in ONE
+// launch whose phases are separated by in-launch segment barriers (seg_topk.h,
+// seg_barrier) instead of the four kernel boundaries of rpn_keys / refine / collect
+// / rank.  The keys stay in registers from the logit load to the collect (no key
+// re-reads); every workgroup of a segment reads the segment's histograms after the
+// barrier and finds the same buckets (no last-workgroup publish hop).  Workgroup x
+// of segment seg owns key chunk x (x < nch) and the records [64x, 64x + 64) of the
+// final order; G(seg) = max(1, nch, ceil(k / 64)) workgroups take part, the rest of
+// the grid row returns at once.  Selection rule, record layout and the order are
+// those of the four-launch path (bit-identical outputs).
+constexpr int kSelRankPer = 64;    // records ordered per workgroup
+constexpr int kSelMaxResident = 768;  // 3/4 of 256 CUs x 4 workgroups (TkSmem: 35 KB of LDS each)
+constexpr int kRpnTieCap = 2048;   // prefix ties sorted in LDS; more: workgroup 0's radix select
+
+__host__ __device__ __forceinline__ int rpn_sel_groups(int n, int pre_nms) {
+  const int nch = (n + kTkChunk - 1) / kTkChunk, k = (pre_nms > 0 && pre_nms < n) ? pre_nms : n;
+  const int r = (k + kSelRankPer - 1) / kSelRankPer;
+  return nch > r ? (nch > 1 ? nch : 1) : (r > 1 ? r : 1);
+}
+
+__device__ __forceinline__ uint64_t rpn_record(uint32_t key, int i, bool live, int slot) {
+  return ((uint64_t)key << 32) | ((~(uint32_t)i & 0xfffffu) << 12) | (live ? 0x800u : 0u) | (uint32_t)slot;
+}
+
+static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs p, ImgArgs ia, TkBufs b) {
+  __shared__ TkSmem sm;
+  static_assert(kRpnTieCap + kRpnSelFused <= kTkCandCap, "ties + records share the candidate area");
+  const int seg = blockIdx.y, x = blockIdx.x, t = threadIdx.x;
+  const int bi = seg / p.L, l = seg % p.L;
+  const int n = p.A * p.h[l] * p.w[l];
+  const int G = rpn_sel_groups(n, p.pre_nms);
+  if (x >= G) return;
+  const int k = rpn_k(p, n);
+  int32_t* st = b.state + seg * TK_WORDS;
+  int32_t* err = st + TK_ERR;
+  const int64_t base = (int64_t)x * kTkChunk;
+  const bool has_keys = base < n;
+  uint32_t* kk = const_cast<uint32_t*>(b.keys) + (int64_t)seg * b.ld;
+  const uint32_t* gh1 = b.hist1 + (int64_t)seg * (1 << kRpnHistBits);
+  uint32_t* gh2 = b.hist2 + (int64_t)seg * kTkBins2;
+  constexpr int sh1 = 32 - kRpnHistBits, sh2 = sh1 - 12;
+
+  // ---- phase 1: keys (registers; an sc1 copy for the degenerate tie path) + first-level histogram
+  uint32_t key[kTkPerThread];
+  tk_hist1_clear(sm.h1, 1 << kRpnHistBits);
+  if (has_keys) {
+    float x0[kTkPerThread], x1[kTkPerThread];  // every logit load in flight at once
+    const int64_t hwa = n;
+    if (p.nchw) {
+      const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
+#pragma unroll
+      for (int r = 0; r < kTkPerThread; ++r) {
+        const int64_t i = base + r * kTkThreads + t;
+        x0[r] = i < hwa ? cls[i] : 0.0f;
+        x1[r] = (p.C == 2 && i < hwa) ? cls[hwa + i] : 0.0f;
+      }
+    } else {
+      const float* cls = p.cls[l];
+#pragma unroll
+      for (int r = 0; r < kTkPerThread; ++r) {
+        const int64_t i = base + r * kTkThreads + t;
+        x0[r] = i < hwa ? cls[rpn_elem(p.cst[l], p.A, p.h[l], p.w[l], bi, 0, i)] : 0.0f;
+        x1[r] = (p.C == 2 && i < hwa) ? cls[rpn_elem(p.cst[l], p.A, p.h[l], p.w[l], bi, 1, i)] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int64_t i = base + r * kTkThreads + t;
+      key[r] = i < hwa ? float_key(score_of2(x0[r], x1[r], p.C)) : 0u;
+      if (i < hwa) xwg_store(kk + i, key[r]);
+      tk_hist_add(sm.h1, i < hwa, key[r] >> sh1);
+    }
+    tk_hist1_flush(sm.h1, 1 << kRpnHistBits, const_cast<uint32_t*>(gh1));
+  } else {
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) key[r] = 0u;
+  }
+  seg_barrier(st + TK_BAR1, G, err);
+
+  // ---- phase 2: bucket b1 (every workgroup reads the same final histogram), then b2
+  tk_find(sm, 1 << kRpnHistBits, k > 0 ? k : 1, [&](int i) { return xwg_load(gh1 + i); });
+  const bool all = k <= 0 || sm.tot <= k;
+  TkPlan plan{all, k <= 0 ? 0 : (all ? sm.tot : k), 0u, sh2, 0};
+  if (!all) {
+    const uint32_t b1 = (uint32_t)sm.bin;
+    const int k1 = k - sm.above;
+    for (int i = t; i < kTkBins2; i += kTkThreads) sm.h2[i] = 0u;
+    __syncthreads();
+    if (has_keys) {
+#pragma unroll
+      for (int r = 0; r < kTkPerThread; ++r)
+        tk_hist_add(sm.h2, key[r] != 0u && (key[r] >> sh1) == b1, (key[r] >> sh2) & 0xfffu);
+      __syncthreads();
+      for (int i = t; i < kTkBins2; i += kTkThreads) {
+        const uint32_t c = sm.h2[i];
+        if (c) atomicAdd(&gh2[i], c);
+      }
+    }
+    seg_barrier(st + TK_BAR2, G, err);
+    tk_find(sm, kTkBins2, k1, [&](int i) { return xwg_load(gh2 + i); });
+    plan.P = (b1 << 12) | (uint32_t)sm.bin;
+    plan.k2 = k1 - sm.above;
+  }
+  const int kv = plan.kv, k2 = all ? 0 : plan.k2, nabove = kv - k2;
+
+  // ---- phase 3: collect from the registers; selections decoded by the selecting workgroup
+  RpnPol pol{p, ia, b, seg, true};
+  uint64_t* cand = b.cand + (int64_t)seg * b.ld;
+  if (kv > 0 && has_keys) {
+    uint32_t sel = 0u, eq = 0u;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const uint32_t pre = key[r] >> plan.sh;
+      sel |= (key[r] != 0u && (all || pre > plan.P)) ? 1u << r : 0u;
+      eq |= (key[r] != 0u && !all && pre == plan.P) ? 1u << r : 0u;
+    }
+    const int2 slots = block_reserve2(__popc(sel), __popc(eq), &st[TK_OUT], sm.part, &sm.base, &sm.cbase);
+    int c = slots.y;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r)
+      if (eq & (1u << r))
+        xwg_store(cand + c++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)(base + r * kTkThreads + t));
+    int s = slots.x;
+    const int gbase = sm.base, nsel = sm.tot_sel;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r)
+      if (sel & (1u << r)) sm.cand[s++ - gbase] = ((uint64_t)key[r] << 32) | (uint32_t)(base + r * kTkThreads + t);
+    __syncthreads();
+    for (int j = t; j < nsel; j += kTkThreads) {
+      const uint64_t e = sm.cand[j];
+      pol.select((int)(uint32_t)e, (uint32_t)(e >> 32), gbase + j);
+    }
+  }
+  seg_barrier(st + TK_BAR3, G, err);
+
+  // ---- phase 4: every record of the segment in LDS (the prefix ties ordered here)
+  uint64_t* tie = sm.cand;                 // [kRpnTieCap], later the live-masked records
+  uint64_t* rec = sm.cand + kRpnTieCap;    // [kRpnSelFused]
+  const uint64_t* grec = p.sel_keys + (int64_t)seg * p.P;
+  const int ncand = k2 > 0 ? xwg_load(st + TK_CAND) : 0;
+  if (k2 > 0 && ncand > kRpnTieCap) {
+    // degenerate key set: workgroup 0 takes the k2 ties by an exact radix select over the
+    // prefix (lowest index first among equal keys), then one more barrier
+    if (x == 0) {
+      int32_t* idx = reinterpret_cast<int32_t*>(cand);  // the consumed candidate row
+      auto key_of = [&](int i) -> uint32_t {
+        const uint32_t kq = xwg_load(kk + i);
+        return (kq >> plan.sh) == plan.P ? kq : 0u;
+      };
+      block_topk_select(key_of, n, k2, idx, sm.fb);
+      for (int j = t; j < k2; j += kTkThreads) {
+        const int i = idx[j];
+        const float4 bx = rpn_decode_one(p, ia, seg, i);
+        xwg_store(const_cast<uint64_t*>(grec) + nabove + j,
+                  rpn_record(xwg_load(kk + i), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j));
+      }
+    }
+    seg_barrier(st + TK_BAR4, G, err);
+    for (int j = t; j < kv; j += kTkThreads) rec[j] = xwg_load(grec + j);
+  } else {
+    for (int j = t; j < nabove; j += kTkThreads) rec[j] = xwg_load(grec + j);
+    if (k2 > 0) {
+      const int P2 = next_pow2(ncand > 1 ? ncand : 1);
+      for (int j = t; j < P2; j += kTkThreads) tie[j] = j < ncand ? xwg_load(cand + j) : 0ull;
+      __syncthreads();
+      block_bitonic_sort_desc(tie, P2);
+      for (int j = t; j < k2; j += kTkThreads) {
+        const uint64_t e = tie[j];
+        const int i = (int)~(uint32_t)e;
+        const float4 bx = rpn_decode_one(p, ia, seg, i);
+        rec[nabove + j] = rpn_record((uint32_t)(e >> 32), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 5: order by counting (rpn_rank_kernel's rule) over the live-masked records
+  const int kv16 = (kv + 15) & ~15;
+  for (int j = t; j < kv16; j += kTkThreads) {
+    const uint64_t r = j < kv ? rec[j] : 0ull;
+    tie[j] = ((r >> 11) & 1u) ? r : 0ull;
+  }
+  __syncthreads();
+  if (x == 0) {  // the segment's kept count
+    int c = 0;
+    for (int j = t; j < kv; j += kTkThreads) c += (int)((rec[j] >> 11) & 1u);
+    c = block_sum(c, sm.part);
+    if (t == 0) p.sel_count[seg] = c;
+  }
+  const int lane8 = t & 7;
+  const uint64_t* stage = reinterpret_cast<const uint64_t*>(p.stage + (int64_t)seg * kRpnSelFused);
+  for (int q0 = x * kSelRankPer; q0 < min(kv, x * kSelRankPer + kSelRankPer); q0 += kTkThreads / 8) {
+    const int q = q0 + (t >> 3);
+    const uint64_t me = q < kv ? rec[q] : ~0ull;
+    int above = 0;
+    for (int j = 2 * lane8; j < kv16; j += 16) above += (tie[j] > me ? 1 : 0) + (tie[j + 1] > me ? 1 : 0);
+    above += __shfl_xor(above, 1, kWave);
+    above += __shfl_xor(above, 2, kWave);
+    above += __shfl_xor(above, 4, kWave);
+    if (lane8 == 0 && q < kv && ((me >> 11) & 1u)) {
+      const int slot = (int)(me & 0x7ffu);
+      float4 bx;
+      if (slot < nabove) {
+        const uint64_t lo = xwg_load(stage + 2 * slot), hi = xwg_load(stage + 2 * slot + 1);
+        bx = make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                         __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
+      } else {
+        bx = rpn_decode_one(p, ia, seg, (int)(~(uint32_t)(me >> 12) & 0xfffffu));
+      }
+      reinterpret_cast<float4*>(p.sel_boxes)[(int64_t)seg * p.P + above] = bx;
+      p.sel_scores[(int64_t)seg * p.P + above] = key_float((uint32_t)(me >> 32));
+    }
+  }
+}
+
 // ... and one 1024-thread block per segment orders them by (score desc, index
 // asc) in LDS (up to kMaxSort) and decodes
 static __global__ void __launch_bounds__(kPropThreads) rpn_sort_decode_kernel(PropArgs p, ImgArgs ia, const int32_t* state) {
@@ -456,6 +672,14 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
 
 static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
+int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                           const float* const* reg_ptrs, const int64_t* cls_strides, const int64_t* reg_strides,
+                           const int32_t* grid_hw, int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                           int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
+                           const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
+                           float* out_boxes, float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
+                           void* stream, bool select_launches);
+
 struct PropLayout {
   int P;
   size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, total;
@@ -557,6 +781,22 @@ extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_level
                                              int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
                                              float* out_scores, int32_t* out_counts, void* workspace,
                                              size_t ws_bytes, void* stream) {
+  return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
+                                 num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
+                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes,
+                                 stream, false);
+}
+
+// select_launches: the four-launch selection even where the one-launch one applies
+// (tools: A/B measurement and equality tests of the two)
+int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                                const float* const* reg_ptrs, const int64_t* cls_strides, const int64_t* reg_strides,
+                                const int32_t* grid_hw, int32_t num_anchors, int32_t cls_channels,
+                                const float* anchors, int64_t anchor_ld, const float* means, const float* stds,
+                                const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
+                                int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
+                                int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream,
+                                bool select_launches) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
@@ -621,9 +861,20 @@ extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_level
             reinterpret_cast<uint64_t*>(ws + z.mem)};
   FRH_HIP(hipMemsetAsync(zb, 0, tk_zero_bytes(S, kRpnHistBits), st));
   const dim3 grid((unsigned)((z.nmax + kTkChunk - 1) / kTkChunk), (unsigned)S);
+  const bool fused = z.P <= kRpnSelFused && z.nmax < (1 << 20);  // record layout limits
+  // one-launch selection: every segment's workgroups resident together (seg_barrier): the
+  // grid's live workgroups stay within what 256 CUs hold at 4 per CU (TkSmem: ~35 KB LDS)
+  int gx = 1, live_wgs = 0;
+  for (int l = 0; l < num_levels; ++l) {
+    const int g = rpn_sel_groups(num_anchors * p.h[l] * p.w[l], pre_nms);
+    gx = g > gx ? g : gx;
+    live_wgs += g * num_imgs;
+  }
+  if (fused && live_wgs <= kSelMaxResident && !select_launches) {
+    hipLaunchKernelGGL(rpn_select_kernel, dim3((unsigned)gx, (unsigned)S), dim3(kTkThreads), 0, st, p, ia, tb);
+  } else {
   hipLaunchKernelGGL(rpn_keys_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
   hipLaunchKernelGGL(rpn_refine_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
-  const bool fused = z.P <= kRpnSelFused && z.nmax < (1 << 20);  // record layout limits
   hipLaunchKernelGGL(rpn_collect_kernel, grid, dim3(kTkThreads), 0, st, p, ia, tb, fused);
   if (fused) {
     hipLaunchKernelGGL(rpn_rank_kernel, dim3(kRpnSelFused / kRankPer, (unsigned)S), dim3(256), 0, st, p, tb.state);
@@ -633,6 +884,7 @@ extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_level
       FRH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rpn_sort_decode_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sel));
     hipLaunchKernelGGL(rpn_sort_decode_kernel, dim3(S), dim3(kPropThreads), lds_sel, st, p, ia, tb.state);
+  }
   }
   int32_t r = check_launch("rpn_select");
   if (r) return r;

@@ -248,6 +248,207 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
   tk_collect_chunk(sb.tk, v, n, plan, pol, sm);
 }
 
+// ---------------------------------------------------------------------------
+// One-launch device sampler for large images (the RPN's anchors): the keys and
+// collect launches above as the phases of ONE launch, separated by in-launch image
+// barriers (seg_topk.h seg_barrier).  Workgroup x of image s owns boxes
+// [4096x, 4096x + 4096) (16 per thread, labels and keys in registers throughout):
+//   1. labels -> positive / negative keys (the same hashes), LDS histograms of
+//      their top 8 bits and the class counts, flushed by atomics;       barrier
+//   2. every workgroup reads the image's counts and histograms: kp, kn
+//      (region.py:43-57) and both two-level plans (tk_plan_direct);
+//   3. its boxes above each plan's prefix are taken: output label and list slot
+//      (one reservation per class); its prefix ties go to the class's candidate
+//      list; every other box gets label -1;                              barrier
+//      (only when a class has ties)
+//   4. workgroup 0 orders each class's ties by (key desc, box asc) and takes the
+//      first k2 (labels of all tied boxes, list slots of the taken ones);
+// then the last workgroup to leave zeroes the image's histograms and state words,
+// which is the workspace contract (frh_sample_zero_bytes: zero before, zero after).
+// The selected set is exactly the two-launch path's.
+constexpr int kSampFusedMaxWgs = 512;  // resident with margin (LDS: 4 workgroups per CU)
+
+struct SampFused {
+  uint32_t* hist;    // [S][2][kSampBins]   zero before and after
+  int32_t* state;    // [S][2][TK_WORDS]     zero before and after (TK_ERR: sticky barrier error)
+  uint64_t* cand;    // [S][2][ld] prefix ties: key << 32 | ~box
+  int64_t ld;
+  int32_t* sel;      // nullable: [S][2][sel_ld]
+  int64_t sel_ld;
+  int32_t* sel_cnt;  // [S][2]
+};
+
+__device__ __forceinline__ uint32_t samp_key(uint64_t seed, int v, int i, bool cand) {
+  return cand ? ((~hash_u32(seed, (uint32_t)v, (uint32_t)i)) | 1u) : 0u;
+}
+
+static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const int64_t* lab_in, int64_t lstride,
+                                                                          const int32_t* num, int max_num,
+                                                                          int pos_num, uint64_t seed, SampFused f,
+                                                                          int64_t* lab_out) {
+  __shared__ TkSmem sm;
+  __shared__ uint32_t hc[2 * kSampBins];
+  const int s = blockIdx.y, x = blockIdx.x, t = threadIdx.x;
+  const int n = num[s];
+  const int G = n > kTkChunk ? (n + kTkChunk - 1) / kTkChunk : 1;
+  if (x >= G) return;
+  int32_t* st = f.state + (int64_t)(2 * s) * TK_WORDS;  // [2][TK_WORDS]: positives, negatives
+  int32_t* err = st + TK_ERR;
+  uint32_t* gh = f.hist + (int64_t)(2 * s) * kSampBins;  // [2][kSampBins]
+  const int64_t* li = lab_in + (int64_t)s * lstride;
+  int64_t* lo = lab_out ? lab_out + (int64_t)s * lstride : nullptr;
+  const int base = x * kTkChunk;
+
+  // ---- phase 1
+  int32_t lab[kTkPerThread];  // box labels (-1, 0, g + 1) fit 32 bits: kept to the end
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int i = base + r * kTkThreads + t;
+    lab[r] = i < n ? (int32_t)li[i] : -1;
+  }
+  for (int i = t; i < 2 * kSampBins; i += kTkThreads) hc[i] = 0u;
+  __syncthreads();
+  uint32_t key[kTkPerThread], posm = 0u, negm = 0u;
+  int cp = 0, cn = 0;
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const int i = base + r * kTkThreads + t;
+    const bool pos = lab[r] > 0, neg = lab[r] == 0;
+    posm |= pos ? 1u << r : 0u;
+    negm |= neg ? 1u << r : 0u;
+    key[r] = samp_key(seed, 2 * s + (neg ? 1 : 0), i, pos || neg);
+    tk_hist_add(hc, pos, key[r] >> (32 - kSampHistBits));
+    tk_hist_add(hc + kSampBins, neg, key[r] >> (32 - kSampHistBits));
+    cp += pos;
+    cn += neg;
+  }
+  cp = block_sum(cp, sm.part);
+  cn = block_sum(cn, sm.part);
+  if (t == 0) {
+    if (cp) atomicAdd(st + TK_N, cp);
+    if (cn) atomicAdd(st + TK_WORDS + TK_N, cn);
+  }
+  for (int i = t; i < 2 * kSampBins; i += kTkThreads) {
+    const uint32_t c = hc[i];
+    if (c) atomicAdd(gh + i, c);
+  }
+  seg_barrier(st + TK_BAR1, G, err);
+
+  // ---- phase 2
+  const int npos = xwg_load(st + TK_N), nneg = xwg_load(st + TK_WORDS + TK_N);
+  const int kp = npos < pos_num ? npos : pos_num;
+  const int kn = nneg < max_num - kp ? nneg : max_num - kp;
+  TkPlan pl[2];
+  pl[0] = tk_plan_direct(kSampHistBits, kp, sm, [&](int i) { return xwg_load(gh + i); });
+  pl[1] = tk_plan_direct(kSampHistBits, kn, sm, [&](int i) { return xwg_load(gh + kSampBins + i); });
+
+  // ---- phase 3 (the plans' fields by select, not by a per-box array index)
+  uint32_t take = 0u, tie = 0u;
+  const int sh = 32 - kSampHistBits;
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r) {
+    const bool neg = (negm >> r) & 1u, cand = ((posm | negm) >> r) & 1u;
+    const uint32_t pre = key[r] >> sh, P = neg ? pl[1].P : pl[0].P;
+    const bool all = neg ? pl[1].all : pl[0].all;
+    const bool live = cand && (neg ? pl[1].kv : pl[0].kv) > 0;
+    take |= (live && (all || pre > P)) ? 1u << r : 0u;
+    tie |= (live && !all && pre == P) ? 1u << r : 0u;
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t m = c ? negm : posm;
+    const int2 slots = block_reserve2(__popc(take & m), __popc(tie & m), st + c * TK_WORDS + TK_OUT, sm.part,
+                                      &sm.base, &sm.cbase);
+    int sp = slots.x, cq = slots.y;
+    int32_t* sl = f.sel ? f.sel + (int64_t)(2 * s + c) * f.sel_ld : nullptr;
+    uint64_t* cl = f.cand + (int64_t)(2 * s + c) * f.ld;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      if (!((m >> r) & 1u)) continue;
+      const int i = base + r * kTkThreads + t;
+      if ((take >> r) & 1u) {
+        if (sl) sl[sp] = i;
+        ++sp;
+      } else if ((tie >> r) & 1u) {
+        xwg_store(cl + cq++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)i);
+      }
+    }
+  }
+  if (lo) {
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int i = base + r * kTkThreads + t;
+      if (i < n && !((tie >> r) & 1u)) lo[i] = ((take >> r) & 1u) ? (int64_t)lab[r] : (int64_t)-1;
+    }
+  }
+  const bool ties = (pl[0].kv > 0 && !pl[0].all) || (pl[1].kv > 0 && !pl[1].all);
+  if (ties) seg_barrier(st + TK_BAR2, G, err);
+
+  // ---- phase 4 (workgroup 0): the prefix ties
+  if (x == 0) {
+    for (int c = 0; c < 2; ++c) {
+      const int v = 2 * s + c, kv = pl[c].kv;
+      if (f.sel_cnt && t == 0) f.sel_cnt[v] = kv;
+      if (kv == 0 || pl[c].all) continue;
+      const int k2 = pl[c].k2, nabove = kv - k2;
+      int32_t* sl = f.sel ? f.sel + (int64_t)v * f.sel_ld : nullptr;
+      const uint64_t* cl = f.cand + (int64_t)v * f.ld;
+      const int ncand = xwg_load(st + c * TK_WORDS + TK_CAND);
+      if (ncand <= kTkCandCap) {
+        const int P2 = next_pow2(ncand > 1 ? ncand : 1);
+        for (int j = t; j < P2; j += kTkThreads) sm.cand[j] = j < ncand ? xwg_load(cl + j) : 0ull;
+        __syncthreads();
+        block_bitonic_sort_desc(sm.cand, P2);
+        for (int j = t; j < ncand; j += kTkThreads) {
+          const int i = (int)~(uint32_t)sm.cand[j];
+          if (lo) lo[i] = j < k2 ? li[i] : -1;
+          if (sl && j < k2) sl[nabove + j] = i;
+        }
+        __syncthreads();  // sm.cand reused by the other class
+      } else {
+        // more ties than the LDS sort holds: an exact radix threshold over the class's prefix
+        // keys (recomputed from the labels), then one ordered pass labels every tied box
+        const uint32_t P = pl[c].P;
+        const int sh = pl[c].sh;
+        auto key_of = [&](int i) -> uint32_t {
+          const int64_t lb = li[i];
+          const uint32_t kq = samp_key(seed, v, i, c ? lb == 0 : lb > 0);
+          return (kq != 0u && (kq >> sh) == P) ? kq : 0u;
+        };
+        const uint2 th = block_topk_threshold(key_of, n, k2, sm.fb);
+        const uint32_t T = th.x;
+        const int krem = (int)th.y, n_gt = k2 - (int)th.y;
+        if (t == 0) sm.fb.cnt_gt = 0;
+        __syncthreads();
+        int eq_taken = 0;
+        for (int b0 = 0; b0 < n; b0 += kTkThreads) {
+          const int i = b0 + t;
+          const uint32_t kq = i < n ? key_of(i) : 0u;
+          const bool gt = kq != 0u && kq > T, eq = kq != 0u && kq == T;
+          int tot;
+          const int rk = block_rank(eq, sm.fb.wave_tot, &tot);
+          const bool tk = gt || (eq && eq_taken + rk < krem);
+          if (kq != 0u && lo) lo[i] = tk ? li[i] : -1;
+          if (sl && gt) sl[nabove + atomicAdd(&sm.fb.cnt_gt, 1)] = i;
+          if (sl && eq && eq_taken + rk < krem) sl[nabove + n_gt + eq_taken + rk] = i;
+          eq_taken += tot;
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  // ---- exit: the last workgroup out leaves the image's zero region zero
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
+  __syncthreads();
+  if (sm.last) {
+    for (int i = t; i < 2 * kSampBins; i += kTkThreads) xwg_store(gh + i, 0u);
+    if (t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
+  }
+}
+
 // Small images (num_boxes <= kSsMax, e.g. the RCNN stage's ~2000 proposal rows): the whole
 // sampler of an image in ONE 1024-thread workgroup -- the same keys (hash of (seed, 2s or
 // 2s + 1, box)), the same selection (the k largest keys, equal keys by ascending box), by
@@ -413,6 +614,11 @@ size_t compact_workspace(int32_t S, int64_t max_n) {
   return (size_t)S * (size_t)n_chunks(max_n > 0 ? max_n : 1) * 2 * sizeof(int32_t);
 }
 
+int32_t sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
+                           const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
+                           uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, void* workspace,
+                           size_t ws_bytes, void* stream, bool two_launches);
+
 }  // namespace frh
 
 using namespace frh;
@@ -425,13 +631,21 @@ struct SampLayout {
   int nchunk;
 };
 
+// The leading zero region (frh_sample_zero_bytes): the one-launch sampler's histograms
+// [V][kSampBins] and state words [V][TK_WORDS]; the rest follows it.
+static size_t samp_zero_hist(int32_t S) { return 0; }
+static size_t samp_zero_state(int32_t S) { return al256((size_t)2 * S * kSampBins * sizeof(uint32_t)); }
+static size_t samp_zero_bytes(int32_t S) {
+  return al256(samp_zero_state(S) + (size_t)2 * S * TK_WORDS * sizeof(int32_t));
+}
+
 static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   SampLayout z{};
   const size_t n = (size_t)(max_boxes > 0 ? max_boxes : 1);
   const int V = 2 * S;
   z.kld = (int64_t)n;
   z.nchunk = (int)((n + kTkChunk - 1) / kTkChunk);
-  z.keys = 0;
+  z.keys = samp_zero_bytes(S);
   z.cand = z.keys + al256((size_t)V * n * sizeof(uint32_t));
   z.state = z.cand + al256((size_t)V * n * sizeof(uint64_t));
   z.phist = z.state + al256((size_t)V * TK_WORDS * sizeof(int32_t));
@@ -445,6 +659,8 @@ extern "C" size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes) {
   size_t b = samp_layout(num_segs, max_boxes).total;
   return a > b ? a : b;
 }
+
+extern "C" size_t frh_sample_zero_bytes(int32_t num_segs) { return num_segs > 0 ? samp_zero_bytes(num_segs) : 0; }
 
 extern "C" int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                                          const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
@@ -488,6 +704,16 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
                                      const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
                                      int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
                                      int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream) {
+  return frh::sample_random_impl(num_segs, labels_in, label_seg_stride, num_boxes, max_boxes, max_num, pos_num, seed,
+                                 labels_out, sel, sel_counts, workspace, ws_bytes, stream, false);
+}
+
+// two_launches: the keys + collect launches even where the one-launch sampler applies
+// (tools: A/B timing and the equality test of the two)
+int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
+                                const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
+                                uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,
+                                void* workspace, size_t ws_bytes, void* stream, bool two_launches) {
   FRH_REQUIRE(num_segs >= 0 && max_boxes >= 0, "negative sizes");
   FRH_REQUIRE(pos_num <= max_num && pos_num >= 0, "pos_num must be in [0, max_num]");
   if (num_segs == 0 || max_boxes == 0) return FRH_OK;
@@ -507,6 +733,14 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
   char* ws = reinterpret_cast<char*>(workspace);
   SampLayout z = samp_layout(num_segs, max_boxes);
   const int V = 2 * num_segs;
+  if (!two_launches && (int64_t)num_segs * z.nchunk <= kSampFusedMaxWgs) {
+    SampFused f{reinterpret_cast<uint32_t*>(ws + samp_zero_hist(num_segs)),
+                reinterpret_cast<int32_t*>(ws + samp_zero_state(num_segs)), reinterpret_cast<uint64_t*>(ws + z.cand),
+                z.kld, sel, (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
+    hipLaunchKernelGGL(sampler_fused_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
+                       labels_in, label_seg_stride, num_boxes, max_num, pos_num, seed, f, labels_out);
+    return check_launch("frh_sample_random");
+  }
   SampBufs sb{TkBufs{reinterpret_cast<uint32_t*>(ws + z.keys), z.kld, nullptr, kSampHistBits, nullptr,
                      reinterpret_cast<int32_t*>(ws + z.state), reinterpret_cast<uint64_t*>(ws + z.cand)},
               reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,

@@ -42,7 +42,8 @@ constexpr int kTkCandCap = 4096;                     // prefix ties sorted in LD
 // per-segment state words (zeroed by the caller's memset; TK_N / TK_K may be
 // seeded by the key kernel)
 enum { TK_N = 0, TK_K = 1, TK_OUT = 2, TK_CAND = 3, TK_DONE1 = 4, TK_DONE2 = 5, TK_CNT = 6,
-       TK_ALL = 7, TK_KV = 8, TK_P = 9, TK_K2 = 10, TK_WORDS = 16 };
+       TK_ALL = 7, TK_KV = 8, TK_P = 9, TK_K2 = 10, TK_BAR1 = 11, TK_BAR2 = 12, TK_BAR3 = 13,
+       TK_BAR4 = 14, TK_ERR = 15, TK_WORDS = 16 };
 
 struct TkBufs {
   const uint32_t* keys;  // [V][ld]
@@ -66,6 +67,9 @@ inline size_t tk_zero_bytes(int V, int hb) {  // hist1 + hist2 + state, contiguo
 // (sc1: L1 bypassed) after every writer's vmcnt(0) wait and its workgroup's
 // done-counter add has been seen (MI355X_MICROARCH.md, hand-off table row 1).
 __device__ __forceinline__ void xwg_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xwg_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t xwg_load(const uint64_t* p) {
@@ -251,6 +255,36 @@ __device__ __forceinline__ bool tk_check_in(int* done, TkSmem& sm) {
   if (threadIdx.x == 0) sm.last = atomicAdd(done, 1) == (int)gridDim.x - 1;
   __syncthreads();
   return sm.last != 0;
+}
+
+// ------------------------------------------------------ in-launch segment barrier
+// The fused selections (rpn_select_kernel, sampler_fused_kernel) keep a segment's
+// workgroups in one launch across their phases: each arrives on a per-segment
+// counter once its own stores and atomics have completed (vmcnt(0) in every wave,
+// then one agent-scope atomic add behind a workgroup barrier) and lane 0 polls
+// the counter with sc1 loads (hand-off table row 1: everything handed across is
+// written sc1 or by memory-side atomics and read back sc1).  Residency: a
+// segment's workgroups are contiguous in dispatch order and the launches keep
+// their total grids far below the chip's resident capacity (host checks), so the
+// polled workgroups are always resident.  The spin is bounded (kSpinTicks of the
+// 100 MHz clock) so a broken assumption ends in a flagged error word, never a hang.
+constexpr uint64_t kSpinTicks = 20000000ull;  // 200 ms
+
+__device__ __forceinline__ void seg_barrier(int32_t* counter, int target, int32_t* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(counter, 1);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (xwg_load(counter) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        atomicOr(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------- refine launch

@@ -31,6 +31,7 @@ SIGNATURES = {
                                   c_f32, c_f32, c_f32, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_size,
                                   c_vp]),
     'frh_sample_workspace': (c_size, [c_i32, c_i64]),
+    'frh_sample_zero_bytes': (c_size, [c_i32]),
     'frh_sample_candidates': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_size,
                                       c_vp]),
     'frh_sample_apply': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,

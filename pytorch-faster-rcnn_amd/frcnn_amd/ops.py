@@ -207,21 +207,40 @@ class SampleLists(object):
         self.labels, self.sel, self.sel_counts, self.max_num = labels, sel, sel_counts, int(max_num)
 
 
-def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None, lists=False):
+_SAMPLE_WS = {}
+
+
+def _sample_workspace(dev, S, max_boxes):
+    """One buffer per (device, stream) for frh_sample_random: zero-filled once; every call
+    leaves its leading frh_sample_zero_bytes(S) bytes zero (the one-launch sampler's counters
+    and histograms), so it is reused as is."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    need = int(_lib.query('frh_sample_workspace', S, max_boxes))
+    ws = _SAMPLE_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _SAMPLE_WS[key] = torch.zeros(need, dtype=torch.uint8, device=dev)
+    return ws
+
+
+def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None, lists=False, _entry=None):
     """Batched RandomSampler over labels [S, >=max_boxes] (region.py:43-57,112-126).
     lists=True (device mode only): return a SampleLists instead of the sampled labels."""
     mode = mode or _SAMPLER['mode']
     S = labels.shape[0]
     dev = labels.device
     if mode == 'device':
-        ws = workspace(_lib.query('frh_sample_workspace', S, max(max_boxes, 1)), dev)
+        ws = _sample_workspace(dev, S, max(max_boxes, 1))
         _SAMPLER['calls'] += 1
         seed = (_SAMPLER['seed'] * 0x9E3779B97F4A7C15 + _SAMPLER['calls']) & 0xFFFFFFFFFFFFFFFF
         out = None if lists else torch.empty_like(labels)
         sel = torch.empty(S, 2, max(int(max_num), 1), dtype=torch.int32, device=dev) if lists else None
         sel_cnt = torch.empty(S, 2, dtype=torch.int32, device=dev) if lists else None
-        call('frh_sample_random', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, int(max_num),
-             int(pos_num), seed, ptr(out), ptr(sel), ptr(sel_cnt), ptr(ws), ws.numel(), stream_of(labels))
+        args = (S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, int(max_num), int(pos_num), seed,
+                ptr(out), ptr(sel), ptr(sel_cnt), ptr(ws), ws.numel(), stream_of(labels))
+        if _entry is None:
+            call('frh_sample_random', *args)
+        elif _entry[0](*args) != 0:  # tests: the tools library's two-launch sampler
+            raise RuntimeError('{} failed'.format(_entry[1]))
         return SampleLists(labels, sel, sel_cnt, max_num) if lists else out
     out = torch.empty_like(labels)
     ld = max(max_boxes, 1)
@@ -435,9 +454,11 @@ def param2bbox(base, param, means, stds, img_size=None):
 
 # ---------------------------------------------------------------- RPN proposals (a9)
 def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means, stds, img_hw, min_sizes, pre_nms,
-                  post_nms, max_num, nms_iou):
+                  post_nms, max_num, nms_iou, _entry=None):
     """All images x levels; returns (boxes [B, 4, cap], scores [B, cap], counts int32 device [B]).
-    cls / reg levels of any layout (NCHW or channels-last: the kernels take their strides)."""
+    cls / reg levels of any layout (NCHW or channels-last: the kernels take their strides).
+    _entry: (ctypes function, name) taking frh_rpn_proposals_strided's arguments instead of it
+    (tests: the tools library's four-launch selection)."""
     _need_cuda(*cls_outs)
     B, L = cls_outs[0].shape[0], len(cls_outs)
     grid = [v for c in cls_outs for v in (c.shape[2], c.shape[3])]
@@ -452,11 +473,15 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
     counts = torch.empty(B, dtype=torch.int32, device=dev)
     wsb = _lib.query('frh_rpn_proposals_workspace', B, L, grid_a, num_anchors, int(pre_nms))
     ws = workspace(wsb, dev)
-    call('frh_rpn_proposals_strided', B, L, ptr_array(cls_outs), ptr_array(reg_outs),
-         i64_array([v for c in cls_outs for v in c.stride()]), i64_array([v for r in reg_outs for v in r.stride()]),
-         grid_a, num_anchors, cls_channels, ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
-         f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
-         int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(), stream_of(boxes))
+    args = (B, L, ptr_array(cls_outs), ptr_array(reg_outs),
+            i64_array([v for c in cls_outs for v in c.stride()]), i64_array([v for r in reg_outs for v in r.stride()]),
+            grid_a, num_anchors, cls_channels, ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
+            f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
+            int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(), stream_of(boxes))
+    if _entry is None:
+        call('frh_rpn_proposals_strided', *args)
+    elif _entry[0](*args) != 0:
+        raise RuntimeError('{} failed'.format(_entry[1]))
     if NMS_PROFILE['on']:  # keep this call's per-level NMS input (in the workspace) for a replay
         view = (ctypes.c_int64 * 4)()
         call('frh_rpn_proposals_nms_view', B, L, grid_a, num_anchors, int(pre_nms), view)

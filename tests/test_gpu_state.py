@@ -26,6 +26,7 @@ def _clear(model):
     from frcnn_amd import ops
     ops._ASSIGN_WS.clear()
     ops._LOSS_WS.clear()
+    ops._SAMPLE_WS.clear()
     del ops._PACKED[:]
     for head in (getattr(model, 'rpn_head', None), getattr(model, 'bbox_head', None)):
         if head is not None:

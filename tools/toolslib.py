@@ -18,6 +18,8 @@ TOOL_SIGNATURES = {
     'frh_roi_align_workspace': (c_size, [c_i64]),
     'frh_nms_sorted_stamped': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, ctypes.c_double, c_i32, c_vp, c_i64, c_vp,
                                        c_vp, c_size, c_vp, c_vp]),
+    'frh_rpn_proposals_launches': _lib.SIGNATURES['frh_rpn_proposals_strided'],
+    'frh_sample_random_launches': _lib.SIGNATURES['frh_sample_random'],
 }
 _lib_t = None
 
