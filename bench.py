@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNEL_GROUPS = [
     ('roi_align_fwd', ('roi_align_fwd',)),
     ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
-    ('proposals', ('rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
+    ('proposals', ('rpn_select', 'rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
     ('sampler', ('sampler_', 'chunk_count', 'chunk_write_lists')),
     ('targets', ('anchor_target', 'bbox_target', 'prepend_gt', 'gather_levels', 'roi_level', 'roi_rows')),
@@ -168,15 +168,18 @@ def group_of(name):
     return None
 
 
+TRUNK_KERNELS = ('bn_act', 'fpn_merge')  # frcnn_amd kernels of the trunk (backbone epilogue, FPN top-down)
+
+
 def summarise_trace(trace, steps):
     """Per-step µs of each kernel group + the detection-path total (frcnn_amd kernels
-    other than the trunk's bn_act epilogue)."""
+    other than the trunk's: the bn_act epilogue and the FPN top-down merge)."""
     per = {g: 0.0 for g, _ in KERNEL_GROUPS}
     names = {g: {} for g, _ in KERNEL_GROUPS}
     det = 0.0
     det_k = {}
     for name, us in trace:
-        if 'frh::' in name and 'bn_act' not in name:
+        if 'frh::' in name and not any(k in name for k in TRUNK_KERNELS):
             det += us
             short = kernel_short(name)
             det_k[short] = det_k.get(short, 0.0) + us
@@ -191,6 +194,24 @@ def summarise_trace(trace, steps):
 
 
 # ------------------------------------------------------------------ RoIAlign replays
+SPAN_SHARDS, SPAN_STRIDE = 256, 16  # include/frcnn_amd.h FRH_SPAN_SHARDS / FRH_SPAN_STRIDE
+
+
+def span_slots(n, dev):
+    """n span slots for frh_roi_align_fwd_strided_timed: [n, shards, stride] int64, each shard's
+    words {0, 1} = {UINT64_MAX (as -1), 0}."""
+    s = torch.zeros(n, SPAN_SHARDS, SPAN_STRIDE, dtype=torch.int64, device=dev)
+    s[:, :, 0] = -1
+    return s
+
+
+def span_of(slot):
+    """µs from the earliest wave start to the latest wave end recorded in one slot (100 MHz)."""
+    starts = slot[:, 0][slot[:, 0] != -1]
+    if starts.numel() == 0:
+        return None
+    return (int(slot[:, 1].max()) - int(starts.min())) * 1e-2
+
 ROI_EVENT_REPLAY_US = None  # median dispatch-bound event duration of the warm replays
 ROI_SPAN_REPLAY_US = {}  # median in-kernel spans of the warm / cold per-launch replays
 
@@ -215,7 +236,7 @@ def roi_align_replays(recs, dev, rounds=3):
     # the same back-to-back launches, each with its dispatch-bound event pair: the per-launch
     # event duration minus the amortised duration is what the event pair adds to one launch
     def triples(n):
-        spans = torch.tensor([[-1, 0]] * n, dtype=torch.int64, device=dev)
+        spans = span_slots(n, dev)
         out = []
         for i in range(n):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -226,7 +247,7 @@ def roi_align_replays(recs, dev, rounds=3):
         return out
 
     def span_us(p):
-        return (int(p[2][1]) - int(p[2][0])) * 1e-2
+        return span_of(p[2])
 
     pairs = triples(3 * len(recs))
     for i, p in enumerate(pairs):
@@ -548,7 +569,7 @@ def main():
     # the timed region; the events are created (recorded once) before it
     # plus a span slot each: the kernel's own first-wave-start / last-wave-end (100 MHz clock)
     pool = []
-    spans = torch.tensor([[-1, 0]] * (4 * args.steps), dtype=torch.int64, device=dev)  # -1 = UINT64_MAX
+    spans = span_slots(4 * args.steps, dev)
     for i in range(4 * args.steps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -565,7 +586,7 @@ def main():
     ops.ROI_ALIGN_PROFILE['timed'] = None
     ops.ROI_ALIGN_PROFILE['event_pool'] = []
     roi_timed_us = [1e3 * e[0].elapsed_time(e[1]) for e in timed_roi]
-    roi_span_us = [(int(e[2][1]) - int(e[2][0])) * 1e-2 for e in timed_roi]  # 10 ns ticks
+    roi_span_us = [span_of(e[2]) for e in timed_roi]
     assert torch.isfinite(loss).all()
     t_max = max_over_ranks(elapsed, dev, world)
 

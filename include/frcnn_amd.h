@@ -372,9 +372,12 @@ int32_t frh_roi_align_fwd_strided(int32_t num_levels, const float* const* feats,
 /* Measurement entry (bench.py's roofline line): frh_roi_align_fwd_strided with the forward
  * kernel launched through hipExtLaunchKernel, which binds the two caller-created hipEvent_t
  * to the dispatch's own start and end timestamps (no extra stream packets).  span (nullable,
- * device, 2 x u64, initialised to {UINT64_MAX, 0}): the kernel's own span on the GPU's
- * 100 MHz s_memrealtime clock -- the earliest wave start and the latest wave end (one lane
- * per wave records both with memory-side atomic min / max). */
+ * device, FRH_SPAN_SHARDS x FRH_SPAN_STRIDE u64, shard k's words {0, 1} initialised to
+ * {UINT64_MAX, 0}): the kernel's own span on the GPU's 100 MHz s_memrealtime clock -- the
+ * earliest wave start (min over shards of word 0) and the latest wave end (max of word 1);
+ * one lane per wave records both with memory-side atomic min / max on its workgroup's shard. */
+#define FRH_SPAN_SHARDS 256
+#define FRH_SPAN_STRIDE 16
 int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const float* const* feats,
                                         const int32_t* feat_hw, const int64_t* strides,
                                         const float* scales, int32_t batch, int32_t channels,

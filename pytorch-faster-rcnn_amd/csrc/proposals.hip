@@ -27,6 +27,7 @@ struct PropArgs {
   const float* reg[FRH_MAX_LEVELS];
   int64_t cst[FRH_MAX_LEVELS][4], rst[FRH_MAX_LEVELS][4];  // element strides (b, c, y, x)
   int nchw;  // every level contiguous [B, C*A, H, W]: flat indexing
+  int nhwc_cls;  // every level's cls output packed channels-last: anchor (a, cell) at cell * C*A + a
   int32_t h[FRH_MAX_LEVELS], w[FRH_MAX_LEVELS];
   int64_t off[FRH_MAX_LEVELS];
   int L, A, C;  // levels, anchors per location, cls channels (1 sigmoid, 2 softmax)
@@ -86,6 +87,30 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_keys_kernel(PropArgs p,
   tk_hist1_clear(h, 1 << kRpnHistBits);
   uint32_t* kk = const_cast<uint32_t*>(b.keys) + (int64_t)seg * b.ld;
   float x0[kTkPerThread], x1[kTkPerThread];  // every logit load in flight at once
+  if (p.nhwc_cls) {  // memory order (cell-major), keys stored at their anchor index
+    const float* cls = p.cls[l] + (int64_t)bi * p.cst[l][0];
+    const int CA = p.C * p.A, hw = p.h[l] * p.w[l];
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int m = (int)base + r * kTkThreads + threadIdx.x;
+      const int cell = (int)((uint32_t)m / (uint32_t)p.A), a = m - cell * p.A;
+      x0[r] = m < hwa ? cls[(int64_t)cell * CA + a] : 0.0f;
+      x1[r] = (p.C == 2 && m < hwa) ? cls[(int64_t)cell * CA + p.A + a] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      const int m = (int)base + r * kTkThreads + threadIdx.x;
+      const int cell = (int)((uint32_t)m / (uint32_t)p.A), a = m - cell * p.A;
+      uint32_t key = 0u;
+      if (m < hwa) {
+        key = float_key(score_of2(x0[r], x1[r], p.C));
+        kk[a * hw + cell] = key;
+      }
+      tk_hist_add(h, m < hwa, key >> (32 - kRpnHistBits));
+    }
+    tk_hist1_flush(h, 1 << kRpnHistBits, b.hist1 + (int64_t)seg * (1 << kRpnHistBits));
+    return;
+  }
   if (p.nchw) {
     const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
 #pragma unroll
@@ -299,13 +324,33 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
   uint32_t* gh2 = b.hist2 + (int64_t)seg * kTkBins2;
   constexpr int sh1 = 32 - kRpnHistBits, sh2 = sh1 - 12;
 
-  // ---- phase 1: keys (registers; an sc1 copy for the degenerate tie path) + first-level histogram
+  // ---- phase 1: keys (registers; an sc1 copy for the degenerate tie path) + first-level histogram.
+  // Register r of thread t holds memory position m = base + 256 r + t of the level: anchor m
+  // itself, or, for packed channels-last outputs (cell-major: m = cell * A + a), anchor
+  // a * H * W + cell -- coalesced logit loads; the anchor index rides along for the ties.
+  const int hw = p.h[l] * p.w[l];
+  auto anchor = [&](int r) -> int {
+    const int m = (int)base + r * kTkThreads + t;
+    if (!p.nhwc_cls) return m;
+    const int cell = (int)((uint32_t)m / (uint32_t)p.A);
+    return (m - cell * p.A) * hw + cell;
+  };
   uint32_t key[kTkPerThread];
   tk_hist1_clear(sm.h1, 1 << kRpnHistBits);
   if (has_keys) {
     float x0[kTkPerThread], x1[kTkPerThread];  // every logit load in flight at once
     const int64_t hwa = n;
-    if (p.nchw) {
+    if (p.nhwc_cls) {
+      const float* cls = p.cls[l] + (int64_t)bi * p.cst[l][0];
+      const int CA = p.C * p.A;
+#pragma unroll
+      for (int r = 0; r < kTkPerThread; ++r) {
+        const int m = (int)base + r * kTkThreads + t;
+        const int cell = (int)((uint32_t)m / (uint32_t)p.A), a = m - cell * p.A;
+        x0[r] = m < n ? cls[(int64_t)cell * CA + a] : 0.0f;
+        x1[r] = (p.C == 2 && m < n) ? cls[(int64_t)cell * CA + p.A + a] : 0.0f;
+      }
+    } else if (p.nchw) {
       const float* cls = p.cls[l] + (int64_t)bi * p.C * hwa;
 #pragma unroll
       for (int r = 0; r < kTkPerThread; ++r) {
@@ -324,10 +369,10 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     }
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r) {
-      const int64_t i = base + r * kTkThreads + t;
-      key[r] = i < hwa ? float_key(score_of2(x0[r], x1[r], p.C)) : 0u;
-      if (i < hwa) xwg_store(kk + i, key[r]);
-      tk_hist_add(sm.h1, i < hwa, key[r] >> sh1);
+      const int64_t m = base + r * kTkThreads + t;
+      key[r] = m < hwa ? float_key(score_of2(x0[r], x1[r], p.C)) : 0u;
+      if (m < hwa) xwg_store(kk + anchor(r), key[r]);
+      tk_hist_add(sm.h1, m < hwa, key[r] >> sh1);
     }
     tk_hist1_flush(sm.h1, 1 << kRpnHistBits, const_cast<uint32_t*>(gh1));
   } else {
@@ -377,13 +422,12 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     int c = slots.y;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r)
-      if (eq & (1u << r))
-        xwg_store(cand + c++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)(base + r * kTkThreads + t));
+      if (eq & (1u << r)) xwg_store(cand + c++, ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)anchor(r));
     int s = slots.x;
     const int gbase = sm.base, nsel = sm.tot_sel;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r)
-      if (sel & (1u << r)) sm.cand[s++ - gbase] = ((uint64_t)key[r] << 32) | (uint32_t)(base + r * kTkThreads + t);
+      if (sel & (1u << r)) sm.cand[s++ - gbase] = ((uint64_t)key[r] << 32) | (uint32_t)anchor(r);
     __syncthreads();
     for (int j = t; j < nsel; j += kTkThreads) {
       const uint64_t e = sm.cand[j];
@@ -823,6 +867,8 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
     const int64_t hw = (int64_t)p.h[l] * p.w[l];
     off += (int64_t)num_anchors * hw;
     for (int q = 0; q < 4; ++q) p.cst[l][q] = cls_strides[4 * l + q], p.rst[l][q] = reg_strides[4 * l + q];
+    p.nhwc_cls = (l == 0 || p.nhwc_cls) && p.cst[l][1] == 1 && p.cst[l][3] == (int64_t)cls_channels * num_anchors &&
+                 p.cst[l][2] == (int64_t)p.w[l] * cls_channels * num_anchors;
     p.nchw = p.nchw && p.cst[l][0] == (int64_t)cls_channels * num_anchors * hw && p.cst[l][1] == hw &&
              p.cst[l][2] == p.w[l] && p.cst[l][3] == 1 && p.rst[l][0] == (int64_t)4 * num_anchors * hw &&
              p.rst[l][1] == hw && p.rst[l][2] == p.w[l] && p.rst[l][3] == 1;

@@ -24,11 +24,14 @@ struct RoiCfg {
   unsigned long long* span;  // measurement builds (kSpan): {min wave start, max wave end}, s_memrealtime
 };
 
-// kSpan kernels: the launch's span on the 100 MHz clock, first wave start to last wave end
-// (one lane per wave: two memory-side atomics)
+// kSpan kernels: the launch's span on the 100 MHz clock, first wave start to last wave end.
+// One lane per wave makes two memory-side atomics on its shard (workgroup id mod
+// FRH_SPAN_SHARDS, one 128-B line each): ~64 waves per line instead of every wave of the
+// launch on one line (which serialises: ~11 ns per atomic, 360 us for a cfg2 launch).
 __device__ __forceinline__ void record_span(const RoiCfg& c, int64_t t_start) {
-  atomicMin(&c.span[0], (unsigned long long)t_start);
-  atomicMax(&c.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  unsigned long long* sh = c.span + (blockIdx.x % FRH_SPAN_SHARDS) * FRH_SPAN_STRIDE;
+  atomicMin(&sh[0], (unsigned long long)t_start);
+  atomicMax(&sh[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 struct Tap {

@@ -254,8 +254,8 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
 // barriers (seg_topk.h seg_barrier).  Workgroup x of image s owns boxes
 // [4096x, 4096x + 4096) (16 per thread, labels and keys in registers throughout):
 //   1. labels -> positive / negative keys (the same hashes), LDS histograms of
-//      their top 8 bits and the class counts, flushed by atomics;       barrier
-//   2. every workgroup reads the image's counts and histograms: kp, kn
+//      their top 8 bits and the class counts, stored per chunk;         barrier
+//   2. every workgroup sums the image's chunk counts and histograms: kp, kn
 //      (region.py:43-57) and both two-level plans (tk_plan_direct);
 //   3. its boxes above each plan's prefix are taken: output label and list slot
 //      (one reservation per class); its prefix ties go to the class's candidate
@@ -263,13 +263,15 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
 //      (only when a class has ties)
 //   4. workgroup 0 orders each class's ties by (key desc, box asc) and takes the
 //      first k2 (labels of all tied boxes, list slots of the taken ones);
-// then the last workgroup to leave zeroes the image's histograms and state words,
-// which is the workspace contract (frh_sample_zero_bytes: zero before, zero after).
+// then the last workgroup to leave zeroes the image's state words, which is the
+// workspace contract (frh_sample_zero_bytes: zero before, zero after).
 // The selected set is exactly the two-launch path's.
 constexpr int kSampFusedMaxWgs = 512;  // resident with margin (LDS: 4 workgroups per CU)
 
 struct SampFused {
-  uint32_t* hist;    // [S][2][kSampBins]   zero before and after
+  uint32_t* part_hist;   // [S][2][nchunk][kSampBins] per-chunk histograms (sc1 stores, every call)
+  int32_t* part_count;   // [S][2][nchunk] per-chunk class counts
+  int nchunk;
   int32_t* state;    // [S][2][TK_WORDS]     zero before and after (TK_ERR: sticky barrier error)
   uint64_t* cand;    // [S][2][ld] prefix ties: key << 32 | ~box
   int64_t ld;
@@ -294,7 +296,6 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   if (x >= G) return;
   int32_t* st = f.state + (int64_t)(2 * s) * TK_WORDS;  // [2][TK_WORDS]: positives, negatives
   int32_t* err = st + TK_ERR;
-  uint32_t* gh = f.hist + (int64_t)(2 * s) * kSampBins;  // [2][kSampBins]
   const int64_t* li = lab_in + (int64_t)s * lstride;
   int64_t* lo = lab_out ? lab_out + (int64_t)s * lstride : nullptr;
   const int base = x * kTkChunk;
@@ -324,23 +325,44 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
   cp = block_sum(cp, sm.part);
   cn = block_sum(cn, sm.part);
+  // this chunk's histograms and counts, write-through (one store per bin: no atomics on
+  // the 256 hot bins of an image, which every chunk's uniform keys fill)
+  uint32_t* ph = f.part_hist + (int64_t)(2 * s) * f.nchunk * kSampBins;  // [2][nchunk][bins]
+  int32_t* pc = f.part_count + (int64_t)(2 * s) * f.nchunk;               // [2][nchunk]
   if (t == 0) {
-    if (cp) atomicAdd(st + TK_N, cp);
-    if (cn) atomicAdd(st + TK_WORDS + TK_N, cn);
+    xwg_store(reinterpret_cast<uint32_t*>(pc) + x, (uint32_t)cp);
+    xwg_store(reinterpret_cast<uint32_t*>(pc) + f.nchunk + x, (uint32_t)cn);
   }
-  for (int i = t; i < 2 * kSampBins; i += kTkThreads) {
-    const uint32_t c = hc[i];
-    if (c) atomicAdd(gh + i, c);
-  }
+  for (int i = t; i < 2 * kSampBins; i += kTkThreads)
+    xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
   seg_barrier(st + TK_BAR1, G, err);
 
-  // ---- phase 2
-  const int npos = xwg_load(st + TK_N), nneg = xwg_load(st + TK_WORDS + TK_N);
+  // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
+  int sp0 = 0, sn0 = 0;
+  for (int c = t; c < G; c += kTkThreads) {
+    sp0 += xwg_load(pc + c);
+    sn0 += xwg_load(pc + f.nchunk + c);
+  }
+  uint32_t hp = 0u, hn = 0u;
+  for (int c0 = 0; c0 < G; c0 += 16) {
+    uint32_t a[16], b[16];  // 32 chunk loads in flight per step
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      a[c] = c0 + c < G ? xwg_load(ph + (int64_t)(c0 + c) * kSampBins + t) : 0u;
+      b[c] = c0 + c < G ? xwg_load(ph + ((int64_t)f.nchunk + c0 + c) * kSampBins + t) : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) hp += a[c], hn += b[c];
+  }
+  const int npos = block_sum(sp0, sm.part), nneg = block_sum(sn0, sm.part);
+  hc[t] = hp;
+  hc[kSampBins + t] = hn;
+  __syncthreads();
   const int kp = npos < pos_num ? npos : pos_num;
   const int kn = nneg < max_num - kp ? nneg : max_num - kp;
   TkPlan pl[2];
-  pl[0] = tk_plan_direct(kSampHistBits, kp, sm, [&](int i) { return xwg_load(gh + i); });
-  pl[1] = tk_plan_direct(kSampHistBits, kn, sm, [&](int i) { return xwg_load(gh + kSampBins + i); });
+  pl[0] = tk_plan_direct(kSampHistBits, kp, sm, [&](int i) { return hc[i]; });
+  pl[1] = tk_plan_direct(kSampHistBits, kn, sm, [&](int i) { return hc[kSampBins + i]; });
 
   // ---- phase 3 (the plans' fields by select, not by a per-box array index)
   uint32_t take = 0u, tie = 0u;
@@ -443,10 +465,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   __syncthreads();
   if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
   __syncthreads();
-  if (sm.last) {
-    for (int i = t; i < 2 * kSampBins; i += kTkThreads) xwg_store(gh + i, 0u);
-    if (t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
-  }
+  if (sm.last && t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
 }
 
 // Small images (num_boxes <= kSsMax, e.g. the RCNN stage's ~2000 proposal rows): the whole
@@ -631,13 +650,9 @@ struct SampLayout {
   int nchunk;
 };
 
-// The leading zero region (frh_sample_zero_bytes): the one-launch sampler's histograms
-// [V][kSampBins] and state words [V][TK_WORDS]; the rest follows it.
-static size_t samp_zero_hist(int32_t S) { return 0; }
-static size_t samp_zero_state(int32_t S) { return al256((size_t)2 * S * kSampBins * sizeof(uint32_t)); }
-static size_t samp_zero_bytes(int32_t S) {
-  return al256(samp_zero_state(S) + (size_t)2 * S * TK_WORDS * sizeof(int32_t));
-}
+// The leading zero region (frh_sample_zero_bytes): the one-launch sampler's state words
+// [V][TK_WORDS]; the rest follows it.
+static size_t samp_zero_bytes(int32_t S) { return al256((size_t)2 * S * TK_WORDS * sizeof(int32_t)); }
 
 static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   SampLayout z{};
@@ -734,9 +749,9 @@ int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int6
   SampLayout z = samp_layout(num_segs, max_boxes);
   const int V = 2 * num_segs;
   if (!two_launches && (int64_t)num_segs * z.nchunk <= kSampFusedMaxWgs) {
-    SampFused f{reinterpret_cast<uint32_t*>(ws + samp_zero_hist(num_segs)),
-                reinterpret_cast<int32_t*>(ws + samp_zero_state(num_segs)), reinterpret_cast<uint64_t*>(ws + z.cand),
-                z.kld, sel, (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
+    SampFused f{reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
+                reinterpret_cast<int32_t*>(ws), reinterpret_cast<uint64_t*>(ws + z.cand), z.kld, sel,
+                (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
     hipLaunchKernelGGL(sampler_fused_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
                        labels_in, label_seg_stride, num_boxes, max_num, pos_num, seed, f, labels_out);
     return check_launch("frh_sample_random");

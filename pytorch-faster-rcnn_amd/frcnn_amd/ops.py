@@ -645,9 +645,11 @@ def _feat_desc(feats):
 # feature tensors only to replay the same launch shape for timing; with a graphed
 # trunk they alias the graph's output buffers, so a replay reads the newest step's
 # values -- never use a record's features for their contents.
-ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True, 'timed': None, 'event_pool': []}
+ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True, 'timed': None, 'event_pool': [], 'launches': 0}
+# 'launches': forward launches so far in this process (tools/roi_dispatch_table.py matches
+# them to rocprofv3's dispatches by order).
 # 'timed': a list -> each forward launch takes a (start, end, span) triple from 'event_pool'
-# (created beforehand; span = a device u64[2] set to {UINT64_MAX, 0}), goes through
+# (created beforehand; span = device span shards, bench.span_slots), goes through
 # frh_roi_align_fwd_strided_timed (the events are bound to the kernel's own dispatch
 # timestamps, the span is the kernel's own first-wave-start / last-wave-end on the 100 MHz
 # GPU clock: nothing is added to the stream) and appends the triple.
@@ -663,6 +665,7 @@ class _RoIAlignMulti(torch.autograd.Function):
         ph, pw = output_size
         out = torch.empty(K, C, ph, pw, dtype=torch.float32, device=rois.device)
         hw, st = _feat_desc(feats)
+        ROI_ALIGN_PROFILE['launches'] += 1
         prof = ROI_ALIGN_PROFILE['on']
         e0 = e1 = None
         if prof and ROI_ALIGN_PROFILE['events']:

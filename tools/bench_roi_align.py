@@ -39,6 +39,8 @@ def calibrate(variants, dev, small=False):
     print('calibration: feature bytes', C * S * S * 4, 'output bytes', C * 49 * 4, flush=True)
     for v in variants:
         feats = [torch.randn(1, C, S, S, device=dev)]
+        if v in NHWC:
+            feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
         hw, st = ops._feat_desc(feats)
         out = torch.empty(1, C, 7, 7, device=dev)
         ws = torch.empty(64, dtype=torch.uint8, device=dev)

@@ -44,7 +44,7 @@ def main():
     ap.add_argument('trace_dir')
     ap.add_argument('--warmup', type=int, required=True)
     ap.add_argument('--steps', type=int, required=True)
-    ap.add_argument('--marker', default='roi_align_fwd_pair_kernel')
+    ap.add_argument('--marker', default='roi_align_fwd')
     ap.add_argument('--out', default=None)
     args = ap.parse_args()
 
