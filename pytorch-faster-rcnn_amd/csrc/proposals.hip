@@ -42,6 +42,7 @@ struct PropArgs {
   uint64_t* sel_keys;  // [S][P] selection records (RpnPol)
   float4* stage;       // [S][kRpnSelFused] boxes decoded at selection (fused path)
   int32_t* sel_count; // [S]
+  int64_t* stamps;    // tools timing only (null in the product): rpn_select_kernel phase times
 };
 
 struct ImgArgs {
@@ -64,6 +65,13 @@ __device__ __forceinline__ int64_t rpn_elem(const int64_t (&st)[4], int A, int H
   const uint32_t hw = (uint32_t)H * (uint32_t)W, u = (uint32_t)i, a = u / hw, sp = u - a * hw;
   const uint32_t y = sp / (uint32_t)W, x = sp - y * (uint32_t)W;
   return (int64_t)b * st[0] + (int64_t)(c * A + (int)a) * st[1] + (int64_t)y * st[2] + (int64_t)x * st[3];
+}
+
+// logit c (0, or 1 for the second softmax channel; 0 when C == 1) of anchor i of level l,
+// image b, any layout (the degenerate tie path's keys, recomputed)
+__device__ __forceinline__ float rpn_logit(const PropArgs& p, int l, int b, int c, int i) {
+  if (c >= p.C) return 0.0f;
+  return p.cls[l][rpn_elem(p.cst[l], p.A, p.h[l], p.w[l], b, c, i)];
 }
 
 constexpr int kRpnHistBits = 12;
@@ -314,17 +322,22 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
   const int n = p.A * p.h[l] * p.w[l];
   const int G = rpn_sel_groups(n, p.pre_nms);
   if (x >= G) return;
+  // tools timing build (p.stamps non-null): 16 int64 per workgroup, s_memrealtime at the phases
+  auto stamp = [&](int q) {
+    if (p.stamps && t == 0)
+      p.stamps[((int64_t)seg * gridDim.x + x) * 16 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int k = rpn_k(p, n);
   int32_t* st = b.state + seg * TK_WORDS;
   int32_t* err = st + TK_ERR;
   const int64_t base = (int64_t)x * kTkChunk;
   const bool has_keys = base < n;
-  uint32_t* kk = const_cast<uint32_t*>(b.keys) + (int64_t)seg * b.ld;
   const uint32_t* gh1 = b.hist1 + (int64_t)seg * (1 << kRpnHistBits);
   uint32_t* gh2 = b.hist2 + (int64_t)seg * kTkBins2;
   constexpr int sh1 = 32 - kRpnHistBits, sh2 = sh1 - 12;
 
-  // ---- phase 1: keys (registers; an sc1 copy for the degenerate tie path) + first-level histogram.
+  // ---- phase 1: keys (registers only: the degenerate tie path recomputes them) + first-level histogram.
   // Register r of thread t holds memory position m = base + 256 r + t of the level: anchor m
   // itself, or, for packed channels-last outputs (cell-major: m = cell * A + a), anchor
   // a * H * W + cell -- coalesced logit loads; the anchor index rides along for the ties.
@@ -371,7 +384,6 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     for (int r = 0; r < kTkPerThread; ++r) {
       const int64_t m = base + r * kTkThreads + t;
       key[r] = m < hwa ? float_key(score_of2(x0[r], x1[r], p.C)) : 0u;
-      if (m < hwa) xwg_store(kk + anchor(r), key[r]);
       tk_hist_add(sm.h1, m < hwa, key[r] >> sh1);
     }
     tk_hist1_flush(sm.h1, 1 << kRpnHistBits, const_cast<uint32_t*>(gh1));
@@ -379,12 +391,15 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r) key[r] = 0u;
   }
+  stamp(1);
   seg_barrier(st + TK_BAR1, G, err);
+  stamp(2);
 
   // ---- phase 2: bucket b1 (every workgroup reads the same final histogram), then b2
   tk_find(sm, 1 << kRpnHistBits, k > 0 ? k : 1, [&](int i) { return xwg_load(gh1 + i); });
   const bool all = k <= 0 || sm.tot <= k;
   TkPlan plan{all, k <= 0 ? 0 : (all ? sm.tot : k), 0u, sh2, 0};
+  stamp(3);
   if (!all) {
     const uint32_t b1 = (uint32_t)sm.bin;
     const int k1 = k - sm.above;
@@ -400,12 +415,15 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
         if (c) atomicAdd(&gh2[i], c);
       }
     }
+    stamp(4);
     seg_barrier(st + TK_BAR2, G, err);
+    stamp(5);
     tk_find(sm, kTkBins2, k1, [&](int i) { return xwg_load(gh2 + i); });
     plan.P = (b1 << 12) | (uint32_t)sm.bin;
     plan.k2 = k1 - sm.above;
   }
   const int kv = plan.kv, k2 = all ? 0 : plan.k2, nabove = kv - k2;
+  stamp(6);
 
   // ---- phase 3: collect from the registers; selections decoded by the selecting workgroup
   RpnPol pol{p, ia, b, seg, true};
@@ -419,6 +437,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       eq |= (key[r] != 0u && !all && pre == plan.P) ? 1u << r : 0u;
     }
     const int2 slots = block_reserve2(__popc(sel), __popc(eq), &st[TK_OUT], sm.part, &sm.base, &sm.cbase);
+    stamp(7);
     int c = slots.y;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r)
@@ -434,7 +453,9 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       pol.select((int)(uint32_t)e, (uint32_t)(e >> 32), gbase + j);
     }
   }
+  stamp(8);
   seg_barrier(st + TK_BAR3, G, err);
+  stamp(9);
 
   // ---- phase 4: every record of the segment in LDS (the prefix ties ordered here)
   uint64_t* tie = sm.cand;                 // [kRpnTieCap], later the live-masked records
@@ -446,8 +467,10 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     // prefix (lowest index first among equal keys), then one more barrier
     if (x == 0) {
       int32_t* idx = reinterpret_cast<int32_t*>(cand);  // the consumed candidate row
+      auto key_at = [&](int i) -> uint32_t { return float_key(score_of2(rpn_logit(p, l, bi, 0, i),
+                                                                        rpn_logit(p, l, bi, 1, i), p.C)); };
       auto key_of = [&](int i) -> uint32_t {
-        const uint32_t kq = xwg_load(kk + i);
+        const uint32_t kq = key_at(i);
         return (kq >> plan.sh) == plan.P ? kq : 0u;
       };
       block_topk_select(key_of, n, k2, idx, sm.fb);
@@ -455,7 +478,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
         const int i = idx[j];
         const float4 bx = rpn_decode_one(p, ia, seg, i);
         xwg_store(const_cast<uint64_t*>(grec) + nabove + j,
-                  rpn_record(xwg_load(kk + i), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j));
+                  rpn_record(key_at(i), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j));
       }
     }
     seg_barrier(st + TK_BAR4, G, err);
@@ -466,7 +489,9 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       const int P2 = next_pow2(ncand > 1 ? ncand : 1);
       for (int j = t; j < P2; j += kTkThreads) tie[j] = j < ncand ? xwg_load(cand + j) : 0ull;
       __syncthreads();
+      stamp(10);
       block_bitonic_sort_desc(tie, P2);
+      stamp(11);
       for (int j = t; j < k2; j += kTkThreads) {
         const uint64_t e = tie[j];
         const int i = (int)~(uint32_t)e;
@@ -478,8 +503,9 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
   __syncthreads();
 
   // ---- phase 5: order by counting (rpn_rank_kernel's rule) over the live-masked records
-  const int kv16 = (kv + 15) & ~15;
-  for (int j = t; j < kv16; j += kTkThreads) {
+  stamp(12);
+  const int kv32 = (kv + 31) & ~31;  // padding records are 0: never above
+  for (int j = t; j < kv32; j += kTkThreads) {
     const uint64_t r = j < kv ? rec[j] : 0ull;
     tie[j] = ((r >> 11) & 1u) ? r : 0ull;
   }
@@ -490,17 +516,27 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     c = block_sum(c, sm.part);
     if (t == 0) p.sel_count[seg] = c;
   }
-  const int lane8 = t & 7;
+  // four threads per record (this workgroup's kSelRankPer records in one pass), each counting
+  // a quarter of the records: 16-B LDS reads (a record pair), four in flight per iteration
+  static_assert(kSelRankPer * 4 == kTkThreads, "one pass");
+  const int lane4 = t & 3;
   const uint64_t* stage = reinterpret_cast<const uint64_t*>(p.stage + (int64_t)seg * kRpnSelFused);
-  for (int q0 = x * kSelRankPer; q0 < min(kv, x * kSelRankPer + kSelRankPer); q0 += kTkThreads / 8) {
-    const int q = q0 + (t >> 3);
+  if (x * kSelRankPer < kv) {
+    const int q = x * kSelRankPer + (t >> 2);
     const uint64_t me = q < kv ? rec[q] : ~0ull;
-    int above = 0;
-    for (int j = 2 * lane8; j < kv16; j += 16) above += (tie[j] > me ? 1 : 0) + (tie[j + 1] > me ? 1 : 0);
+    const ulonglong2* tv = reinterpret_cast<const ulonglong2*>(tie);
+    int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int j = lane4; j < kv32 / 2; j += 16) {
+      const ulonglong2 v0 = tv[j], v1 = tv[j + 4], v2 = tv[j + 8], v3 = tv[j + 12];
+      a0 += (v0.x > me ? 1 : 0) + (v0.y > me ? 1 : 0);
+      a1 += (v1.x > me ? 1 : 0) + (v1.y > me ? 1 : 0);
+      a2 += (v2.x > me ? 1 : 0) + (v2.y > me ? 1 : 0);
+      a3 += (v3.x > me ? 1 : 0) + (v3.y > me ? 1 : 0);
+    }
+    int above = (a0 + a1) + (a2 + a3);
     above += __shfl_xor(above, 1, kWave);
     above += __shfl_xor(above, 2, kWave);
-    above += __shfl_xor(above, 4, kWave);
-    if (lane8 == 0 && q < kv && ((me >> 11) & 1u)) {
+    if (lane4 == 0 && q < kv && ((me >> 11) & 1u)) {
       const int slot = (int)(me & 0x7ffu);
       float4 bx;
       if (slot < nabove) {
@@ -514,6 +550,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       p.sel_scores[(int64_t)seg * p.P + above] = key_float((uint32_t)(me >> 32));
     }
   }
+  stamp(13);
 }
 
 // ... and one 1024-thread block per segment orders them by (score desc, index
@@ -722,7 +759,7 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
                            float* out_boxes, float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
-                           void* stream, bool select_launches);
+                           void* stream, bool select_launches, int64_t* select_stamps = nullptr);
 
 struct PropLayout {
   int P;
@@ -840,7 +877,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
                                 int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream,
-                                bool select_launches) {
+                                bool select_launches, int64_t* select_stamps) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
@@ -890,6 +927,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   p.sel_keys = reinterpret_cast<uint64_t*>(ws + z.idx);
   p.stage = reinterpret_cast<float4*>(ws + z.stage);
   p.sel_count = reinterpret_cast<int32_t*>(ws + z.cnt);
+  p.stamps = select_stamps;
   // per-image sizes travel by value in the kernel arguments
   ImgArgs ia{};
   for (int b = 0; b < num_imgs; ++b) {

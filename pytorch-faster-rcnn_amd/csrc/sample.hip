@@ -278,6 +278,7 @@ struct SampFused {
   int32_t* sel;      // nullable: [S][2][sel_ld]
   int64_t sel_ld;
   int32_t* sel_cnt;  // [S][2]
+  int64_t* stamps;   // tools timing only (null in the product): 16 int64 per workgroup
 };
 
 __device__ __forceinline__ uint32_t samp_key(uint64_t seed, int v, int i, bool cand) {
@@ -294,6 +295,11 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   const int n = num[s];
   const int G = n > kTkChunk ? (n + kTkChunk - 1) / kTkChunk : 1;
   if (x >= G) return;
+  auto stamp = [&](int q) {
+    if (f.stamps && t == 0)
+      f.stamps[((int64_t)s * gridDim.x + x) * 16 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   int32_t* st = f.state + (int64_t)(2 * s) * TK_WORDS;  // [2][TK_WORDS]: positives, negatives
   int32_t* err = st + TK_ERR;
   const int64_t* li = lab_in + (int64_t)s * lstride;
@@ -323,6 +329,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     cp += pos;
     cn += neg;
   }
+  stamp(1);
   cp = block_sum(cp, sm.part);
   cn = block_sum(cn, sm.part);
   // this chunk's histograms and counts, write-through (one store per bin: no atomics on
@@ -335,24 +342,26 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
   for (int i = t; i < 2 * kSampBins; i += kTkThreads)
     xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
+  stamp(2);
   seg_barrier(st + TK_BAR1, G, err);
+  stamp(3);
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
+  // the count loads (threads < G) and the first 2 x 32 chunk-histogram loads are issued together
   int sp0 = 0, sn0 = 0;
-  for (int c = t; c < G; c += kTkThreads) {
-    sp0 += xwg_load(pc + c);
-    sn0 += xwg_load(pc + f.nchunk + c);
-  }
   uint32_t hp = 0u, hn = 0u;
-  for (int c0 = 0; c0 < G; c0 += 16) {
-    uint32_t a[16], b[16];  // 32 chunk loads in flight per step
+  for (int c0 = 0; c0 < G; c0 += 32) {
+    uint32_t a[32], b[32];
+    const int cc = c0 + t;
+    const int32_t cpv = cc < G && t < 32 ? xwg_load(pc + cc) : 0, cnv = cc < G && t < 32 ? xwg_load(pc + f.nchunk + cc) : 0;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < 32; ++c) {
       a[c] = c0 + c < G ? xwg_load(ph + (int64_t)(c0 + c) * kSampBins + t) : 0u;
       b[c] = c0 + c < G ? xwg_load(ph + ((int64_t)f.nchunk + c0 + c) * kSampBins + t) : 0u;
     }
+    sp0 += cpv, sn0 += cnv;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) hp += a[c], hn += b[c];
+    for (int c = 0; c < 32; ++c) hp += a[c], hn += b[c];
   }
   const int npos = block_sum(sp0, sm.part), nneg = block_sum(sn0, sm.part);
   hc[t] = hp;
@@ -363,6 +372,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   TkPlan pl[2];
   pl[0] = tk_plan_direct(kSampHistBits, kp, sm, [&](int i) { return hc[i]; });
   pl[1] = tk_plan_direct(kSampHistBits, kn, sm, [&](int i) { return hc[kSampBins + i]; });
+  stamp(4);
 
   // ---- phase 3 (the plans' fields by select, not by a per-box array index)
   uint32_t take = 0u, tie = 0u;
@@ -376,12 +386,13 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     take |= (live && (all || pre > P)) ? 1u << r : 0u;
     tie |= (live && !all && pre == P) ? 1u << r : 0u;
   }
+  // both classes' (selection, candidate) slots in one round trip
+  const int4 sl4 = block_reserve4(__popc(take & posm), __popc(tie & posm), __popc(take & negm), __popc(tie & negm),
+                                  st + TK_OUT, st + TK_WORDS + TK_OUT, sm.part, sm.res4);
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const uint32_t m = c ? negm : posm;
-    const int2 slots = block_reserve2(__popc(take & m), __popc(tie & m), st + c * TK_WORDS + TK_OUT, sm.part,
-                                      &sm.base, &sm.cbase);
-    int sp = slots.x, cq = slots.y;
+    int sp = c ? sl4.z : sl4.x, cq = c ? sl4.w : sl4.y;
     int32_t* sl = f.sel ? f.sel + (int64_t)(2 * s + c) * f.sel_ld : nullptr;
     uint64_t* cl = f.cand + (int64_t)(2 * s + c) * f.ld;
 #pragma unroll
@@ -404,11 +415,14 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     }
   }
   const bool ties = (pl[0].kv > 0 && !pl[0].all) || (pl[1].kv > 0 && !pl[1].all);
+  stamp(5);
   if (ties) seg_barrier(st + TK_BAR2, G, err);
+  stamp(6);
 
-  // ---- phase 4 (workgroup 0): the prefix ties
-  if (x == 0) {
-    for (int c = 0; c < 2; ++c) {
+  // ---- phase 4: the prefix ties, positives by workgroup 0, negatives by workgroup 1 (0 if alone)
+  for (int c = 0; c < 2; ++c) {
+    if (x != (c < G ? c : 0)) continue;
+    {
       const int v = 2 * s + c, kv = pl[c].kv;
       if (f.sel_cnt && t == 0) f.sel_cnt[v] = kv;
       if (kv == 0 || pl[c].all) continue;
@@ -417,14 +431,19 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
       const uint64_t* cl = f.cand + (int64_t)v * f.ld;
       const int ncand = xwg_load(st + c * TK_WORDS + TK_CAND);
       if (ncand <= kTkCandCap) {
-        const int P2 = next_pow2(ncand > 1 ? ncand : 1);
-        for (int j = t; j < P2; j += kTkThreads) sm.cand[j] = j < ncand ? xwg_load(cl + j) : 0ull;
+        // the k2 largest (key, ~box) of the prefix ties by radix passes over the key's
+        // next bits (its top kSampHistBits are the plan's prefix): no sort
+        for (int j = t; j < ncand; j += kTkThreads) sm.cand[j] = xwg_load(cl + j);
+        if (t == 0) sm.fb.cnt_gt = 0;
         __syncthreads();
-        block_bitonic_sort_desc(sm.cand, P2);
+        const LdsCut cut = lds_topk_cut(sm.cand, ncand, k2, 64 - kSampHistBits,
+                                        (uint64_t)pl[c].P << (64 - kSampHistBits), sm);
         for (int j = t; j < ncand; j += kTkThreads) {
-          const int i = (int)~(uint32_t)sm.cand[j];
-          if (lo) lo[i] = j < k2 ? li[i] : -1;
-          if (sl && j < k2) sl[nabove + j] = i;
+          const uint64_t e = sm.cand[j];
+          const int i = (int)~(uint32_t)e;
+          const bool tk = (e >> cut.sh) >= (cut.P >> cut.sh);
+          if (lo) lo[i] = tk ? li[i] : -1;
+          if (sl && tk) sl[nabove + atomicAdd(&sm.fb.cnt_gt, 1)] = i;
         }
         __syncthreads();  // sm.cand reused by the other class
       } else {
@@ -461,11 +480,13 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
 
   // ---- exit: the last workgroup out leaves the image's zero region zero
+  stamp(7);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
   __syncthreads();
   if (sm.last && t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
+  stamp(8);
 }
 
 // Small images (num_boxes <= kSsMax, e.g. the RCNN stage's ~2000 proposal rows): the whole
@@ -636,7 +657,7 @@ size_t compact_workspace(int32_t S, int64_t max_n) {
 int32_t sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                            const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                            uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, void* workspace,
-                           size_t ws_bytes, void* stream, bool two_launches);
+                           size_t ws_bytes, void* stream, bool two_launches, int64_t* stamps = nullptr);
 
 }  // namespace frh
 
@@ -728,7 +749,8 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
 int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                 const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                                 uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,
-                                void* workspace, size_t ws_bytes, void* stream, bool two_launches) {
+                                void* workspace, size_t ws_bytes, void* stream, bool two_launches,
+                                int64_t* stamps) {
   FRH_REQUIRE(num_segs >= 0 && max_boxes >= 0, "negative sizes");
   FRH_REQUIRE(pos_num <= max_num && pos_num >= 0, "pos_num must be in [0, max_num]");
   if (num_segs == 0 || max_boxes == 0) return FRH_OK;
@@ -751,7 +773,7 @@ int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int6
   if (!two_launches && (int64_t)num_segs * z.nchunk <= kSampFusedMaxWgs) {
     SampFused f{reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
                 reinterpret_cast<int32_t*>(ws), reinterpret_cast<uint64_t*>(ws + z.cand), z.kld, sel,
-                (int64_t)(max_num > 0 ? max_num : 1), sel_counts};
+                (int64_t)(max_num > 0 ? max_num : 1), sel_counts, stamps};
     hipLaunchKernelGGL(sampler_fused_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
                        labels_in, label_seg_stride, num_boxes, max_num, pos_num, seed, f, labels_out);
     return check_launch("frh_sample_random");

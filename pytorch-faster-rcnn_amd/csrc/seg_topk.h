@@ -161,6 +161,42 @@ __device__ __forceinline__ int2 block_reserve2(int nsel, int ncand, int* c, int*
   return make_int2(sh[0] + (ex & 0xffff), *cb + (ex >> 16));
 }
 
+// Two block_reserve2 reservations (counter pairs c0 and c1, each 8-byte aligned) in one
+// round trip: both 64-bit atomics issued by thread 0 before either result is used.  Returns
+// the first (selection, candidate) slots of this thread in list 0 (.x, .y) and list 1 (.z, .w).
+__device__ __forceinline__ int4 block_reserve4(int nsel0, int ncand0, int nsel1, int ncand1, int* c0, int* c1,
+                                               int* part, int* sh) {
+  const int t = threadIdx.x, w = t / kWave, nw = (int)blockDim.x / kWave;
+  __syncthreads();  // part / sh free
+  int a = nsel0 | (ncand0 << 16), b = nsel1 | (ncand1 << 16);
+  int ia = a, ib = b;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+    if (lane_id() >= o) ia += xa, ib += xb;
+  }
+  if (lane_id() == kWave - 1) part[w] = ia, part[nw + w] = ib;
+  __syncthreads();
+  int pa = 0, ta = 0, pb = 0, tb = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int va = part[i], vb = part[nw + i];
+    pa += i < w ? va : 0;
+    ta += va;
+    pb += i < w ? vb : 0;
+    tb += vb;
+  }
+  if (t == 0) {
+    auto pack = [](int tot) { return ((unsigned long long)((uint32_t)tot >> 16) << 32) | ((uint32_t)tot & 0xffffu); };
+    const unsigned long long oa = ta ? atomicAdd(reinterpret_cast<unsigned long long*>(c0), pack(ta)) : 0ull;
+    const unsigned long long ob = tb ? atomicAdd(reinterpret_cast<unsigned long long*>(c1), pack(tb)) : 0ull;
+    sh[0] = (int)(uint32_t)oa, sh[1] = (int)(uint32_t)(oa >> 32);
+    sh[2] = (int)(uint32_t)ob, sh[3] = (int)(uint32_t)(ob >> 32);
+  }
+  __syncthreads();
+  const int ea = pa + ia - a, eb = pb + ib - b;
+  return make_int4(sh[0] + (ea & 0xffff), sh[1] + (ea >> 16), sh[2] + (eb & 0xffff), sh[3] + (eb >> 16));
+}
+
 // --------------------------------------------- first-level histogram (keys)
 // The key kernels build it per chunk: clear, add, flush (block-uniform calls).
 __device__ __forceinline__ void tk_hist1_clear(uint32_t* h, int bins) {
@@ -176,7 +212,7 @@ __device__ __forceinline__ void tk_hist1_flush(const uint32_t* h, int bins, uint
 }
 
 // ------------------------------------------------------------ select state
-struct TkSmem {
+struct alignas(16) TkSmem {  // 16-B aligned: the fused selection reads record pairs with ds_read_b128
   union {
     struct {
       uint32_t h1[4096];
@@ -185,10 +221,11 @@ struct TkSmem {
     uint64_t cand[kTkCandCap];
   };
   TopkSmem fb;
-  int part[kTkThreads / kWave];
+  int part[2 * kTkThreads / kWave];
   int last, bin, above, tot, ncand;
   int base, tot_sel;  // block_reserve's (first slot, count); adjacent
   int cbase;          // block_reserve2's first candidate slot
+  int res4[4];        // block_reserve4's first slots
 };
 
 // Suffix search over 2^hb bins (highest first), 256 threads: sm.bin / sm.above
@@ -285,6 +322,40 @@ __device__ __forceinline__ void seg_barrier(int32_t* counter, int target, int32_
     }
   }
   __syncthreads();
+}
+
+// ------------------------------------------------- top-k of a small LDS list
+// The k largest (1 <= k <= n) of n DISTINCT u64 values v[0..n) in LDS whose bits above
+// `top` all equal those of P0: radix passes of 8 bits downwards from `top`, each an LDS
+// histogram (sm.fb.hist) of the values still matching the prefix + tk_find, stopping as soon
+// as the bin holding the k-th value is taken whole.  v is taken iff (v >> sh) >= (P >> sh).
+// No sort: a few passes where a bitonic network over n takes log2(n)^2 / 2 barriers.
+struct LdsCut {
+  uint64_t P;
+  int sh;
+};
+
+__device__ LdsCut lds_topk_cut(const uint64_t* v, int n, int k, int top, uint64_t P0, TkSmem& sm) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  uint64_t P = P0;
+  int krem = k;
+  for (int sh = top - 8; sh >= 0; sh -= 8) {
+    for (int i = t; i < 256; i += nt) sm.fb.hist[i] = 0u;
+    __syncthreads();
+    for (int j = t; j < n; j += nt) {
+      const uint64_t x = v[j];
+      if ((x >> (sh + 8)) == (P >> (sh + 8))) atomicAdd(&sm.fb.hist[(x >> sh) & 255u], 1u);
+    }
+    __syncthreads();
+    tk_find(sm, 256, krem, [&](int i) { return sm.fb.hist[i]; });
+    const int b = sm.bin, above = sm.above;
+    const int cnt = (int)sm.fb.hist[b];
+    __syncthreads();  // hist / bin read by every thread before the next pass
+    P |= (uint64_t)b << sh;
+    krem -= above;
+    if (cnt == krem) return LdsCut{P, sh};
+  }
+  return LdsCut{P, 0};
 }
 
 // ------------------------------------------------------------- refine launch
