@@ -478,8 +478,11 @@ struct PairLane {
   uint32_t tb0[2][2], tdq[2], tdr[2];
 };
 
-// kUnit: bytes of one cell's entry in a slab region (8: a channel pair; 16: a quad)
-template <int kUnit = 8>
+// kUnit: bytes of one cell's entry in a slab region (8: a channel pair; 16: a quad).
+// kSwz (quad slabs): slab column of window column q is q + q / 8 -- one hole per 8 units --
+// so the 16-B tap reads of bins two columns apart (c and c + 8 units) fall on different
+// LDS bank groups (ds_read_b128 serves 8 lanes per cycle over 8 groups of 4 banks).
+template <int kUnit = 8, bool kSwz = false>
 __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c, const RoiRaw& raw, int lane,
                                            PairGeom& G, PairLane& P) {
   constexpr int SR = 2;
@@ -515,7 +518,9 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
   G.dx = dx;
   G.R = dy ? y1 - y0 + 1 : nly;
   G.Cs = dx ? x1 - x0 + 1 : nlx;
-  G.Cs2 = G.Cs | 1;  // slab row stride: odd, so the b64 tap reads of a wave spread over the banks
+  auto pc = [](int q) { return kSwz ? q + (q >> 3) : q; };
+  // slab row stride: odd, so the tap reads of a wave spread over the banks
+  G.Cs2 = kSwz ? ((pc(G.Cs - 1) + 1) | 1) : (G.Cs | 1);
   // feature byte offsets of slab row / column `lane`
   P.rsrc = (dy ? y0 + min(lane, G.R - 1) : (yrow >= 0 ? yrow : y0)) * G.sy * 4;
   P.csrc = (dx ? x0 + min(lane, G.Cs - 1) : (xcol >= 0 ? xcol : x0)) * G.sx * 4;
@@ -537,9 +542,9 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
       if (iy == 0) {
         P.fxh[ix] = b.valid ? b.h : 0.f;
         P.fxl[ix] = b.valid ? b.l : 0.f;
-        P.tdq[ix] = (uint32_t)kUnit * (uint32_t)(q1 - q0);
+        P.tdq[ix] = (uint32_t)kUnit * (uint32_t)(pc(q1) - pc(q0));
       }
-      P.tb0[iy][ix] = (a.valid && b.valid) ? (uint32_t)kUnit * (uint32_t)(r0 * G.Cs2 + q0) : 0u;
+      P.tb0[iy][ix] = (a.valid && b.valid) ? (uint32_t)kUnit * (uint32_t)(r0 * G.Cs2 + pc(q0)) : 0u;
     }
   }
   G.base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
@@ -768,24 +773,24 @@ __device__ __forceinline__ f32x4 quad_val(const float (&w)[4], const f32x4* x) {
 // kQW: channel quads per item (4: 16 channels).  kOut: 0 = per-channel 4-B stores of the
 // bin row (lane = bin), 1 = [channel][bin] staged in LDS (obuf), then 16-B stores of the
 // item's contiguous output block, 2 = no stores (tools-only diagnostic).
-template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0>
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, bool kSwz = false>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf);
 
-template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0>
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, bool kSwz = false>
 __device__ __forceinline__ void quad_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane,
                                           float* obuf = nullptr) {
   PairGeom G;
   PairLane P;
   const RoiRaw raw = roi_fetch(c, k);
-  pair_setup<16>(lv, c, raw, lane, G, P);
-  quad_body<kStAux, kStamp, kQW, kOut>(G, P, c, out, k, chunk, item, sbase, t_start, lane, obuf);
+  pair_setup<16, kSwz>(lv, c, raw, lane, G, P);
+  quad_body<kStAux, kStamp, kQW, kOut, kSwz>(G, P, c, out, k, chunk, item, sbase, t_start, lane, obuf);
 }
 
 // the item after its setup (G, P): staging, evaluation, stores
-template <int kStAux, bool kStamp, int kQW, int kOut>
+template <int kStAux, bool kStamp, int kQW, int kOut, bool kSwz>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf) {
@@ -837,7 +842,8 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
     auto goff_at = [&](int j) {
       int e = j * kWave + lane;
       e = e < ncell ? e : 0;
-      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
+      const int r = (int)(((uint32_t)e * inv) >> 16), pcol = e - r * Cs2;
+      const int col = min(kSwz ? pcol - pcol / 9 : pcol, Cs - 1);  // kSwz holes load a neighbour
       return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave);
     };
     int goff[RP];
@@ -927,8 +933,10 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
         for (int ix = 0; ix < SR; ++ix) {
           // slab offsets -> feature offsets: slab cell (r, col) = tap-list / window entry
           const uint32_t t0 = P.tb0[iy][ix] / 16u;
-          const int r0 = (int)(t0 / (uint32_t)Cs2), c0 = (int)(t0 - (uint32_t)r0 * (uint32_t)Cs2);
-          const int r1 = r0 + (int)(P.tdr[iy] / 16u / (uint32_t)Cs2), c1 = c0 + (int)(P.tdq[ix] / 16u);
+          const int r0 = (int)(t0 / (uint32_t)Cs2), p0 = (int)(t0 - (uint32_t)r0 * (uint32_t)Cs2);
+          const int p1 = p0 + (int)(P.tdq[ix] / 16u);
+          const int r1 = r0 + (int)(P.tdr[iy] / 16u / (uint32_t)Cs2);
+          const int c0 = kSwz ? p0 - p0 / 9 : p0, c1 = kSwz ? p1 - p1 / 9 : p1;
           const int ro0 = __shfl(rsrc, r0, kWave), ro1 = __shfl(rsrc, r1, kWave);
           const int co0 = __shfl(csrc, c0, kWave), co1 = __shfl(csrc, c1, kWave);
           f32x4 x[4];
@@ -975,7 +983,7 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
 // 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups, chunk-major per XCD (as the
 // pair kernel: the two 16-channel chunks of a 128-B line share an XCD)
 template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 4, int kQW = kQuadWave, int kOut = 0,
-          bool kSpan = false>
+          bool kSpan = false, bool kSwz = false>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe))) roi_align_fwd_quad_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   __shared__ __attribute__((aligned(16))) float slab[kQuadSlab];
@@ -988,7 +996,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe
   if (w >= wend) return;
   const int ch0 = (int)(w / K32);
   const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
-  quad_item<kStAux, kStamp, kQW, kOut>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
+  quad_item<kStAux, kStamp, kQW, kOut, kSwz>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 

@@ -23,6 +23,19 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   hipStream_t st = as_stream(stream);
+  if (variant == 21 || variant == 22) {  // quad kernel with the bank-group column swizzle (22: + LDS-staged stores)
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
+    const int64_t tq = num_rois * ((channels + 4 * kQuadWave - 1) / (4 * kQuadWave));
+    const dim3 gq((unsigned)(8 * ((tq + 7) / 8)));
+    if (variant == 21)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, false, true>), gq, dim3(kWave), 0,
+                         st, lv, c, out);
+    else
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 1, false, true>), gq, dim3(kWave), 0,
+                         st, lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
   if (variant == 19 || variant == 20) {  // quad kernel, RoI setup shared by a 4-wave workgroup (20: LDS-staged stores)
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
