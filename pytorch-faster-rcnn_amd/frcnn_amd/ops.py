@@ -13,7 +13,19 @@ import torch
 from torch import nn
 
 from . import _lib
-from ._lib import call, ptr, stream_of, i32_array, i64_array, f32_array, ptr_array, workspace
+from ._lib import call as _call, ptr, stream_of, i32_array, i64_array, f32_array, ptr_array, workspace
+
+
+def call(name, *args):
+    """_lib.call; a failed entry point drops the zero-contract workspaces (their counters
+    are left zero only by calls that ran to completion), so the next call starts from
+    freshly zeroed buffers."""
+    try:
+        _call(name, *args)
+    except RuntimeError:
+        for ws in (_ASSIGN_WS, _SAMPLE_WS, _LOSS_WS):
+            ws.clear()
+        raise
 
 
 def _need_cuda(*ts):
