@@ -486,9 +486,6 @@ def main():
                          '+5.8%% img/s on cfg2 fwd, ~1 min of search).  auto = on for fwd, off for train (the '
                          'backward-convolution search takes several minutes)')
     ap.add_argument('--no-conv-search', dest='conv_search', action='store_const', const='off')
-    ap.add_argument('--overlap-proposals', action='store_true',
-                    help='run the RPN proposal chain on a side stream beside the RPN target / loss chain '
-                         '(CascadeRCNN.overlap_proposals; opt-in, measured in DESIGN.md §2)')
     ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
                     help='replay backbone + neck + RPN head convs as one captured hipGraph (frcnn_amd.graphs) '
                          'after the warmup.  auto = on for fwd with a two-stage detector, off for train')
@@ -516,8 +513,6 @@ def main():
     torch.backends.cudnn.benchmark = args.conv_search
     model, cfg = make_model(dev, seed=0, config=os.path.join(CONFIG_DIR, args.config + '.py'))
     batch = make_batch(dev, args.batch, seed=0, rank=rank)
-    if args.overlap_proposals:
-        model.overlap_proposals = True
 
     if args.mode == 'train':
         from frcnn_amd.train import TrainStep, DEFAULT_BUCKET_MB
@@ -659,8 +654,7 @@ def main():
                        'global_batch': world * args.batch, 'imgs_per_gpu': args.batch,
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
                        'backend': args.backend if world > 1 else None,
-                       'sampler': args.sampler, 'mode': args.mode,
-                       'proposals': 'side stream' if args.overlap_proposals else 'in line'},
+                       'sampler': args.sampler, 'mode': args.mode},
         }
         if recs:
             out['roofline'] = {

@@ -5,7 +5,6 @@ import torch
 from torch import nn
 
 from .. import ops, utils
-from ..heads.rpn_head import RPNHead
 from ..region import RoiBatch
 
 
@@ -43,10 +42,6 @@ class CascadeRCNN(nn.Module):
         self.test_cfg = test_cfg
         # optional hipGraph of backbone + neck + RPN head convs (frcnn_amd.graphs.capture_trunk)
         self.graphed_trunk = None
-        # proposals on a second stream, concurrent with the RPN targets / loss (forward_train);
-        # opt-in until its GPU measurement lands (the in-line order is the measured default)
-        self.overlap_proposals = False
-        self._streams = {}
 
     def init_weights(self):
         self.backbone.init_weights()
@@ -58,17 +53,6 @@ class CascadeRCNN(nn.Module):
             h.init_weights()
         if self.with_shared_head:
             self.shared_head.init_weights()
-
-    def _side_stream(self, device):
-        """The second stream of the proposal chain (None: run it in line).  Only when the
-        batched proposals come back as device buffers (RPNHead) -- their consumers are joined
-        to this stream before reading them."""
-        if not (self.overlap_proposals and device.type == 'cuda' and isinstance(self.rpn_head, RPNHead)):
-            return None
-        st = self._streams.get(device)
-        if st is None:
-            st = self._streams[device] = torch.cuda.Stream(device)
-        return st
 
     def _sync_free_rcnn(self, feats):
         """Faster R-CNN (one stage) with the device sampler, RoIAlign extraction and the fused
@@ -99,22 +83,10 @@ class CascadeRCNN(nn.Module):
             rpn_cls, rpn_reg = self.rpn_head(feats)
         cfg = self.train_cfg
         rpn_gt_labels = [torch.ones_like(g) for g in gt_labels]
-        side = self._side_stream(rpn_cls[0].device)
-        if side is None:
-            props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
-            l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
-        else:
-            # the proposal chain (rpn_head.py:68-120) and the RPN target + loss chain
-            # (anchor_head.py:177-192) are independent: the proposals run on a second stream
-            # while the RPN targets / loss run on this one, joined before the RCNN stage
-            main = torch.cuda.current_stream(rpn_cls[0].device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
-            l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
-            main.wait_stream(side)
-            for t in (props.buffer, props.counts_dev):  # made on the side stream, read on this one
-                t.record_stream(main)
+        # (the proposal chain on a second stream beside the RPN target / loss chain was built and
+        # measured slower in round 4: 309.4 vs 315.4 img/s; removed)
+        props = self.rpn_head.predict_bboxes_from_output(rpn_cls, rpn_reg, img_metas, cfg.rpn_proposal)[0]
+        l_cls, l_reg = self.rpn_head.loss(rpn_cls, rpn_reg, gt_bboxes, rpn_gt_labels, img_metas, cfg.rpn)
         losses['rpn_cls_loss'] = l_cls
         losses['rpn_reg_loss'] = l_reg
         if self._sync_free_rcnn(feats):

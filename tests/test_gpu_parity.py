@@ -1501,31 +1501,3 @@ def test_sync_free_targets_match_synced(dev, max_props):
             assert a is None and b is None
             continue
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * float(b.abs().max()) + 1e-12)
-
-
-def test_proposals_side_stream_equal_inline(dev):
-    """CascadeRCNN.forward_train runs the RPN proposal chain on a second stream while the RPN
-    targets / loss run on the current one (joined before the RCNN stage).  On fixed trunk
-    outputs the losses equal the in-line order bit for bit, over several steps (the caching
-    allocator's cross-stream reuse of the proposal buffers is covered by record_stream)."""
-    import bench
-    from frcnn_amd import set_sampler_mode
-    model, _ = bench.make_model(dev, seed=0)
-    imgs, boxes, labels, metas = bench.make_batch(dev, 2, seed=3)
-    with torch.no_grad():
-        feats = [f.detach().clone() for f in model.extract_feat(imgs)]
-        rc, rr = model.rpn_head(feats)
-    model.extract_feat = lambda x: feats
-    model.rpn_head.forward = lambda xs: (rc, rr)
-    out = {}
-    for overlap in (True, False):
-        model.overlap_proposals = overlap
-        set_sampler_mode('device', seed=9)
-        with torch.no_grad():
-            out[overlap] = [{k: v.clone() for k, v in model.forward_train(imgs, boxes, labels, metas).items()}
-                            for _ in range(3)]
-    assert model._streams, 'the side stream was never used'
-    for a, b in zip(out[True], out[False]):
-        assert a.keys() == b.keys()
-        for k in a:
-            assert torch.equal(a[k], b[k]), (k, float(a[k]), float(b[k]))
