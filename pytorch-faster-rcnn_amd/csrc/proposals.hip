@@ -331,6 +331,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
   const int k = rpn_k(p, n);
   int32_t* st = b.state + seg * TK_WORDS;
   int32_t* err = st + TK_ERR;
+  int32_t* bar = b.state + tk_bars_offset((int)gridDim.y) + seg * kBarWords;  // its own line
   const int64_t base = (int64_t)x * kTkChunk;
   const bool has_keys = base < n;
   const uint32_t* gh1 = b.hist1 + (int64_t)seg * (1 << kRpnHistBits);
@@ -392,7 +393,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     for (int r = 0; r < kTkPerThread; ++r) key[r] = 0u;
   }
   stamp(1);
-  seg_barrier(st + TK_BAR1, G, err);
+  seg_barrier(bar + 0, G, err);
   stamp(2);
 
   // ---- phase 2: bucket b1 (every workgroup reads the same final histogram), then b2
@@ -416,7 +417,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       }
     }
     stamp(4);
-    seg_barrier(st + TK_BAR2, G, err);
+    seg_barrier(bar + 1, G, err);
     stamp(5);
     tk_find(sm, kTkBins2, k1, [&](int i) { return xwg_load(gh2 + i); });
     plan.P = (b1 << 12) | (uint32_t)sm.bin;
@@ -454,7 +455,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     }
   }
   stamp(8);
-  seg_barrier(st + TK_BAR3, G, err);
+  seg_barrier(bar + 2, G, err);
   stamp(9);
 
   // ---- phase 4: every record of the segment in LDS (the prefix ties ordered here)
@@ -481,10 +482,22 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
                   rpn_record(key_at(i), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j));
       }
     }
-    seg_barrier(st + TK_BAR4, G, err);
+    seg_barrier(bar + 3, G, err);
     for (int j = t; j < kv; j += kTkThreads) rec[j] = xwg_load(grec + j);
   } else {
-    for (int j = t; j < nabove; j += kTkThreads) rec[j] = xwg_load(grec + j);
+    {  // every record load of this thread in flight at once (<= kRpnSelFused / 256 = 8)
+      uint64_t rv[kRpnSelFused / kTkThreads];
+#pragma unroll
+      for (int u = 0; u < kRpnSelFused / kTkThreads; ++u) {
+        const int j = u * kTkThreads + t;
+        rv[u] = j < nabove ? xwg_load(grec + j) : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kRpnSelFused / kTkThreads; ++u) {
+        const int j = u * kTkThreads + t;
+        if (j < nabove) rec[j] = rv[u];
+      }
+    }
     if (k2 > 0) {
       const int P2 = next_pow2(ncand > 1 ? ncand : 1);
       for (int j = t; j < P2; j += kTkThreads) tie[j] = j < ncand ? xwg_load(cand + j) : 0ull;
@@ -516,38 +529,61 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     c = block_sum(c, sm.part);
     if (t == 0) p.sel_count[seg] = c;
   }
-  // four threads per record (this workgroup's kSelRankPer records in one pass), each counting
-  // a quarter of the records: 16-B LDS reads (a record pair), four in flight per iteration
-  static_assert(kSelRankPer * 4 == kTkThreads, "one pass");
-  const int lane4 = t & 3;
+  // register-blocked count: thread (group g = t / 16, slice q = t % 16) holds this workgroup's
+  // records 4g .. 4g + 3 and counts them against every 16th record pair of the segment (16-B
+  // LDS reads, each compared with four records: a quarter of the LDS traffic of one record per
+  // thread); the 16 slices of a group are lanes of one wave, summed by shuffles.  Lane q < 4 of
+  // the group then writes record 4g + q, whose box it fetched before the count.
+  static_assert(kSelRankPer == 4 * (kTkThreads / 16), "one pass");
+  const int grp = t >> 4, slc = t & 15;
   const uint64_t* stage = reinterpret_cast<const uint64_t*>(p.stage + (int64_t)seg * kRpnSelFused);
   if (x * kSelRankPer < kv) {
-    const int q = x * kSelRankPer + (t >> 2);
-    const uint64_t me = q < kv ? rec[q] : ~0ull;
-    const ulonglong2* tv = reinterpret_cast<const ulonglong2*>(tie);
-    int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    for (int j = lane4; j < kv32 / 2; j += 16) {
-      const ulonglong2 v0 = tv[j], v1 = tv[j + 4], v2 = tv[j + 8], v3 = tv[j + 12];
-      a0 += (v0.x > me ? 1 : 0) + (v0.y > me ? 1 : 0);
-      a1 += (v1.x > me ? 1 : 0) + (v1.y > me ? 1 : 0);
-      a2 += (v2.x > me ? 1 : 0) + (v2.y > me ? 1 : 0);
-      a3 += (v3.x > me ? 1 : 0) + (v3.y > me ? 1 : 0);
-    }
-    int above = (a0 + a1) + (a2 + a3);
-    above += __shfl_xor(above, 1, kWave);
-    above += __shfl_xor(above, 2, kWave);
-    if (lane4 == 0 && q < kv && ((me >> 11) & 1u)) {
-      const int slot = (int)(me & 0x7ffu);
-      float4 bx;
-      if (slot < nabove) {
-        const uint64_t lo = xwg_load(stage + 2 * slot), hi = xwg_load(stage + 2 * slot + 1);
-        bx = make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
-                         __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
+    const int q0 = x * kSelRankPer + 4 * grp;
+    uint64_t me[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) me[i] = q0 + i < kv ? rec[q0 + i] : ~0ull;
+    // the written record's box, in flight during the count
+    const int qw = q0 + (slc & 3);
+    const uint64_t mw = qw < kv ? rec[qw] : 0ull;
+    const bool writes = slc < 4 && qw < kv && ((mw >> 11) & 1u);
+    const int wslot = (int)(mw & 0x7ffu);
+    float4 bx = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint64_t blo = 0ull, bhi = 0ull;
+    if (writes) {
+      if (wslot < nabove) {
+        blo = xwg_load(stage + 2 * wslot);
+        bhi = xwg_load(stage + 2 * wslot + 1);
       } else {
-        bx = rpn_decode_one(p, ia, seg, (int)(~(uint32_t)(me >> 12) & 0xfffffu));
+        bx = rpn_decode_one(p, ia, seg, (int)(~(uint32_t)(mw >> 12) & 0xfffffu));
       }
+    }
+    const ulonglong2* tv = reinterpret_cast<const ulonglong2*>(tie);
+    int a[4] = {0, 0, 0, 0};
+    const int np = kv32 / 2;  // record pairs, a multiple of 16
+    for (int j = slc; j < np; j += 64) {
+      ulonglong2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = j + 16 * u < np ? tv[j + 16 * u] : make_ulonglong2(0ull, 0ull);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] += (v[u].x > me[i] ? 1 : 0) + (v[u].y > me[i] ? 1 : 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] += __shfl_xor(a[i], 1, kWave);
+      a[i] += __shfl_xor(a[i], 2, kWave);
+      a[i] += __shfl_xor(a[i], 4, kWave);
+      a[i] += __shfl_xor(a[i], 8, kWave);
+    }
+    if (writes) {
+      const int i = slc & 3;
+      const int above = i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+      if (wslot < nabove)
+        bx = make_float4(__uint_as_float((uint32_t)blo), __uint_as_float((uint32_t)(blo >> 32)),
+                         __uint_as_float((uint32_t)bhi), __uint_as_float((uint32_t)(bhi >> 32)));
       reinterpret_cast<float4*>(p.sel_boxes)[(int64_t)seg * p.P + above] = bx;
-      p.sel_scores[(int64_t)seg * p.P + above] = key_float((uint32_t)(me >> 32));
+      p.sel_scores[(int64_t)seg * p.P + above] = key_float((uint32_t)(mw >> 32));
     }
   }
   stamp(13);

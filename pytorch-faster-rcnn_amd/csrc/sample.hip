@@ -302,6 +302,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   stamp(0);
   int32_t* st = f.state + (int64_t)(2 * s) * TK_WORDS;  // [2][TK_WORDS]: positives, negatives
   int32_t* err = st + TK_ERR;
+  int32_t* bar = f.state + tk_bars_offset(2 * (int)gridDim.y) + s * kBarWords;  // its own line
   const int64_t* li = lab_in + (int64_t)s * lstride;
   int64_t* lo = lab_out ? lab_out + (int64_t)s * lstride : nullptr;
   const int base = x * kTkChunk;
@@ -343,7 +344,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   for (int i = t; i < 2 * kSampBins; i += kTkThreads)
     xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
   stamp(2);
-  seg_barrier(st + TK_BAR1, G, err);
+  seg_barrier(bar, G, err);
   stamp(3);
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
@@ -416,7 +417,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
   const bool ties = (pl[0].kv > 0 && !pl[0].all) || (pl[1].kv > 0 && !pl[1].all);
   stamp(5);
-  if (ties) seg_barrier(st + TK_BAR2, G, err);
+  if (ties) seg_barrier(bar + 1, G, err);
   stamp(6);
 
   // ---- phase 4: the prefix ties, positives by workgroup 0, negatives by workgroup 1 (0 if alone)
@@ -486,6 +487,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
   __syncthreads();
   if (sm.last && t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
+  if (sm.last && t < 2) xwg_store(reinterpret_cast<uint32_t*>(bar) + t, 0u);
   stamp(8);
 }
 
@@ -672,8 +674,10 @@ struct SampLayout {
 };
 
 // The leading zero region (frh_sample_zero_bytes): the one-launch sampler's state words
-// [V][TK_WORDS]; the rest follows it.
-static size_t samp_zero_bytes(int32_t S) { return al256((size_t)2 * S * TK_WORDS * sizeof(int32_t)); }
+// [V][TK_WORDS] and barrier lines; the rest follows it.
+static size_t samp_zero_bytes(int32_t S) {  // state words [2S][TK_WORDS] + a barrier line per image
+  return al256(((size_t)tk_bars_offset(2 * S) + (size_t)S * kBarWords) * sizeof(int32_t));
+}
 
 static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   SampLayout z{};

@@ -56,8 +56,15 @@ struct TkBufs {
 };
 
 
-inline size_t tk_zero_bytes(int V, int hb) {  // hist1 + hist2 + state, contiguous
-  return (size_t)V * (((size_t)1 << hb) + kTkBins2 + TK_WORDS) * sizeof(uint32_t);
+// The one-launch kernels' barrier counters: 32 words (one 128-B line) per segment after the
+// state words, so the lanes polling a barrier never share a line with the list reservations'
+// atomics.  bars = state + tk_bars_offset(V) words.
+__host__ __device__ inline int tk_bars_offset(int V) { return (V * TK_WORDS + 31) & ~31; }
+constexpr int kBarWords = 32;
+
+inline size_t tk_zero_bytes(int V, int hb) {  // hist1 + hist2 + state + barrier lines, contiguous
+  return (size_t)V * (((size_t)1 << hb) + kTkBins2) * sizeof(uint32_t) +
+         ((size_t)tk_bars_offset(V) + (size_t)V * kBarWords) * sizeof(int32_t);
 }
 
 // ------------------------------------------- cross-workgroup hand-off words
@@ -85,7 +92,8 @@ __device__ __forceinline__ int32_t xwg_load(const int32_t* p) {
 // ------------------------------------------------------------ wave helpers
 // histogram add aggregated over the wave's most common bin (the first active
 // lane's): a concentrated key set costs one LDS atomic per wave, not 64
-// conflicting ones.  Wave-uniform call.
+// conflicting ones.  Wave-uniform call.  (A second aggregation round -- for key sets
+// straddling two bins -- measured slower on both the RPN and the sampler keys: round 4.)
 __device__ __forceinline__ void tk_hist_add(uint32_t* h, bool act, uint32_t bin) {
   const uint64_t am = __ballot(act);
   if (!am) return;
@@ -314,7 +322,7 @@ __device__ __forceinline__ void seg_barrier(int32_t* counter, int target, int32_
     atomicAdd(counter, 1);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (xwg_load(counter) < target) {
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
         atomicOr(err, 1);
         break;
