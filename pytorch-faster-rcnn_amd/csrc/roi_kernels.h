@@ -1000,56 +1000,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 
-// The quad kernel with the RoI setup shared by a workgroup: 4 waves per (RoI, 64 channels),
-// wave 0 computes the RoI's tap state (pair_setup) and hands it to the other three through
-// LDS (18 dwords per lane), so the ~480-instruction setup runs once per 64 channels, not
-// once per 16; each wave then stages and evaluates its own 16 channels.  Tools-only
-// candidate (roi_lab variant 19).  Grid: 8 * ceil(K * groups / 8) workgroups of 256.
-template <int kStAux = kCpolNT, int kOut = 0>
-__global__ void __launch_bounds__(4 * kWave) roi_align_fwd_quad4_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float slab[4][kQuadSlab];
-  __shared__ __attribute__((aligned(16))) float obuf[4][kOut == 1 ? 4 * kQuadWave * kWave : 4];
-  __shared__ PairLane sp[kWave];
-  __shared__ PairGeom sg;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave)), lane = threadIdx.x & (kWave - 1);
-  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab[wave]);
-  const uint32_t NG = (uint32_t)(c.C + 16 * kQuadWave - 1) / (uint32_t)(16 * kQuadWave), K32 = (uint32_t)c.K;
-  const uint32_t total = K32 * NG, per = (total + 7u) / 8u;
-  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
-  if (w >= wend) return;
-  const int grp = (int)(w / K32);
-  const int64_t k0 = (int64_t)(w - (uint32_t)grp * K32);
-  PairGeom G;
-  PairLane P;
-  if (wave == 0) {
-    const RoiRaw raw = roi_fetch(c, k0);
-    pair_setup<16>(lv, c, raw, lane, G, P);
-    sp[lane] = P;
-    if (lane == 0) sg = G;
-  }
-  __syncthreads();
-  if (wave != 0) {
-    P = sp[lane];
-    G.empty = __builtin_amdgcn_readfirstlane(sg.empty);
-    G.y0 = __builtin_amdgcn_readfirstlane(sg.y0), G.x0 = __builtin_amdgcn_readfirstlane(sg.x0);
-    G.R = __builtin_amdgcn_readfirstlane(sg.R), G.Cs = __builtin_amdgcn_readfirstlane(sg.Cs);
-    G.Cs2 = __builtin_amdgcn_readfirstlane(sg.Cs2);
-    G.dy = __builtin_amdgcn_readfirstlane(sg.dy), G.dx = __builtin_amdgcn_readfirstlane(sg.dx);
-    G.sy = __builtin_amdgcn_readfirstlane(sg.sy), G.sx = __builtin_amdgcn_readfirstlane(sg.sx);
-    G.scs = __builtin_amdgcn_readfirstlane(sg.scs);
-    G.inv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sg.inv);
-    G.extent = (uint32_t)__builtin_amdgcn_readfirstlane((int)sg.extent);
-    const uint64_t b = reinterpret_cast<uint64_t>(sg.base);
-    G.base = reinterpret_cast<const float*>(
-        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
-        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b));
-  }
-  const int chunk = grp * 4 + wave;
-  if (chunk * 4 * kQuadWave >= c.C) return;
-  quad_body<kStAux, false, kQuadWave, kOut>(G, P, c, out, k0, chunk, w, sbase, 0, lane, obuf[wave]);
-}
-
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
                                                                     const float* __restrict__ gout) {
   __shared__ Tap ty[kMaxSamplesPerDim], tx[kMaxSamplesPerDim];

@@ -3,6 +3,7 @@
 // build.
 #include "frcnn_tools.h"
 #include "roi_kernels.h"
+#include "roi_lab_kernels.h"
 
 using namespace frh;
 
@@ -23,6 +24,18 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   hipStream_t st = as_stream(stream);
+  if (variant == 23 || variant == 24) {  // software-pipelined persistent quad kernel (23: 8 waves per CU, 24: 12;
+                                        // 2 waves per SIMD by registers: 24 queues its surplus)
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
+    int dev = 0, ncu = 0;
+    FRH_HIP(hipGetDevice(&dev));
+    FRH_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int wpc = variant == 23 ? 8 : 12;
+    const dim3 gq((unsigned)(8 * ((ncu * wpc + 7) / 8)));
+    hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
   if (variant == 21 || variant == 22) {  // quad kernel with the bank-group column swizzle (22: + LDS-staged stores)
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
