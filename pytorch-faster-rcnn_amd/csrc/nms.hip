@@ -26,8 +26,8 @@
 #include <atomic>
 #include <type_traits>
 
-#include "block_ops.h"
 #include "cdna.h"
+#include "seg_topk.h"
 
 namespace frh {
 
@@ -132,34 +132,12 @@ __device__ __forceinline__ int64_t seg_tile_base(const int64_t* seg_base, int s,
   return seg_base ? seg_base[s] : (int64_t)s * tri_tiles(nbw);
 }
 
-// Four tiles per 256-thread workgroup, each wave staging its tile's 64 ROW boxes in
-// LDS; lane = column.  Lane j sweeps the rows and sets bit i of its column word when
-// row i suppresses box j.  IoU is symmetric bit for bit (min / max and the area sum
-// (area_i + area_j) - inter commute exactly), so this is the reference's test of the
-// kept box i against candidate j.
-__global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
-                                                       const int32_t* __restrict__ counts, int n_max, int nbw,
-                                                       NmsThr T, uint64_t* __restrict__ mask,
-                                                       const int64_t* __restrict__ seg_base) {
-  __shared__ float4 rb_box_all[4][64];
-  __shared__ float rb_area_all[4][64];
-  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
-  if (tile >= nbw * (nbw + 1) / 2) return;
-  int rb, cb;
-  tri_tile(__builtin_amdgcn_readfirstlane(tile), &rb, &cb);
-  rb = __builtin_amdgcn_readfirstlane(rb);
-  cb = __builtin_amdgcn_readfirstlane(cb);
-  // the count, the row box and the column box in flight together (indices clamped to
-  // the buffer: slots past the count are read, never used)
-  const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
+// One wave's tile (rb, cb) of a segment of n boxes: r = row box rb * 64 + t, a = column box
+// cb * 64 + t (lane t); returns lane t's column word (0 past the count).  rb_box / rb_area:
+// the wave's own 64-slot LDS staging.
+__device__ __forceinline__ uint64_t mask_tile_word(float4 r, float4 a, int n, int rb, int cb, int t, const NmsThr& T,
+                                                   float4* rb_box, float* rb_area) {
   const int row = rb * 64 + t, col = cb * 64 + t;
-  const int n = counts[s];
-  const float4 r = bx[min(row, n_max - 1)];
-  const float4 a = bx[min(col, n_max - 1)];
-  if (rb * 64 >= n || cb * 64 >= n) return;
-  float4* rb_box = rb_box_all[wv];
-  float* rb_area = rb_area_all[wv];
   const bool row_nn = row >= n || nn_finite(r);
   rb_box[t] = r;
   rb_area[t] = (r.z - r.x) * (r.w - r.y);
@@ -227,7 +205,36 @@ __global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__
   const int nrows = min(64, n - rb * 64);
   if (nrows < 64) colw &= (1ull << nrows) - 1ull;
   if (cb == rb) colw &= t == 0 ? 0ull : (~0ull >> (64 - t));  // rows before the column only
-  mask[tile_word(seg_tile_base(seg_base, s, nbw), rb, cb) + t] = cvalid ? colw : 0ull;
+  return cvalid ? colw : 0ull;
+}
+
+// Four tiles per 256-thread workgroup, each wave staging its tile's 64 ROW boxes in
+// LDS; lane = column.  Lane j sweeps the rows and sets bit i of its column word when
+// row i suppresses box j.  IoU is symmetric bit for bit (min / max and the area sum
+// (area_i + area_j) - inter commute exactly), so this is the reference's test of the
+// kept box i against candidate j.
+__global__ void __launch_bounds__(256) nms_mask_kernel(const float* __restrict__ boxes, int64_t seg_stride,
+                                                       const int32_t* __restrict__ counts, int n_max, int nbw,
+                                                       NmsThr T, uint64_t* __restrict__ mask,
+                                                       const int64_t* __restrict__ seg_base) {
+  __shared__ float4 rb_box_all[4][64];
+  __shared__ float rb_area_all[4][64];
+  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int s = blockIdx.y, tile = blockIdx.x * 4 + wv;
+  if (tile >= nbw * (nbw + 1) / 2) return;
+  int rb, cb;
+  tri_tile(__builtin_amdgcn_readfirstlane(tile), &rb, &cb);
+  rb = __builtin_amdgcn_readfirstlane(rb);
+  cb = __builtin_amdgcn_readfirstlane(cb);
+  // the count, the row box and the column box in flight together (indices clamped to
+  // the buffer: slots past the count are read, never used)
+  const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
+  const int n = counts[s];
+  const float4 r = bx[min(rb * 64 + t, n_max - 1)];
+  const float4 a = bx[min(cb * 64 + t, n_max - 1)];
+  if (rb * 64 >= n || cb * 64 >= n) return;
+  mask[tile_word(seg_tile_base(seg_base, s, nbw), rb, cb) + t] =
+      mask_tile_word(r, a, n, rb, cb, t, T, rb_box_all[wv], rb_area_all[wv]);
 }
 
 __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
@@ -472,6 +479,204 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
   }
 }
 
+// ---------------------------------------------------------------- one-launch NMS
+// The RPN proposals' NMS (rpn_proposals_impl): mask and scan of every segment in ONE
+// launch, so a segment's scan resolves its early blocks while the mask of its later
+// columns is still being computed (the two-launch form above runs them back to back).
+//  Grid (1-D, 512 threads): S scan workgroups first (blockIdx < S, dispatched first), then
+//  mask workgroups of 8 tiles (one per wave) in COLUMN order across segments: global tile g
+//  is column cb, segment s, row block rb with g = S cb (cb + 1) / 2 + s (cb + 1) + rb, so the
+//  columns every scan needs first are dispatched first; mask waves of the first columns also
+//  issue at a higher s_setprio than those of the last ones, and the scan waves at the top.
+//  Hand-off (hand-off table row 1): a mask wave writes its 64 column words with sc1 stores,
+//  waits vmcnt(0), then sets its tile's flag word (sc1 store); a loader polls a column's
+//  flags and reads its tiles with sc1 loads.  Flags are zero on entry (the caller's
+//  memset).  Mask workgroups wait for nothing, so no residency is assumed: a scan
+//  workgroup only waits for mask workgroups, which always finish (S <= kFzMaxSegs leaves
+//  every CU room for them).  Every global wait is bounded (kSpinTicks): a broken
+//  assumption sets the error word and ends the kernel, never hangs it.
+//  Scan workgroup: wave 0 resolves exactly as nms_scan_kernel's resolver (slot layout
+//  below); waves 1..7 stage block p (p = wave - 1 mod 7): once the ring slot is free and
+//  column p is complete, the near tiles (p-2, p), (p-1, p), (p, p) go to the slot, and the
+//  fold of the kept rows of blocks <= p - 3 (tiles read into registers, eight per batch, the
+//  next batch in flight) into the slot's partial word; then ready[slot] = p + 1.
+constexpr int kFzThreads = 512;
+constexpr int kFzWaves = kFzThreads / kWave;
+constexpr int kFzLoaders = kFzWaves - 1;
+constexpr int kFzRing = 16;
+constexpr int kFzSlotWords = 4 * kWave;  // [partial | tile (p-2, p) | tile (p-1, p) | tile (p, p)] x 64 lanes
+constexpr int kFzMaxSegs = 256;
+
+__device__ __forceinline__ void fz_setprio(int q) {  // s_setprio takes an immediate
+  if (q >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (q == 2) __builtin_amdgcn_s_setprio(2);
+  else if (q == 1) __builtin_amdgcn_s_setprio(1);
+}
+
+// wait until the flags of tiles (0..p, p) -- contiguous from col_flags -- are all set
+__device__ __forceinline__ void fz_wait_column(const uint32_t* col_flags, int p, int lane, uint32_t* err) {
+  for (int j0 = 0; j0 <= p; j0 += kWave) {
+    const int cnt = min(kWave, p + 1 - j0);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      const uint32_t v = lane < cnt ? xwg_load(col_flags + j0 + lane) : 1u;
+      if (!__ballot(v == 0u)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        if (lane == 0) atomicOr(err, 1u);
+        return;
+      }
+    }
+  }
+}
+
+// kStamp (tools-only timing build): s_memrealtime per (segment, block) at stamps +
+// (s * nbw + b) * 4: [0] loader starts b (slot free), [1] column b seen complete, [2] b
+// published, [3] b resolved; then per tile at stamps + S * nbw * 4 + s * tri + tile: its
+// flag set.
+template <bool kStamp>
+__global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(8))) nms_fused_kernel(int S, const float* __restrict__ boxes,
+                                                               int64_t seg_stride, const int32_t* __restrict__ counts,
+                                                               int n_max, int nbw, NmsThr T, uint64_t* mask,
+                                                               uint32_t* flags, int max_keep,
+                                                               int32_t* __restrict__ keep, int64_t kstride,
+                                                               int32_t* __restrict__ kcounts, int64_t* stamps) {
+  // scan: ring [kFzRing][kFzSlotWords] then kept[kMaxNmsWords]; mask: per wave 64 row boxes + areas
+  __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kMaxNmsWords];
+  __shared__ int ready[kFzRing];
+  __shared__ int s_resolved, s_stop;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int64_t tri = tri_tiles(nbw);
+  uint32_t* err = flags + (int64_t)S * tri;
+  if ((int)blockIdx.x >= S) {
+    // ---------------- mask: one tile per wave
+    const int64_t g = ((int64_t)blockIdx.x - S) * kFzWaves + wave;
+    if (g >= (int64_t)S * tri) return;
+    int cb = (int)((sqrtf(8.0f * (float)g / (float)S + 1.0f) - 1.0f) * 0.5f);
+    cb = max(cb, 0);
+    while (cb > 0 && (int64_t)S * cb * (cb + 1) / 2 > g) --cb;
+    while ((int64_t)S * (cb + 1) * (cb + 2) / 2 <= g) ++cb;
+    const int rem = (int)(g - (int64_t)S * cb * (cb + 1) / 2);
+    const int s = __builtin_amdgcn_readfirstlane(rem / (cb + 1));
+    const int rb = __builtin_amdgcn_readfirstlane(rem - s * (cb + 1));
+    cb = __builtin_amdgcn_readfirstlane(cb);
+    fz_setprio(2 - min(2, (3 * cb) / nbw));
+    const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
+    const int n = counts[s];
+    const float4 r = bx[min(rb * 64 + lane, n_max - 1)];
+    const float4 a = bx[min(cb * 64 + lane, n_max - 1)];
+    if (rb * 64 >= n || cb * 64 >= n) return;
+    float4* rows = reinterpret_cast<float4*>(fz_lds) + wave * kWave;
+    float* areas = reinterpret_cast<float*>(reinterpret_cast<float4*>(fz_lds) + kFzWaves * kWave) + wave * kWave;
+    const uint64_t w = mask_tile_word(r, a, n, rb, cb, lane, T, rows, areas);
+    xwg_store(mask + tile_word((int64_t)s * tri, rb, cb) + lane, w);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) xwg_store(flags + (int64_t)s * tri + (int64_t)cb * (cb + 1) / 2 + rb, 1u);
+    if (kStamp && lane == 0)
+      stamps[(int64_t)S * nbw * 4 + (int64_t)s * tri + (int64_t)cb * (cb + 1) / 2 + rb] =
+          (int64_t)__builtin_amdgcn_s_memrealtime();
+    return;
+  }
+  // ---------------- scan of segment s
+  const int s = blockIdx.x;
+  const int n = counts[s];
+  const int nb = (n + 63) >> 6;
+  uint64_t* ring = fz_lds;
+  uint64_t* kept = fz_lds + kFzRing * kFzSlotWords;
+  if (tid < kFzRing) ready[tid] = 0;
+  if (tid == 0) {
+    s_resolved = 0;
+    s_stop = nb;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_setprio(3);
+  if (wave == 0) {
+    int32_t* K = keep + (int64_t)s * kstride;
+    int nk = 0;
+    uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
+    for (int b = 0; b < nb; ++b) {
+      const uint64_t* slot = ring + (b % kFzRing) * kFzSlotWords + lane;
+      uint64_t pw, t1, t2, d;
+      if (lds_block_reads(&ready[b % kFzRing], slot, slot + 2 * kWave, slot + kWave, slot + 3 * kWave, pw, t1, t2,
+                          d) != b + 1) {
+        while (lds_poll(&ready[b % kFzRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
+        lds_block_reads(&ready[b % kFzRing], slot, slot + 2 * kWave, slot + kWave, slot + 3 * kWave, pw, t1, t2, d);
+      }
+      const uint64_t acc = pw | (t1 & kb1) | (t2 & kb2);
+      uint64_t r = __ballot(acc != 0ull);
+      const int valid = n - b * 64;
+      if (valid < 64) r |= (~0ull) << valid;
+      uint64_t kb = 0, und = ~r;
+      while (und) {
+        const uint64_t sup = __ballot((d & und) != 0ull);
+        const uint64_t nkp = und & ~sup;
+        kb |= nkp;
+        const uint64_t vic = __ballot((d & nkp) != 0ull);
+        und &= ~(nkp | vic);
+      }
+      bool stop = false;
+      if (max_keep >= 0) {
+        const int room = max_keep - nk;
+        while (__popcll(kb) > room) kb &= ~(1ull << (63 - __clzll(kb)));  // drop lowest-score extras
+        stop = nk + __popcll(kb) >= max_keep;
+      }
+      if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
+      nk += __popcll(kb);
+      kb2 = kb1;
+      kb1 = kb;
+      if (lane == 0) {  // in-order LDS: the loaders see kept[b] / s_stop once they see the count
+        kept[b] = kb;
+        if (stop) s_stop = b;
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(&s_resolved, stop ? nb + kFzRing + 1 : b + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kStamp) stamps[((int64_t)s * nbw + b) * 4 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      }
+      if (stop) break;
+    }
+    if (lane == 0) kcounts[s] = nk;
+    return;
+  }
+  const uint32_t* sflags = flags + (int64_t)s * tri;
+  const uint64_t* smask = mask + (int64_t)s * tri * 64;
+  for (int p = wave - 1; p < nb; p += kFzLoaders) {
+    while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
+    if (s_stop < p) break;
+    const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    fz_wait_column(sflags + c0, p, lane, err);
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    const uint64_t* col = smask + c0 * 64 + lane;
+    const uint64_t d = xwg_load(col + (int64_t)p * 64);
+    const uint64_t t1 = p >= 1 ? xwg_load(col + (int64_t)(p - 1) * 64) : 0ull;
+    const uint64_t t2 = p >= 2 ? xwg_load(col + (int64_t)(p - 2) * 64) : 0ull;
+    // fold blocks j < jf = p - 2 (their kept sets appear as the resolver passes them)
+    const int jf = p - 2;
+    uint64_t acc = 0, cur[8], nxt[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cur[u] = u < jf ? xwg_load(col + (int64_t)u * 64) : 0ull;
+    for (int j0 = 0; j0 < jf; j0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) nxt[u] = j0 + 8 + u < jf ? xwg_load(col + (int64_t)(j0 + 8 + u) * 64) : 0ull;
+      const int need = min(j0 + 8, jf);
+      while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u < jf) acc |= cur[u] & kept[j0 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+    }
+    uint64_t* slot = ring + (p % kFzRing) * kFzSlotWords + lane;
+    slot[0] = acc;
+    slot[kWave] = t2;
+    slot[2 * kWave] = t1;
+    slot[3 * kWave] = d;
+    if (lane == 0) lds_flag(&ready[p % kFzRing], p + 1);
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
 // The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
 // set for every device the first time a launch runs on it (one bit per device id;
 // setting it twice from racing threads is harmless).
@@ -509,6 +714,35 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
     hipLaunchKernelGGL(nms_scan_kernel<false>, dim3(S), dim3(256), lds, st, mask, counts, nbw, span, max_keep, keep,
                        kstride, kcounts, seg_base, nullptr);
   return check_launch("nms");
+}
+
+// One-launch NMS (nms_fused_kernel) of S segments at most n_max boxes each, tiles at
+// s * tri(nbw) (no seg_base); flags: nms_fused_flag_bytes(S, n_max) bytes, zero on entry
+// (left set: the caller zeroes them again before the next call).
+bool nms_fused_fits(int32_t S, int32_t n_max) {
+  return S >= 1 && S <= kFzMaxSegs && n_max >= 1 && (n_max + 63) / 64 <= kMaxNmsWords;
+}
+
+size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile + the error word
+  return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
+}
+
+int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
+                         double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
+                         uint64_t* mask, uint32_t* flags, hipStream_t st, int64_t* stamps = nullptr) {
+  FRH_REQUIRE(nms_fused_fits(S, n_max), "one-launch NMS: %d segments of %d boxes out of range", S, n_max);
+  const int nbw = (n_max + 63) / 64;
+  const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves;
+  FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many mask tiles");
+  if (stamps)
+    hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
+                       seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
+                       stamps);
+  else
+    hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
+                       seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
+                       nullptr);
+  return check_launch("nms_fused");
 }
 
 size_t nms_mask_bytes(int32_t S, int32_t n_max) {  // S triangles of the n_max segment, 64 column words per tile

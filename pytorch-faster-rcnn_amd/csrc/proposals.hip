@@ -7,7 +7,8 @@
 //     workgroup per 4096 anchors; a selected anchor is decoded + clamped by
 //     the workgroup that selects it), then rank: each selection's position in
 //     (score desc, index asc) order after the min-size compaction, by counting.
-//  2. NMS mask + scan over all segments (nms.hip), keep <= post_nms.
+//  2. NMS mask + scan over all segments in one launch (nms.hip, nms_fused_kernel),
+//     keep <= post_nms.
 //  3. merge   (1 block per image): concatenate the levels' survivors and, if
 //     more than max_num, keep the best max_num by (score desc, concat order).
 #include "seg_topk.h"
@@ -18,6 +19,11 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
                           double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                           uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps = nullptr);
 size_t nms_mask_bytes(int32_t S, int32_t n_max);
+bool nms_fused_fits(int32_t S, int32_t n_max);
+size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
+int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
+                         double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
+                         uint64_t* mask, uint32_t* flags, hipStream_t st, int64_t* stamps = nullptr);
 
 constexpr int kPropThreads = 1024;
 constexpr int kMaxSort = 16384;
@@ -795,11 +801,12 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
                            float* out_boxes, float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
-                           void* stream, bool select_launches, int64_t* select_stamps = nullptr);
+                           void* stream, bool select_launches, int64_t* select_stamps = nullptr,
+                           bool nms_launches = false);
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, total;
+  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, nflags, zero_bytes, total;
   int64_t nmax, kld;
 };
 
@@ -831,7 +838,11 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
   z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
   z.mem = z.keys + al(S * (size_t)z.kld * sizeof(uint32_t));
   z.zero = z.mem + al(S * (size_t)z.kld * sizeof(uint64_t));
-  z.total = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
+  // zeroed by one memset per call: the selection's histograms / state / barriers, then the
+  // one-launch NMS's tile flags
+  z.nflags = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
+  z.zero_bytes = z.nflags - z.zero + nms_fused_flag_bytes((int32_t)S, P);
+  z.total = z.zero + al(z.zero_bytes);
   return z;
 }
 
@@ -913,7 +924,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
                                 int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream,
-                                bool select_launches, int64_t* select_stamps) {
+                                bool select_launches, int64_t* select_stamps, bool nms_launches) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
@@ -979,7 +990,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
             reinterpret_cast<uint32_t*>(zb + (size_t)S * (1 << kRpnHistBits) * sizeof(uint32_t)),
             reinterpret_cast<int32_t*>(zb + (size_t)S * ((1 << kRpnHistBits) + kTkBins2) * sizeof(uint32_t)),
             reinterpret_cast<uint64_t*>(ws + z.mem)};
-  FRH_HIP(hipMemsetAsync(zb, 0, tk_zero_bytes(S, kRpnHistBits), st));
+  FRH_HIP(hipMemsetAsync(zb, 0, z.zero_bytes, st));
   const dim3 grid((unsigned)((z.nmax + kTkChunk - 1) / kTkChunk), (unsigned)S);
   const bool fused = z.P <= kRpnSelFused && z.nmax < (1 << 20);  // record layout limits
   // one-launch selection: every segment's workgroups resident together (seg_barrier): the
@@ -1010,8 +1021,13 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   if (r) return r;
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);
   int32_t* kcnt = reinterpret_cast<int32_t*>(ws + z.kcnt);
-  r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
-                        (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, reinterpret_cast<uint64_t*>(ws + z.mask), nullptr, st);
+  uint64_t* nmask = reinterpret_cast<uint64_t*>(ws + z.mask);
+  if (!nms_launches && nms_fused_fits(S, z.P))
+    r = launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou, (post_nms > 0) ? post_nms : -1,
+                         keep, z.P, kcnt, nmask, reinterpret_cast<uint32_t*>(ws + z.nflags), st);
+  else
+    r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
+                          (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask, nullptr, st);
   if (r) return r;
   MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
                (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};

@@ -10,6 +10,13 @@
   channels-last outputs, a min-size filter, 1, 2 and 4 images, and three calls in a row on
   the same shapes (workspace reuse).  The reference semantics of the selection are pinned
   by test_gpu_parity.py (rpn fixtures, tie-heavy oracle cases), which run the one-launch path.
+* RPN NMS: frh_rpn_proposals_strided's one-launch NMS (nms_fused_kernel: the mask tiles and
+  the scan of every segment in one launch, tile flags between them) against the tools
+  library's two-launch NMS (mask kernel, then scan kernel; frh_rpn_proposals_nms2) on the
+  same selection: outputs equal, over segments of 5..125 blocks (scans of more than 64
+  columns poll their flags in two loads), a post_nms cut that stops the scan early,
+  tie-heavy and sparse score sets, 1, 2 and 4 images, three calls in a row (the flags are
+  zeroed per call).  The two-launch NMS is pinned by test_gpu_parity.py's oracle cases.
 * Device sampler: frh_sample_random's one-launch sampler (sampler_fused_kernel) against the
   tools library's keys + collect launches (frh_sample_random_launches): labels, selection
   sets and counts equal; the workspace's zero region is zero after every call.  The sampler's
@@ -50,7 +57,7 @@ def _scores(case, rng, c):
         c[...] = (rng.standard_normal(c.shape) * 0.01).astype(np.float32)
 
 
-def _run(dev, case, cls_ch, nhwc, batch, min_size, pre, post, mx, seed):
+def _run(dev, case, cls_ch, nhwc, batch, min_size, pre, post, mx, seed, other='frh_rpn_proposals_launches'):
     from frcnn_amd import ops
     from frcnn_amd.heads.rpn_head import RPNHead
     head = RPNHead(256, 256, loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=cls_ch == 1),
@@ -69,7 +76,7 @@ def _run(dev, case, cls_ch, nhwc, batch, min_size, pre, post, mx, seed):
     args = (cls, reg, anchors, 3, cls_ch, [0.0] * 4, [1.0] * 4, [(600.0, 1000.0)] * batch, [min_size] * batch,
             pre, post, mx, 0.7)
     fused = [ops.rpn_proposals(*args) for _ in range(3)]
-    launches = ops.rpn_proposals(*args, _entry=(lib.frh_rpn_proposals_launches, 'frh_rpn_proposals_launches'))
+    launches = ops.rpn_proposals(*args, _entry=(getattr(lib, other), other))
     torch.cuda.synchronize()
     return fused, launches
 
@@ -105,6 +112,26 @@ def test_rpn_one_launch_selection_pre_nms_sizes(dev, pre, post, mx):
     for i, n in enumerate(rc.tolist()):
         assert torch.equal(fb[i, :, :n], rb[i, :, :n])
         assert torch.equal(fs[i, :n], rs[i, :n])
+
+
+@pytest.mark.parametrize('case,batch,pre,post,mx', [
+    ('random_init', 2, 2000, 2000, 2000),   # the bench's call
+    ('random_init', 2, 2000, 300, 1000),    # post_nms stops every scan early
+    ('four_values', 1, 1000, 1000, 1000),
+    ('sparse_high', 2, 2000, 2000, 2000),
+    ('near_half', 4, 2000, 2000, 4000),
+    ('random_init', 1, 4000, 3000, 4000),   # 63 blocks (four-launch selection)
+    ('random_init', 1, 8000, 2000, 2000),   # 125 blocks: column flags polled in two loads
+])
+def test_rpn_one_launch_nms_equals_two_launches(dev, case, batch, pre, post, mx):
+    fused, ref = _run(dev, case, 1, True, batch, 0.0, pre, post, mx, 90 + batch, other='frh_rpn_proposals_nms2')
+    rb, rs, rc = ref
+    assert int(rc.min()) > 0
+    for fb, fs, fc in fused:
+        assert torch.equal(fc, rc), (fc, rc)
+        for i, n in enumerate(rc.tolist()):
+            assert torch.equal(fb[i, :, :n], rb[i, :, :n]), (case, i)
+            assert torch.equal(fs[i, :n], rs[i, :n]), (case, i)
 
 
 # ------------------------------------------------------------------ device sampler

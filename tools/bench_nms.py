@@ -5,7 +5,10 @@ proposals), replayed with the product kernels and with the stamped scan build.
 Prints µs per call (mask + scan, back to back) and, from the stamped build, the per-block
 timeline of the scan of every segment: when the resolver started waiting for block b, when
 b was ready (its staged span folded by a loader), when it was resolved, and when the
-loader issued b's copies / published b's fold (µs from the launch's first stamp)."""
+loader issued b's copies / published b's fold (µs from the launch's first stamp).  Then the
+same for the RPN's one-launch NMS (nms_fused_kernel, the product's path inside
+frh_rpn_proposals): µs per call, and per block of segment 0 when its column's last tile was
+flagged, when the loader started / saw the column complete / published, when it was resolved."""
 import argparse
 import os
 import sys
@@ -83,6 +86,47 @@ def main():
             for b in range(nb):
                 print('   b={:2d} wait {:6.2f} ready {:6.2f} resolved {:6.2f} | copies {:6.2f} fold {:6.2f}'.format(
                     b, *x[b, [0, 1, 2, 4, 3]]))
+
+    # ---------------- the RPN's one-launch NMS (nms_fused_kernel)
+    tri = nbw * (nbw + 1) // 2
+    fws = _lib.workspace(_lib.query('frh_nms_workspace', S, P) + lib.frh_nms_fused_flag_bytes(S, P), dev)
+    fst = torch.zeros(S * nbw * 4 + S * tri, dtype=torch.int64, device=dev)
+
+    def fused(stm=None):
+        r = lib.frh_nms_fused_stamped(S, _lib.ptr(rows), rows.stride(0), _lib.ptr(cnt), P, thr, max_keep,
+                                      _lib.ptr(keep), keep.stride(0), _lib.ptr(kc), _lib.ptr(fws), fws.numel(),
+                                      _lib.ptr(stm), _lib.stream_of(rows))
+        assert r == 0, lib.frh_last_error()
+    for fn, name in ((fused, 'one-launch'), (lambda: fused(fst), 'one-launch stamped')):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print('{}: {:.2f} us per call (flag memset + kernel)'.format(name, e0.elapsed_time(e1) / args.iters * 1e3),
+              flush=True)
+        assert torch.equal(kc, ref_kc) and all(torch.equal(keep[s, :int(kc[s])], ref_keep[s, :int(kc[s])])
+                                               for s in range(S))
+    fs = fst.cpu().numpy()
+    blk = fs[:S * nbw * 4].reshape(S, nbw, 4)
+    til = fs[S * nbw * 4:].reshape(S, tri)
+    t0 = min(blk[blk > 0].min(), til[til > 0].min())
+    print('one-launch timeline (us from the first stamp): last tile flagged {:.2f}'.format((til.max() - t0) / 100.0))
+    for s in range(S):
+        nb = (counts[s] + 63) // 64
+        x = (blk[s, :nb] - t0) / 100.0
+        print('segment {} ({} boxes): resolver done at {:.2f}, last column complete {:.2f}'.format(
+            s, counts[s], x[:, 3].max(), max(((til[s, c * (c + 1) // 2:c * (c + 1) // 2 + c + 1].max() - t0) / 100.0)
+                                            for c in range(nb))))
+        if s == 0:
+            for b in range(nb):
+                colc = (til[s, b * (b + 1) // 2:b * (b + 1) // 2 + b + 1].max() - t0) / 100.0
+                print('   b={:2d} column flagged {:6.2f} | loader start {:6.2f} seen {:6.2f} published {:6.2f} | '
+                      'resolved {:6.2f}'.format(b, colc, *x[b]))
 
 
 if __name__ == '__main__':

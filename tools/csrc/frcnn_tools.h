@@ -29,6 +29,15 @@ int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, int64_t seg
                                int64_t keep_seg_stride, int32_t* keep_counts, void* workspace, size_t ws_bytes,
                                int64_t* stamps, void* stream);
 
+/* The RPN's one-launch NMS (nms_fused_kernel) on pre-sorted segments: workspace = the
+ * frh_nms_workspace mask bytes followed by frh_nms_fused_flag_bytes flag bytes (zeroed by the
+ * call); stamps null (plain build) or num_segs * ceil(n_max / 64) * 4 + num_segs * tri int64
+ * (timing build). */
+size_t frh_nms_fused_flag_bytes(int32_t num_segs, int32_t n_max);
+int32_t frh_nms_fused_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
+                              int32_t n_max, double iou_thr, int32_t max_keep, int32_t* keep, int64_t keep_seg_stride,
+                              int32_t* keep_counts, void* workspace, size_t ws_bytes, int64_t* stamps, void* stream);
+
 /* frh_rpn_proposals_strided with the four-launch selection (keys, refine, collect, rank)
  * instead of the one-launch rpn_select_kernel; same arguments and outputs. */
 int32_t frh_rpn_proposals_launches(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
@@ -39,6 +48,16 @@ int32_t frh_rpn_proposals_launches(int32_t num_imgs, int32_t num_levels, const f
                                    int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
                                    float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
                                    void* stream);
+
+/* frh_rpn_proposals_strided with the two-launch NMS (mask, scan) instead of the one-launch
+ * nms_fused_kernel; same arguments and outputs. */
+int32_t frh_rpn_proposals_nms2(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                               const float* const* reg_ptrs, const int64_t* cls_strides, const int64_t* reg_strides,
+                               const int32_t* grid_hw, int32_t num_anchors, int32_t cls_channels, const float* anchors,
+                               int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
+                               const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num,
+                               double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
+                               void* workspace, size_t ws_bytes, void* stream);
 
 /* frh_sample_random with the keys + collect launches instead of the one-launch sampler. */
 int32_t frh_sample_random_launches(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
