@@ -55,7 +55,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # in-step kernel groups of the detection path (substrings of the dispatched kernel names)
 KERNEL_GROUPS = [
     ('roi_align_fwd', ('roi_align_fwd',)),
-    ('nms', ('nms_mask_kernel', 'nms_scan_kernel')),
+    ('nms', ('nms_fused_kernel', 'nms_mask_kernel', 'nms_scan_kernel')),
     ('proposals', ('rpn_select', 'rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
     ('sampler', ('sampler_', 'chunk_count', 'chunk_write_lists')),
@@ -168,7 +168,7 @@ def group_of(name):
     return None
 
 
-TRUNK_KERNELS = ('bn_act', 'fpn_merge')  # frcnn_amd kernels of the trunk (backbone epilogue, FPN top-down)
+TRUNK_KERNELS = ('bn_act', 'fpn_merge', 'bias_act')  # frcnn_amd kernels of the trunk / head convs' epilogues
 
 
 def summarise_trace(trace, steps):
@@ -699,8 +699,8 @@ def main():
             lines['nms'] = line(per_group.get('nms'), nbytes_nms,
                                 '20*N + 16*N*ceil(N/64) + 8*K_keep per segment (SURVEY §8(d)); RPN call, {} '
                                 'segments'.format(nrecs[0][1].shape[0] if nrecs else 0))
-            if nrep:
-                lines['nms']['us_replay_warm'] = nrep[0]
+            if nrep:  # frh_nms_sorted: the standalone two-launch NMS (the RPN's own is one launch)
+                lines['nms']['us_replay_warm_two_launch'] = nrep[0]
             if args.config in ('faster_rcnn_r50_fpn', 'cascade_rcnn_r50_fpn'):
                 n_all = sum(model.rpn_head.num_anchors * h * w for h, w in
                             [(int(np.ceil(PAD_SHAPE[0] / s)), int(np.ceil(PAD_SHAPE[1] / s)))

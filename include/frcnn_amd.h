@@ -440,14 +440,22 @@ int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gam
                    int64_t n, int32_t c, int64_t hw, int32_t relu, void* stream);
 
 /* FPN top-down merge into channels-last levels (lib/necks.py:72-84):
- * out[b, y, x, c] = lat[b, c, y, x] + up[b, iy, ix, c] with torch's nearest rule
+ * out[b, y, x, c] = (lat[b, c, y, x] + bias[c]) + up[b, iy, ix, c] with torch's nearest rule
  * (iy = min(floor(y * (float)up_h / height), up_h - 1); y / 2 when height == 2 * up_h);
- * lat: any strides (lat_strides = element strides b, c, y, x); up: NHWC contiguous
- * [batch, up_h, up_w, channels] or NULL (the top level: a transpose); out: NHWC
- * contiguous [batch, height, width, channels].  One f32 add per element. */
-int32_t frh_fpn_merge_nhwc(const float* lat, const int64_t* lat_strides, const float* up, int32_t up_h,
-                           int32_t up_w, float* out, int32_t batch, int32_t channels, int32_t height,
+ * lat: any strides (lat_strides = element strides b, c, y, x) -- the lateral conv's output
+ * without its bias when bias ([channels]) is given, with it when bias is NULL; up: NHWC
+ * contiguous [batch, up_h, up_w, channels] or NULL (the top level: a transpose); out: NHWC
+ * contiguous [batch, height, width, channels].  f32 adds in that order (bit-identical to
+ * the conv's bias add followed by the reference's upsample add). */
+int32_t frh_fpn_merge_nhwc(const float* lat, const int64_t* lat_strides, const float* bias, const float* up,
+                           int32_t up_h, int32_t up_w, float* out, int32_t batch, int32_t channels, int32_t height,
                            int32_t width, void* stream);
+
+/* Conv epilogue on a channels-last map viewed as [rows, channels] (rows = batch * H * W):
+ * y = relu ? max(y + bias[c], 0) : y + bias[c], in place -- the RPN head's
+ * relu(conv(x)) (lib/heads/rpn_head.py, RPNHead.forward) after a bias-free NHWC conv, one
+ * pass for PyTorch's bias add + ReLU.  channels % 4 == 0, y and bias 16-byte aligned. */
+int32_t frh_bias_act_nhwc(float* y, const float* bias, int64_t rows, int32_t channels, int32_t relu, void* stream);
 
 /* ---------------------------------------------------------------- f1: fused losses
  * Classification losses of lib/losses.py on the head outputs, summed (the reference's

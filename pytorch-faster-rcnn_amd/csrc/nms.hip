@@ -495,16 +495,44 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
 //  workgroup only waits for mask workgroups, which always finish (S <= kFzMaxSegs leaves
 //  every CU room for them).  Every global wait is bounded (kSpinTicks): a broken
 //  assumption sets the error word and ends the kernel, never hangs it.
-//  Scan workgroup: wave 0 resolves exactly as nms_scan_kernel's resolver (slot layout
-//  below); waves 1..7 stage block p (p = wave - 1 mod 7): once the ring slot is free and
-//  column p is complete, the near tiles (p-2, p), (p-1, p), (p, p) go to the slot, and the
-//  fold of the kept rows of blocks <= p - 3 (tiles read into registers, eight per batch, the
-//  next batch in flight) into the slot's partial word; then ready[slot] = p + 1.
+//  Scan workgroup: wave 0 resolves as nms_scan_kernel's resolver, but ORs in FOUR near
+//  tiles itself (p-1 .. p-4: the loaders' fold then waits for the resolver four blocks back,
+//  not two -- with two, the fold hand-off chain, about 0.9 us per round, bounded the scan to
+//  0.3 us per block); waves 1..7 stage block p (p = wave - 1 mod 7): once the ring slot is
+//  free and column p is complete, the near tiles (p-i, p) and the diagonal (p, p) go to the
+//  slot, and the fold of the kept rows of blocks <= p - 5 (tiles read into registers, eight
+//  per batch, the next batch in flight) into the slot's partial word; then ready = p + 1.
 constexpr int kFzThreads = 512;
 constexpr int kFzWaves = kFzThreads / kWave;
 constexpr int kFzLoaders = kFzWaves - 1;
-constexpr int kFzRing = 16;
-constexpr int kFzSlotWords = 4 * kWave;  // [partial | tile (p-2, p) | tile (p-1, p) | tile (p, p)] x 64 lanes
+constexpr int kFzRing = 8;
+constexpr int kFzNear = 4;  // near tiles (p - i, p), i = 1..kFzNear, ORed in by the resolver
+constexpr int kFzSlotWords = (kFzNear + 2) * kWave;  // [partial | tile (p-1, p) .. (p-4, p) | tile (p, p)] x 64 lanes
+
+// The resolver's reads for one block of the one-launch scan in ONE asm statement: the
+// ready flag, then the slot's partial word, its kFzNear near tiles and the diagonal tile
+// (consecutive 512-byte rows of the slot), one wait -- as lds_block_reads.
+__device__ __forceinline__ int fz_block_reads(const int* flag, const uint64_t* slot, uint64_t& pw, uint64_t (&nr)[4],
+                                              uint64_t& d) {
+  static_assert(kFzNear == 4, "fz_block_reads reads four near tiles");
+  auto la = [](const void* q) {
+    return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)q);
+  };
+  int f;
+  asm volatile(
+      "ds_read_b32 %0, %7\n\t"
+      "ds_read_b64 %1, %8\n\t"
+      "ds_read_b64 %2, %8 offset:512\n\t"
+      "ds_read_b64 %3, %8 offset:1024\n\t"
+      "ds_read_b64 %4, %8 offset:1536\n\t"
+      "ds_read_b64 %5, %8 offset:2048\n\t"
+      "ds_read_b64 %6, %8 offset:2560\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(f), "=&v"(pw), "=&v"(nr[0]), "=&v"(nr[1]), "=&v"(nr[2]), "=&v"(nr[3]), "=&v"(d)
+      : "v"(la(flag)), "v"(la(slot))
+      : "memory");
+  return __builtin_amdgcn_readfirstlane(f);
+}
 constexpr int kFzMaxSegs = 256;
 
 __device__ __forceinline__ void fz_setprio(int q) {  // s_setprio takes an immediate
@@ -512,6 +540,10 @@ __device__ __forceinline__ void fz_setprio(int q) {  // s_setprio takes an immed
   else if (q == 2) __builtin_amdgcn_s_setprio(2);
   else if (q == 1) __builtin_amdgcn_s_setprio(1);
 }
+
+// a staged tile word, read sc1 like every hand-off word (a plain load measured no faster:
+// the words come from other XCDs' write-through stores either way)
+__device__ __forceinline__ uint64_t fz_tile(const uint64_t* p) { return xwg_load(p); }
 
 // wait until the flags of tiles (0..p, p) -- contiguous from col_flags -- are all set
 __device__ __forceinline__ void fz_wait_column(const uint32_t* col_flags, int p, int lane, uint32_t* err) {
@@ -531,9 +563,9 @@ __device__ __forceinline__ void fz_wait_column(const uint32_t* col_flags, int p,
 }
 
 // kStamp (tools-only timing build): s_memrealtime per (segment, block) at stamps +
-// (s * nbw + b) * 4: [0] loader starts b (slot free), [1] column b seen complete, [2] b
-// published, [3] b resolved; then per tile at stamps + S * nbw * 4 + s * tri + tile: its
-// flag set.
+// (s * nbw + b) * 8: [0] loader starts b (slot free), [1] column b seen complete, [2] b
+// published, [3] b resolved, [4] / [5] the fold's last batch waits for / got the kept sets;
+// then per tile at stamps + S * nbw * 8 + s * tri + tile: its flag set.
 template <bool kStamp>
 __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu(8))) nms_fused_kernel(int S, const float* __restrict__ boxes,
                                                                int64_t seg_stride, const int32_t* __restrict__ counts,
@@ -574,7 +606,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) xwg_store(flags + (int64_t)s * tri + (int64_t)cb * (cb + 1) / 2 + rb, 1u);
     if (kStamp && lane == 0)
-      stamps[(int64_t)S * nbw * 4 + (int64_t)s * tri + (int64_t)cb * (cb + 1) / 2 + rb] =
+      stamps[(int64_t)S * nbw * 8 + (int64_t)s * tri + (int64_t)cb * (cb + 1) / 2 + rb] =
           (int64_t)__builtin_amdgcn_s_memrealtime();
     return;
   }
@@ -594,16 +626,17 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
   if (wave == 0) {
     int32_t* K = keep + (int64_t)s * kstride;
     int nk = 0;
-    uint64_t kb1 = 0, kb2 = 0;  // kept sets of blocks b-1, b-2
+    uint64_t kbh[kFzNear] = {};  // kept sets of blocks b-1 .. b-kFzNear
     for (int b = 0; b < nb; ++b) {
       const uint64_t* slot = ring + (b % kFzRing) * kFzSlotWords + lane;
-      uint64_t pw, t1, t2, d;
-      if (lds_block_reads(&ready[b % kFzRing], slot, slot + 2 * kWave, slot + kWave, slot + 3 * kWave, pw, t1, t2,
-                          d) != b + 1) {
+      uint64_t pw, nr[kFzNear], d;
+      if (fz_block_reads(&ready[b % kFzRing], slot, pw, nr, d) != b + 1) {
         while (lds_poll(&ready[b % kFzRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
-        lds_block_reads(&ready[b % kFzRing], slot, slot + 2 * kWave, slot + kWave, slot + 3 * kWave, pw, t1, t2, d);
+        fz_block_reads(&ready[b % kFzRing], slot, pw, nr, d);
       }
-      const uint64_t acc = pw | (t1 & kb1) | (t2 & kb2);
+      uint64_t acc = pw;
+#pragma unroll
+      for (int i = 0; i < kFzNear; ++i) acc |= nr[i] & kbh[i];
       uint64_t r = __ballot(acc != 0ull);
       const int valid = n - b * 64;
       if (valid < 64) r |= (~0ull) << valid;
@@ -623,15 +656,16 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       }
       if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
       nk += __popcll(kb);
-      kb2 = kb1;
-      kb1 = kb;
+#pragma unroll
+      for (int i = kFzNear - 1; i > 0; --i) kbh[i] = kbh[i - 1];
+      kbh[0] = kb;
       if (lane == 0) {  // in-order LDS: the loaders see kept[b] / s_stop once they see the count
         kept[b] = kb;
         if (stop) s_stop = b;
         asm volatile("" ::: "memory");
         __hip_atomic_store(&s_resolved, stop ? nb + kFzRing + 1 : b + 1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (kStamp) stamps[((int64_t)s * nbw + b) * 4 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (kStamp) stamps[((int64_t)s * nbw + b) * 8 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
       }
       if (stop) break;
     }
@@ -644,23 +678,26 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
     if (s_stop < p) break;
     const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
     fz_wait_column(sflags + c0, p, lane, err);
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
     const uint64_t* col = smask + c0 * 64 + lane;
-    const uint64_t d = xwg_load(col + (int64_t)p * 64);
-    const uint64_t t1 = p >= 1 ? xwg_load(col + (int64_t)(p - 1) * 64) : 0ull;
-    const uint64_t t2 = p >= 2 ? xwg_load(col + (int64_t)(p - 2) * 64) : 0ull;
-    // fold blocks j < jf = p - 2 (their kept sets appear as the resolver passes them)
-    const int jf = p - 2;
+    const uint64_t d = fz_tile(col + (int64_t)p * 64);
+    uint64_t nr[kFzNear];
+#pragma unroll
+    for (int i = 0; i < kFzNear; ++i) nr[i] = p > i ? fz_tile(col + (int64_t)(p - 1 - i) * 64) : 0ull;
+    // fold blocks j < jf = p - kFzNear (their kept sets appear as the resolver passes them)
+    const int jf = p - kFzNear;
     uint64_t acc = 0, cur[8], nxt[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = u < jf ? xwg_load(col + (int64_t)u * 64) : 0ull;
+    for (int u = 0; u < 8; ++u) cur[u] = u < jf ? fz_tile(col + (int64_t)u * 64) : 0ull;
     for (int j0 = 0; j0 < jf; j0 += 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) nxt[u] = j0 + 8 + u < jf ? xwg_load(col + (int64_t)(j0 + 8 + u) * 64) : 0ull;
+      for (int u = 0; u < 8; ++u) nxt[u] = j0 + 8 + u < jf ? fz_tile(col + (int64_t)(j0 + 8 + u) * 64) : 0ull;
       const int need = min(j0 + 8, jf);
+      if (kStamp && lane == 0 && j0 + 8 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
       while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
+      if (kStamp && lane == 0 && j0 + 8 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (j0 + u < jf) acc |= cur[u] & kept[j0 + u];
@@ -669,11 +706,11 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     }
     uint64_t* slot = ring + (p % kFzRing) * kFzSlotWords + lane;
     slot[0] = acc;
-    slot[kWave] = t2;
-    slot[2 * kWave] = t1;
-    slot[3 * kWave] = d;
+#pragma unroll
+    for (int i = 0; i < kFzNear; ++i) slot[(1 + i) * kWave] = nr[i];
+    slot[(1 + kFzNear) * kWave] = d;
     if (lane == 0) lds_flag(&ready[p % kFzRing], p + 1);
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 4 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
 }
 

@@ -77,7 +77,8 @@ class RPNHead(AnchorHead):
             init_module_normal(m, mean=0.0, std=0.01)
 
     def forward(self, xs):
-        hidden = [self.relu(self.conv(x)) for x in xs]
+        # relu(conv(x)); on channels-last HIP levels the bias add + ReLU is one pass (ops.conv_bias_relu)
+        hidden = [ops.conv_bias_relu(self.conv, x) for x in xs]
         return [self.classifier(h) for h in hidden], [self.regressor(h) for h in hidden]
 
     def predict_bboxes_from_output(self, cls_outs, reg_outs, img_metas, test_cfg):

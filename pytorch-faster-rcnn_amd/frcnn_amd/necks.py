@@ -6,14 +6,15 @@ levels either by stride-2 subsampling of the last output
 (`max_pool2d(k=1, s=2)`, `necks.py:89`) or by stride-2 3x3 convs.
 
 On a HIP device the levels come out channels-last (NHWC): the top-down merge
-of every level is one HIP pass (`ops.fpn_merge_nhwc`: lateral + nearest
-upsample of the merged coarser level, written NHWC), and the output convs run
+of every level is one HIP pass (`ops.fpn_merge_nhwc`: lateral + its conv bias +
+nearest upsample of the merged coarser level, written NHWC), and the output convs run
 in MIOpen's NHWC layout (channels-last weights, `utils.ChannelsLastConvs`) --
 2.64 -> 2.41 ms for the FPN output convs + RPN head at cfg2 on MI355X
 (`tools/probe_fpn_layout.py`).  The heads and the RoIAlign read NHWC levels
 directly (strided kernels, the channel-quad RoIAlign).  CPU tensors take the
 reference's NCHW ops.
 """
+import torch
 import torch.nn.functional as F
 from torch import nn
 
@@ -63,15 +64,20 @@ class FPN(ChannelsLastConvs):
     def forward(self, inputs):
         if len(inputs) != self.num_ins:
             raise AssertionError('FPN expects {} inputs'.format(self.num_ins))
-        lat = [conv(inputs[self.start_level + i]) for i, conv in enumerate(self.lateral_convs)]
-        if lat[0].is_cuda and lat[0].dtype.is_floating_point and lat[0].dtype.itemsize == 4:
-            # top-down merge straight into channels-last levels (one HIP pass per level)
+        x0 = inputs[self.start_level]
+        if x0.is_cuda and x0.dtype == torch.float32:
+            # lateral 1x1 convs without their bias; the bias add and the top-down merge into
+            # channels-last levels are one HIP pass per level
+            lat = [F.conv2d(inputs[self.start_level + i], conv.weight, None, conv.stride, conv.padding)
+                   for i, conv in enumerate(self.lateral_convs)]
+            bias = [conv.bias for conv in self.lateral_convs]
             merged = [None] * self.used_ins
-            merged[-1] = ops.fpn_merge_nhwc(lat[-1])
+            merged[-1] = ops.fpn_merge_nhwc(lat[-1], None, bias[-1])
             for i in range(self.used_ins - 1, 0, -1):
-                merged[i - 1] = ops.fpn_merge_nhwc(lat[i - 1], merged[i])
+                merged[i - 1] = ops.fpn_merge_nhwc(lat[i - 1], merged[i], bias[i - 1])
             lat = merged
         else:
+            lat = [conv(inputs[self.start_level + i]) for i, conv in enumerate(self.lateral_convs)]
             for i in range(self.used_ins - 1, 0, -1):
                 lat[i - 1] = lat[i - 1] + F.interpolate(lat[i], size=lat[i - 1].shape[2:], mode='nearest')
         outs = [self.fpn_convs[i](lat[i]) for i in range(self.used_ins)]

@@ -849,16 +849,16 @@ def atss_assign(anchors, grid_sizes, strides, gt_list, label_list, img_shapes, t
 
 # ---------------------------------------------------------------- FPN top-down merge (channels-last levels)
 class _FpnMerge(torch.autograd.Function):
-    """out = lat + nearest_upsample(up) as a channels-last tensor (frh_fpn_merge_nhwc);
-    lat: any layout; up: the merged coarser level (channels-last) or None."""
+    """out = (lat + bias) + nearest_upsample(up) as a channels-last tensor (frh_fpn_merge_nhwc);
+    lat: any layout; bias: [C] or None; up: the merged coarser level (channels-last) or None."""
 
     @staticmethod
-    def forward(ctx, lat, up):
+    def forward(ctx, lat, up, bias):
         B, C, H, W = lat.shape
         out = torch.empty(B, C, H, W, dtype=torch.float32, device=lat.device, memory_format=torch.channels_last)
         uh, uw = (int(up.shape[2]), int(up.shape[3])) if up is not None else (0, 0)
-        call('frh_fpn_merge_nhwc', ptr(lat), i64_array(lat.stride()), ptr(up), uh, uw, ptr(out), B, C, H, W,
-             stream_of(out))
+        call('frh_fpn_merge_nhwc', ptr(lat), i64_array(lat.stride()), ptr(bias), ptr(up), uh, uw, ptr(out), B, C, H,
+             W, stream_of(out))
         ctx.has_up = up is not None
         if ctx.has_up:
             ctx.save_for_backward(up)
@@ -873,17 +873,55 @@ class _FpnMerge(torch.autograd.Function):
                 u = up.detach().requires_grad_(True)
                 y = torch.nn.functional.interpolate(u, size=g.shape[2:], mode='nearest')
                 gup, = torch.autograd.grad(y, u, g)
-        return g if ctx.needs_input_grad[0] else None, gup
+        gb = g.sum((0, 2, 3)) if ctx.needs_input_grad[2] else None
+        return g if ctx.needs_input_grad[0] else None, gup, gb
 
 
-def fpn_merge_nhwc(lat, up=None):
+def fpn_merge_nhwc(lat, up=None, bias=None):
     """The FPN's top-down step lat + interpolate(up, size=lat.shape[2:], mode='nearest')
-    (lib/necks.py:72-84) as one HIP pass writing a channels-last level."""
-    _need_cuda(lat, up)
+    (lib/necks.py:72-84) as one HIP pass writing a channels-last level; bias: the lateral
+    conv's bias when lat was computed without it (its add folded into the pass)."""
+    _need_cuda(lat, up, bias)
     if lat.dtype != torch.float32 or (up is not None and (up.dtype != torch.float32 or
                                                           not up.is_contiguous(memory_format=torch.channels_last))):
         raise AssertionError('fpn_merge_nhwc: f32 lateral and a channels-last f32 coarser level')
-    return _FpnMerge.apply(lat, up)
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != lat.shape[1] or not bias.is_contiguous()):
+        raise AssertionError('fpn_merge_nhwc: bias must be a contiguous f32 [C]')
+    return _FpnMerge.apply(lat, up, bias)
+
+
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, bias, relu):
+        B, C, H, W = y.shape
+        call('frh_bias_act_nhwc', ptr(y), ptr(bias), B * H * W, C, int(bool(relu)), stream_of(y))
+        ctx.relu = relu
+        ctx.mark_dirty(y)
+        ctx.save_for_backward(y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        if ctx.relu:
+            g = g * (y > 0)
+        return g, (g.sum((0, 2, 3)) if ctx.needs_input_grad[1] else None), None
+
+
+def conv_bias_relu(conv, x, relu=True):
+    """act(conv(x)) for a biased Conv2d: on a HIP device with channels-last f32 input and weights
+    the conv runs without its bias (MIOpen NHWC) and frh_bias_act_nhwc adds the bias and applies
+    the ReLU in one pass (bit-identical to conv + bias, then relu); otherwise the module ops."""
+    ok = (x.is_cuda and x.dtype == torch.float32 and conv.bias is not None and conv.weight.dtype == torch.float32
+          and conv.out_channels % 4 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+          and conv.weight.is_contiguous(memory_format=torch.channels_last))
+    if not ok:
+        y = conv(x)
+        return torch.relu(y) if relu else y
+    y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        y = y.contiguous(memory_format=torch.channels_last)
+    return _BiasAct.apply(y, conv.bias, relu)
 
 
 # ---------------------------------------------------------------- backbone epilogue (frozen BN + add + ReLU)

@@ -2,8 +2,10 @@
 
 * ops.fpn_merge_nhwc -- the FPN top-down step lat + interpolate(up, 'nearest')
   (reference lib/necks.py:72-84) written as an NHWC level: bit-identical to torch's
-  NCHW expression (exact 2x and non-2x level sizes, the top level alone), gradients
-  equal to torch's autograd of the same expression;
+  NCHW expression (exact 2x and non-2x level sizes, the top level alone), also with the
+  lateral conv's bias folded in; gradients equal to torch's autograd of the same expression;
+* ops.conv_bias_relu -- the RPN head's relu(conv(x)) as a bias-free NHWC conv + one HIP bias
+  + ReLU pass: bit-identical to conv-with-bias + relu, same gradients;
 * the FPN module's NHWC path against its NCHW torch path on the same weights (the merge is
   exact; the 3x3 convs run MIOpen NHWC vs NCHW solvers: f32 summation-order tolerance);
 * RPN proposals (frh_rpn_proposals_strided) and the level gather / scatter
@@ -42,6 +44,64 @@ def test_fpn_merge_nhwc_bit_exact(dev, shape, up_shape):
     want2 = lat[:, :, :, :-1] if up is None else lat[:, :, :, :-1] + F.interpolate(up, size=(shape[2], shape[3] - 1),
                                                                                     mode='nearest')
     assert torch.equal(out2, want2)
+
+
+@pytest.mark.parametrize('shape,up_shape', [((2, 256, 76, 128), (38, 64)), ((1, 96, 19, 30), None),
+                                            ((2, 6, 7, 6), (4, 3))])
+def test_fpn_merge_nhwc_bias_fold_bit_exact(dev, shape, up_shape):
+    """The lateral conv's bias folded into the merge: (conv(x) + bias) + upsample, bit for bit
+    (6 channels: the scalar path)."""
+    from frcnn_amd import ops
+    g = torch.Generator().manual_seed(6)
+    lat = torch.randn(*shape, generator=g).to(dev)
+    bias = torch.randn(shape[1], generator=g).to(dev)
+    up = torch.randn(shape[0], shape[1], *up_shape, generator=g).to(dev) if up_shape else None
+    out = ops.fpn_merge_nhwc(lat, _cl(up) if up is not None else None, bias)
+    with_bias = lat + bias.view(1, -1, 1, 1)
+    want = with_bias if up is None else with_bias + F.interpolate(up, size=shape[2:], mode='nearest')
+    assert torch.equal(out, want)
+
+
+def test_fpn_merge_nhwc_bias_gradient(dev):
+    from frcnn_amd import ops
+    g = torch.Generator().manual_seed(7)
+    lat = torch.randn(2, 32, 38, 64, generator=g).to(dev).requires_grad_(True)
+    bias = torch.randn(32, generator=g).to(dev).requires_grad_(True)
+    gout = torch.randn(2, 32, 38, 64, generator=g).to(dev)
+    ops.fpn_merge_nhwc(lat, None, bias).backward(gout)
+    torch.testing.assert_close(bias.grad, gout.sum((0, 2, 3)), rtol=1e-6, atol=1e-5)
+    assert torch.equal(lat.grad, gout)
+
+
+@pytest.mark.parametrize('shape', [(2, 256, 152, 256), (2, 256, 10, 16), (1, 64, 7, 9)])
+def test_conv_bias_relu_bit_exact(dev, shape):
+    """RPN head's relu(conv(x)) on a channels-last level: bias-free MIOpen conv + the HIP bias +
+    ReLU pass against the module's conv (bias included) + relu, bit for bit; the same
+    gradients as torch's autograd of conv + relu."""
+    from frcnn_amd import ops
+    from frcnn_amd.utils import conv_layout
+    torch.manual_seed(8)
+    conv = torch.nn.Conv2d(shape[1], shape[1], 3, padding=1).to(dev)
+    torch.nn.init.normal_(conv.bias, std=0.5)
+    conv_layout(conv)
+    x = _cl(torch.randn(*shape, device=dev))
+    with torch.no_grad():
+        out = ops.conv_bias_relu(conv, x)
+        ref = torch.relu(torch.nn.functional.conv2d(x, conv.weight, None, 1, 1) + conv.bias.view(1, -1, 1, 1))
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, ref)
+    if shape[2] > 100:
+        return
+    xg = x.clone().requires_grad_(True)
+    gout = torch.randn(*shape, device=dev)
+    ops.conv_bias_relu(conv, xg).backward(gout)
+    gx, gw, gb = xg.grad, conv.weight.grad.clone(), conv.bias.grad.clone()
+    conv.zero_grad()
+    x2 = x.clone().requires_grad_(True)
+    torch.relu(conv(x2)).backward(gout)
+    torch.testing.assert_close(gx, x2.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gw, conv.weight.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gb, conv.bias.grad, rtol=1e-5, atol=1e-4)
 
 
 def test_fpn_merge_nhwc_gradients(dev):

@@ -90,7 +90,7 @@ def main():
     # ---------------- the RPN's one-launch NMS (nms_fused_kernel)
     tri = nbw * (nbw + 1) // 2
     fws = _lib.workspace(_lib.query('frh_nms_workspace', S, P) + lib.frh_nms_fused_flag_bytes(S, P), dev)
-    fst = torch.zeros(S * nbw * 4 + S * tri, dtype=torch.int64, device=dev)
+    fst = torch.zeros(S * nbw * 8 + S * tri, dtype=torch.int64, device=dev)
 
     def fused(stm=None):
         r = lib.frh_nms_fused_stamped(S, _lib.ptr(rows), rows.stride(0), _lib.ptr(cnt), P, thr, max_keep,
@@ -112,21 +112,22 @@ def main():
         assert torch.equal(kc, ref_kc) and all(torch.equal(keep[s, :int(kc[s])], ref_keep[s, :int(kc[s])])
                                                for s in range(S))
     fs = fst.cpu().numpy()
-    blk = fs[:S * nbw * 4].reshape(S, nbw, 4)
-    til = fs[S * nbw * 4:].reshape(S, tri)
+    blk = fs[:S * nbw * 8].reshape(S, nbw, 8)
+    til = fs[S * nbw * 8:].reshape(S, tri)
     t0 = min(blk[blk > 0].min(), til[til > 0].min())
     print('one-launch timeline (us from the first stamp): last tile flagged {:.2f}'.format((til.max() - t0) / 100.0))
     for s in range(S):
         nb = (counts[s] + 63) // 64
-        x = (blk[s, :nb] - t0) / 100.0
+        x = (blk[s, :nb].astype(np.float64) - t0) / 100.0
+        x[blk[s, :nb] == 0] = np.nan
         print('segment {} ({} boxes): resolver done at {:.2f}, last column complete {:.2f}'.format(
             s, counts[s], x[:, 3].max(), max(((til[s, c * (c + 1) // 2:c * (c + 1) // 2 + c + 1].max() - t0) / 100.0)
                                             for c in range(nb))))
         if s == 0:
             for b in range(nb):
                 colc = (til[s, b * (b + 1) // 2:b * (b + 1) // 2 + b + 1].max() - t0) / 100.0
-                print('   b={:2d} column flagged {:6.2f} | loader start {:6.2f} seen {:6.2f} published {:6.2f} | '
-                      'resolved {:6.2f}'.format(b, colc, *x[b]))
+                print('   b={:2d} column flagged {:6.2f} | loader start {:6.2f} seen {:6.2f} last-batch wait {:6.2f} '
+                      'got {:6.2f} published {:6.2f} | resolved {:6.2f}'.format(b, colc, *x[b, [0, 1, 4, 5, 2, 3]]))
 
 
 if __name__ == '__main__':

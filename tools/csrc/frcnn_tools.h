@@ -31,7 +31,7 @@ int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, int64_t seg
 
 /* The RPN's one-launch NMS (nms_fused_kernel) on pre-sorted segments: workspace = the
  * frh_nms_workspace mask bytes followed by frh_nms_fused_flag_bytes flag bytes (zeroed by the
- * call); stamps null (plain build) or num_segs * ceil(n_max / 64) * 4 + num_segs * tri int64
+ * call); stamps null (plain build) or num_segs * ceil(n_max / 64) * 8 + num_segs * tri int64
  * (timing build). */
 size_t frh_nms_fused_flag_bytes(int32_t num_segs, int32_t n_max);
 int32_t frh_nms_fused_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,

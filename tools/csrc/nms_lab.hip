@@ -29,7 +29,7 @@ int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, cons
 
 // The RPN's one-launch NMS (nms_fused_kernel) on pre-sorted segments, tiles at s * tri(nbw):
 // workspace = frh_nms_workspace bytes of mask + frh_nms_fused_flag_bytes of flags (zeroed
-// here); stamps (or null): the kernel's timing build, S * nbw * 4 + S * tri(nbw) int64.
+// here); stamps (or null): the kernel's timing build, S * nbw * 8 + S * tri(nbw) int64.
 extern "C" size_t frh_nms_fused_flag_bytes(int32_t num_segs, int32_t n_max) {
   return frh::nms_fused_flag_bytes(num_segs, n_max);
 }

@@ -24,6 +24,7 @@ CLASSES = [
     ('sampler compaction', ('chunk_',)),
     ('fused losses', ('cls_loss', 'smooth_l1', 'loss_finalize')),
     ('frozen-BN/residual/ReLU bn_act', ('bn_act',)),
+    ('FPN merge (+ lateral bias), RPN conv bias + ReLU', ('fpn_merge', 'bias_act')),
     ('other frcnn_amd kernels', ('frh::',)),
     ('MIOpen convolutions', ('miopenSp3AsmConv', 'igemm_', 'naive_conv', 'kernel_grouped_conv', 'conv_', 'Im2d2Col')),
     ('MIOpen layout transposes', ('batched_transpose', 'transpose_')),
