@@ -439,6 +439,13 @@ int32_t frh_bn_act(const float* x, const float* skip, float* y, const float* gam
                    const float* beta, const float* mean, const float* var, float eps,
                    int64_t n, int32_t c, int64_t hw, int32_t relu, void* stream);
 
+/* The ResNet stem's frozen BN + ReLU + max_pool2d(kernel 3, stride 2, padding 1)
+ * (lib/backbones.py, ResNet stem) in one pass: y [n, c, (h - 1) / 2 + 1, w / 2] =
+ * maxpool(act(x * s + b)); x contiguous NCHW f32 [n, c, h, w], w % 8 == 0, x / y 16-byte
+ * aligned.  Equal to frh_bn_act followed by the max pool, bit for bit. */
+int32_t frh_bn_act_maxpool(const float* x, float* y, const float* gamma, const float* beta, const float* mean,
+                           const float* var, float eps, int64_t n, int32_t c, int32_t h, int32_t w, void* stream);
+
 /* FPN top-down merge into channels-last levels (lib/necks.py:72-84):
  * out[b, y, x, c] = (lat[b, c, y, x] + bias[c]) + up[b, iy, ix, c] with torch's nearest rule
  * (iy = min(floor(y * (float)up_h / height), up_h - 1); y / 2 when height == 2 * up_h);

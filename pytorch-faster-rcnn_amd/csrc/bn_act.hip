@@ -72,3 +72,68 @@ extern "C" int32_t frh_bn_act(const float* x, const float* skip, float* y, const
                      reinterpret_cast<float4*>(y), gamma, beta, mean, var, eps, (int)c, hw4, (int)tiles, (int)relu);
   return check_launch("frh_bn_act");
 }
+
+// Stem: frozen BN + ReLU + 3x3 / stride-2 / pad-1 max pool (lib/backbones.py: the ResNet
+// stem relu(bn1(conv1(x))) -> maxpool) in one pass: the conv1 output is read once and only
+// the pooled map is written (PyTorch: BN-act pass + max_pool2d_with_indices, which also
+// writes int64 indices).  Thread = four consecutive outputs of one row: input columns
+// 8q - 1 .. 8q + 7 of the (up to) three input rows, as two float4 + one scalar each.
+// Max over the window's in-bounds elements (the pool's -inf padding); same f32 BN
+// arithmetic as bn_act_kernel, so every output equals max_pool2d(bn_act(x)) bit for bit.
+namespace frh {
+
+__global__ void __launch_bounds__(kBnThreads) bn_act_maxpool_kernel(const float* __restrict__ x, float4* y,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta,
+                                                                   const float* __restrict__ mean,
+                                                                   const float* __restrict__ var, float eps, int C,
+                                                                   int H, int W, int OH, int64_t total) {
+  const int64_t t = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
+  if (t >= total) return;
+  const int OW4 = W / 8;  // (OW = W / 2) / 4 output quads per row
+  const int q = (int)(t % OW4);
+  const int64_t r = t / OW4;
+  const int oy = (int)(r % OH);
+  const int64_t plane = r / OH;
+  const int c = (int)(plane % C);
+  const float s = (gamma ? gamma[c] : 1.0f) / sqrtf(var[c] + eps);
+  const float b = (beta ? beta[c] : 0.0f) - mean[c] * s;
+  auto act = [&](float v) { return fmaxf(v * s + b, 0.0f); };
+  float m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+  const float* xp = x + plane * (int64_t)H * W;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int iy = 2 * oy + dy;
+    if (iy < 0 || iy >= H) continue;
+    const float* row = xp + (int64_t)iy * W + 8 * q;
+    const float4 a = *reinterpret_cast<const float4*>(row);
+    const float4 e = *reinterpret_cast<const float4*>(row + 4);
+    const float l = q > 0 ? act(row[-1]) : -INFINITY;
+    const float a0 = act(a.x), a1 = act(a.y), a2 = act(a.z), a3 = act(a.w);
+    const float e0 = act(e.x), e1 = act(e.y), e2 = act(e.z), e3 = act(e.w);
+    m0 = fmaxf(m0, fmaxf(l, fmaxf(a0, a1)));
+    m1 = fmaxf(m1, fmaxf(a1, fmaxf(a2, a3)));
+    m2 = fmaxf(m2, fmaxf(a3, fmaxf(e0, e1)));
+    m3 = fmaxf(m3, fmaxf(e1, fmaxf(e2, e3)));
+  }
+  y[t] = make_float4(m0, m1, m2, m3);
+}
+
+}  // namespace frh
+
+extern "C" int32_t frh_bn_act_maxpool(const float* x, float* y, const float* gamma, const float* beta,
+                                      const float* mean, const float* var, float eps, int64_t n, int32_t c, int32_t h,
+                                      int32_t w, void* stream) {
+  FRH_REQUIRE(n >= 0 && c >= 1 && h >= 1 && w >= 8, "bad sizes");
+  if (n == 0) return FRH_OK;
+  FRH_REQUIRE(x && y && mean && var, "null pointer argument");
+  FRH_REQUIRE(w % 8 == 0, "width %d must be a multiple of 8", w);
+  FRH_REQUIRE(((uintptr_t)x | (uintptr_t)y) % 16 == 0, "tensors must be 16-byte aligned");
+  const int oh = (h - 1) / 2 + 1;
+  const int64_t total = n * (int64_t)c * oh * (w / 8);
+  const int64_t blocks = (total + kBnThreads - 1) / kBnThreads;
+  FRH_REQUIRE(blocks < ((int64_t)1 << 31), "too many blocks");
+  hipLaunchKernelGGL(bn_act_maxpool_kernel, dim3((unsigned)blocks), dim3(kBnThreads), 0, as_stream(stream), x,
+                     reinterpret_cast<float4*>(y), gamma, beta, mean, var, eps, (int)c, (int)h, (int)w, oh, total);
+  return check_launch("frh_bn_act_maxpool");
+}

@@ -95,6 +95,7 @@ SIGNATURES = {
                                  c_vp]),
     'frh_atss_workspace': (c_size, [c_i32, c_i32, c_i32, c_i32, c_i64]),
     'frh_bn_act': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_i64, c_i32, c_vp]),
+    'frh_bn_act_maxpool': (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_i32, c_i32, c_vp]),
     'frh_loss_workspace': (c_size, []),
     'frh_fpn_merge_nhwc': (c_i32, [c_vp, P(c_i64), c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
     'frh_bias_act_nhwc': (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp]),

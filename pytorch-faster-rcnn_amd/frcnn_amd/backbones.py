@@ -16,7 +16,7 @@ import logging
 import torch
 from torch import nn
 
-from .ops import bn_act
+from .ops import bn_act, bn_act_maxpool
 
 # blocks per stage for each depth
 _STAGE_BLOCKS = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
@@ -70,7 +70,8 @@ class ResNet(nn.Module):
             setattr(self, 'layer{}'.format(s + 1), nn.Sequential(*blocks))
 
     def forward(self, x):
-        x = self.maxpool(bn_act(self.conv1(x), self.bn1))
+        # frozen stem: BN + ReLU + max pool as one HIP pass (ops.bn_act_maxpool)
+        x = bn_act_maxpool(self.conv1(x), self.bn1, self.maxpool)
         outs = []
         for s in range(1, 5):
             x = getattr(self, 'layer{}'.format(s))(x)

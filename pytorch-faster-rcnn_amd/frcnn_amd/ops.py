@@ -968,6 +968,25 @@ def bn_act(x, bn, skip=None, relu=True):
     return _FrozenBNAct.apply(x, skip, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu)
 
 
+def bn_act_maxpool(x, bn, pool):
+    """pool(relu(bn(x))) for the ResNet stem (eval-mode BN, MaxPool2d(3, 2, 1)) in one HIP pass
+    (frh_bn_act_maxpool) when nothing needs a gradient through it (the reference freezes the
+    stem: frozen_stages >= 0); otherwise bn_act then the pool module."""
+    fused = (x.is_cuda and x.dtype == torch.float32 and not bn.training and x.is_contiguous()
+             and x.shape[3] % 8 == 0 and x.shape[3] >= 8
+             and (pool.kernel_size, pool.stride, pool.padding, pool.dilation) in ((3, 2, 1, 1), ((3, 3), (2, 2), (1, 1), (1, 1)))
+             and not pool.ceil_mode and not pool.return_indices
+             and not (torch.is_grad_enabled() and (x.requires_grad or (bn.weight is not None and bn.weight.requires_grad)
+                                                   or (bn.bias is not None and bn.bias.requires_grad))))
+    if not fused:
+        return pool(bn_act(x, bn))
+    n, c, h, w = x.shape
+    y = torch.empty(n, c, (h - 1) // 2 + 1, w // 2, dtype=torch.float32, device=x.device)
+    call('frh_bn_act_maxpool', ptr(x), ptr(y), ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+         ptr(bn.running_var), float(bn.eps), n, c, h, w, stream_of(x))
+    return y
+
+
 # ---------------------------------------------------------------- f1: fused losses
 CLS_FOCAL, CLS_SIGMOID_BCE, CLS_SOFTMAX_CE = 0, 1, 2
 _LOSS_WS = {}

@@ -1331,6 +1331,31 @@ def test_bn_act_matches_torch(dev, skip, relu, shape):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize('shape', [(2, 64, 304, 512), (1, 8, 7, 16), (1, 4, 10, 24)])
+def test_bn_act_maxpool_stem_bit_exact(dev, shape):
+    """ResNet stem: frh_bn_act_maxpool (frozen BN + ReLU + max_pool2d(3, 2, 1) in one pass) equals
+    frh_bn_act followed by torch's max pool bit for bit (even and odd heights, the cfg2 stem
+    shape); with a gradient needed, the unfused ops run."""
+    from frcnn_amd import ops
+    torch.manual_seed(1)
+    C = shape[1]
+    bn = torch.nn.BatchNorm2d(C).to(dev).eval()
+    pool = torch.nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2.0)
+        x = torch.randn(*shape, device=dev)
+        y = ops.bn_act_maxpool(x, bn, pool)
+        ref = pool(ops.bn_act(x, bn))
+    assert y.shape == ref.shape
+    assert torch.equal(y, ref)
+    xg = x.clone().requires_grad_(True)
+    yg = ops.bn_act_maxpool(xg, bn, pool)
+    assert yg.requires_grad and torch.equal(yg.detach(), ref)
+
+
 def test_graphed_trunk_matches_eager(dev):
     """frcnn_amd.graphs: backbone + neck + RPN head convs replayed as one hipGraph give the
     eager trunk's features, RPN outputs and parameter gradients, for the captured batch and
