@@ -51,54 +51,6 @@ __global__ void __launch_bounds__(kBnThreads) bn_act_kernel(const float4* x, con
   }
 }
 
-// Small planes (stages 3-4: 2432 and 608 pixels): one workgroup per plane leaves most of
-// a 256-thread block idle and each block's few loads latency-bound (~5 us per launch
-// whatever the size).  Here a block streams a contiguous range of kBnSmallSpan float4 of
-// the flat [n * C * hw4] array (a float4 never straddles planes: hw % 4 == 0), with the
-// s / b of the few planes it touches computed once into LDS.  Same f32 arithmetic.
-constexpr int kBnSmallSpan = kBnThreads * kBnVec;
-constexpr int kBnSmallPlanes = 64;  // planes a span can touch when hw4 >= 17
-
-__global__ void __launch_bounds__(kBnThreads) bn_act_small_kernel(const float4* x, const float4* skip, float4* y,
-                                                                  const float* __restrict__ gamma,
-                                                                  const float* __restrict__ beta,
-                                                                  const float* __restrict__ mean,
-                                                                  const float* __restrict__ var, float eps, int C,
-                                                                  int hw4, int64_t total4, int relu) {
-  __shared__ float sb[2][kBnSmallPlanes];
-  const int64_t i0 = (int64_t)blockIdx.x * kBnSmallSpan;
-  const int64_t p0 = i0 / hw4;
-  const int np = (int)((min(i0 + kBnSmallSpan, total4) - 1) / hw4 - p0) + 1;
-  if ((int)threadIdx.x < np) {
-    const int c = (int)((p0 + threadIdx.x) % C);
-    const float s = (gamma ? gamma[c] : 1.0f) / sqrtf(var[c] + eps);
-    sb[0][threadIdx.x] = s;
-    sb[1][threadIdx.x] = (beta ? beta[c] : 0.0f) - mean[c] * s;
-  }
-  __syncthreads();
-  float4 v[kBnVec], k[kBnVec];
-#pragma unroll
-  for (int u = 0; u < kBnVec; ++u) {
-    const int64_t i = i0 + u * kBnThreads + threadIdx.x;
-    if (i < total4) {
-      v[u] = x[i];
-      if (skip) k[u] = skip[i];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kBnVec; ++u) {
-    const int64_t i = i0 + u * kBnThreads + threadIdx.x;
-    if (i < total4) {
-      const int q = (int)(i / hw4 - p0);
-      const float s = sb[0][q], b = sb[1][q];
-      float4 r = make_float4(v[u].x * s + b, v[u].y * s + b, v[u].z * s + b, v[u].w * s + b);
-      if (skip) r = make_float4(r.x + k[u].x, r.y + k[u].y, r.z + k[u].z, r.w + k[u].w);
-      if (relu) r = make_float4(fmaxf(r.x, 0.0f), fmaxf(r.y, 0.0f), fmaxf(r.z, 0.0f), fmaxf(r.w, 0.0f));
-      y[i] = r;
-    }
-  }
-}
-
 }  // namespace frh
 
 using namespace frh;
@@ -113,16 +65,6 @@ extern "C" int32_t frh_bn_act(const float* x, const float* skip, float* y, const
   FRH_REQUIRE(((uintptr_t)x | (uintptr_t)y | (uintptr_t)skip) % 16 == 0, "tensors must be 16-byte aligned");
   const int64_t hw4 = hw / 4;
   const int64_t per_block = (int64_t)kBnThreads * kBnVec;
-  if (hw4 < per_block && hw4 * (kBnSmallPlanes - 2) >= per_block) {  // small planes: flat spans
-    const int64_t total4 = n * (int64_t)c * hw4;
-    const int64_t blocks = (total4 + kBnSmallSpan - 1) / kBnSmallSpan;
-    FRH_REQUIRE(blocks < ((int64_t)1 << 31), "too many blocks");
-    hipLaunchKernelGGL(bn_act_small_kernel, dim3((unsigned)blocks), dim3(kBnThreads), 0, as_stream(stream),
-                       reinterpret_cast<const float4*>(x), reinterpret_cast<const float4*>(skip),
-                       reinterpret_cast<float4*>(y), gamma, beta, mean, var, eps, (int)c, (int)hw4, total4,
-                       (int)relu);
-    return check_launch("frh_bn_act");
-  }
   const int64_t tiles = (hw4 + per_block - 1) / per_block;
   FRH_REQUIRE(n * (int64_t)c * tiles < ((int64_t)1 << 31), "too many blocks");
   hipLaunchKernelGGL(bn_act_kernel, dim3((unsigned)(n * c * tiles)), dim3(kBnThreads), 0, as_stream(stream),
