@@ -274,7 +274,7 @@ int32_t frh_rpn_proposals_nms_view(int32_t num_imgs, int32_t num_levels, const i
 
 /* ---- a10: torchvision.ops.nms on pre-sorted segments --------------------------
  * boxes [S, n_max, 4] row-major xyxy, already in descending-score order
- * (stable); count[s] valid rows, n_max <= 65536 (the offset-trick batched_nms of
+ * (stable); count[s] valid rows, n_max <= 184320 (the offset-trick batched_nms of
  * lib/utils.py:211-221 runs one NMS over up to 1000 proposals x 20 classes).
  * keep[s, :] = kept row positions (ascending = score order), keep_counts[s].
  * max_keep >= 0 stops after that many.  Workspace: one upper-triangle suppression

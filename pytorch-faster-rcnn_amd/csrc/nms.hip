@@ -31,7 +31,10 @@
 
 namespace frh {
 
-constexpr int kMaxNmsWords = 1024;  // n <= 65536 boxes per segment
+// n <= 184 320 boxes per segment: the scan's kept sets (23 KB of static LDS) beside its
+// 128-KB staging ring fit a CU's 160 KB, and a segment's mask triangle (tri(nbw) x 512 B)
+// stays below the 2 GB its buffer descriptor's 32-bit offsets address
+constexpr int kMaxNmsWords = 2880;
 
 // The suppression test IoU > thr without the division.  v = RN(inter / union) is
 // a float, so v > thr (double) <=> v >= t_up, the smallest float above thr, <=>
@@ -534,6 +537,7 @@ __device__ __forceinline__ int fz_block_reads(const int* flag, const uint64_t* s
   return __builtin_amdgcn_readfirstlane(f);
 }
 constexpr int kFzMaxSegs = 256;
+constexpr int kFzMaxBlocks = 1024;  // kept sets in LDS: segments of up to 65 536 boxes
 
 __device__ __forceinline__ void fz_setprio(int q) {  // s_setprio takes an immediate
   if (q >= 3) __builtin_amdgcn_s_setprio(3);
@@ -573,8 +577,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
                                                                uint32_t* flags, int max_keep,
                                                                int32_t* __restrict__ keep, int64_t kstride,
                                                                int32_t* __restrict__ kcounts, int64_t* stamps) {
-  // scan: ring [kFzRing][kFzSlotWords] then kept[kMaxNmsWords]; mask: per wave 64 row boxes + areas
-  __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kMaxNmsWords];
+  // scan: ring [kFzRing][kFzSlotWords] then kept[kFzMaxBlocks]; mask: per wave 64 row boxes + areas
+  __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kFzMaxBlocks];
   __shared__ int ready[kFzRing];
   __shared__ int s_resolved, s_stop;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -757,7 +761,7 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
 // s * tri(nbw) (no seg_base); flags: nms_fused_flag_bytes(S, n_max) bytes, zero on entry
 // (left set: the caller zeroes them again before the next call).
 bool nms_fused_fits(int32_t S, int32_t n_max) {
-  return S >= 1 && S <= kFzMaxSegs && n_max >= 1 && (n_max + 63) / 64 <= kMaxNmsWords;
+  return S >= 1 && S <= kFzMaxSegs && n_max >= 1 && (n_max + 63) / 64 <= kFzMaxBlocks;
 }
 
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile + the error word

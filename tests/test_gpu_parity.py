@@ -593,6 +593,38 @@ def test_nms_empty_and_batched(dev):
     np.testing.assert_array_equal(ks.cpu().numpy(), scores[k])
 
 
+@pytest.mark.parametrize('n', [100000, 184320])
+def test_nms_large_segment_structured(dev, n):
+    """Segments past 65 536 boxes (up to the 184 320 limit): kept sets beyond 1024 words and the
+    loaders' global-memory fold of tiles older than the staged span.  Structured input with a
+    known answer (an O(n^2) oracle run is too slow at this size): disjoint 10 x 10 cells, each
+    with a twin shifted by one pixel (IoU 90/110 = 0.818 > 0.7), rows in a random score order;
+    the keep list is every box whose twin comes later.  One past the limit is refused."""
+    from frcnn_amd import ops
+    pairs = n // 2
+    gx = 512
+    cell = np.arange(pairs)
+    x = (cell % gx).astype(np.float32) * 20.0
+    y = (cell // gx).astype(np.float32) * 20.0
+    base = np.stack([x, y, x + 10.0, y + 10.0], 1)
+    twin = base + np.array([1.0, 0.0, 1.0, 0.0], np.float32)
+    boxes = np.concatenate([base, twin]).astype(np.float32)
+    order = np.random.default_rng(n).permutation(n)
+    rows = boxes[order][None]
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)  # row position of box i
+    partner = np.concatenate([np.arange(pairs) + pairs, np.arange(pairs)])
+    want = np.sort(pos[np.arange(n)[pos < pos[partner]]])
+    keep, kc = ops.nms_sorted(T(rows, dev), T(np.array([n], np.int32), dev), n, 0.7)
+    k = int(kc.cpu()[0])
+    assert k == pairs
+    np.testing.assert_array_equal(keep[0, :k].cpu().numpy(), want)
+    if n == 184320:
+        with pytest.raises(RuntimeError, match='exceeds'):
+            ops.nms_sorted(T(np.zeros((1, n + 64, 4), np.float32), dev), T(np.array([n + 64], np.int32), dev),
+                           n + 64, 0.7)
+
+
 @pytest.mark.parametrize('S,max_keep', [(12, -1), (12, 1), (12, 37), (12, 500), (150, 20)])
 def test_nms_sorted_segments_max_keep(dev, S, max_keep):
     """frh_nms_sorted over S pre-sorted segments of ragged counts (0, 1, 63, 64, 65, ...,
