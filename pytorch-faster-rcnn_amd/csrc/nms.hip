@@ -17,6 +17,8 @@
 //        time; the suppression of b's candidates by all earlier kept rows is
 //        one per-lane AND/OR pass over the span plus one ballot, and the
 //        bit-parallel greedy over the 64 candidates is two ballots per round.
+// The RPN proposals run the same mask and scan as ONE launch (nms_fused_kernel, below
+// nms_scan_kernel): mask tiles and per-segment scans together, tile flags between them.
 #include <stdlib.h>
 #include <string.h>
 
