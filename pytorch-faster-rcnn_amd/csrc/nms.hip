@@ -505,8 +505,8 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
 //  not two -- with two, the fold hand-off chain, about 0.9 us per round, bounded the scan to
 //  0.3 us per block); waves 1..7 stage block p (p = wave - 1 mod 7): once the ring slot is
 //  free and column p is complete, the near tiles (p-i, p) and the diagonal (p, p) go to the
-//  slot, and the fold of the kept rows of blocks <= p - 5 (tiles read into registers, eight
-//  per batch, the next batch in flight) into the slot's partial word; then ready = p + 1.
+//  slot, and the fold of the kept rows of blocks <= p - 5 (tiles read into registers, 16
+//  per batch) into the slot's partial word; then ready = p + 1.
 constexpr int kFzThreads = 512;
 constexpr int kFzWaves = kFzThreads / kWave;
 constexpr int kFzLoaders = kFzWaves - 1;
@@ -693,22 +693,28 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int i = 0; i < kFzNear; ++i) nr[i] = p > i ? fz_tile(col + (int64_t)(p - 1 - i) * 64) : 0ull;
     // fold blocks j < jf = p - kFzNear (their kept sets appear as the resolver passes them)
+    // Batches of 16 tile words, branch-free (indices clamped to the last fold tile, extra
+    // words masked out): one memory round trip per 16 tiles.  (Eight per batch with the next
+    // batch prefetched needs 16 more VGPRs than the 64 that 8 waves per SIMD allow, so the
+    // compiler reused the registers and waited for each batch before issuing the next.)
     const int jf = p - kFzNear;
-    uint64_t acc = 0, cur[8], nxt[8];
+    uint64_t acc = 0;
+    if (jf > 0) {
+      const int jl = jf - 1;
+      for (int j0 = 0; j0 < jf; j0 += 16) {
+        uint64_t t[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = u < jf ? fz_tile(col + (int64_t)u * 64) : 0ull;
-    for (int j0 = 0; j0 < jf; j0 += 8) {
+        for (int u = 0; u < 16; ++u) t[u] = fz_tile(col + (int64_t)min(j0 + u, jl) * 64);
+        const int need = min(j0 + 16, jf);
+        if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
+        if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
-      for (int u = 0; u < 8; ++u) nxt[u] = j0 + 8 + u < jf ? fz_tile(col + (int64_t)(j0 + 8 + u) * 64) : 0ull;
-      const int need = min(j0 + 8, jf);
-      if (kStamp && lane == 0 && j0 + 8 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
-      if (kStamp && lane == 0 && j0 + 8 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (j0 + u < jf) acc |= cur[u] & kept[j0 + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < 16; ++u) {
+          const uint64_t k = kept[min(j0 + u, jl)];
+          acc |= (j0 + u < jf) ? (t[u] & k) : 0ull;
+        }
+      }
     }
     uint64_t* slot = ring + (p % kFzRing) * kFzSlotWords + lane;
     slot[0] = acc;
