@@ -5,6 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`python bench.py --gpus N` (N > 1, no torchrun WORLD_SIZE) launches the N ranks itself:
+the parent never touches the GPU; it starts N fresh child processes of this script with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, rank 0 prints the
+line, and the parent exits with the first non-zero child status (stopping the others).
+Under torchrun, an explicit --gpus must equal WORLD_SIZE.
+
 One process per GPU, 2 images per GPU (imgs_per_gpu=2), synthetic 600x1000
 images padded to 608x1024, VOC ground-truth boxes (tests/golden/voc_gts.npz),
 random-init weights.  A step = CascadeRCNN(1 stage).forward_train on the
@@ -462,9 +468,65 @@ def shard_images(world, rank, batch):
     return [(rank * batch + i) % n for i in range(batch)]
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, timeout=None):
+    """Start n ranks of this script as fresh child processes (one per GPU: LOCAL_RANK = rank)
+    and wait for them.  Returns the exit status: 0 if every rank exited 0, else the first
+    failing rank's status (the other ranks are then terminated, so none waits forever in a
+    collective for a dead peer).  The caller must not have initialised the GPU."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status, t0 = 0, time.time()
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print('bench: rank {} exited with {}; stopping the other ranks'.format(procs.index(p), rc),
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        if timeout is not None and time.time() - t0 > timeout and live:
+            for q in live:
+                q.kill()
+            status = status or 124
+        time.sleep(0.05)
+    return status
+
+
+def _selftest_child():
+    """FRCNN_BENCH_SELFTEST=1 (tests/test_distributed.py): a rank reports what the launcher
+    gave it and exits without touching torch; the ranks in FRCNN_BENCH_SELFTEST_FAIL exit 3,
+    the ranks in FRCNN_BENCH_SELFTEST_HANG sleep (a peer that would wait forever)."""
+    rank = int(os.environ['RANK'])
+    print(json.dumps({'rank': rank, 'local_rank': int(os.environ['LOCAL_RANK']),
+                      'world': int(os.environ['WORLD_SIZE']), 'master': os.environ['MASTER_ADDR'],
+                      'port': int(os.environ['MASTER_PORT'])}), flush=True)
+    if str(rank) in os.environ.get('FRCNN_BENCH_SELFTEST_FAIL', '').split(','):
+        sys.exit(3)
+    if str(rank) in os.environ.get('FRCNN_BENCH_SELFTEST_HANG', '').split(','):
+        time.sleep(600)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='GPUs (= ranks, one process each) of this node; default 1, or WORLD_SIZE under torchrun')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=2, help='images per GPU (imgs_per_gpu=2 in cfg2)')
@@ -486,11 +548,23 @@ def main():
                          '+5.8%% img/s on cfg2 fwd, ~1 min of search).  auto = on for fwd, off for train (the '
                          'backward-convolution search takes several minutes)')
     ap.add_argument('--no-conv-search', dest='conv_search', action='store_const', const='off')
+    ap.add_argument('--dump-rois', help='after the timed region, save the last RoIAlign launch\'s RoIs / levels / '
+                         'level shapes / scales to this .npz (tests/golden/cfg2_rois_train.npz: the RoIs of a '
+                         'training step, for tools/bench_roi_sets.py and the bit-exact RoIAlign test)')
     ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
                     help='replay backbone + neck + RPN head convs as one captured hipGraph (frcnn_amd.graphs) '
                          'after the warmup.  auto = on for fwd with a two-stage detector, off for train')
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' in os.environ:  # torchrun (or launch_ranks) started this rank
+        if args.gpus is not None and args.gpus != int(os.environ['WORLD_SIZE']):
+            raise SystemExit('bench: --gpus {} disagrees with WORLD_SIZE {}'.format(args.gpus,
+                                                                                os.environ['WORLD_SIZE']))
+        if os.environ.get('FRCNN_BENCH_SELFTEST') == '1':
+            return _selftest_child()
+    elif (args.gpus or 1) > 1:
+        # launch the ranks ourselves; nothing here has touched the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -588,6 +662,7 @@ def main():
     roi_timed_us = [1e3 * e[0].elapsed_time(e[1]) for e in timed_roi]
     roi_span_us = [span_of(e[2]) for e in timed_roi]
     assert torch.isfinite(loss).all()
+    ops.check_device_status(dev)  # the one-launch kernels' in-launch waits all completed (FRH_DEVERR_*)
     t_max = max_over_ranks(elapsed, dev, world)
 
     # ---- after the timed region: kernel lines (rank 0 only; other ranks idle)
@@ -605,6 +680,10 @@ def main():
         steps_traced = max(args.trace_steps, 1)
         recs = list(ops.ROI_ALIGN_PROFILE['records'])
         nrecs = list(ops.NMS_PROFILE['records'])
+        if args.dump_rois and recs:
+            _, _, r_rois, r_lv, r_shapes, _, _, r_scales, _ = recs[-1]
+            np.savez_compressed(args.dump_rois, r5=r_rois.cpu().numpy(), lv=r_lv.cpu().numpy(),
+                                shapes=np.array(r_shapes, np.int64), scales=np.array(r_scales, np.float32))
         per_group, det_us, group_names, det_kernels = (summarise_trace(trace, steps_traced) if trace else
                                                         ({}, None, {}, {}))
         roi_launches = [(n, us) for n, us in (trace or []) if 'roi_align_fwd' in n]

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FRH_ABI_VERSION 1
+#define FRH_ABI_VERSION 2
 
 #define FRH_OK 0
 #define FRH_EINVAL (-1)
@@ -39,6 +39,19 @@ extern "C" {
 
 int32_t frh_abi_version(void);
 const char* frh_last_error(void);
+
+/* Device status word (ABI 2).  The one-launch kernels of frh_rpn_proposals* and
+ * frh_sample_random hand data between the workgroups of ONE launch through bounded
+ * in-launch waits, sized to the device's resident capacity (CU count x occupancy, queried
+ * per device).  A wait that runs out -- a workgroup it needs was never scheduled, e.g. beside
+ * other kernels or on a partitioned GPU -- ORs one of these bits into the caller's device
+ * int32 `status` word and ends that workgroup's work: the call's outputs are then undefined
+ * and the workspace's zero region may be left dirty (re-zero it).  The library never reads
+ * the word: the caller checks it where it synchronises anyway (frcnn_amd: the loss read, the
+ * numpy sampler's count read, or after every call with FRCNN_AMD_DEBUG=1) and clears it. */
+#define FRH_DEVERR_SELECT_BARRIER 1   /* rpn_select_kernel: a segment barrier timed out */
+#define FRH_DEVERR_NMS_COLUMN 2       /* nms_fused_kernel: a mask column never completed */
+#define FRH_DEVERR_SAMPLER_BARRIER 4  /* sampler_fused_kernel: an image barrier timed out */
 
 /* ---- a1: AnchorCreator.__call__ over all FPN levels in one launch ------------
  * Replaces lib/anchor.py:107-129 (called per level from
@@ -110,11 +123,12 @@ int32_t frh_maxiou_assign(int32_t num_segs, const float* boxes, int64_t box_ld,
  *      without a compaction pass over every box. */
 size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes);
 /* frh_sample_random's workspace contract: its leading frh_sample_zero_bytes(num_segs) bytes
- * are zero before the call and every call leaves them zero (images above 16 384 boxes take
- * a one-launch sampler whose per-image counters and histograms live there and are reset by
- * the launch's last workgroup), so a caller zero-fills the buffer once and reuses it for
- * calls ordered on one stream.  A word in it that stays nonzero after a call flags a
- * workgroup that waited out its bounded in-launch barrier (never seen). */
+ * (the same for every num_segs <= 64: nothing else is placed there) are zero before the call
+ * and every completed call leaves them zero (images above 16 384 boxes take a one-launch
+ * sampler whose per-image counters and histograms live there and are reset by the launch's
+ * last workgroup), so a caller zero-fills the buffer once and reuses it for calls ordered on
+ * one stream, whatever their num_segs.  After FRH_DEVERR_SAMPLER_BARRIER, re-zero it.
+ * num_segs <= 64. */
 size_t frh_sample_zero_bytes(int32_t num_segs);
 int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                               const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
@@ -128,7 +142,8 @@ int32_t frh_sample_apply(int32_t num_segs, const int64_t* labels_in, int64_t lab
 int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                           const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
                           int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
-                          int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream);
+                          int32_t* sel_counts, int32_t* status, void* workspace, size_t ws_bytes,
+                          void* stream);
 
 /* ---- a6: anchor_target (lib/anchor.py:11-76) after assign+sample -------------
  * Chosen = boxes with sampled label >= 0, ascending.  Segment outputs are
@@ -238,7 +253,8 @@ int32_t frh_param2bbox(const float* base, int64_t ldb, const float* param, int64
  * in (score desc, concat order) order.  cls level l: [B, C*A, H_l, W_l],
  * reg level l: [B, 4*A, H_l, W_l]; anchors [4, anchor_ld] from
  * frh_anchor_grid.  img_hw / min_size are host arrays [B*2] / [B].
- * Outputs: boxes [B, 4, max_num], scores [B, max_num], counts [B] (device). */
+ * Outputs: boxes [B, 4, max_num], scores [B, max_num], counts [B] (device).
+ * status: the device status word (FRH_DEVERR_SELECT_BARRIER, FRH_DEVERR_NMS_COLUMN). */
 size_t frh_rpn_proposals_workspace(int32_t num_imgs, int32_t num_levels,
                                    const int32_t* grid_hw, int32_t num_anchors,
                                    int32_t pre_nms);
@@ -248,7 +264,7 @@ int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* con
                           int64_t anchor_ld, const float* means, const float* stds,
                           const float* img_hw, const float* min_size, int32_t pre_nms,
                           int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                          float* out_scores, int32_t* out_counts, void* workspace,
+                          float* out_scores, int32_t* out_counts, int32_t* status, void* workspace,
                           size_t ws_bytes, void* stream);
 
 /* The same for head outputs of any layout (NCHW or the channels-last outputs of an NHWC
@@ -262,8 +278,8 @@ int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_levels, const fl
                                   int64_t anchor_ld, const float* means, const float* stds,
                                   const float* img_hw, const float* min_size, int32_t pre_nms,
                                   int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                  float* out_scores, int32_t* out_counts, void* workspace,
-                                  size_t ws_bytes, void* stream);
+                                  float* out_scores, int32_t* out_counts, int32_t* status,
+                                  void* workspace, size_t ws_bytes, void* stream);
 
 /* Measurement hook: byte offsets in the frh_rpn_proposals workspace of its per-level
  * NMS input (out[0] boxes [S, P, 4] in descending-score order, out[1] counts [S]
@@ -396,6 +412,21 @@ int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
                                   const float* rois, const int64_t* roi_levels, int64_t num_rois,
                                   int32_t pooled_h, int32_t pooled_w, int32_t sampling_ratio,
                                   int32_t aligned, const float* grad_out, void* stream);
+
+/* Deterministic backward (parity runs; SURVEY §5 race detection): the gradient of
+ * frh_roi_align_bwd_strided, accumulated in fixed point -- int64 in units of 2^-40, each
+ * (RoI, row, column) partial sum rounded once and added with integer atomics, which are
+ * associative -- so the result is bit-identical across runs whatever order the RoIs are
+ * scheduled in (float atomics reorder sums).  acc_feats: per level an int64 buffer with the
+ * element strides of grad_feats, zeroed by the caller; grad_feats (dense: every element is
+ * written) = acc * 2^-40 rounded to f32.  |gradient element| < 2^23.  sampling_ratio 2 and
+ * up to 8 x 8 bins (the reference configs' 7 x 7). */
+int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* grad_feats, int64_t* const* acc_feats,
+                                const int32_t* feat_hw, const int64_t* strides, const float* scales,
+                                int32_t batch, int32_t channels, const float* rois,
+                                const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
+                                int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                                const float* grad_out, void* stream);
 
 /* ---- RoIPool (torchvision.ops.RoIPool; C4 config configs/faster_rcnn_r50.py:26) --
  * feat [B, C, H, W] with element strides strides[0..3] = (b, c, y, x); rois

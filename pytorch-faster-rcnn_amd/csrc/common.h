@@ -36,6 +36,13 @@ int32_t check_launch(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Workgroups of `kernel` (block threads, dynamic LDS bytes) the current device holds at
+// once: its CU count x hipOccupancyMaxActiveBlocksPerMultiprocessor, cached per (device,
+// kernel).  The one-launch kernels whose workgroups wait for each other size their grids
+// from it (a partitioned GPU has fewer CUs).  0 when the query fails: callers then take
+// their multi-launch forms.
+int resident_capacity(const void* kernel, int block, size_t dyn_lds = 0);
+
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------- box math

@@ -496,10 +496,15 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(const uint64_t* __restric
 //  Hand-off (hand-off table row 1): a mask wave writes its 64 column words with sc1 stores,
 //  waits vmcnt(0), then sets its tile's flag word (sc1 store); a loader polls a column's
 //  flags and reads its tiles with sc1 loads.  Flags are zero on entry (the caller's
-//  memset).  Mask workgroups wait for nothing, so no residency is assumed: a scan
-//  workgroup only waits for mask workgroups, which always finish (S <= kFzMaxSegs leaves
-//  every CU room for them).  Every global wait is bounded (kSpinTicks): a broken
-//  assumption sets the error word and ends the kernel, never hangs it.
+//  memset).  Mask workgroups wait for nothing; a scan workgroup waits only for mask
+//  workgroups, but workgroups are dispatched in order, so no mask workgroup starts before
+//  all S scan workgroups have: the S scan workgroups must be resident together with room
+//  left for mask workgroups.  The host admits S <= a quarter of the device's resident
+//  capacity of this kernel (nms_fused_fits: CU count x occupancy; 256 on a whole MI355X).
+//  Every global wait is bounded (kSpinTicks): a wait that runs out ORs
+//  FRH_DEVERR_NMS_COLUMN into the caller's status word and ends the scan workgroup's work
+//  (the loader sets s_stop = -1 and wakes the resolver, which then stops and releases the
+//  other loaders) -- never a hang, never a keep list from tiles that were not published.
 //  Scan workgroup: wave 0 resolves as nms_scan_kernel's resolver, but ORs in FOUR near
 //  tiles itself (p-1 .. p-4: the loaders' fold then waits for the resolver four blocks back,
 //  not two -- with two, the fold hand-off chain, about 0.9 us per round, bounded the scan to
@@ -551,8 +556,10 @@ __device__ __forceinline__ void fz_setprio(int q) {  // s_setprio takes an immed
 // the words come from other XCDs' write-through stores either way)
 __device__ __forceinline__ uint64_t fz_tile(const uint64_t* p) { return xwg_load(p); }
 
-// wait until the flags of tiles (0..p, p) -- contiguous from col_flags -- are all set
-__device__ __forceinline__ void fz_wait_column(const uint32_t* col_flags, int p, int lane, uint32_t* err) {
+// wait until the flags of tiles (0..p, p) -- contiguous from col_flags -- are all set;
+// false when the wait ran out (status flagged) or the workgroup is stopping (s_stop < 0)
+__device__ __forceinline__ bool fz_wait_column(const uint32_t* col_flags, int p, int lane, int32_t* status,
+                                               int* s_stop) {
   for (int j0 = 0; j0 <= p; j0 += kWave) {
     const int cnt = min(kWave, p + 1 - j0);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -560,12 +567,14 @@ __device__ __forceinline__ void fz_wait_column(const uint32_t* col_flags, int p,
       const uint32_t v = lane < cnt ? xwg_load(col_flags + j0 + lane) : 1u;
       if (!__ballot(v == 0u)) break;
       __builtin_amdgcn_s_sleep(1);
+      if (lds_poll(s_stop) < 0) return false;
       if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-        if (lane == 0) atomicOr(err, 1u);
-        return;
+        if (lane == 0) atomicOr(status, FRH_DEVERR_NMS_COLUMN);
+        return false;
       }
     }
   }
+  return true;
 }
 
 // kStamp (tools-only timing build): s_memrealtime per (segment, block) at stamps +
@@ -578,7 +587,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
                                                                int n_max, int nbw, NmsThr T, uint64_t* mask,
                                                                uint32_t* flags, int max_keep,
                                                                int32_t* __restrict__ keep, int64_t kstride,
-                                                               int32_t* __restrict__ kcounts, int64_t* stamps) {
+                                                               int32_t* __restrict__ kcounts, int32_t* status,
+                                                               int64_t* stamps) {
   // scan: ring [kFzRing][kFzSlotWords] then kept[kFzMaxBlocks]; mask: per wave 64 row boxes + areas
   __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kFzMaxBlocks];
   __shared__ int ready[kFzRing];
@@ -586,7 +596,6 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int64_t tri = tri_tiles(nbw);
-  uint32_t* err = flags + (int64_t)S * tri;
   if ((int)blockIdx.x >= S) {
     // ---------------- mask: one tile per wave
     const int64_t g = ((int64_t)blockIdx.x - S) * kFzWaves + wave;
@@ -601,7 +610,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     cb = __builtin_amdgcn_readfirstlane(cb);
     fz_setprio(2 - min(2, (3 * cb) / nbw));
     const float4* bx = reinterpret_cast<const float4*>(boxes + (int64_t)s * seg_stride);
-    const int n = counts[s];
+    const int n = min(max(counts[s], 0), n_max);  // clamped: memory-safe after a flagged upstream abort
     const float4 r = bx[min(rb * 64 + lane, n_max - 1)];
     const float4 a = bx[min(cb * 64 + lane, n_max - 1)];
     if (rb * 64 >= n || cb * 64 >= n) return;
@@ -618,7 +627,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
   }
   // ---------------- scan of segment s
   const int s = blockIdx.x;
-  const int n = counts[s];
+  const int n = min(max(counts[s], 0), n_max);
   const int nb = (n + 63) >> 6;
   uint64_t* ring = fz_lds;
   uint64_t* kept = fz_lds + kFzRing * kFzSlotWords;
@@ -639,6 +648,11 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       if (fz_block_reads(&ready[b % kFzRing], slot, pw, nr, d) != b + 1) {
         while (lds_poll(&ready[b % kFzRing]) != b + 1) __builtin_amdgcn_s_sleep(1);
         fz_block_reads(&ready[b % kFzRing], slot, pw, nr, d);
+      }
+      if (lds_poll(&s_stop) < 0) {  // a loader's wait ran out (status flagged): stop, release the loaders
+        if (lane == 0)
+          __hip_atomic_store(&s_resolved, nb + kFzRing + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
       }
       uint64_t acc = pw;
 #pragma unroll
@@ -685,7 +699,16 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     if (s_stop < p) break;
     const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
     if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    fz_wait_column(sflags + c0, p, lane, err);
+    if (!fz_wait_column(sflags + c0, p, lane, status, &s_stop)) {
+      // stop the workgroup: s_stop < 0 first, then wake the resolver on this block's flag (LDS is
+      // served in order: the resolver sees s_stop once it sees the flag)
+      if (lane == 0) {
+        __hip_atomic_store(&s_stop, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
+        lds_flag(&ready[p % kFzRing], p + 1);
+      }
+      break;
+    }
     if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
     const uint64_t* col = smask + c0 * 64 + lane;
     const uint64_t d = fz_tile(col + (int64_t)p * 64);
@@ -767,30 +790,33 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
 
 // One-launch NMS (nms_fused_kernel) of S segments at most n_max boxes each, tiles at
 // s * tri(nbw) (no seg_base); flags: nms_fused_flag_bytes(S, n_max) bytes, zero on entry
-// (left set: the caller zeroes them again before the next call).
+// (left set: the caller zeroes them again before the next call).  S scan workgroups must be
+// resident beside mask workgroups: at most a quarter of the device's capacity of the kernel.
 bool nms_fused_fits(int32_t S, int32_t n_max) {
-  return S >= 1 && S <= kFzMaxSegs && n_max >= 1 && (n_max + 63) / 64 <= kFzMaxBlocks;
+  return S >= 1 && S <= kFzMaxSegs && n_max >= 1 && (n_max + 63) / 64 <= kFzMaxBlocks &&
+         S <= resident_capacity(reinterpret_cast<const void*>(nms_fused_kernel<false>), kFzThreads) / 4;
 }
 
-size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile + the error word
+size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+ one spare)
   return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
 }
 
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                         uint64_t* mask, uint32_t* flags, hipStream_t st, int64_t* stamps = nullptr) {
+                         uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps = nullptr) {
   FRH_REQUIRE(nms_fused_fits(S, n_max), "one-launch NMS: %d segments of %d boxes out of range", S, n_max);
+  FRH_REQUIRE(status, "null status word");
   const int nbw = (n_max + 63) / 64;
   const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves;
   FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many mask tiles");
   if (stamps)
     hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       stamps);
+                       status, stamps);
   else
     hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       nullptr);
+                       status, nullptr);
   return check_launch("nms_fused");
 }
 

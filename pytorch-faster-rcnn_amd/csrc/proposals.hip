@@ -23,7 +23,8 @@ bool nms_fused_fits(int32_t S, int32_t n_max);
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                         uint64_t* mask, uint32_t* flags, hipStream_t st, int64_t* stamps = nullptr);
+                         uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st,
+                         int64_t* stamps = nullptr);
 
 constexpr int kPropThreads = 1024;
 constexpr int kMaxSort = 16384;
@@ -49,6 +50,7 @@ struct PropArgs {
   float4* stage;       // [S][kRpnSelFused] boxes decoded at selection (fused path)
   int32_t* sel_count; // [S]
   int64_t* stamps;    // tools timing only (null in the product): rpn_select_kernel phase times
+  int32_t* status;    // the caller's device status word (include/frcnn_amd.h FRH_DEVERR_*)
 };
 
 struct ImgArgs {
@@ -307,7 +309,6 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_collect_kernel(PropArgs
 // the grid row returns at once.  Selection rule, record layout and the order are
 // those of the four-launch path (bit-identical outputs).
 constexpr int kSelRankPer = 64;    // records ordered per workgroup
-constexpr int kSelMaxResident = 768;  // 3/4 of 256 CUs x 4 workgroups (TkSmem: 35 KB of LDS each)
 constexpr int kRpnTieCap = 2048;   // prefix ties sorted in LDS; more: workgroup 0's radix select
 
 __host__ __device__ __forceinline__ int rpn_sel_groups(int n, int pre_nms) {
@@ -336,7 +337,6 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
   stamp(0);
   const int k = rpn_k(p, n);
   int32_t* st = b.state + seg * TK_WORDS;
-  int32_t* err = st + TK_ERR;
   int32_t* bar = b.state + tk_bars_offset((int)gridDim.y) + seg * kBarWords;  // its own line
   const int64_t base = (int64_t)x * kTkChunk;
   const bool has_keys = base < n;
@@ -399,7 +399,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     for (int r = 0; r < kTkPerThread; ++r) key[r] = 0u;
   }
   stamp(1);
-  seg_barrier(bar + 0, G, err);
+  if (!seg_barrier(bar + 0, G, p.status, FRH_DEVERR_SELECT_BARRIER)) return;
   stamp(2);
 
   // ---- phase 2: bucket b1 (every workgroup reads the same final histogram), then b2
@@ -423,7 +423,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
       }
     }
     stamp(4);
-    seg_barrier(bar + 1, G, err);
+    if (!seg_barrier(bar + 1, G, p.status, FRH_DEVERR_SELECT_BARRIER)) return;
     stamp(5);
     tk_find(sm, kTkBins2, k1, [&](int i) { return xwg_load(gh2 + i); });
     plan.P = (b1 << 12) | (uint32_t)sm.bin;
@@ -461,7 +461,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
     }
   }
   stamp(8);
-  seg_barrier(bar + 2, G, err);
+  if (!seg_barrier(bar + 2, G, p.status, FRH_DEVERR_SELECT_BARRIER)) return;
   stamp(9);
 
   // ---- phase 4: every record of the segment in LDS (the prefix ties ordered here)
@@ -488,7 +488,7 @@ static __global__ void __launch_bounds__(kTkThreads) rpn_select_kernel(PropArgs 
                   rpn_record(key_at(i), i, rpn_big_enough(bx, ia.min_size[bi]), nabove + j));
       }
     }
-    seg_barrier(bar + 3, G, err);
+    if (!seg_barrier(bar + 3, G, p.status, FRH_DEVERR_SELECT_BARRIER)) return;
     for (int j = t; j < kv; j += kTkThreads) rec[j] = xwg_load(grec + j);
   } else {
     {  // every record load of this thread in flight at once (<= kRpnSelFused / 256 = 8)
@@ -800,9 +800,9 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            const int32_t* grid_hw, int32_t num_anchors, int32_t cls_channels, const float* anchors,
                            int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
-                           float* out_boxes, float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
-                           void* stream, bool select_launches, int64_t* select_stamps = nullptr,
-                           bool nms_launches = false);
+                           float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
+                           void* workspace, size_t ws_bytes, void* stream, bool select_launches,
+                           int64_t* select_stamps = nullptr, bool nms_launches = false);
 
 struct PropLayout {
   int P;
@@ -877,8 +877,8 @@ extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_level
                                              int64_t anchor_ld, const float* means, const float* stds,
                                              const float* img_hw, const float* min_size, int32_t pre_nms,
                                              int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                             float* out_scores, int32_t* out_counts, void* workspace,
-                                             size_t ws_bytes, void* stream);
+                                             float* out_scores, int32_t* out_counts, int32_t* status,
+                                             void* workspace, size_t ws_bytes, void* stream);
 
 extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                      const float* const* reg_ptrs, const int32_t* grid_hw, int32_t num_anchors,
@@ -886,7 +886,7 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
                                      const float* means, const float* stds, const float* img_hw,
                                      const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num,
                                      double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
-                                     void* workspace, size_t ws_bytes, void* stream) {
+                                     int32_t* status, void* workspace, size_t ws_bytes, void* stream) {
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS && grid_hw, "bad level count %d", num_levels);
   int64_t cs[4 * FRH_MAX_LEVELS], rs[4 * FRH_MAX_LEVELS];
   for (int l = 0; l < num_levels; ++l) {  // contiguous [B, R*A, H, W]
@@ -897,7 +897,8 @@ extern "C" int32_t frh_rpn_proposals(int32_t num_imgs, int32_t num_levels, const
   }
   return frh_rpn_proposals_strided(num_imgs, num_levels, cls_ptrs, reg_ptrs, cs, rs, grid_hw, num_anchors,
                                    cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms, post_nms,
-                                   max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes, stream);
+                                   max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
+                                   stream);
 }
 
 extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
@@ -907,12 +908,12 @@ extern "C" int32_t frh_rpn_proposals_strided(int32_t num_imgs, int32_t num_level
                                              int64_t anchor_ld, const float* means, const float* stds,
                                              const float* img_hw, const float* min_size, int32_t pre_nms,
                                              int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                             float* out_scores, int32_t* out_counts, void* workspace,
-                                             size_t ws_bytes, void* stream) {
+                                             float* out_scores, int32_t* out_counts, int32_t* status,
+                                             void* workspace, size_t ws_bytes, void* stream) {
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
-                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes,
-                                 stream, false);
+                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace,
+                                 ws_bytes, stream, false);
 }
 
 // select_launches: the four-launch selection even where the one-launch one applies
@@ -923,14 +924,14 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* anchors, int64_t anchor_ld, const float* means, const float* stds,
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
-                                int32_t* out_counts, void* workspace, size_t ws_bytes, void* stream,
+                                int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes, void* stream,
                                 bool select_launches, int64_t* select_stamps, bool nms_launches) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
   FRH_REQUIRE(cls_channels == 1 || cls_channels == 2, "cls_channels must be 1 (sigmoid) or 2 (softmax)");
   FRH_REQUIRE(cls_ptrs && reg_ptrs && grid_hw && anchors && img_hw && min_size && out_boxes && out_scores &&
-                  out_counts && means && stds,
+                  out_counts && means && stds && status,
               "null pointer argument");
   PropLayout z = prop_layout(num_imgs, num_levels, grid_hw, num_anchors, pre_nms);
   FRH_REQUIRE(z.P <= kMaxSort, "per-level candidate count %d exceeds %d (set pre_nms)", z.P, kMaxSort);
@@ -975,6 +976,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   p.stage = reinterpret_cast<float4*>(ws + z.stage);
   p.sel_count = reinterpret_cast<int32_t*>(ws + z.cnt);
   p.stamps = select_stamps;
+  p.status = status;
   // per-image sizes travel by value in the kernel arguments
   ImgArgs ia{};
   for (int b = 0; b < num_imgs; ++b) {
@@ -994,14 +996,16 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   const dim3 grid((unsigned)((z.nmax + kTkChunk - 1) / kTkChunk), (unsigned)S);
   const bool fused = z.P <= kRpnSelFused && z.nmax < (1 << 20);  // record layout limits
   // one-launch selection: every segment's workgroups resident together (seg_barrier): the
-  // grid's live workgroups stay within what 256 CUs hold at 4 per CU (TkSmem: ~35 KB LDS)
+  // grid's live workgroups stay within 3/4 of what the device holds of this kernel (CU
+  // count x occupancy; TkSmem ~35 KB of LDS: 4 per CU on a whole MI355X = 1024)
   int gx = 1, live_wgs = 0;
   for (int l = 0; l < num_levels; ++l) {
     const int g = rpn_sel_groups(num_anchors * p.h[l] * p.w[l], pre_nms);
     gx = g > gx ? g : gx;
     live_wgs += g * num_imgs;
   }
-  if (fused && live_wgs <= kSelMaxResident && !select_launches) {
+  if (fused && live_wgs <= resident_capacity(reinterpret_cast<const void*>(rpn_select_kernel), kTkThreads) * 3 / 4 &&
+      !select_launches) {
     hipLaunchKernelGGL(rpn_select_kernel, dim3((unsigned)gx, (unsigned)S), dim3(kTkThreads), 0, st, p, ia, tb);
   } else {
   hipLaunchKernelGGL(rpn_keys_kernel, grid, dim3(kTkThreads), 0, st, p, tb);
@@ -1024,7 +1028,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   uint64_t* nmask = reinterpret_cast<uint64_t*>(ws + z.mask);
   if (!nms_launches && nms_fused_fits(S, z.P))
     r = launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou, (post_nms > 0) ? post_nms : -1,
-                         keep, z.P, kcnt, nmask, reinterpret_cast<uint32_t*>(ws + z.nflags), st);
+                         keep, z.P, kcnt, nmask, reinterpret_cast<uint32_t*>(ws + z.nflags), status, st);
   else
     r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
                           (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask, nullptr, st);

@@ -27,6 +27,8 @@
 
 namespace frh {
 
+constexpr int kBandCells = 208;  // the band kernel's slab: 13 KB = 208 cells x 16 channels
+
 // region.py:256-264: floor(log2(sqrt(area) / finest + 1e-6)) clamped to [0, L-1]
 __device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, float y2, float finest, int L) {
   float area = ((x2 - x1) + 1.0f) * ((y2 - y1) + 1.0f);
@@ -154,15 +156,22 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     else
       hipLaunchKernelGGL(kern, grid, block, 0, st, lv, c, out);
   };
-  if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
-    // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels), 16-B DMA
+  if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
+    // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels), the
+    // window staged in row bands of [cell][16 channels], 64 B per cell and request
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
     const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
     if (span)
-      go(roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, true>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true>, grid, dim3(kWave));
     else
-      go(roi_align_fwd_quad_kernel<kCpolNT, false, 3>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells>, grid, dim3(kWave));
+  } else if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
+    // channels-last, shapes the band kernel does not take: one quad per 16-B DMA lane
+    const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
+    FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
+    const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
+    go(roi_align_fwd_quad_kernel<kCpolNT, false, 3>, grid, dim3(kWave));
   } else if (pair_ok(f, channels, pooled_h, pooled_w)) {
     // chunk-major XCD order, nt output stores, one 6.5 KB slab per wave, lean tap state
     const int64_t total = num_rois * ((channels + kPairChunk - 1) / kPairChunk);
@@ -220,12 +229,53 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
   if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
-    hipLaunchKernelGGL(roi_align_bwd_sep_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
+    hipLaunchKernelGGL(roi_align_bwd_sep_kernel<false>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
+                       grad_out);
   else if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
     hipLaunchKernelGGL(roi_align_bwd_lds_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   else
     hipLaunchKernelGGL(roi_align_bwd_kernel, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c, grad_out);
   return check_launch("frh_roi_align_bwd");
+}
+
+extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* grad_feats, int64_t* const* acc_feats,
+                                           const int32_t* feat_hw, const int64_t* strides, const float* scales,
+                                           int32_t batch, int32_t channels, const float* rois,
+                                           const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
+                                           int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
+                                           const float* grad_out, void* stream) {
+  int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
+  if (r) return r;
+  FRH_REQUIRE(grad_feats && acc_feats, "null pointer argument");
+  FRH_REQUIRE(sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt,
+              "the deterministic backward takes sampling_ratio 2 and up to %d x %d bins", kSepEnt / 4, kSepEnt / 4);
+  RoiLevels lv;
+  // the kernel adds into the accumulators through lv.grad (same element strides)
+  r = make_levels(num_levels, nullptr, reinterpret_cast<float* const*>(acc_feats), feat_hw, strides, scales, &lv);
+  if (r) return r;
+  hipStream_t st = as_stream(stream);
+  int64_t numel[FRH_MAX_LEVELS];
+  for (int l = 0; l < num_levels; ++l) {
+    FRH_REQUIRE(grad_feats[l] && acc_feats[l], "null level buffer");
+    const int64_t n = (int64_t)batch * channels * lv.h[l] * lv.w[l];
+    const int64_t last = (int64_t)(batch - 1) * lv.sb[l] + (int64_t)(channels - 1) * lv.sc[l] +
+                         (int64_t)(lv.h[l] - 1) * lv.sy[l] + (int64_t)(lv.w[l] - 1) * lv.sx[l];
+    FRH_REQUIRE(lv.sb[l] > 0 && lv.sc[l] > 0 && lv.sy[l] > 0 && lv.sx[l] > 0 && last == n - 1,
+                "level %d: the deterministic backward needs dense gradient buffers", l);
+    numel[l] = n;
+  }
+  if (num_rois > 0) {
+    FRH_REQUIRE(grad_out, "null grad_out");
+    RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
+    hipLaunchKernelGGL(roi_align_bwd_sep_kernel<true>, grid, dim3(kRoiThreads), 0, st, lv, c, grad_out);
+  }
+  for (int l = 0; l < num_levels; ++l) {
+    const int64_t blocks = std::min<int64_t>((numel[l] + 255) / 256, 4096);
+    hipLaunchKernelGGL(roi_bwd_fixed_to_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const long long*>(acc_feats[l]), grad_feats[l], numel[l]);
+  }
+  return check_launch("frh_roi_align_bwd_fixed");
 }
 
 static void dense_strides(int32_t L, const int32_t* hw, int32_t C, int32_t layout, int64_t* st) {

@@ -476,13 +476,12 @@ struct PairLane {
   int rsrc, csrc;
   float fyh[2], fyl[2], fxh[2], fxl[2];
   uint32_t tb0[2][2], tdq[2], tdr[2];
+  int rlo, rhi;  // slab rows of the bin's valid samples (INT_MAX / -1: none, or an idle lane)
+  uint32_t vmask;  // bit 2 iy + ix: sample (iy, ix) valid (tb0 meaningful)
 };
 
 // kUnit: bytes of one cell's entry in a slab region (8: a channel pair; 16: a quad).
-// kSwz (quad slabs): slab column of window column q is q + q / 8 -- one hole per 8 units --
-// so the 16-B tap reads of bins two columns apart (c and c + 8 units) fall on different
-// LDS bank groups (ds_read_b128 serves 8 lanes per cycle over 8 groups of 4 banks).
-template <int kUnit = 8, bool kSwz = false>
+template <int kUnit = 8>
 __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c, const RoiRaw& raw, int lane,
                                            PairGeom& G, PairLane& P) {
   constexpr int SR = 2;
@@ -518,9 +517,8 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
   G.dx = dx;
   G.R = dy ? y1 - y0 + 1 : nly;
   G.Cs = dx ? x1 - x0 + 1 : nlx;
-  auto pc = [](int q) { return kSwz ? q + (q >> 3) : q; };
   // slab row stride: odd, so the tap reads of a wave spread over the banks
-  G.Cs2 = kSwz ? ((pc(G.Cs - 1) + 1) | 1) : (G.Cs | 1);
+  G.Cs2 = G.Cs | 1;
   // feature byte offsets of slab row / column `lane`
   P.rsrc = (dy ? y0 + min(lane, G.R - 1) : (yrow >= 0 ? yrow : y0)) * G.sy * 4;
   P.csrc = (dx ? x0 + min(lane, G.Cs - 1) : (xcol >= 0 ? xcol : x0)) * G.sx * 4;
@@ -528,12 +526,19 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
   // and tap bases + row / column deltas
   const int bin = lane < nbins ? lane : 0;
   const int py = (int)(((uint32_t)bin * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bin - py * c.pw;
+  P.rlo = 0x7fffffff;
+  P.rhi = -1;
+  P.vmask = 0u;
 #pragma unroll
   for (int iy = 0; iy < SR; ++iy) {
     const Tap a = make_tap(pos_y(py, iy), H);
     P.fyh[iy] = a.valid ? a.h : 0.f;
     P.fyl[iy] = a.valid ? a.l : 0.f;
     const int r0 = dy ? a.lo - y0 : 2 * (py * SR + iy), r1 = dy ? a.hi - y0 : 2 * (py * SR + iy) + 1;
+    if (a.valid && lane < nbins) {
+      P.rlo = min(P.rlo, r0);
+      P.rhi = max(P.rhi, r1);
+    }
     P.tdr[iy] = (uint32_t)kUnit * (uint32_t)((r1 - r0) * G.Cs2);
 #pragma unroll
     for (int ix = 0; ix < SR; ++ix) {
@@ -542,9 +547,10 @@ __device__ __forceinline__ void pair_setup(const RoiLevels& lv, const RoiCfg& c,
       if (iy == 0) {
         P.fxh[ix] = b.valid ? b.h : 0.f;
         P.fxl[ix] = b.valid ? b.l : 0.f;
-        P.tdq[ix] = (uint32_t)kUnit * (uint32_t)(pc(q1) - pc(q0));
+        P.tdq[ix] = (uint32_t)kUnit * (uint32_t)(q1 - q0);
       }
-      P.tb0[iy][ix] = (a.valid && b.valid) ? (uint32_t)kUnit * (uint32_t)(r0 * G.Cs2 + pc(q0)) : 0u;
+      P.tb0[iy][ix] = (a.valid && b.valid) ? (uint32_t)kUnit * (uint32_t)(r0 * G.Cs2 + q0) : 0u;
+      P.vmask |= (a.valid && b.valid) ? 1u << (2 * iy + ix) : 0u;
     }
   }
   G.base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
@@ -731,20 +737,29 @@ __global__ void __launch_bounds__(kWave) roi_align_fwd_pair_kernel(RoiLevels lv,
 // (4 channels = 16 B) of every staged cell, filled by 16-B LDS-DMA (lane = cell: one
 // instruction stages 64 cells of a quad; the 4 quads of an item read each cell's 64
 // contiguous bytes), and every tap is ONE ds_read_b128 giving 4 channels.  A stage holds
-// the D quads (D = 4, 2, 1) whose regions fit the 8-KB slab; windows of more cells than
-// D = 1 holds are gathered per lane from global memory.  Same operation order:
+// the D quads (D = 4, 2, 1) whose regions fit the slab.  The slab is 13 KB: 832 cells,
+// so the largest tap grid of 7x7 bins at sampling 2 -- 28 rows (a dense window of <= 28
+// rows or the 28-entry tap list) by 29 columns (28, rounded up to the odd row stride)
+// = 812 cells -- is staged whole (VOC-sized RoIs: about a fifth of them; an 8-KB slab sent
+// those to per-lane global gathers, 3.6x slower per launch).  12 slabs per CU = the
+// 3 waves per SIMD the kernel's registers are sized for.  Same operation order:
 // bit-identical to the other kernels.
 constexpr int kQuadWave = 4;     // channel quads per wave (= workgroup): 16 channels
-constexpr int kQuadSlab = 2048;  // dwords per slab (8 KB)
+constexpr int kQuadSlab = 3328;  // dwords per slab (13 KB = 13 whole 64-cell DMA rounds of one quad)
 constexpr int kQuadChunk = 4 * kQuadWave;
 
-template <int D>
+template <int D, int kSlab = kQuadSlab>
 struct QuadLayout {
-  static constexpr int RS = (kQuadSlab / D) / 256 * 256;  // dwords per quad region: whole 64-cell DMA rounds
-  static constexpr int RP = RS / 256;                      // DMA rounds per region
+  static constexpr int RS = (kSlab / D) / 256 * 256;  // dwords per quad region: whole 64-cell DMA rounds
+  static constexpr int RP = RS / 256;                  // DMA rounds per region
   static constexpr int kCells = RS / 4;
   static_assert(D * RP < 64, "vmcnt is 6 bits");
 };
+
+// the largest tap grid of ph x pw bins at sampling 2 (rows x odd row stride): what the
+// quad kernel's D = 1 region must hold
+constexpr int quad_max_cells(int ph, int pw) { return (4 * ph) * ((4 * pw) | 1); }
+static_assert(quad_max_cells(7, 7) <= QuadLayout<1>::kCells, "7x7 tap grids must fit one slab");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -773,24 +788,25 @@ __device__ __forceinline__ f32x4 quad_val(const float (&w)[4], const f32x4* x) {
 // kQW: channel quads per item (4: 16 channels).  kOut: 0 = per-channel 4-B stores of the
 // bin row (lane = bin), 1 = [channel][bin] staged in LDS (obuf), then 16-B stores of the
 // item's contiguous output block, 2 = no stores (tools-only diagnostic).
-template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, bool kSwz = false>
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, int kSlab = kQuadSlab, bool kOnly4 = false>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf);
 
-template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, bool kSwz = false>
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, int kSlab = kQuadSlab>
 __device__ __forceinline__ void quad_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane,
                                           float* obuf = nullptr) {
   PairGeom G;
   PairLane P;
   const RoiRaw raw = roi_fetch(c, k);
-  pair_setup<16, kSwz>(lv, c, raw, lane, G, P);
-  quad_body<kStAux, kStamp, kQW, kOut, kSwz>(G, P, c, out, k, chunk, item, sbase, t_start, lane, obuf);
+  pair_setup<16>(lv, c, raw, lane, G, P);
+  quad_body<kStAux, kStamp, kQW, kOut, kSlab>(G, P, c, out, k, chunk, item, sbase, t_start, lane, obuf);
 }
 
-// the item after its setup (G, P): staging, evaluation, stores
-template <int kStAux, bool kStamp, int kQW, int kOut, bool kSwz>
+// the item after its setup (G, P): staging, evaluation, stores.  The host admits only
+// shapes whose largest tap grid fits one region (quad_ok: quad_max_cells <= kCells of D = 1).
+template <int kStAux, bool kStamp, int kQW, int kOut, int kSlab, bool kOnly4>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf) {
@@ -836,14 +852,13 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.w), orr, vo, (4 * q + 3) * ostep, kStAux);
   };
   auto run = [&](auto dd) {
-    constexpr int D = decltype(dd)::value, RS = QuadLayout<D>::RS, RP = QuadLayout<D>::RP;
+    constexpr int D = decltype(dd)::value, RS = QuadLayout<D, kSlab>::RS, RP = QuadLayout<D, kSlab>::RP;
     const int nst = (nquads + D - 1) / D;
     // region 16-B unit j * 64 + lane of every quad  <-  that quad of cell j * 64 + lane
     auto goff_at = [&](int j) {
       int e = j * kWave + lane;
       e = e < ncell ? e : 0;
-      const int r = (int)(((uint32_t)e * inv) >> 16), pcol = e - r * Cs2;
-      const int col = min(kSwz ? pcol - pcol / 9 : pcol, Cs - 1);  // kSwz holes load a neighbour
+      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
       return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave);
     };
     int goff[RP];
@@ -915,43 +930,15 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   };
-  if (ncell <= QuadLayout<4>::kCells) {
+  if constexpr (kOnly4) {  // the caller took ncell <= kCells of D = 4
     run(std::integral_constant<int, 4>{});
-  } else if (ncell <= QuadLayout<2>::kCells) {
-    run(std::integral_constant<int, 2>{});
-  } else if (ncell <= QuadLayout<1>::kCells) {
-    run(std::integral_constant<int, 1>{});
   } else {
-    // more tap cells than the slab holds (tap lists of a RoI wider than 28 cells on both
-    // axes): lane = bin gathers its taps from global memory, 4 channels per load
-    for (int q = 0; q < nquads; ++q) {
-      const int soff = (cw0 + 4 * q) * 4;
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int iy = 0; iy < SR; ++iy)
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-          // slab offsets -> feature offsets: slab cell (r, col) = tap-list / window entry
-          const uint32_t t0 = P.tb0[iy][ix] / 16u;
-          const int r0 = (int)(t0 / (uint32_t)Cs2), p0 = (int)(t0 - (uint32_t)r0 * (uint32_t)Cs2);
-          const int p1 = p0 + (int)(P.tdq[ix] / 16u);
-          const int r1 = r0 + (int)(P.tdr[iy] / 16u / (uint32_t)Cs2);
-          const int c0 = kSwz ? p0 - p0 / 9 : p0, c1 = kSwz ? p1 - p1 / 9 : p1;
-          const int ro0 = __shfl(rsrc, r0, kWave), ro1 = __shfl(rsrc, r1, kWave);
-          const int co0 = __shfl(csrc, c0, kWave), co1 = __shfl(csrc, c1, kWave);
-          f32x4 x[4];
-          const int offs[4] = {ro0 + co0, ro0 + co1, ro1 + co0, ro1 + co1};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(fr, offs[t], soff, 0);
-            x[t] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
-          }
-          const float w[4] = {P.fyh[iy] * P.fxh[ix], P.fyh[iy] * P.fxl[ix], P.fyl[iy] * P.fxh[ix],
-                              P.fyl[iy] * P.fxl[ix]};
-          acc = acc + quad_val(w, x);
-        }
-      store4(q, acc * 0.25f);
-    }
+    if (ncell <= QuadLayout<4, kSlab>::kCells)
+      run(std::integral_constant<int, 4>{});
+    else if (ncell <= QuadLayout<2, kSlab>::kCells)
+      run(std::integral_constant<int, 2>{});
+    else  // ncell <= quad_max_cells(ph, pw) <= QuadLayout<1, kSlab>::kCells (quad_ok)
+      run(std::integral_constant<int, 1>{});
   }
   if constexpr (kOut == 1) {  // the item's [channel][bin] block: contiguous, 16-B stores
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -980,13 +967,16 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
   }
 }
 
-// 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups, chunk-major per XCD (as the
-// pair kernel: the two 16-channel chunks of a 128-B line share an XCD)
-template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 4, int kQW = kQuadWave, int kOut = 0,
-          bool kSpan = false, bool kSwz = false>
+// 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups; XCD x takes the x-th eighth
+// of the item list (as the pair kernel: the two 16-channel chunks of a 128-B line share an
+// XCD).  kOrder 0: chunk-major (chunk, RoI); 1: chunk-pair-major, the pair's two chunks of
+// a RoI adjacent (2p, k), (2p + 1, k) -- the two waves reading the two halves of the same
+// lines run together, so the second finds them in L2.
+template <int kStAux = kCpolNT, bool kStamp = false, int kWpe = 3, int kQW = kQuadWave, int kOut = 0,
+          bool kSpan = false, int kSlab = kQuadSlab, int kOrder = 0>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe))) roi_align_fwd_quad_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  __shared__ __attribute__((aligned(16))) float slab[kQuadSlab];
+  __shared__ __attribute__((aligned(16))) float slab[kSlab];
   __shared__ __attribute__((aligned(16))) float obuf[kOut == 1 ? 4 * kQW * kWave : 4];  // [channel][bin], <= 64 bins
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   const uint32_t G = (uint32_t)(c.C + 4 * kQW - 1) / (uint32_t)(4 * kQW), K32 = (uint32_t)c.K;
@@ -994,11 +984,259 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe
   const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
   const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
   if (w >= wend) return;
-  const int ch0 = (int)(w / K32);
-  const int64_t k0 = (int64_t)(w - (uint32_t)ch0 * K32);
-  quad_item<kStAux, kStamp, kQW, kOut, kSwz>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
+  int ch0;
+  int64_t k0;
+  if (kOrder == 0) {
+    ch0 = (int)(w / K32);
+    k0 = (int64_t)(w - (uint32_t)ch0 * K32);
+  } else {
+    const uint32_t p = w / (2u * K32), r = w - p * 2u * K32;
+    if (2u * p + 1u < G) {
+      ch0 = (int)(2u * p + (r & 1u));
+      k0 = (int64_t)(r >> 1);
+    } else {  // odd chunk count: the last chunk alone
+      ch0 = (int)(2u * p);
+      k0 = (int64_t)r;
+    }
+  }
+  quad_item<kStAux, kStamp, kQW, kOut, kSlab>(lv, c, out, k0, ch0, w, sbase, t_start, threadIdx.x & (kWave - 1), obuf);
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
+
+// ---------------------------------------------------------------------------
+// Channel-quad forward with coalesced band staging (channels-last features).  The quad
+// kernel stages one channel quad of every window cell per LDS-DMA instruction: lane =
+// cell, 16 B from each of 64 cells 1 KB apart, so every lane is its own L2 request --
+// VOC-sized windows (hundreds of cells) made the launch L2-request-rate bound (24 M
+// 16-B requests for 410 MB staged, 93 % L2 hits, 111 us).  Here lane = 4 x cell + quad:
+// the four lanes of a cell read its 64 contiguous bytes (the item's 16 channels), one
+// 64-B request, and the slab holds [cell][16 channels] (64 B per cell).  A window larger
+// than the slab is staged in row bands: each band holds the rows of the next bin rows
+// whose samples fit (rows of the lowest pending bin first; every bin's rows span <= 5
+// <= kSlabCells / 29), evaluated by the lanes (bins) of those rows; windows within the slab
+// are one band (the random-init RoIs of the bench: all of them).  Tap reads: lane l reads
+// quad (d + l) mod 4 at step d, so the 16 lanes of a ds_read_b128 group spread over the
+// 64 banks (a fixed quad would put them on the 4 bank groups of cell mod 4); its stores
+// go to those quads' channels.  Same operation order per output: bit-identical to the
+// other kernels.
+template <int kSlabCells>
+struct BandLayout {
+  static_assert(kSlabCells % 16 == 0, "whole 16-cell DMA instructions");
+  static constexpr int kMaxDma = kSlabCells / 16;
+  static_assert(kMaxDma < 64, "vmcnt is 6 bits");
+};
+
+// kRot: 0 = every lane reads quad d at step d (bank conflicts: 4 bank groups per quad);
+// 1 = lane l reads quad (d + l) mod 4, results kept and stored per channel after the 4 steps
+// (each store instruction writes one channel plane, 49 contiguous floats); 2 = as 1 but
+// each step's quad stored at once (lane-dependent channel planes: 4 partial lines each).
+// kHybrid: windows of at most QuadLayout<4, kSlabCells * 16>::kCells cells (every random-init
+// RoI of the bench, most small RoIs) take the quad kernel's one-stage path instead -- lane =
+// cell, 64 cells and one address per DMA instruction: fewer instructions where the window
+// is small and the L2 request rate is not the bound -- the rest the bands.
+template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, bool kHybrid = false>
+__device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
+                                          int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
+  constexpr int SR = 2;
+  int64_t t_setup = 0, t_land = 0;
+  PairGeom G;
+  PairLane P;
+  const RoiRaw raw = roi_fetch(c, k);
+  pair_setup<kHybrid ? 16 : 64>(lv, c, raw, lane, G, P);
+  if constexpr (kHybrid) {
+    if (!G.empty && G.R * G.Cs2 <= QuadLayout<4, kSlabCells * 16>::kCells) {
+      quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, true>(G, P, c, out, k, chunk, item, sbase, t_start,
+                                                                    lane, nullptr);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {  // the band layout's 64-B cells
+      P.tdq[i] <<= 2;
+      P.tdr[i] <<= 2;
+#pragma unroll
+      for (int j = 0; j < SR; ++j) P.tb0[i][j] <<= 2;
+    }
+  }
+  const int cw0 = chunk * 4 * kQuadWave;
+  const int nquads = min(kQuadWave, (c.C - cw0) / 4);  // host: C % 4 == 0
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)4 * nquads * nbins * 4);
+  const int ostep = nbins * 4;
+  if (G.empty) {  // no valid sample: all bins 0
+    const int vo = active ? lane * 4 : 0x40000000;
+    for (int ch = 0; ch < 4 * nquads; ++ch) __builtin_amdgcn_raw_buffer_store_b32(0u, orr, vo, ch * ostep, kStAux);
+    return;
+  }
+  if (kStamp) t_setup = (int64_t)__builtin_amdgcn_s_memrealtime();
+  const int y0 = G.y0, x0 = G.x0, Cs = G.Cs, Cs2 = G.Cs2, sy = G.sy, sx = G.sx, R = G.R;
+  const bool dense = G.dy && G.dx;
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(G.base, (int64_t)G.extent);
+  const uint32_t inv = G.inv;
+  const int rows_cap = kSlabCells / Cs2;
+  // this lane's share of a DMA instruction: cell (lane >> 2) of the instruction's 16, quad lane & 3
+  const int dq = min(lane & 3, nquads - 1);
+  const int soff = cw0 * 4;
+  bool pending = active;
+  int nbands = 0;
+  while (true) {
+    const uint64_t pend = __ballot(pending);
+    if (!pend) break;
+    // the band: rows [rs, re) -- from the lowest row of a pending bin, the bins whose rows all fit
+    const int rmin = __builtin_amdgcn_readfirstlane(wave_min_i32(pending ? P.rlo : 0x7fffffff));
+    const int rs = rmin == 0x7fffffff ? 0 : max(0, rmin);  // only bins without a valid row left: one row
+    const int rcap = min(rs + rows_cap, R);
+    bool in = pending && P.rhi < rcap;
+    if (!__ballot(in)) in = pending;  // unreachable by the rows bound (host: 5 rows fit); never loops forever
+    const int re = min(R, max(rs + 1, __builtin_amdgcn_readfirstlane(wave_max_i32(in ? P.rhi + 1 : 0))));
+    const int nb = (re - rs) * Cs2;
+    const int nj = (nb + 15) >> 4;
+    // stage rows [rs, re): instruction j, lane -> cell 16 j + (lane >> 2) of the band, quad dq
+    for (int j = 0; j < nj; ++j) {
+      int e = 16 * j + (lane >> 2);
+      e = e < nb ? e : 0;
+      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
+      const int goff = dense ? ((y0 + rs + r) * sy + (x0 + col) * sx) * 4
+                             : __shfl(P.rsrc, rs + r, kWave) + __shfl(P.csrc, col, kWave);
+      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, goff + dq * 16, soff);
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kStamp && nbands == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (in) {
+      const uint32_t boff = 64u * (uint32_t)(rs * Cs2);
+      f32x4 v[2][8];
+      float ly_h[SR], ly_l[SR], lx_h[SR], lx_l[SR];
+      uint32_t lb[SR][SR], ldq[SR], ldr[SR];
+#pragma unroll
+      for (int i = 0; i < SR; ++i) {
+        ly_h[i] = P.fyh[i], ly_l[i] = P.fyl[i], lx_h[i] = P.fxh[i], lx_l[i] = P.fxl[i], ldq[i] = P.tdq[i],
+        ldr[i] = P.tdr[i];
+#pragma unroll
+        for (int jx = 0; jx < SR; ++jx)  // invalid samples read band cell 0 (finite) with zero weights
+          lb[i][jx] = sbase + (((P.vmask >> (2 * i + jx)) & 1u) ? P.tb0[i][jx] - boff : 0u);
+      }
+      f32x4 res0 = {}, res1 = {}, res2 = {}, res3 = {};  // kRot 1: the step results (named: no indexed array)
+      static_for<0, kQuadWave>([&](auto dd) {
+        constexpr int d = decltype(dd)::value;
+        const int qq = kRot ? (d + lane) & 3 : d;  // this lane's quad at step d
+        const uint32_t qo = 16u * (uint32_t)qq;
+        uint32_t lq[SR][SR];
+#pragma unroll
+        for (int iy = 0; iy < SR; ++iy)
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix) lq[iy][ix] = lb[iy][ix] + qo;
+        auto tap = [&](int iy, int ix, int q) -> uint32_t {
+          return lq[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
+        };
+        auto load = [&](auto hh) {
+          constexpr int iy = decltype(hh)::value;
+#pragma unroll
+          for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[iy][ix * 4 + q] = lds_read_b128<0>(tap(iy, ix, q));
+        };
+        load(std::integral_constant<int, 0>{});
+        load(std::integral_constant<int, 1>{});
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        lds_wait4<8>(v[0]);
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const float w[4] = {ly_h[0] * lx_h[ix], ly_h[0] * lx_l[ix], ly_l[0] * lx_h[ix], ly_l[0] * lx_l[ix]};
+          acc = acc + quad_val(w, &v[0][ix * 4]);
+        }
+        lds_wait4<0>(v[1]);
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const float w[4] = {ly_h[1] * lx_h[ix], ly_h[1] * lx_l[ix], ly_l[1] * lx_h[ix], ly_l[1] * lx_l[ix]};
+          acc = acc + quad_val(w, &v[1][ix * 4]);
+        }
+        const f32x4 r4 = acc * 0.25f;  // count 4: / 4 == * 0.25
+        if constexpr (kRot == 1) {
+          if constexpr (d == 0) res0 = r4;
+          if constexpr (d == 1) res1 = r4;
+          if constexpr (d == 2) res2 = r4;
+          if constexpr (d == 3) res3 = r4;
+        } else {
+          const int vo = qq < nquads ? lane * 4 + 4 * qq * ostep : 0x40000000;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, vo, 0, kStAux);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, vo, ostep, kStAux);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, vo, 2 * ostep, kStAux);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, vo, 3 * ostep, kStAux);
+        }
+      });
+      if constexpr (kRot == 1) {  // quad Q was computed at step (Q - lane) mod 4: one channel plane per store
+#pragma unroll
+        for (int Q = 0; Q < kQuadWave; ++Q) {
+          const int sel = (Q - lane) & 3;
+          const bool s0 = sel == 0, s1 = sel == 1, s2 = sel == 2;
+          const float o[4] = {s0 ? res0.x : s1 ? res1.x : s2 ? res2.x : res3.x,
+                              s0 ? res0.y : s1 ? res1.y : s2 ? res2.y : res3.y,
+                              s0 ? res0.z : s1 ? res1.z : s2 ? res2.z : res3.z,
+                              s0 ? res0.w : s1 ? res1.w : s2 ? res2.w : res3.w};
+          const int vo = Q < nquads ? lane * 4 : 0x40000000;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[e]), orr, vo, (4 * Q + e) * ostep, kStAux);
+        }
+      }
+      pending = false;
+    }
+    ++nbands;
+    // the band's tap reads are complete (lds_wait4<0>) before the next band's DMA overwrites it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (kStamp && lane == 0) {
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + item * 8;
+    st[0] = t_start;
+    st[1] = t_setup;
+    st[2] = t_land;
+    st[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[4] = nbands;
+    st[5] = R * Cs2;
+    st[6] = t_setup;
+    st[7] = blockIdx.x & 7;
+  }
+}
+
+// 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups; XCD x takes the x-th eighth of
+// the item list in chunk-pair-major order (quad kernel, kOrder 1: the two 16-channel chunks of
+// a 128-B line, adjacent, on one XCD).
+template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
+          int kRot = 1, bool kHybrid = false>
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
+roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) float slab[kSlabCells * 16];
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const uint32_t G = (uint32_t)(c.C + kQuadChunk - 1) / (uint32_t)kQuadChunk, K32 = (uint32_t)c.K;
+  const uint32_t total = K32 * G, per = (total + 7u) / 8u;
+  const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
+  if (w >= wend) return;
+  const uint32_t p = w / (2u * K32), r = w - p * 2u * K32;
+  int ch0;
+  int64_t k0;
+  if (2u * p + 1u < G) {
+    ch0 = (int)(2u * p + (r & 1u));
+    k0 = (int64_t)(r >> 1);
+  } else {  // odd chunk count: the last chunk alone
+    ch0 = (int)(2u * p);
+    k0 = (int64_t)r;
+  }
+  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid>(lv, c, out, k0, ch0, w, sbase, t_start,
+                                                       threadIdx.x & (kWave - 1));
+  if (kSpan && threadIdx.x == 0) record_span(c, t_start);
+}
+
+// the band kernel's shape limits: a bin's rows (sampling 2: its two y samples' taps, <= 5
+// rows -- dense windows of <= 4 ph rows space the 2 ph samples <= (4 ph - 1) / (2 ph - 1) <= 3
+// rows apart, tap lists give 4) fit a band of the widest window row (4 pw entries, odd stride)
+constexpr bool band_fits(int ph, int pw, int slab_cells) { return 5 * ((4 * pw) | 1) <= slab_cells; }
 
 static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_kernel(RoiLevels lv, RoiCfg c,
                                                                     const float* __restrict__ gout) {
@@ -1184,8 +1422,14 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_lds_kernel(R
 // as in torchvision's CUDA backward).
 constexpr int kSepEnt = 32;  // tap entries per axis and wave half: 4 * ph, 4 * pw <= 32
 
-static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
-                                                                        const float* __restrict__ gout) {
+// kFixed (deterministic backward, frh_roi_align_bwd_fixed): lv.grad[l] points at int64
+// accumulators with the gradient's element strides; each (RoI, row, column) sum is added as
+// rint(sum * 2^40) by an integer atomic -- integer adds are associative, so the total is the
+// same whatever order the RoIs arrive in (the float-atomic form's order is the scheduler's).
+constexpr double kBwdFixedScale = 1099511627776.0;  // 2^40: |gradient element| < 2^23 fits int64
+template <bool kFixed = false>
+__global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
+                                                                         const float* __restrict__ gout) {
   constexpr int kCh = kRoiChanChunk / (kRoiThreads / kWave);  // channels per wave (even)
   __shared__ int yent_all[kRoiThreads / kWave][kSepEnt];      // row << 16 | py, sorted by (row, entry)
   __shared__ float yw_all[kRoiThreads / kWave][kSepEnt];
@@ -1277,7 +1521,7 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(R
   }
   const bool head = xv && (j == 0 || (xs[j - 1] >> 16) != my_col);
   const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
-  float* gbase = lv.grad[l] + (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
+  const int64_t goff0 = (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
   const float* go = gout + (k * c.C + cw0) * nbins;
   for (int ch = 0; ch < nch; ch += 2) {
     // grad_out of channels ch, ch + 1 (a missing odd last channel reads 0 and is not written)
@@ -1288,7 +1532,7 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(R
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float* f = gbase + (int64_t)(ch + h) * scs;
+    const int64_t fo = goff0 + (int64_t)(ch + h) * scs;
     const bool live = xv && ch + h < nch;
     float acc = 0.0f;
     for (int i = 0; i < nyv; ++i) {
@@ -1304,7 +1548,14 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(R
           const float t = __shfl_down(sum, d, 32);
           if (d <= trail) sum = sum + t;
         }
-        if (head && live && sum != 0.0f) atomicAdd(&f[(int64_t)row * sy + (int64_t)my_col * sx], sum);
+        if (head && live && sum != 0.0f) {
+          const int64_t e = fo + (int64_t)row * sy + (int64_t)my_col * sx;
+          if constexpr (kFixed)
+            atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
+                      (unsigned long long)(long long)rint((double)sum * kBwdFixedScale));
+          else
+            atomicAdd(lv.grad[l] + e, sum);
+        }
         acc = 0.0f;
       }
     }
@@ -1312,6 +1563,12 @@ static __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(R
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+}
+
+// the fixed-point accumulators to the f32 gradient, element by element (dense buffers)
+static __global__ void roi_bwd_fixed_to_f32_kernel(const long long* __restrict__ acc, float* __restrict__ grad, int64_t n) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+    grad[q] = (float)((double)acc[q] * (1.0 / kBwdFixedScale));
 }
 
 // ---------------------------------------------------------------------------
@@ -1574,8 +1831,11 @@ static inline bool nhwc_ok(const RoiLevels& lv, int32_t channels, int32_t ph, in
 }
 
 // channels-last features for the quad kernel: unit channel stride, C % 4 == 0, 16-B aligned
-static inline bool quad_ok(const FwdCaps& f, const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw) {
-  if (!f.buf || channels % 4 != 0 || 4 * ph > kWave || 4 * pw > kWave || ph * pw > kWave) return false;
+static inline bool quad_ok(const FwdCaps& f, const RoiLevels& lv, int32_t channels, int32_t ph, int32_t pw,
+                           int slab_cells = QuadLayout<1>::kCells) {
+  if (!f.buf || channels % 4 != 0 || 4 * ph > kWave || 4 * pw > kWave || ph * pw > kWave ||
+      quad_max_cells(ph, pw) > slab_cells)
+    return false;
   for (int l = 0; l < lv.L; ++l)
     if (lv.sc[l] != 1 || lv.sx[l] % 4 || lv.sy[l] % 4 || lv.sb[l] % 4 || (reinterpret_cast<uintptr_t>(lv.feat[l]) & 15))
       return false;

@@ -266,19 +266,22 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
 // then the last workgroup to leave zeroes the image's state words, which is the
 // workspace contract (frh_sample_zero_bytes: zero before, zero after).
 // The selected set is exactly the two-launch path's.
-constexpr int kSampFusedMaxWgs = 512;  // resident with margin (LDS: 4 workgroups per CU)
+// The grid's live workgroups must be resident together: the host admits at most half the
+// device's resident capacity of the kernel (CU count x occupancy: 4 per CU by LDS on a whole
+// MI355X, so 512), else the keys + collect launches.
 
 struct SampFused {
   uint32_t* part_hist;   // [S][2][nchunk][kSampBins] per-chunk histograms (sc1 stores, every call)
   int32_t* part_count;   // [S][2][nchunk] per-chunk class counts
   int nchunk;
-  int32_t* state;    // [S][2][TK_WORDS]     zero before and after (TK_ERR: sticky barrier error)
+  int32_t* state;    // [S][2][TK_WORDS]     zero before and after
   uint64_t* cand;    // [S][2][ld] prefix ties: key << 32 | ~box
   int64_t ld;
   int32_t* sel;      // nullable: [S][2][sel_ld]
   int64_t sel_ld;
   int32_t* sel_cnt;  // [S][2]
   int64_t* stamps;   // tools timing only (null in the product): 16 int64 per workgroup
+  int32_t* status;   // the caller's device status word (FRH_DEVERR_SAMPLER_BARRIER)
 };
 
 __device__ __forceinline__ uint32_t samp_key(uint64_t seed, int v, int i, bool cand) {
@@ -301,7 +304,6 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   };
   stamp(0);
   int32_t* st = f.state + (int64_t)(2 * s) * TK_WORDS;  // [2][TK_WORDS]: positives, negatives
-  int32_t* err = st + TK_ERR;
   int32_t* bar = f.state + tk_bars_offset(2 * (int)gridDim.y) + s * kBarWords;  // its own line
   const int64_t* li = lab_in + (int64_t)s * lstride;
   int64_t* lo = lab_out ? lab_out + (int64_t)s * lstride : nullptr;
@@ -344,7 +346,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   for (int i = t; i < 2 * kSampBins; i += kTkThreads)
     xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
   stamp(2);
-  seg_barrier(bar, G, err);
+  if (!seg_barrier(bar, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return;
   stamp(3);
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
@@ -417,7 +419,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
   const bool ties = (pl[0].kv > 0 && !pl[0].all) || (pl[1].kv > 0 && !pl[1].all);
   stamp(5);
-  if (ties) seg_barrier(bar + 1, G, err);
+  if (ties && !seg_barrier(bar + 1, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return;
   stamp(6);
 
   // ---- phase 4: the prefix ties, positives by workgroup 0, negatives by workgroup 1 (0 if alone)
@@ -486,7 +488,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   __syncthreads();
   if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
   __syncthreads();
-  if (sm.last && t < 2 * TK_WORDS && t % TK_WORDS != TK_ERR) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
+  if (sm.last && t < 2 * TK_WORDS) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
   if (sm.last && t < 2) xwg_store(reinterpret_cast<uint32_t*>(bar) + t, 0u);
   stamp(8);
 }
@@ -658,8 +660,9 @@ size_t compact_workspace(int32_t S, int64_t max_n) {
 
 int32_t sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                            const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
-                           uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, void* workspace,
-                           size_t ws_bytes, void* stream, bool two_launches, int64_t* stamps = nullptr);
+                           uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, int32_t* status,
+                           void* workspace, size_t ws_bytes, void* stream, bool two_launches,
+                           int64_t* stamps = nullptr);
 
 }  // namespace frh
 
@@ -674,7 +677,10 @@ struct SampLayout {
 };
 
 // The leading zero region (frh_sample_zero_bytes): the one-launch sampler's state words
-// [V][TK_WORDS] and barrier lines; the rest follows it.
+// [V][TK_WORDS] and barrier lines, sized for the largest num_segs (kSampMaxSegs) whatever
+// the call's, so that no other buffer of any call lies in it (a reused workspace stays
+// zero there across calls of different num_segs and paths); the rest follows it.
+constexpr int32_t kSampMaxSegs = 64;
 static size_t samp_zero_bytes(int32_t S) {  // state words [2S][TK_WORDS] + a barrier line per image
   return al256(((size_t)tk_bars_offset(2 * S) + (size_t)S * kBarWords) * sizeof(int32_t));
 }
@@ -685,7 +691,7 @@ static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   const int V = 2 * S;
   z.kld = (int64_t)n;
   z.nchunk = (int)((n + kTkChunk - 1) / kTkChunk);
-  z.keys = samp_zero_bytes(S);
+  z.keys = samp_zero_bytes(kSampMaxSegs);
   z.cand = z.keys + al256((size_t)V * n * sizeof(uint32_t));
   z.state = z.cand + al256((size_t)V * n * sizeof(uint64_t));
   z.phist = z.state + al256((size_t)V * TK_WORDS * sizeof(int32_t));
@@ -700,7 +706,9 @@ extern "C" size_t frh_sample_workspace(int32_t num_segs, int64_t max_boxes) {
   return a > b ? a : b;
 }
 
-extern "C" size_t frh_sample_zero_bytes(int32_t num_segs) { return num_segs > 0 ? samp_zero_bytes(num_segs) : 0; }
+extern "C" size_t frh_sample_zero_bytes(int32_t num_segs) {
+  return num_segs > 0 ? samp_zero_bytes(kSampMaxSegs) : 0;
+}
 
 extern "C" int32_t frh_sample_candidates(int32_t num_segs, const int64_t* labels, int64_t label_seg_stride,
                                          const int32_t* num_boxes, int64_t max_boxes, int32_t* pos_list,
@@ -743,9 +751,10 @@ extern "C" int32_t frh_sample_apply(int32_t num_segs, const int64_t* labels_in, 
 extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                      const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
                                      int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
-                                     int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream) {
+                                     int32_t* sel_counts, int32_t* status, void* workspace, size_t ws_bytes,
+                                     void* stream) {
   return frh::sample_random_impl(num_segs, labels_in, label_seg_stride, num_boxes, max_boxes, max_num, pos_num, seed,
-                                 labels_out, sel, sel_counts, workspace, ws_bytes, stream, false);
+                                 labels_out, sel, sel_counts, status, workspace, ws_bytes, stream, false);
 }
 
 // two_launches: the keys + collect launches even where the one-launch sampler applies
@@ -753,9 +762,11 @@ extern "C" int32_t frh_sample_random(int32_t num_segs, const int64_t* labels_in,
 int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                 const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                                 uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,
-                                void* workspace, size_t ws_bytes, void* stream, bool two_launches,
+                                int32_t* status, void* workspace, size_t ws_bytes, void* stream, bool two_launches,
                                 int64_t* stamps) {
   FRH_REQUIRE(num_segs >= 0 && max_boxes >= 0, "negative sizes");
+  FRH_REQUIRE(num_segs <= kSampMaxSegs, "num_segs %d exceeds %d", num_segs, kSampMaxSegs);
+  FRH_REQUIRE(status, "null status word");
   FRH_REQUIRE(pos_num <= max_num && pos_num >= 0, "pos_num must be in [0, max_num]");
   if (num_segs == 0 || max_boxes == 0) return FRH_OK;
   FRH_REQUIRE(labels_in && num_boxes && (labels_out || sel), "null pointer argument");
@@ -774,10 +785,11 @@ int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int6
   char* ws = reinterpret_cast<char*>(workspace);
   SampLayout z = samp_layout(num_segs, max_boxes);
   const int V = 2 * num_segs;
-  if (!two_launches && (int64_t)num_segs * z.nchunk <= kSampFusedMaxWgs) {
+  if (!two_launches &&
+      (int64_t)num_segs * z.nchunk <= resident_capacity(reinterpret_cast<const void*>(sampler_fused_kernel), kTkThreads) / 2) {
     SampFused f{reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
                 reinterpret_cast<int32_t*>(ws), reinterpret_cast<uint64_t*>(ws + z.cand), z.kld, sel,
-                (int64_t)(max_num > 0 ? max_num : 1), sel_counts, stamps};
+                (int64_t)(max_num > 0 ? max_num : 1), sel_counts, stamps, status};
     hipLaunchKernelGGL(sampler_fused_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
                        labels_in, label_seg_stride, num_boxes, max_num, pos_num, seed, f, labels_out);
     return check_launch("frh_sample_random");

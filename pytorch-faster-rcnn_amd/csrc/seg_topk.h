@@ -309,27 +309,39 @@ __device__ __forceinline__ bool tk_check_in(int* done, TkSmem& sm) {
 // then one agent-scope atomic add behind a workgroup barrier) and lane 0 polls
 // the counter with sc1 loads (hand-off table row 1: everything handed across is
 // written sc1 or by memory-side atomics and read back sc1).  Residency: a
-// segment's workgroups are contiguous in dispatch order and the launches keep
-// their total grids far below the chip's resident capacity (host checks), so the
-// polled workgroups are always resident.  The spin is bounded (kSpinTicks of the
-// 100 MHz clock) so a broken assumption ends in a flagged error word, never a hang.
-constexpr uint64_t kSpinTicks = 20000000ull;  // 200 ms
+// segment's workgroups are contiguous in dispatch order and the host keeps the
+// grid's live workgroups within a fraction of the device's resident capacity
+// (resident_capacity: CU count x occupancy of the kernel, queried per device), so
+// the polled workgroups are normally resident.  The spin is bounded (kSpinTicks of
+// the 100 MHz clock): a wait that runs out ORs `bit` into the caller's device status
+// word and returns false in every thread of the workgroup, which then ends its work
+// (include/frcnn_amd.h FRH_DEVERR_*): a loud error, never a hang, never a selection
+// from partial histograms.
+#ifndef FRH_SPIN_TICKS
+#define FRH_SPIN_TICKS 20000000ull  // 200 ms (tools: a build with 0 makes every unmet wait run out)
+#endif
+constexpr uint64_t kSpinTicks = FRH_SPIN_TICKS;
 
-__device__ __forceinline__ void seg_barrier(int32_t* counter, int target, int32_t* err) {
+__device__ __forceinline__ bool seg_barrier(int32_t* counter, int target, int32_t* status, int32_t bit) {
+  __shared__ int s_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    int ok = 1;
     atomicAdd(counter, 1);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (xwg_load(counter) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-        atomicOr(err, 1);
+        atomicOr(status, bit);
+        ok = 0;
         break;
       }
     }
+    s_ok = ok;
   }
   __syncthreads();
+  return s_ok != 0;
 }
 
 // ------------------------------------------------- top-k of a small LDS list

@@ -148,16 +148,26 @@ __global__ void anchor_target_kernel(AnchorTargetArgs p) {
 // box order: each item's output position is the number of listed boxes below it (rank by
 // counting over the list staged in LDS) -- the reference's nonzero(labels >= 0) order
 // (anchor.py:49-50, bbox.py:52-58) without a compaction pass over every box.
-// Dynamic LDS: 2 * sel_ld + 4 int32.
+// Dynamic LDS: 2 * sel_ld + 4 int32.  Counts are clamped to the capacity and box indices
+// to [0, lim): a no-op for a sampler call that completed, and memory safety for one whose
+// in-launch wait ran out (its lists are undefined; the status word says so).
 template <class F, class P>
 __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32_t* sel_cnt, int64_t sel_ld, int S,
-                                                 int32_t* out_counts, int64_t cap, F&& item, P&& pad) {
+                                                 int32_t* out_counts, int64_t cap, int64_t lim, F&& item, P&& pad) {
   extern __shared__ __attribute__((aligned(16))) int32_t su[];
   const int s = blockIdx.y;
-  const int np = sel_cnt[2 * s], cnt = np + sel_cnt[2 * s + 1];
+  const int icap = (int)min(cap, sel_ld);
+  auto counts_of = [&](int q, int& pos) {
+    const int a = min(max(sel_cnt[2 * q], 0), icap);
+    pos = a;
+    return a + min(max(sel_cnt[2 * q + 1], 0), icap - a);
+  };
+  int np;
+  const int cnt = counts_of(s, np);
   int64_t off = 0, total = 0;
   for (int q = 0; q < S; ++q) {
-    const int64_t c = sel_cnt[2 * q] + sel_cnt[2 * q + 1];
+    int pq;
+    const int64_t c = counts_of(q, pq);
     off += q < s ? c : 0;
     total += c;
   }
@@ -180,7 +190,7 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
   __syncthreads();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= cnt) return;
-  const int32_t x = su[j];
+  const int32_t x = min(max(su[j], 0), (int32_t)(lim > 0 ? lim - 1 : 0));
   int rank = 0;
   const int4* s4 = reinterpret_cast<const int4*>(su);
   for (int q = 0; q < cnt4 / 4; ++q) {
@@ -191,7 +201,7 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
 }
 
 __global__ void anchor_target_sel_kernel(AnchorTargetArgs p) {
-  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap,
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap, p.list_seg_stride,
                    [&](int s, int64_t n, int64_t o) { anchor_target_item(p, s, n, o); },
                    [&](int64_t o) {  // padding row: no anchor (seg -1), label -1 (ignored), zero targets
                      p.chosen_idx[o] = 0;
@@ -328,7 +338,7 @@ __global__ void bbox_target_kernel(BBoxTargetArgs p) {
 }
 
 __global__ void bbox_target_sel_kernel(BBoxTargetArgs p) {
-  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap,
+  ranked_selection(p.sel, p.sel_cnt, p.sel_ld, p.S, p.out_counts, p.cap, p.list_seg_stride,
                    [&](int s, int64_t row, int64_t o) { bbox_target_item(p, s, row, o); },
                    [&](int64_t o) {  // padding row: zero box, label -1 (ignored), not a gt
                      p.tar_label[o] = -1;
@@ -434,7 +444,8 @@ extern "C" int32_t frh_anchor_target(int32_t num_segs, const int64_t* labels, in
   unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
   if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
     FRH_REQUIRE((2 * max_out_per_seg + 4) * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
-    AnchorTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, anchors, anchor_ld, anchor_seg_stride,
+    // sel mode: list_seg_stride carries max_boxes, the bound of the lists' box indices
+    AnchorTargetArgs p{labels, label_seg_stride, nullptr, nullptr, max_boxes, anchors, anchor_ld, anchor_seg_stride,
                        gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                        max_out_per_seg, chosen_idx, seg_of, tar_labels, tar_anchors, tar_bbox, tar_param, out_ld,
                        out_counts, num_segs, sel, sel_counts, max_out_per_seg};
@@ -606,7 +617,8 @@ extern "C" int32_t frh_bbox_target(int32_t num_segs, const int64_t* labels, int6
   unsigned gx = (unsigned)((max_out_per_seg + 255) / 256);
   if (sel) {  // the device sampler's lists: no compaction pass (sel_ld = max_out_per_seg)
     FRH_REQUIRE((2 * max_out_per_seg + 4) * sizeof(int32_t) <= 65536, "sampler lists exceed the LDS stage");
-    BBoxTargetArgs p{labels, label_seg_stride, nullptr, nullptr, 0, num_gts, props, prop_ld, prop_seg_stride,
+    // sel mode: list_seg_stride carries max_rows, the bound of the lists' row indices
+    BBoxTargetArgs p{labels, label_seg_stride, nullptr, nullptr, max_rows, num_gts, props, prop_ld, prop_seg_stride,
                      gts, gt_ld, gt_seg_stride, gt_labels, gt_label_seg_stride, make_norm(means, stds),
                      max_out_per_seg, tar_props, tar_bbox, tar_param, tar_label, tar_is_gt, out_ld, out_counts,
                      num_segs, sel, sel_counts, max_out_per_seg};

@@ -36,7 +36,7 @@ SIGNATURES = {
                                       c_vp]),
     'frh_sample_apply': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                  c_vp, c_vp]),
-    'frh_sample_random': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp, c_vp,
+    'frh_sample_random': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_size, c_vp]),
     'frh_anchor_target_workspace': (c_size, [c_i32, c_i64]),
     'frh_anchor_target': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
@@ -62,10 +62,10 @@ SIGNATURES = {
     'frh_rpn_proposals_nms_view': (c_i32, [c_i32, c_i32, P(c_i32), c_i32, c_i32, P(ctypes.c_int64)]),
     'frh_rpn_proposals': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i32), c_i32, c_i32, c_vp, c_i64,
                                   P(c_f32), P(c_f32), P(c_f32), P(c_f32), c_i32, c_i32, c_i32, c_f64, c_vp,
-                                  c_vp, c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_rpn_proposals_strided': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i64), P(c_i64), P(c_i32), c_i32, c_i32,
                                           c_vp, c_i64, P(c_f32), P(c_f32), P(c_f32), P(c_f32), c_i32, c_i32, c_i32,
-                                          c_f64, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                          c_f64, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_nms_workspace': (c_size, [c_i32, c_i32]),
     'frh_nms_sorted': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, c_f64, c_i32, c_vp, c_i64, c_vp, c_vp, c_size,
                                c_vp]),
@@ -89,6 +89,8 @@ SIGNATURES = {
                                                 c_vp]),
     'frh_roi_align_bwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    'frh_roi_align_bwd_fixed': (c_i32, [c_i32, P(c_vp), P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
+                                        c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_pool_fwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp,
                                  c_vp, c_vp]),
     'frh_roi_pool_bwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,
@@ -116,7 +118,7 @@ SIGNATURES = {
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

@@ -7,6 +7,7 @@ these.  The torchvision drop-ins the reference imports (`nms`, `roi_align`,
 `RoIAlign`, `RoIPool`) live here too.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -23,9 +24,60 @@ def call(name, *args):
     try:
         _call(name, *args)
     except RuntimeError:
-        for ws in (_ASSIGN_WS, _SAMPLE_WS, _LOSS_WS):
-            ws.clear()
+        _drop_zero_workspaces()
         raise
+
+
+def _drop_zero_workspaces():
+    for ws in (_ASSIGN_WS, _SAMPLE_WS, _LOSS_WS):
+        ws.clear()
+
+
+# ---------------------------------------------------------------- device status word
+# include/frcnn_amd.h FRH_DEVERR_*: the one-launch kernels (RPN selection, RPN NMS, device
+# sampler) OR a bit into this per-device int32 word when an in-launch wait runs out, and
+# end that workgroup's work.  The word is read (one 4-byte copy, a synchronisation) by
+# check_device_status(): at the points that synchronise anyway -- the numpy sampler's count
+# read, bench.py's loss read after the timed region, the tester -- and after every one-launch
+# call when FRCNN_AMD_DEBUG=1.
+DEVERR_BITS = {1: 'RPN selection segment barrier (rpn_select_kernel)',
+               2: 'RPN NMS mask column wait (nms_fused_kernel)',
+               4: 'device sampler image barrier (sampler_fused_kernel)'}
+_STATUS = {}
+DEBUG = os.environ.get('FRCNN_AMD_DEBUG', '') not in ('', '0')
+
+
+def status_word(dev):
+    """The device status word of `dev` (int32 [1], zero until a one-launch kernel flags)."""
+    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    w = _STATUS.get(key)
+    if w is None:
+        w = _STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device('cuda', key))
+    return w
+
+
+def check_device_status(dev=None):
+    """Raise RuntimeError if a one-launch kernel on `dev` (default: every device used) flagged
+    a timed-out in-launch wait since the last check.  Synchronises with the word's device.
+    The word is cleared and the zero-contract workspaces are dropped (their counters may be
+    left dirty by the aborted launch), so later calls start clean."""
+    keys = list(_STATUS) if dev is None else [torch.device(dev).index or 0]
+    for k in keys:
+        w = _STATUS.get(k)
+        if w is None:
+            continue
+        v = int(w.item())
+        if v:
+            w.zero_()
+            _drop_zero_workspaces()
+            what = ', '.join(m for b, m in DEVERR_BITS.items() if v & b) or 'unknown'
+            raise RuntimeError('frcnn_amd: device status 0x{:x} on cuda:{}: an in-launch wait timed out ({}); '
+                               'the outputs of that call are undefined'.format(v, k, what))
+
+
+def _debug_check(dev):
+    if DEBUG:
+        check_device_status(dev)
 
 
 def _need_cuda(*ts):
@@ -248,11 +300,12 @@ def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None, lis
         sel = torch.empty(S, 2, max(int(max_num), 1), dtype=torch.int32, device=dev) if lists else None
         sel_cnt = torch.empty(S, 2, dtype=torch.int32, device=dev) if lists else None
         args = (S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, int(max_num), int(pos_num), seed,
-                ptr(out), ptr(sel), ptr(sel_cnt), ptr(ws), ws.numel(), stream_of(labels))
+                ptr(out), ptr(sel), ptr(sel_cnt), ptr(status_word(dev)), ptr(ws), ws.numel(), stream_of(labels))
         if _entry is None:
             call('frh_sample_random', *args)
         elif _entry[0](*args) != 0:  # tests: the tools library's two-launch sampler
             raise RuntimeError('{} failed'.format(_entry[1]))
+        _debug_check(dev)
         return SampleLists(labels, sel, sel_cnt, max_num) if lists else out
     out = torch.empty_like(labels)
     ld = max(max_boxes, 1)
@@ -263,6 +316,7 @@ def sample_labels(labels, num_boxes, max_boxes, max_num, pos_num, mode=None, lis
     call('frh_sample_candidates', S, ptr(labels), labels.stride(0), ptr(num_boxes), max_boxes, ptr(pos_list),
          ptr(neg_list), ld, ptr(counts), ptr(ws), ws.numel(), stream_of(labels))
     cnt = counts.cpu().numpy()  # host round trip, as the reference's .cpu().numpy() (region.py:48,55)
+    check_device_status(dev)  # the stream is drained here anyway: a 4-byte read
     keep_ld = max(int(max_num), 1)
     keep = np.zeros((2, S, keep_ld), dtype=np.int32)
     kc = np.zeros((S, 2), dtype=np.int32)
@@ -489,11 +543,13 @@ def rpn_proposals(cls_outs, reg_outs, anchors, num_anchors, cls_channels, means,
             i64_array([v for c in cls_outs for v in c.stride()]), i64_array([v for r in reg_outs for v in r.stride()]),
             grid_a, num_anchors, cls_channels, ptr(anchors), anchors.stride(0), f32_array(means), f32_array(stds),
             f32_array([v for hw in img_hw for v in hw]), f32_array(min_sizes), int(pre_nms), int(post_nms),
-            int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(ws), ws.numel(), stream_of(boxes))
+            int(max_num), float(nms_iou), ptr(boxes), ptr(scores), ptr(counts), ptr(status_word(dev)), ptr(ws),
+            ws.numel(), stream_of(boxes))
     if _entry is None:
         call('frh_rpn_proposals_strided', *args)
     elif _entry[0](*args) != 0:
         raise RuntimeError('{} failed'.format(_entry[1]))
+    _debug_check(dev)
     if NMS_PROFILE['on']:  # keep this call's per-level NMS input (in the workspace) for a replay
         view = (ctypes.c_int64 * 4)()
         call('frh_rpn_proposals_nms_view', B, L, grid_a, num_anchors, int(pre_nms), view)
@@ -667,6 +723,21 @@ ROI_ALIGN_PROFILE = {'on': False, 'records': [], 'events': True, 'timed': None, 
 # GPU clock: nothing is added to the stream) and appends the triple.
 
 
+_DETERMINISTIC = {'on': os.environ.get('FRCNN_AMD_DETERMINISTIC', '') not in ('', '0')}
+
+
+def set_deterministic_backward(on):
+    """Force (True) / release (False) the RoIAlign backward's deterministic form."""
+    _DETERMINISTIC['on'] = bool(on)
+
+
+def deterministic_backward():
+    """The RoIAlign backward runs its fixed-point form (bit-identical across runs) when
+    torch.use_deterministic_algorithms(True) is in effect, FRCNN_AMD_DETERMINISTIC=1 is set, or
+    set_deterministic_backward(True) was called; otherwise float atomics (faster)."""
+    return _DETERMINISTIC['on'] or torch.are_deterministic_algorithms_enabled()
+
+
 class _RoIAlignMulti(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, levels, scales, output_size, sampling_ratio, aligned, *feats):
@@ -711,7 +782,18 @@ class _RoIAlignMulti(torch.autograd.Function):
         scales, (ph, pw), sr, aligned, shapes = ctx.cfg
         grad = grad.contiguous()
         K, B, C = rois.shape[0], shapes[0][0], shapes[0][1]
-        # the gradient keeps each feature map's memory format (NCHW or channels_last); it is
+        # the gradient keeps each feature map's memory format (NCHW or channels_last)
+        if deterministic_backward() and int(sr) == 2 and ph <= 8 and pw <= 8:
+            # bit-identical across runs: fixed-point (int64, 2^-40) integer atomics, then one
+            # conversion pass that writes every gradient element (frh_roi_align_bwd_fixed)
+            grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt)
+                     for s, fmt in zip(shapes, ctx.formats)]
+            accs = [torch.empty(s, dtype=torch.int64, device=grad.device, memory_format=fmt).zero_()
+                    for s, fmt in zip(shapes, ctx.formats)]
+            hw, st = _feat_desc(grads)
+            call('frh_roi_align_bwd_fixed', len(grads), ptr_array(grads), ptr_array(accs), hw, st, f32_array(scales),
+                 B, C, ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), stream_of(grad))
+            return (None, None, None, None, None, None) + tuple(grads)
         # cleared here and accumulated with float atomics (one per row run of a RoI's taps)
         grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt).zero_()
                  for s, fmt in zip(shapes, ctx.formats)]

@@ -13,6 +13,8 @@ import os.path as osp
 
 import torch
 
+from . import ops
+
 from . import utils
 
 
@@ -42,6 +44,8 @@ class BasicTester:
             for ith, batch in enumerate(dataloader):
                 img_metas = batch['img_meta']
                 bboxes, scores, categories = self.inference_one(batch['img'], img_metas)
+                if self.device.type == 'cuda':  # forward_test synchronises (mcnms counts): a 4-byte read
+                    ops.check_device_status(self.device)
                 for i, meta in enumerate(img_metas):
                     res = image_result(bboxes[i], scores[i], categories[i], meta)
                     if res is None:

@@ -18,6 +18,8 @@ so no SyncBN and no buffer broadcast.
 import torch
 from torch import nn
 
+from . import ops
+
 # Gradient bucket size for the all-reduce.  cfg2 has 41 M trainable f32 parameters
 # (165 MB): 25 MB buckets give ~7 all-reduces that start while backward is still
 # producing the earlier layers' gradients, and each is large enough to keep RCCL's
@@ -50,8 +52,10 @@ class TrainStep:
     """Callable training iteration on this rank's batch; returns the (detached) local loss."""
 
     def __init__(self, detector, optimizer_cfg=None, grad_clip=None, world_size=1, device=None,
-                 bucket_mb=DEFAULT_BUCKET_MB):
+                 bucket_mb=DEFAULT_BUCKET_MB, status_every=50):
         self.detector = detector
+        self.device = device
+        self.status_every, self.steps = status_every, 0
         self.params = [p for p in detector.parameters() if p.requires_grad]
         net = DetectorLoss(detector)
         if world_size > 1:
@@ -70,4 +74,8 @@ class TrainStep:
             nn.utils.clip_grad_norm_(self.params, self.grad_clip['max_norm'],
                                      self.grad_clip.get('norm_type', 2))
         self.optimizer.step()
+        self.steps += 1
+        if self.status_every and self.steps % self.status_every == 0 and self.device is not None and \
+                self.device.type == 'cuda':
+            ops.check_device_status(self.device)  # one synchronising 4-byte read per status_every steps
         return loss.detach()

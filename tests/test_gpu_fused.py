@@ -178,3 +178,31 @@ def test_sampler_one_launch_equals_two_launches(dev, S, n, nums, max_num, pos_nu
         zb = int(ops._lib.query('frh_sample_zero_bytes', S))
         assert ops._SAMPLE_WS and all(int(ws[:zb].count_nonzero()) == 0 for ws in ops._SAMPLE_WS.values())
     ops.set_sampler_mode('numpy')
+
+
+def test_sampler_workspace_reuse_across_num_segs_and_paths(dev):
+    """a two-launch call (keys at the end of the zero region) with S = 2, then a
+    one-launch call with S = 4 on the same cached workspace, dense positives: the zero region
+    is the same for every S (frh_sample_zero_bytes), so the S = 4 call equals one on a fresh
+    workspace."""
+    from frcnn_amd import ops
+    lib = _tools()
+    rng = np.random.default_rng(11)
+    n = 40000
+    lab2 = torch.from_numpy(rng.choice([0, 1, 2], size=(2, n), p=[0.2, 0.4, 0.4]).astype(np.int64)).to(dev)
+    lab4 = torch.from_numpy(rng.choice([0, 1, 2], size=(4, n), p=[0.2, 0.4, 0.4]).astype(np.int64)).to(dev)
+    num2 = torch.full((2,), n, dtype=torch.int32, device=dev)
+    num4 = torch.full((4,), n, dtype=torch.int32, device=dev)
+    assert ops._lib.query('frh_sample_zero_bytes', 2) == ops._lib.query('frh_sample_zero_bytes', 64)
+    ops._SAMPLE_WS.clear()
+    ops.set_sampler_mode('device', seed=5)
+    fresh = ops.sample_labels(lab4, num4, n, 512, 128, mode='device')
+    ops._SAMPLE_WS.clear()
+    ops.set_sampler_mode('device', seed=6)
+    ops.sample_labels(lab2, num2, n, 512, 128, mode='device', _entry=(lib.frh_sample_random_launches, 'launches'))
+    ops.set_sampler_mode('device', seed=5)
+    reused = ops.sample_labels(lab4, num4, n, 512, 128, mode='device')
+    torch.cuda.synchronize()
+    ops.check_device_status(dev)
+    assert torch.equal(fresh, reused)
+    ops.set_sampler_mode('numpy')

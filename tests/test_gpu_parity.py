@@ -5,6 +5,7 @@ Bars: bit-exact for anchors, masks, IoU tables, assignment labels/IoUs,
 sampling (numpy-parity mode), chosen indices and NMS keep lists; float
 tolerances are stated per test (encode/decode log/exp, RoIAlign 1e-5)."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -738,14 +739,20 @@ def test_roi_align_forward_default_vs_oracle_p2(dev, layout):
 
 
 @pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
-def test_roi_align_forward_bench_config_bit_exact(dev, layout):
-    """The forward at the bench's own configuration: the 1024 RoIs of a cfg2 training step
-    (tests/golden/cfg2_rois.npz, 873 / 102 / 42 / 7 on P2..P5), C = 256, P2-P5 of a
-    2-image 608x1024 batch (152x256 ... 19x32), NCHW (channel-pair kernel) and
-    channels-last (the FPN's NHWC levels: channel-quad kernel): every output bit-identical
-    to the oracle (lib/region.py:271-296, torchvision legacy RoIAlign semantics)."""
+@pytest.mark.parametrize('roi_set', ['cfg2_rois.npz', 'cfg2_rois_voc.npz', 'cfg2_rois_train.npz'])
+def test_roi_align_forward_bench_config_bit_exact(dev, layout, roi_set):
+    """The forward at the bench's own configuration, C = 256, P2-P5 of a 2-image 608x1024
+    batch (152x256 ... 19x32), NCHW (channel-pair kernel) and channels-last (the FPN's NHWC
+    levels: channel-quad kernel), on three RoI sets: the 1024 RoIs of a random-init cfg2
+    step (cfg2_rois.npz, 873 / 102 / 42 / 7 on P2..P5: tiny), VOC-sized RoIs in the RCNN
+    sampler's mix around the bench images' gts (cfg2_rois_voc.npz, gen_voc_rois.py: 235 /
+    369 / 219 / 201, tap grids up to 27 x 29 cells) and the RoIs of a `bench.py --mode
+    train` step (cfg2_rois_train.npz, when dumped): every output bit-identical to the oracle
+    (lib/region.py:271-296, torchvision legacy RoIAlign semantics)."""
     from frcnn_amd import ops
-    z = np.load(inputs.golden_path('cfg2_rois.npz'))
+    if not os.path.exists(inputs.golden_path(roi_set)):
+        pytest.skip('{} not generated'.format(roi_set))
+    z = np.load(inputs.golden_path(roi_set))
     rois, levels = z['r5'], z['lv']
     shapes = [tuple(int(v) for v in s) for s in z['shapes']]
     scales = [float(v) for v in z['scales']]
@@ -813,6 +820,46 @@ def test_roi_align_backward_vs_oracle(dev, case):
     ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, sr)
     for a, r in zip(ft, ref):
         np.testing.assert_allclose(a.grad.cpu().numpy(), r, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize('case', ['p2', 'p2_nhwc', 'voc_nhwc'])
+def test_roi_align_backward_deterministic(dev, case):
+    """The deterministic backward (frh_roi_align_bwd_fixed: fixed-point integer atomics,
+    SURVEY §5): within f32-accumulation tolerance of the oracle, bit-identical across runs AND
+    under any permutation of the RoIs (the sum over RoIs is order-independent), where the
+    float-atomic form is not (reference: autograd of lib/region.py:276)."""
+    from frcnn_amd import ops
+    if case == 'voc_nhwc':
+        z = np.load(inputs.golden_path('cfg2_rois_voc.npz'))
+        rois, levels = z['r5'][::4].copy(), z['lv'][::4].copy()
+        grids, scales, C = [tuple(int(v) for v in s[2:]) for s in z['shapes']], [float(v) for v in z['scales']], 64
+    else:
+        grids, scales, C = [(152, 256), (76, 128)], [1 / 4, 1 / 8], 80
+        rois = _rois(61, 300, 2)
+        levels = oracle.roi_level_map(rois, 56.0, 2)
+    K = rois.shape[0]
+    feats = inputs.feature_maps(60, grids, C, 2)
+    g = np.random.default_rng(62).standard_normal((K, C, 7, 7)).astype(np.float32)
+    ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, 2)
+
+    def run(order):
+        ft = [T(f, dev) for f in feats]
+        if case.endswith('nhwc'):
+            ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
+        ft = [f.requires_grad_(True) for f in ft]
+        out = ops.roi_align_multilevel(ft, T(rois[order], dev), T(levels[order], dev), scales, (7, 7), 2)
+        out.backward(T(g[order], dev))
+        return [f.grad.clone() for f in ft]
+    ops.set_deterministic_backward(True)
+    try:
+        a = run(np.arange(K))
+        b = run(np.arange(K))
+        c = run(np.random.default_rng(63).permutation(K))
+    finally:
+        ops.set_deterministic_backward(False)
+    for x, y, z_, r in zip(a, b, c, ref):
+        assert torch.equal(x, y) and torch.equal(x, z_)
+        np.testing.assert_allclose(x.cpu().numpy(), r, rtol=1e-4, atol=2e-5)
 
 
 def test_roi_pool_vs_oracle(dev):

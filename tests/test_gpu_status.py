@@ -1,0 +1,136 @@
+"""The device status word (include/frcnn_amd.h FRH_DEVERR_*, ABI 2).
+
+The one-launch kernels (rpn_select_kernel, nms_fused_kernel, sampler_fused_kernel) hand data
+between workgroups of one launch through bounded waits.  A wait that runs out must surface
+as an error -- the kernel ORs a bit into the caller's status word and stops its work, and
+frcnn_amd.ops.check_device_status() raises -- never as a silently wrong selection or keep
+list (reference semantics that would break: lib/heads/rpn_head.py:68-120,
+lib/region.py:43-57).  tools/lib/libfrcnn_spin.so is the product library rebuilt with
+FRH_SPIN_TICKS=0: every wait not met at its first poll runs out at once."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import inputs
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SPIN = os.path.join(REPO, 'tools', 'lib', 'libfrcnn_spin.so')
+
+
+def _spin():
+    from frcnn_amd import _lib
+    if not os.path.exists(SPIN):
+        pytest.fail('{} missing: python tools/build_tools.py'.format(SPIN))
+    lib = ctypes.CDLL(SPIN)
+    for name in ('frh_rpn_proposals_strided', 'frh_sample_random'):
+        res, args = _lib.SIGNATURES[name]
+        getattr(lib, name).restype, getattr(lib, name).argtypes = res, args
+    return lib
+
+
+def _rpn_inputs(dev, batch=2):
+    from frcnn_amd.heads.rpn_head import RPNHead
+    head = RPNHead(256, 256, loss_cls=dict(type='CrossEntropyLoss', use_sigmoid=True),
+                   loss_bbox=dict(type='SmoothL1Loss', beta=1.0 / 9.0)).to(dev)
+    anchors = head._flat_anchors(inputs.FPN_GRIDS, dev)
+    cls, reg = inputs.head_outputs(5, inputs.FPN_GRIDS, 3, 1, batch=batch, cls_scale=0.01, reg_scale=0.5)
+    cls = [torch.from_numpy(c).to(dev).contiguous(memory_format=torch.channels_last) for c in cls]
+    reg = [torch.from_numpy(r).to(dev).contiguous(memory_format=torch.channels_last) for r in reg]
+    return (cls, reg, anchors, 3, 1, [0.0] * 4, [1.0] * 4, [(600.0, 1000.0)] * batch, [0.0] * batch,
+            2000, 2000, 2000, 0.7)
+
+
+def test_status_word_stays_zero_on_the_product_path(dev):
+    from frcnn_amd import ops
+    args = _rpn_inputs(dev)
+    for _ in range(3):
+        ops.rpn_proposals(*args)
+    lab = torch.from_numpy(np.random.default_rng(1).choice([-1, 0, 1], size=(2, 155520), p=[0.3, 0.69, 0.01])).to(dev)
+    num = torch.full((2,), 155520, dtype=torch.int32, device=dev)
+    ops.sample_labels(lab, num, 155520, 256, 128, mode='device')
+    ops.check_device_status(dev)  # no raise
+    assert int(ops.status_word(dev).item()) == 0
+
+
+def test_rpn_wait_timeout_raises_not_wrong_proposals(dev):
+    """RPN proposals through the zero-spin library: the selection's segment barriers and the
+    one-launch NMS's column waits run out; the status word carries their bits and
+    check_device_status raises.  The product path afterwards is clean and matches the
+    outputs of a fresh call."""
+    from frcnn_amd import ops
+    lib = _spin()
+    args = _rpn_inputs(dev)
+    ref = ops.rpn_proposals(*args)
+    ops.rpn_proposals(*args, _entry=(lib.frh_rpn_proposals_strided, 'spin'))
+    torch.cuda.synchronize()
+    v = int(ops.status_word(dev).item())
+    assert v & 1, v  # FRH_DEVERR_SELECT_BARRIER (the NMS then runs on whatever the aborted selection left)
+    with pytest.raises(RuntimeError, match='in-launch wait timed out'):
+        ops.check_device_status(dev)
+    assert int(ops.status_word(dev).item()) == 0  # cleared by the check
+    again = ops.rpn_proposals(*args)
+    ops.check_device_status(dev)
+    for a, b in zip(ref, again):
+        assert torch.equal(a, b)
+
+
+def test_sampler_wait_timeout_raises(dev):
+    from frcnn_amd import ops
+    lib = _spin()
+    lab = torch.from_numpy(np.random.default_rng(2).choice([-1, 0, 1], size=(2, 155520), p=[0.3, 0.69, 0.01])).to(dev)
+    num = torch.full((2,), 155520, dtype=torch.int32, device=dev)
+    ops.set_sampler_mode('device', seed=3)
+    ref = ops.sample_labels(lab, num, 155520, 256, 128, mode='device')
+    ops.set_sampler_mode('device', seed=3)
+    ops.sample_labels(lab, num, 155520, 256, 128, mode='device', _entry=(lib.frh_sample_random, 'spin'))
+    torch.cuda.synchronize()
+    assert int(ops.status_word(dev).item()) & 4
+    with pytest.raises(RuntimeError, match='device sampler image barrier'):
+        ops.check_device_status(dev)
+    assert not ops._SAMPLE_WS  # the possibly dirty zero-contract workspace was dropped
+    ops.set_sampler_mode('device', seed=3)
+    again = ops.sample_labels(lab, num, 155520, 256, 128, mode='device')
+    ops.check_device_status(dev)
+    assert torch.equal(ref, again)
+    ops.set_sampler_mode('numpy')
+
+
+def test_one_launch_nms_column_timeout_sets_its_bit(dev):
+    """The one-launch NMS alone (tools entry, valid inputs) in the zero-spin build: its loaders'
+    column waits run out, the scan stops (the kept counts stay within the segment) and
+    FRH_DEVERR_NMS_COLUMN is set."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    from frcnn_amd import ops, _lib
+    lib = ctypes.CDLL(SPIN)
+    fn = lib.frh_nms_fused_stamped
+    import toolslib
+    fn.restype, fn.argtypes = toolslib.TOOL_SIGNATURES['frh_nms_fused_stamped']
+    S, P = 4, 2000
+    rng = np.random.default_rng(9)
+    xy = rng.uniform(0, 900, (S, P, 2)).astype(np.float32)
+    wh = rng.uniform(8, 120, (S, P, 2)).astype(np.float32)
+    rows = torch.from_numpy(np.concatenate([xy, xy + wh], 2)).to(dev)
+    cnt = torch.full((S,), P, dtype=torch.int32, device=dev)
+    keep = torch.empty(S, P, dtype=torch.int32, device=dev)
+    kc = torch.empty(S, dtype=torch.int32, device=dev)
+    nb = int(_lib.query('frh_nms_workspace', S, P)) + int(fn_flags(lib)(S, P))
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    r = fn(S, _lib.ptr(rows), rows.stride(0), _lib.ptr(cnt), P, 0.7, -1, _lib.ptr(keep), keep.stride(0), _lib.ptr(kc),
+           _lib.ptr(ops.status_word(dev)), _lib.ptr(ws), ws.numel(), None, _lib.stream_of(rows))
+    assert r == 0
+    torch.cuda.synchronize()
+    assert int(ops.status_word(dev).item()) & 2
+    assert int(kc.min()) >= 0 and int(kc.max()) <= P
+    with pytest.raises(RuntimeError, match='RPN NMS mask column'):
+        ops.check_device_status(dev)
+
+
+def fn_flags(lib):
+    f = lib.frh_nms_fused_flag_bytes
+    f.restype, f.argtypes = ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32]
+    return f

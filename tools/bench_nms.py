@@ -94,7 +94,8 @@ def main():
 
     def fused(stm=None):
         r = lib.frh_nms_fused_stamped(S, _lib.ptr(rows), rows.stride(0), _lib.ptr(cnt), P, thr, max_keep,
-                                      _lib.ptr(keep), keep.stride(0), _lib.ptr(kc), _lib.ptr(fws), fws.numel(),
+                                      _lib.ptr(keep), keep.stride(0), _lib.ptr(kc),
+                                      _lib.ptr(ops.status_word(dev)), _lib.ptr(fws), fws.numel(),
                                       _lib.ptr(stm), _lib.stream_of(rows))
         assert r == 0, lib.frh_last_error()
     for fn, name in ((fused, 'one-launch'), (lambda: fused(fst), 'one-launch stamped')):

@@ -35,8 +35,41 @@ def _compile(src, hdr_mtime):
     return obj
 
 
+SPIN_OBJ = os.path.join(HERE, 'lib', 'obj_spin')
+SPIN_OUT = os.path.join(HERE, 'lib', 'libfrcnn_spin.so')
+
+
+def build_spin():
+    """tools/lib/libfrcnn_spin.so: the product library rebuilt with FRH_SPIN_TICKS=0, so every
+    in-launch wait of the one-launch kernels that is not met at its first poll runs out at
+    once -- the failure path of the device status word (tests/test_gpu_status.py)."""
+    os.makedirs(SPIN_OBJ, exist_ok=True)
+    hm = build_lib._deps_mtime()
+    srcs = sorted(glob.glob(os.path.join(build_lib.CSRC, '*.hip'))) + [os.path.join(SRC, 'nms_lab.hip')]
+
+    def one(src):
+        obj = os.path.join(SPIN_OBJ, os.path.basename(src) + '.o')
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hm):
+            return obj
+        r = subprocess.run([build_lib.HIPCC] + FLAGS + ['-DFRH_SPIN_TICKS=0ull', '-c', src, '-o', obj],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError('hipcc failed for {}:\n{}{}'.format(src, r.stdout, r.stderr))
+        return obj
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(one, srcs))
+    if os.path.exists(SPIN_OUT) and os.path.getmtime(SPIN_OUT) >= max(os.path.getmtime(o) for o in objs):
+        return SPIN_OUT
+    r = subprocess.run([build_lib.HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', SPIN_OUT] + objs,
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('link failed:\n{}{}'.format(r.stdout, r.stderr))
+    return SPIN_OUT
+
+
 def build():
     build_lib.build()
+    build_spin()
     os.makedirs(OBJ, exist_ok=True)
     # any product header / source or tools header / include can change a tools object
     deps = glob.glob(os.path.join(SRC, '*.h')) + glob.glob(os.path.join(SRC, '*.inc')) + \

@@ -36,7 +36,8 @@ int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, int64_t seg
 size_t frh_nms_fused_flag_bytes(int32_t num_segs, int32_t n_max);
 int32_t frh_nms_fused_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride, const int32_t* counts,
                               int32_t n_max, double iou_thr, int32_t max_keep, int32_t* keep, int64_t keep_seg_stride,
-                              int32_t* keep_counts, void* workspace, size_t ws_bytes, int64_t* stamps, void* stream);
+                              int32_t* keep_counts, int32_t* status, void* workspace, size_t ws_bytes, int64_t* stamps,
+                              void* stream);
 
 /* frh_rpn_proposals_strided with the four-launch selection (keys, refine, collect, rank)
  * instead of the one-launch rpn_select_kernel; same arguments and outputs. */
@@ -46,7 +47,7 @@ int32_t frh_rpn_proposals_launches(int32_t num_imgs, int32_t num_levels, const f
                                    int32_t cls_channels, const float* anchors, int64_t anchor_ld, const float* means,
                                    const float* stds, const float* img_hw, const float* min_size, int32_t pre_nms,
                                    int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                   float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
+                                   float* out_scores, int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes,
                                    void* stream);
 
 /* frh_rpn_proposals_strided with the two-launch NMS (mask, scan) instead of the one-launch
@@ -57,13 +58,13 @@ int32_t frh_rpn_proposals_nms2(int32_t num_imgs, int32_t num_levels, const float
                                int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
                                const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num,
                                double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
-                               void* workspace, size_t ws_bytes, void* stream);
+                               int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
 /* frh_sample_random with the keys + collect launches instead of the one-launch sampler. */
 int32_t frh_sample_random_launches(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                    const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                                    uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,
-                                   void* workspace, size_t ws_bytes, void* stream);
+                                   int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
 /* the one-launch selection kernels with per-workgroup phase stamps (16 int64 of s_memrealtime
  * per workgroup of the grid): rpn_select_kernel [S][grid x][16] (frh_rpn_proposals_strided's
@@ -74,12 +75,12 @@ int32_t frh_rpn_proposals_stamped(int32_t num_imgs, int32_t num_levels, const fl
                                   int32_t cls_channels, const float* anchors, int64_t anchor_ld, const float* means,
                                   const float* stds, const float* img_hw, const float* min_size, int32_t pre_nms,
                                   int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                  float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
+                                  float* out_scores, int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes,
                                   int64_t* stamps, void* stream);
 int32_t frh_sample_random_stamped(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                   const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                                   uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,
-                                  void* workspace, size_t ws_bytes, int64_t* stamps, void* stream);
+                                  int32_t* status, void* workspace, size_t ws_bytes, int64_t* stamps, void* stream);
 
 #ifdef __cplusplus
 }

@@ -24,7 +24,7 @@ bool nms_fused_fits(int32_t S, int32_t n_max);
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                         uint64_t* mask, uint32_t* flags, hipStream_t st, int64_t* stamps);
+                         uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps);
 }  // namespace frh
 
 // The RPN's one-launch NMS (nms_fused_kernel) on pre-sorted segments, tiles at s * tri(nbw):
@@ -37,11 +37,13 @@ extern "C" size_t frh_nms_fused_flag_bytes(int32_t num_segs, int32_t n_max) {
 extern "C" int32_t frh_nms_fused_stamped(int32_t num_segs, const float* boxes, int64_t seg_stride,
                                          const int32_t* counts, int32_t n_max, double iou_thr, int32_t max_keep,
                                          int32_t* keep, int64_t keep_seg_stride, int32_t* keep_counts,
-                                         void* workspace, size_t ws_bytes, int64_t* stamps, void* stream) {
+                                         int32_t* status, void* workspace, size_t ws_bytes, int64_t* stamps,
+                                         void* stream) {
   const size_t mb = frh_nms_workspace(num_segs, n_max), fb = frh::nms_fused_flag_bytes(num_segs, n_max);
   FRH_REQUIRE(workspace && ws_bytes >= mb + fb, "workspace too small");
   uint32_t* flags = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + mb);
   FRH_HIP(hipMemsetAsync(flags, 0, fb, frh::as_stream(stream)));
   return frh::launch_nms_fused(num_segs, boxes, seg_stride, counts, n_max, iou_thr, max_keep, keep, keep_seg_stride,
-                               keep_counts, static_cast<uint64_t*>(workspace), flags, frh::as_stream(stream), stamps);
+                               keep_counts, static_cast<uint64_t*>(workspace), flags, status, frh::as_stream(stream),
+                               stamps);
 }

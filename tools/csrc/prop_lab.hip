@@ -12,13 +12,14 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            const int32_t* grid_hw, int32_t num_anchors, int32_t cls_channels, const float* anchors,
                            int64_t anchor_ld, const float* means, const float* stds, const float* img_hw,
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
-                           float* out_boxes, float* out_scores, int32_t* out_counts, void* workspace, size_t ws_bytes,
-                           void* stream, bool select_launches, int64_t* select_stamps = nullptr,
-                           bool nms_launches = false);
+                           float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
+                           void* workspace, size_t ws_bytes, void* stream, bool select_launches,
+                           int64_t* select_stamps = nullptr, bool nms_launches = false);
 int32_t sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                            const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
-                           uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, void* workspace,
-                           size_t ws_bytes, void* stream, bool two_launches, int64_t* stamps = nullptr);
+                           uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, int32_t* status,
+                           void* workspace, size_t ws_bytes, void* stream, bool two_launches,
+                           int64_t* stamps = nullptr);
 }  // namespace frh
 
 extern "C" int32_t frh_rpn_proposals_launches(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
@@ -28,11 +29,11 @@ extern "C" int32_t frh_rpn_proposals_launches(int32_t num_imgs, int32_t num_leve
                                               int64_t anchor_ld, const float* means, const float* stds,
                                               const float* img_hw, const float* min_size, int32_t pre_nms,
                                               int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                              float* out_scores, int32_t* out_counts, void* workspace,
+                                              float* out_scores, int32_t* out_counts, int32_t* status, void* workspace,
                                               size_t ws_bytes, void* stream) {
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
-                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes,
+                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
                                  stream, true);
 }
 
@@ -43,19 +44,20 @@ extern "C" int32_t frh_rpn_proposals_nms2(int32_t num_imgs, int32_t num_levels, 
                                           const float* means, const float* stds, const float* img_hw,
                                           const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num,
                                           double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
-                                          void* workspace, size_t ws_bytes, void* stream) {
+                                          int32_t* status, void* workspace, size_t ws_bytes, void* stream) {
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
-                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes,
+                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
                                  stream, false, nullptr, true);
 }
 
 extern "C" int32_t frh_sample_random_launches(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                               const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
                                               int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
-                                              int32_t* sel_counts, void* workspace, size_t ws_bytes, void* stream) {
+                                              int32_t* sel_counts, int32_t* status, void* workspace, size_t ws_bytes,
+                                              void* stream) {
   return frh::sample_random_impl(num_segs, labels_in, label_seg_stride, num_boxes, max_boxes, max_num, pos_num, seed,
-                                 labels_out, sel, sel_counts, workspace, ws_bytes, stream, true);
+                                 labels_out, sel, sel_counts, status, workspace, ws_bytes, stream, true);
 }
 
 // the one-launch kernels with per-workgroup phase stamps (16 int64 per workgroup of the grid,
@@ -67,19 +69,19 @@ extern "C" int32_t frh_rpn_proposals_stamped(int32_t num_imgs, int32_t num_level
                                              int64_t anchor_ld, const float* means, const float* stds,
                                              const float* img_hw, const float* min_size, int32_t pre_nms,
                                              int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                             float* out_scores, int32_t* out_counts, void* workspace,
+                                             float* out_scores, int32_t* out_counts, int32_t* status, void* workspace,
                                              size_t ws_bytes, int64_t* stamps, void* stream) {
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
-                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, workspace, ws_bytes,
+                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
                                  stream, false, stamps);
 }
 
 extern "C" int32_t frh_sample_random_stamped(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                              const int32_t* num_boxes, int64_t max_boxes, int32_t max_num,
                                              int32_t pos_num, uint64_t seed, int64_t* labels_out, int32_t* sel,
-                                             int32_t* sel_counts, void* workspace, size_t ws_bytes, int64_t* stamps,
+                                             int32_t* sel_counts, int32_t* status, void* workspace, size_t ws_bytes, int64_t* stamps,
                                              void* stream) {
   return frh::sample_random_impl(num_segs, labels_in, label_seg_stride, num_boxes, max_boxes, max_num, pos_num, seed,
-                                 labels_out, sel, sel_counts, workspace, ws_bytes, stream, false, stamps);
+                                 labels_out, sel, sel_counts, status, workspace, ws_bytes, stream, false, stamps);
 }

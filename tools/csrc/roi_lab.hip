@@ -36,17 +36,68 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant == 21 || variant == 22) {  // quad kernel with the bank-group column swizzle (22: + LDS-staged stores)
+  if (variant >= 28 && variant <= 39) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+                                         // 31 256 cells, 32 208 cells at 4 waves per SIMD
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
+                "the band kernel does not take this shape");
+    const int64_t tq = num_rois * ((channels + 4 * kQuadWave - 1) / (4 * kQuadWave));
+    const dim3 gq((unsigned)(8 * ((tq + 7) / 8)));
+    if (variant == 28)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 29)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 208>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 30)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 176>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 31)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 256>), gq, dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 32)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 4>), gq, dim3(kWave), 0, st, lv, c,
+                         out);
+    else if (variant == 33)  // no quad rotation
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 0>), gq, dim3(kWave), 0, st, lv,
+                         c, out);
+    else if (variant == 34)  // rotation, per-step stores
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 2>), gq, dim3(kWave), 0, st, lv,
+                         c, out);
+    else if (variant == 35)  // hybrid: small windows by the quad path
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 1, true>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 36)  // hybrid, 160-cell slab (10 KB)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 3, 1, true>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 37)  // hybrid, 160-cell slab, 4 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 4, 1, true>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 38)  // hybrid, bands without quad rotation
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 0, true>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else  // 39: hybrid, bands without rotation, stamped
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 208, false, 3, 0, true>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
+  if (variant == 26 || variant == 27) {  // quad kernel, chunk-pair-major item order (27: + stamps)
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");
     const int64_t tq = num_rois * ((channels + 4 * kQuadWave - 1) / (4 * kQuadWave));
     const dim3 gq((unsigned)(8 * ((tq + 7) / 8)));
-    if (variant == 21)
-      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, false, true>), gq, dim3(kWave), 0,
-                         st, lv, c, out);
+    if (variant == 26)
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, false, kQuadSlab, 1>), gq,
+                         dim3(kWave), 0, st, lv, c, out);
     else
-      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 1, false, true>), gq, dim3(kWave), 0,
-                         st, lv, c, out);
+      hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, true, 3, kQuadWave, 0, false, kQuadSlab, 1>), gq,
+                         dim3(kWave), 0, st, lv, c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
+  if (variant == 25) {  // quad kernel with a 16-KB slab (10 waves per CU by LDS; D = 4 up to 256 cells)
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w, QuadLayout<1, 4096>::kCells),
+                "the quad kernel does not take this shape");
+    const int64_t tq = num_rois * ((channels + 4 * kQuadWave - 1) / (4 * kQuadWave));
+    const dim3 gq((unsigned)(8 * ((tq + 7) / 8)));
+    hipLaunchKernelGGL((roi_align_fwd_quad_kernel<kCpolNT, false, 3, kQuadWave, 0, false, 4096>), gq, dim3(kWave), 0,
+                       st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
   if (variant == 19 || variant == 20) {  // quad kernel, RoI setup shared by a 4-wave workgroup (20: LDS-staged stores)

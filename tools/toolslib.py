@@ -20,7 +20,7 @@ TOOL_SIGNATURES = {
                                        c_vp, c_size, c_vp, c_vp]),
     'frh_nms_fused_flag_bytes': (c_size, [c_i32, c_i32]),
     'frh_nms_fused_stamped': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, ctypes.c_double, c_i32, c_vp, c_i64, c_vp,
-                                      c_vp, c_size, c_vp, c_vp]),
+                                      c_vp, c_vp, c_size, c_vp, c_vp]),
     'frh_rpn_proposals_launches': _lib.SIGNATURES['frh_rpn_proposals_strided'],
     'frh_rpn_proposals_nms2': _lib.SIGNATURES['frh_rpn_proposals_strided'],
     'frh_sample_random_launches': _lib.SIGNATURES['frh_sample_random'],
