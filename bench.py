@@ -296,6 +296,40 @@ def roi_align_replays(recs, dev, rounds=3):
     return warm, float(np.median(colds))
 
 
+def roi_set_line(rec, fixture, dev, iters=20):
+    """The product RoIAlign forward on this step's own FPN levels (the record's features, their
+    layout and strides) with a fixed RoI set instead of the step's random-init RoIs:
+    tests/golden/cfg2_rois_voc.npz (VOC-sized RoIs in the RCNN sampler's mix around the bench
+    images' gts) or cfg2_rois_train.npz (a training step's RoIs).  Back-to-back
+    launches between one event pair, µs per launch, algorithmic bytes as the headline's."""
+    from frcnn_amd import ops
+    path = os.path.join(REPO, 'tests', 'golden', fixture)
+    if rec is None or not os.path.exists(path):
+        return None
+    z = np.load(path)
+    rois = torch.from_numpy(np.ascontiguousarray(z['r5'], np.float32)).to(dev)
+    levels = torch.from_numpy(z['lv'].astype(np.int64)).to(dev)
+    e0, e1, _, _, shapes, osz, feats, scales, sr = rec
+    if [tuple(int(v) for v in q) for q in z['shapes']] != [tuple(q) for q in shapes[:len(z['shapes'])]]:
+        return {'note': 'fixture shapes differ from this run\'s levels'}
+    r = (None, None, rois, levels, shapes, osz, feats, scales, sr)
+    for _ in range(3):
+        ops.roi_align_replay(r)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        ops.roi_align_replay(r)
+    b.record()
+    torch.cuda.synchronize(dev)
+    us = a.elapsed_time(b) * 1e3 / iters
+    nbytes = roi_align_bytes(r)
+    gbs = nbytes / (us * 1e-6) / 1e9
+    return {'fixture': 'tests/golden/' + fixture, 'rois': int(rois.shape[0]),
+            'levels': np.bincount(z['lv'], minlength=4).tolist(), 'avg_launch_us': us,
+            'algorithmic_bytes_per_launch': nbytes, 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': gbs / HBM_PEAK_GBS, 'timing': 'back-to-back launches on this run\'s FPN levels, warm'}
+
+
 def nms_replay_us(recs, dev):
     """The recorded RPN NMS calls replayed back to back (warm); µs per call."""
     from frcnn_amd import _lib
@@ -707,7 +741,10 @@ def main():
         us_for_frac = roi_in_step if roi_in_step else warm
         achieved = avg_bytes / (us_for_frac * 1e-6) / 1e9 if recs and us_for_frac else None
         traffic = None
-        pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json')
+        # PMC traffic of this mode's own RoIAlign launches (tools/profile_r05.sh: FETCH_SIZE / WRITE_SIZE
+        # passes over `bench.py` and `bench.py --mode train`)
+        pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json' if args.mode == 'fwd' else
+                           'roi_align_pmc_train.json')
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
 
@@ -765,6 +802,8 @@ def main():
                            'each launch after a 768 MB read (L2 + Infinity Cache evicted)'.format(steps_traced)) +
                           '; traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per launch, '
                           'profiles/roi_align_pmc.json'}
+            out['roofline_voc_rois'] = roi_set_line(recs[-1], 'cfg2_rois_voc.npz', dev)
+            out['roofline_train_rois'] = roi_set_line(recs[-1], 'cfg2_rois_train.npz', dev)
         else:
             out['roofline'] = None  # no RoIAlign on this model's path
         if trace:

@@ -88,7 +88,8 @@ int32_t frh_elem_iou(const float* a, int64_t lda, const float* b, int64_t ldb, i
  * and take no part in the per-gt maxima), gts at gts + s*gt_seg_stride
  * ([4, gt_ld]), count num_gts[s] (device).  Labels are int64:
  * -1 ignore, 0 negative, g+1 positive for gt g; max_iou f32.  Thresholds are
- * compared in f32 like the reference (`f32 tensor < python float`).
+ * compared in f32 like the reference (`f32 tensor < python float`).  Rows in
+ * [num_boxes[s], max_boxes) are padding: label -1, max_iou 0.
  * max_boxes / max_gts bound the launch (host-known maxima of the counts).  One launch: the
  * last workgroup of each segment labels the boxes tied at a gt's maximum (hand-off inside
  * the launch).  Workspace: frh_maxiou_assign_workspace bytes whose leading
@@ -207,7 +208,8 @@ int32_t frh_scatter_level_grads_strided(int32_t num_levels, float* const* level_
 /* ---- a12: bbox_target (lib/bbox.py:6-82) ------------------------------------
  * frh_prepend_gt_labels builds the reference's candidate list
  * [gts ; proposals] (bbox.py:27-29): rows_out[s, j] = j+1 for j < G_s, else
- * prop_labels[s, j-G_s]; num_rows[s] = G_s + n_s.  After sampling those rows,
+ * prop_labels[s, j-G_s]; num_rows[s] = G_s + n_s; rows in [G_s + n_s, max_rows) are
+ * padding, label -1.  After sampling those rows,
  * frh_bbox_target (labels = the sampled rows, num_rows from the prepend)
  * gathers the chosen rows (ascending) into concatenated
  * outputs: tar_props/tar_bbox/tar_param [4, out_ld], tar_label (int64, gt

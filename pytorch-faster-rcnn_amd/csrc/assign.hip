@@ -235,8 +235,8 @@ __global__ void __launch_bounds__(kAssignThreads) maxiou_assign_kernel(AssignArg
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t i = base + r * kAssignThreads;
-    if (cand[r] || i >= n) continue;
-    const bool lab = live[r] && G > 0;
+    if (cand[r] || i >= p.cand_ld) continue;  // cand_ld = max_boxes: rows past the count are padding
+    const bool lab = live[r] && G > 0;  // padding rows (i >= n) and masked boxes: label -1, IoU 0
     p.labels[(int64_t)s * p.label_seg_stride + i] = lab ? threshold_label(p, m[r], arg[r]) : -1;
     if (p.max_iou) p.max_iou[(int64_t)s * p.iou_seg_stride + i] = lab ? m[r] : 0.0f;
   }

@@ -6,9 +6,12 @@
 //
 // Forward (all bit-identical: -ffp-contract=off, reference op order; kernels in
 // roi_kernels.h):
-//  * roi_align_fwd_quad_kernel -- channels-last features (unit channel stride, C % 4
-//    == 0, sampling 2, up to 8x8 bins): the pair kernel's structure with channel quads:
-//    16-B LDS-DMA staging (lane = cell), one ds_read_b128 per tap for 4 channels.
+//  * roi_align_fwd_band_kernel -- channels-last features (unit channel stride, C % 4
+//    == 0, sampling 2, 7x7 bins and smaller): small windows as the quad kernel (16-B
+//    LDS-DMA staging, lane = cell, one ds_read_b128 per tap for 4 channels), larger ones
+//    in row bands of [cell][16 channels] with one 64-B request per cell (roi_kernels.h).
+//  * roi_align_fwd_quad_kernel -- the quad path alone, for channels-last shapes the band
+//    kernel does not take.
 //  * roi_align_fwd_pair_kernel -- the default (sampling 2, up to 8x8 bins, even C):
 //    one wave per (RoI, 16 channels); the RoI's tap window staged by LDS-DMA with
 //    channel pairs interleaved into one slab buffer per wave, packed-f32 bilinear sums.
@@ -27,7 +30,15 @@
 
 namespace frh {
 
-constexpr int kBandCells = 208;  // the band kernel's slab: 13 KB = 208 cells x 16 channels
+// The band kernel's slab: 232 cells x 16 channels = 14.5 KB (11 waves per CU by LDS, 3 per
+// SIMD by registers): 8-row bands of the widest (29-column) windows, i.e. two bin rows of a
+// tap-list window per band.  Windows of <= 192 cells take the quad path (kHybrid = 4).
+// The bands' results are stored after the last band (kRot 3: whole channel rows per store).
+// Measured (tools/bench_roi_sets.py, MI355X, µs per launch, bench / VOC / train-step RoIs):
+// this form 40.9 / 76.2 / 65.2 (stores per band: 40.9-42.9 / 77.2-79.0 / 67.2-69.3); bands
+// only 44.1-47.3 / 76-78 / 66-70; quad kernel (13 KB slab, pair order) 37.7-39.1 / 103-106 /
+// 96-98; round 4's 37.1-39.5 / 142 / 150.
+constexpr int kBandCells = 232;
 
 // region.py:256-264: floor(log2(sqrt(area) / finest + 1e-6)) clamped to [0, L-1]
 __device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, float y2, float finest, int L) {
@@ -163,9 +174,9 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
     const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
     if (span)
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true, 3, 3, 4>, grid, dim3(kWave));
     else
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, false, 3, 3, 4>, grid, dim3(kWave));
   } else if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
     // channels-last, shapes the band kernel does not take: one quad per 16-B DMA lane
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);

@@ -1029,12 +1029,15 @@ struct BandLayout {
 // kRot: 0 = every lane reads quad d at step d (bank conflicts: 4 bank groups per quad);
 // 1 = lane l reads quad (d + l) mod 4, results kept and stored per channel after the 4 steps
 // (each store instruction writes one channel plane, 49 contiguous floats); 2 = as 1 but
-// each step's quad stored at once (lane-dependent channel planes: 4 partial lines each).
-// kHybrid: windows of at most QuadLayout<4, kSlabCells * 16>::kCells cells (every random-init
-// RoI of the bench, most small RoIs) take the quad kernel's one-stage path instead -- lane =
-// cell, 64 cells and one address per DMA instruction: fewer instructions where the window
-// is small and the L2 request rate is not the bound -- the rest the bands.
-template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, bool kHybrid = false>
+// each step's quad stored at once (lane-dependent channel planes: 4 partial lines each);
+// 3 = as 0, the results kept until the last band and stored by every bin at once (a band's
+// own stores cover only its bins' part of each channel row: partial lines).
+// kHybrid = D > 0: windows that the quad kernel stages D quads at a time (at most
+// QuadLayout<D, kSlabCells * 16>::kCells cells: every random-init RoI of the bench but a few,
+// most small RoIs) take its path instead -- lane = cell, 64 cells and one address per DMA
+// instruction: fewer instructions where the window is small and the L2 request rate is not
+// the bound -- the rest the bands.
+template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0>
 __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
   constexpr int SR = 2;
@@ -1043,10 +1046,10 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
   PairLane P;
   const RoiRaw raw = roi_fetch(c, k);
   pair_setup<kHybrid ? 16 : 64>(lv, c, raw, lane, G, P);
-  if constexpr (kHybrid) {
-    if (!G.empty && G.R * G.Cs2 <= QuadLayout<4, kSlabCells * 16>::kCells) {
-      quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, true>(G, P, c, out, k, chunk, item, sbase, t_start,
-                                                                    lane, nullptr);
+  if constexpr (kHybrid > 0) {
+    if (!G.empty && G.R * G.Cs2 <= QuadLayout<kHybrid, kSlabCells * 16>::kCells) {
+      quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, kHybrid == 4>(G, P, c, out, k, chunk, item, sbase,
+                                                                            t_start, lane, nullptr);
       return;
     }
 #pragma unroll
@@ -1079,6 +1082,7 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
   const int soff = cw0 * 4;
   bool pending = active;
   int nbands = 0;
+  f32x4 res0 = {}, res1 = {}, res2 = {}, res3 = {};  // kRot 1 / 3: the step results (named: no indexed array)
   while (true) {
     const uint64_t pend = __ballot(pending);
     if (!pend) break;
@@ -1118,10 +1122,9 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
         for (int jx = 0; jx < SR; ++jx)  // invalid samples read band cell 0 (finite) with zero weights
           lb[i][jx] = sbase + (((P.vmask >> (2 * i + jx)) & 1u) ? P.tb0[i][jx] - boff : 0u);
       }
-      f32x4 res0 = {}, res1 = {}, res2 = {}, res3 = {};  // kRot 1: the step results (named: no indexed array)
       static_for<0, kQuadWave>([&](auto dd) {
         constexpr int d = decltype(dd)::value;
-        const int qq = kRot ? (d + lane) & 3 : d;  // this lane's quad at step d
+        const int qq = kRot == 1 || kRot == 2 ? (d + lane) & 3 : d;  // this lane's quad at step d
         const uint32_t qo = 16u * (uint32_t)qq;
         uint32_t lq[SR][SR];
 #pragma unroll
@@ -1154,7 +1157,7 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
           acc = acc + quad_val(w, &v[1][ix * 4]);
         }
         const f32x4 r4 = acc * 0.25f;  // count 4: / 4 == * 0.25
-        if constexpr (kRot == 1) {
+        if constexpr (kRot == 1 || kRot == 3) {
           if constexpr (d == 0) res0 = r4;
           if constexpr (d == 1) res1 = r4;
           if constexpr (d == 2) res2 = r4;
@@ -1190,6 +1193,18 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if constexpr (kRot == 3) {  // every bin's 16 channels after the last band: whole channel rows per store
+    const int vo = active ? lane * 4 : 0x40000000;
+    static_for<0, kQuadWave>([&](auto qd) {
+      constexpr int Q = decltype(qd)::value;
+      const f32x4 r4 = Q == 0 ? res0 : Q == 1 ? res1 : Q == 2 ? res2 : res3;
+      const int v = Q < nquads ? vo : 0x40000000;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, v, (4 * Q) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, v, (4 * Q + 1) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, v, (4 * Q + 2) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, v, (4 * Q + 3) * ostep, kStAux);
+    });
+  }
   if (kStamp && lane == 0) {
     int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + item * 8;
     st[0] = t_start;
@@ -1207,7 +1222,7 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
 // the item list in chunk-pair-major order (quad kernel, kOrder 1: the two 16-channel chunks of
 // a 128-B line, adjacent, on one XCD).
 template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
-          int kRot = 1, bool kHybrid = false>
+          int kRot = 1, int kHybrid = 0>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;

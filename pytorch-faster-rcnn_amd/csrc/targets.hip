@@ -292,8 +292,8 @@ __global__ void prepend_gt_kernel(const int64_t* prop_labels, int64_t pstride, c
   const int64_t G = num_gts[s], n = num_props[s];
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) num_rows[s] = (int32_t)(G + n);
-  if (j >= G + n || j >= max_rows) return;
-  rows[(int64_t)s * rstride + j] = j < G ? j + 1 : prop_labels[(int64_t)s * pstride + (j - G)];
+  if (j >= max_rows) return;  // rows past G + n: padding label -1
+  rows[(int64_t)s * rstride + j] = j < G ? j + 1 : (j < G + n ? prop_labels[(int64_t)s * pstride + (j - G)] : -1);
 }
 
 struct BBoxTargetArgs {

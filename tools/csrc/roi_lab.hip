@@ -36,7 +36,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant >= 28 && variant <= 39) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+  if (variant >= 28 && variant <= 46) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
                                          // 31 256 cells, 32 208 cells at 4 waves per SIMD
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
@@ -61,19 +61,40 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 2>), gq, dim3(kWave), 0, st, lv,
                          c, out);
     else if (variant == 35)  // hybrid: small windows by the quad path
-      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 1, true>), gq, dim3(kWave), 0, st,
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 1, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
     else if (variant == 36)  // hybrid, 160-cell slab (10 KB)
-      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 3, 1, true>), gq, dim3(kWave), 0, st,
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 3, 1, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
     else if (variant == 37)  // hybrid, 160-cell slab, 4 waves per SIMD
-      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 4, 1, true>), gq, dim3(kWave), 0, st,
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 160, false, 4, 1, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
     else if (variant == 38)  // hybrid, bands without quad rotation
-      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 0, true>), gq, dim3(kWave), 0, st,
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
-    else  // 39: hybrid, bands without rotation, stamped
-      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 208, false, 3, 0, true>), gq, dim3(kWave), 0, st,
+    else if (variant == 39)  // hybrid, bands without rotation, stamped
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 208, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 40)  // hybrid up to the quad path's D = 2 windows (<= 384 cells), bands above
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 0, 2>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 41)  // hybrid (D = 4), 232-cell slab: 8-row bands
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 42)  // hybrid (D = 2), 232-cell slab
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 0, 2>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 43)  // hybrid (D = 4), 232-cell slab, rotated quads in the bands
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 1, 4>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 44)  // hybrid (D = 4), 256-cell slab
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 256, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 46)  // hybrid (D = 4), 232-cell slab, stores after the last band
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 3, 4>), gq, dim3(kWave), 0, st,
+                         lv, c, out);
+    else  // 45: hybrid (D = 4), 232-cell slab, stamped
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
