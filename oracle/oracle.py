@@ -260,9 +260,12 @@ def random_sampler(labels, max_num, pos_num):
 
 def anchor_target(cls_out, reg_out, cls_channels, in_anchors, in_mask, gt_bbox, gt_label, assign, sampler,
                   means, stds):
-    """lib/anchor.py:11-76.  assign = (pos, neg, min_pos); sampler = (max_num, pos_num) or None."""
+    """lib/anchor.py:11-76.  assign = (pos, neg, min_pos); sampler = (max_num, pos_num), None, or a
+    callable labels -> sampled labels (tests: a given selection, e.g. the device sampler's)."""
     labels, _ = maxiou_assign(in_anchors, gt_bbox, *assign)
-    if sampler is not None:
+    if callable(sampler):
+        labels = sampler(labels)
+    elif sampler is not None:
         labels = random_sampler(labels, *sampler)
     non_neg = labels >= 0
     zero = labels == 0
@@ -292,7 +295,7 @@ def bbox_target(props, gt_bbox, gt_label, assign, sampler, means=None, stds=None
     G = gt_bbox.shape[1]
     props = np.concatenate([gt_bbox, np.asarray(props, np.float32)], 1)
     labels = np.concatenate([np.arange(1, G + 1, dtype=np.int64), labels])
-    labels = random_sampler(labels, *sampler)
+    labels = sampler(labels) if callable(sampler) else random_sampler(labels, *sampler)
     chosen = labels >= 0
     neg = labels == 0
     is_gt = np.zeros(props.shape[1], np.int64)

@@ -26,7 +26,10 @@ def _in_mask(head, flat, grids, img_size, border):
     return ingrid & oracle.inside_anchor_mask(flat, img_size, border)
 
 
-def forward_train_cpu(model, cfg, imgs, gt_bboxes, gt_labels, img_metas):
+def forward_train_cpu(model, cfg, imgs, gt_bboxes, gt_labels, img_metas, sampler_hook=None):
+    """sampler_hook (tests): callable(stage, image, labels) -> sampled labels replacing the numpy
+    RandomSampler; stage 'rpn' (labels over the image's inside anchors) or 'rcnn<k>' (labels over
+    the prepended [gts; proposals] rows)."""
     tc = cfg.train_cfg
     feats = model.extract_feat(imgs)
     head = model.rpn_head
@@ -44,7 +47,8 @@ def forward_train_cpu(model, cfg, imgs, gt_bboxes, gt_labels, img_metas):
         gb = gt_bboxes[i].numpy()
         out = oracle.anchor_target(co.detach().numpy(), ro.detach().numpy(), head.cls_channels, flat[:, mask], mask, gb,
                                    np.ones(gb.shape[1], np.int64), (a.pos_iou, a.neg_iou, a.min_pos_iou),
-                                   (s.max_num, s.pos_num) if s else None, head.target_means, head.target_stds)
+                                   ((lambda lab, i=i: sampler_hook('rpn', i, lab)) if sampler_hook else
+                                    (s.max_num, s.pos_num)) if s else None, head.target_means, head.target_stds)
         chosen = torch.from_numpy(out[6])
         t_cls.append(co[:, chosen])
         t_reg.append(ro[:, chosen])
@@ -68,7 +72,9 @@ def forward_train_cpu(model, cfg, imgs, gt_bboxes, gt_labels, img_metas):
         for i in range(len(img_metas)):
             out = oracle.bbox_target(props[i], gt_bboxes[i].numpy(), gt_labels[i].numpy(),
                                      (sc.assigner.pos_iou, sc.assigner.neg_iou, sc.assigner.min_pos_iou),
-                                     (sc.sampler.max_num, sc.sampler.pos_num), rh.target_means, rh.target_stds)
+                                     (lambda lab, i=i, st=st: sampler_hook('rcnn{}'.format(st), i, lab))
+                                     if sampler_hook else (sc.sampler.max_num, sc.sampler.pos_num),
+                                     rh.target_means, rh.target_stds)
             tl.append(torch.from_numpy(out[2]))
             tp.append(torch.from_numpy(out[3]))
             rois.append(np.concatenate([np.full((1, out[0].shape[1]), i, np.float32), out[0]], 0).T)
