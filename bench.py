@@ -686,6 +686,7 @@ def main():
     ops.ROI_ALIGN_PROFILE['event_pool'] = pool
     ops.ROI_ALIGN_PROFILE['timed'] = timed_roi = []
     barrier()
+    roi_launches_before = ops.ROI_ALIGN_PROFILE['launches']  # warmup + graph-capture steps (step_breakdown)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -779,6 +780,7 @@ def main():
                 'frac': achieved / HBM_PEAK_GBS if achieved else None, 'traffic': traffic,
                 'avg_launch_us': us_for_frac, 'algorithmic_bytes_per_launch': avg_bytes,
                 'launches': len(recs),
+                'launches_before_timed_region': roi_launches_before,
                 'in_step_event_us_median': roi_events, 'in_step_event_us': roi_in_step_all,
                 'in_step_span_us_median': roi_span, 'in_step_span_us': [round(us, 2) for us in roi_span_us],
                 'achieved_in_step': avg_bytes / (roi_span * 1e-6) / 1e9 if roi_span else None,

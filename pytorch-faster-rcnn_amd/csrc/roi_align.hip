@@ -168,15 +168,17 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
       hipLaunchKernelGGL(kern, grid, block, 0, st, lv, c, out);
   };
   if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
-    // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels), the
-    // window staged in row bands of [cell][16 channels], 64 B per cell and request
+    // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels); tap
+    // windows of <= ~232 cells staged whole, 4 quads at a time ([quad][cell]); <= 464 cells
+    // whole in two stages of [cell][2 quads] (32 B per cell and request); larger in row bands
+    // of [cell][16 channels], 64 B per cell and request
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
     const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
     if (span)
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true, 3, 3, 4>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true, 3, 3, 4, 0, 2>, grid, dim3(kWave));
     else
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, false, 3, 3, 4>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, false, 3, 3, 4, 0, 2>, grid, dim3(kWave));
   } else if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
     // channels-last, shapes the band kernel does not take: one quad per 16-B DMA lane
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);

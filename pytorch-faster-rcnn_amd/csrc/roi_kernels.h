@@ -1032,12 +1032,106 @@ struct BandLayout {
 // each step's quad stored at once (lane-dependent channel planes: 4 partial lines each);
 // 3 = as 0, the results kept until the last band and stored by every bin at once (a band's
 // own stores cover only its bins' part of each channel row: partial lines).
+// Whole-window stages of two channel quads, cell-interleaved: the slab holds [cell][2 quads]
+// (32 B per cell), the two lanes of a cell read its 32 contiguous bytes (one request for two
+// quads, the quad layout's [quad][cell] takes two), quads {0, 1} then {2, 3}.  G / P carry the
+// quad layout's 16-B tap offsets (pair_setup<16>); every lane evaluates every stage (no band
+// masking) and stores whole channel rows.  For windows of up to kSlabCells * 2 cells.
+template <int kStAux, int kSlabCells, int D = 2>
+__device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
+                                          float* __restrict__ out, int64_t k, int chunk, uint32_t sbase, int lane) {
+  constexpr int SR = 2;
+  const int cw0 = chunk * 4 * kQuadWave;
+  const int nquads = min(kQuadWave, (c.C - cw0) / 4);  // host: C % 4 == 0
+  const int nbins = c.ph * c.pw;
+  const bool active = lane < nbins;
+  const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + cw0) * nbins, (int64_t)4 * nquads * nbins * 4);
+  const int ovoff = active ? lane * 4 : 0x40000000;
+  const int ostep = nbins * 4;
+  const int y0 = G.y0, x0 = G.x0, Cs = G.Cs, Cs2 = G.Cs2, sy = G.sy, sx = G.sx;
+  const bool dense = G.dy && G.dx;
+  const int ncell = G.R * Cs2;
+  constexpr int kLg = D == 4 ? 2 : 1;
+  const int nj = (ncell + (kWave / D - 1)) >> (6 - kLg);  // 64 / D cells per DMA instruction
+  const __amdgpu_buffer_rsrc_t fr = uniform_rsrc(G.base, (int64_t)G.extent);
+  const uint32_t inv = G.inv;
+  const int soff = cw0 * 4;
+  for (int s = 0; s < 4 / D; ++s) {
+    const int dq = min(D * s + (lane & (D - 1)), nquads - 1);
+    for (int j = 0; j < nj; ++j) {
+      int e = (kWave / D) * j + (lane >> kLg);
+      e = e < ncell ? e : 0;
+      const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
+      const int goff = dense ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(P.rsrc, r, kWave) + __shfl(P.csrc, col, kWave);
+      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, goff + dq * 16, soff);
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x4 v[2][8];
+    float ly_h[SR], ly_l[SR], lx_h[SR], lx_l[SR];
+    uint32_t lb[SR][SR], ldq[SR], ldr[SR];
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {  // 16*D-B cells: the quad layout's offsets times D
+      ly_h[i] = P.fyh[i], ly_l[i] = P.fyl[i], lx_h[i] = P.fxh[i], lx_l[i] = P.fxl[i], ldq[i] = P.tdq[i] << kLg,
+      ldr[i] = P.tdr[i] << kLg;
+      asm volatile("" : "+v"(ly_h[i]), "+v"(ly_l[i]), "+v"(lx_h[i]), "+v"(lx_l[i]), "+v"(ldq[i]), "+v"(ldr[i]));
+#pragma unroll
+      for (int jx = 0; jx < SR; ++jx) {
+        lb[i][jx] = sbase + (P.tb0[i][jx] << kLg);
+        asm volatile("" : "+v"(lb[i][jx]));
+      }
+    }
+    auto tap = [&](int iy, int ix, int q) -> uint32_t {
+      return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
+    };
+    static_for<0, D>([&](auto dd) {
+      constexpr int d = decltype(dd)::value;
+      auto load = [&](auto hh) {
+        constexpr int iy = decltype(hh)::value;
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[iy][ix * 4 + q] = lds_read_b128<16 * d>(tap(iy, ix, q));
+      };
+      load(std::integral_constant<int, 0>{});
+      load(std::integral_constant<int, 1>{});
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      lds_wait4<8>(v[0]);
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const float w[4] = {ly_h[0] * lx_h[ix], ly_h[0] * lx_l[ix], ly_l[0] * lx_h[ix], ly_l[0] * lx_l[ix]};
+        acc = acc + quad_val(w, &v[0][ix * 4]);
+      }
+      lds_wait4<0>(v[1]);
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const float w[4] = {ly_h[1] * lx_h[ix], ly_h[1] * lx_l[ix], ly_l[1] * lx_h[ix], ly_l[1] * lx_l[ix]};
+        acc = acc + quad_val(w, &v[1][ix * 4]);
+      }
+      const f32x4 r4 = acc * 0.25f;  // count 4: / 4 == * 0.25
+      const int Q = D * s + d;
+      const int vo = Q < nquads ? ovoff : 0x40000000;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, vo, (4 * Q) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, vo, (4 * Q + 1) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, vo, (4 * Q + 2) * ostep, kStAux);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, vo, (4 * Q + 3) * ostep, kStAux);
+    });
+    // this stage's tap reads are complete (lds_wait4<0>) before the next stage's DMA
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // kHybrid = D > 0: windows that the quad kernel stages D quads at a time (at most
 // QuadLayout<D, kSlabCells * 16>::kCells cells: every random-init RoI of the bench but a few,
 // most small RoIs) take its path instead -- lane = cell, 64 cells and one address per DMA
 // instruction: fewer instructions where the window is small and the L2 request rate is not
 // the bound -- the rest the bands.
-template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0>
+template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0, int kHybridHi = 0,
+          int kIlv = 0>
 __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
   constexpr int SR = 2;
@@ -1045,12 +1139,33 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
   PairGeom G;
   PairLane P;
   const RoiRaw raw = roi_fetch(c, k);
-  pair_setup<kHybrid ? 16 : 64>(lv, c, raw, lane, G, P);
-  if constexpr (kHybrid > 0) {
-    if (!G.empty && G.R * G.Cs2 <= QuadLayout<kHybrid, kSlabCells * 16>::kCells) {
-      quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, kHybrid == 4>(G, P, c, out, k, chunk, item, sbase,
-                                                                            t_start, lane, nullptr);
-      return;
+  pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, G, P);
+  if constexpr (kHybrid > 0 || kIlv > 0) {
+    if constexpr (kHybrid > 0) {
+      if (!G.empty && G.R * G.Cs2 <= QuadLayout<kHybrid, kSlabCells * 16>::kCells) {
+        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, kHybrid == 4>(G, P, c, out, k, chunk, item, sbase,
+                                                                              t_start, lane, nullptr);
+        return;
+      }
+    }
+    if constexpr ((kIlv & 1) != 0) {  // up to kSlabCells cells: one whole-window stage of [cell][4 quads]
+      if (!G.empty && G.R * G.Cs2 <= kSlabCells) {
+        ilv_body<kStAux, kSlabCells, 4>(G, P, c, out, k, chunk, sbase, lane);
+        return;
+      }
+    }
+    if constexpr ((kIlv & 2) != 0) {  // up to 2 * kSlabCells cells: two whole-window stages of [cell][2 quads]
+      if (!G.empty && G.R * G.Cs2 <= 2 * kSlabCells) {
+        ilv_body<kStAux, kSlabCells, 2>(G, P, c, out, k, chunk, sbase, lane);
+        return;
+      }
+    }
+    if constexpr (kHybridHi > 0) {  // windows of many bands: the quad kernel's D = 2 / 1 stages instead
+      if (!G.empty && G.R * G.Cs2 > kHybridHi) {
+        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, false>(G, P, c, out, k, chunk, item, sbase,
+                                                                       t_start, lane, nullptr);
+        return;
+      }
     }
 #pragma unroll
     for (int i = 0; i < SR; ++i) {  // the band layout's 64-B cells
@@ -1222,7 +1337,7 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
 // the item list in chunk-pair-major order (quad kernel, kOrder 1: the two 16-channel chunks of
 // a 128-B line, adjacent, on one XCD).
 template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
-          int kRot = 1, int kHybrid = 0>
+          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -1243,7 +1358,7 @@ roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     ch0 = (int)(2u * p);
     k0 = (int64_t)r;
   }
-  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid>(lv, c, out, k0, ch0, w, sbase, t_start,
+  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(lv, c, out, k0, ch0, w, sbase, t_start,
                                                        threadIdx.x & (kWave - 1));
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }

@@ -13,7 +13,9 @@ export TMPDIR=/tmp
 run() { timeout -k 10 "$@"; }
 run 300 python bench.py --no-cpu-baseline > $OUT/bench_plain.json 2> $OUT/bench_plain.err || exit 1
 run 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/stats.log || exit 1
-python tools/step_breakdown.py $OUT/stats --warmup 3 --steps 10 > $OUT/step_breakdown.json || exit 1
+# the timed steps start after the warmup AND the graph-capture steps: the bench line says where
+W=$(python -c "import json; print(json.loads(open('$OUT/bench_under_rocprof.json').read().strip().splitlines()[-1])['roofline']['launches_before_timed_region'])")
+python tools/step_breakdown.py $OUT/stats --warmup $W --steps 10 > $OUT/step_breakdown.json || exit 1
 rm -f $OUT/stats/run_kernel_trace.csv
 for m in fwd train; do
   A="--steps 3 --warmup 2 --no-cpu-baseline --trace-steps 0 --mode $m"
