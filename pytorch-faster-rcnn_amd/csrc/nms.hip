@@ -577,6 +577,75 @@ __device__ __forceinline__ bool fz_wait_column(const uint32_t* col_flags, int p,
   return true;
 }
 
+// The RPN merge (m.L > 0, NmsMerge in seg_topk.h), after segment s's keep list: the scan
+// workgroups of image b meet on its arrival counter (seg_barrier: all S scan workgroups are
+// resident, see above), then each ranks ITS level's survivors among the image's (score
+// descending, level order on ties -- the rank a stable sort of the level concatenation gives
+// them): a binary search per other level over that level's kept scores, staged in the
+// (now free) scan LDS, 8192 floats: the host folds the merge in only when (L - 1) * P fits.
+// Without a cut (total <= max_num) the rank is the concatenation position.  The kept scores
+// came from the ring (the loaders stage block p's 64 scores beside its tiles) and were
+// handed over with sc1 stores before the arrival (hand-off table row 1).
+constexpr int kFzMergeFloats = (kFzRing * kFzSlotWords + kFzMaxBlocks) * 2;
+
+__device__ void fz_merge_tail(const NmsMerge& m, int s, float* ms, const int32_t* kcounts, const int32_t* keep,
+                              int64_t kstride, int32_t* status) {
+  __shared__ int cnt_s[FRH_MAX_LEVELS];
+  const int L = m.L, b = s / L, l = s - b * L, t = threadIdx.x, nt = blockDim.x;
+  if (!seg_barrier(m.img_bar + (int64_t)b * kBarWords, L, status, FRH_DEVERR_NMS_COLUMN)) return;
+  if (t < L) cnt_s[t] = min(max(xwg_load(kcounts + b * L + t), 0), m.P);
+  __syncthreads();
+  int total = 0, base = 0;
+  for (int q = 0; q < L; ++q) {
+    base += q < l ? cnt_s[q] : 0;
+    total += cnt_s[q];
+  }
+  const bool cut = m.max_num > 0 && total > m.max_num;
+  if (l == 0 && t == 0) m.out_counts[b] = cut ? m.max_num : total;
+  if (cut) {  // the other levels' kept scores, packed in level order
+    int o = 0;
+    for (int q = 0; q < L; ++q) {
+      if (q == l) continue;
+      const uint32_t* src = m.kscore + (int64_t)(b * L + q) * m.P;
+      for (int j = t; j < cnt_s[q]; j += nt) ms[o + j] = __uint_as_float(xwg_load(src + j));
+      o += cnt_s[q];
+    }
+    __syncthreads();
+  }
+  const int cnt = cnt_s[l];
+  float* ob = m.out_boxes + (int64_t)b * 4 * m.out_cap;
+  for (int j = t; j < cnt; j += nt) {
+    const int pos = min(max(xwg_load(keep + (int64_t)s * kstride + j), 0), m.P - 1);
+    const float sc = __uint_as_float(xwg_load(m.kscore + (int64_t)s * m.P + j));
+    const float4 bx = reinterpret_cast<const float4*>(m.sel_boxes)[(int64_t)s * m.P + pos];
+    int rank = base + j;
+    if (cut) {
+      rank = j;
+      int o = 0;
+      for (int q = 0; q < L; ++q) {
+        if (q == l) continue;
+        int lo = 0, hi = cnt_s[q];  // survivors of level q ordered before (sc, level l)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const float v = ms[o + mid];
+          if (q < l ? (v >= sc) : (v > sc))
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        rank += lo;
+        o += cnt_s[q];
+      }
+      if (rank >= m.max_num) continue;
+    }
+    ob[rank] = bx.x;
+    ob[m.out_cap + rank] = bx.y;
+    ob[2 * m.out_cap + rank] = bx.z;
+    ob[3 * m.out_cap + rank] = bx.w;
+    m.out_scores[(int64_t)b * m.out_cap + rank] = sc;
+  }
+}
+
 // kStamp (tools-only timing build): s_memrealtime per (segment, block) at stamps +
 // (s * nbw + b) * 8: [0] loader starts b (slot free), [1] column b seen complete, [2] b
 // published, [3] b resolved, [4] / [5] the fold's last batch waits for / got the kept sets;
@@ -588,11 +657,12 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
                                                                uint32_t* flags, int max_keep,
                                                                int32_t* __restrict__ keep, int64_t kstride,
                                                                int32_t* __restrict__ kcounts, int32_t* status,
-                                                               int64_t* stamps) {
+                                                               int64_t* stamps, NmsMerge mg) {
   // scan: ring [kFzRing][kFzSlotWords] then kept[kFzMaxBlocks]; mask: per wave 64 row boxes + areas
   __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kFzMaxBlocks];
   __shared__ int ready[kFzRing];
   __shared__ int s_resolved, s_stop;
+  __shared__ float ring_sc[kFzRing * kWave];  // merge: block p's 64 row scores beside its tiles
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int64_t tri = tri_tiles(nbw);
@@ -674,7 +744,12 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
         while (__popcll(kb) > room) kb &= ~(1ull << (63 - __clzll(kb)));  // drop lowest-score extras
         stop = nk + __popcll(kb) >= max_keep;
       }
-      if ((kb >> lane) & 1ull) K[nk + __popcll(kb & lanemask_lt())] = b * 64 + lane;
+      if ((kb >> lane) & 1ull) {
+        const int at = nk + __popcll(kb & lanemask_lt());
+        K[at] = b * 64 + lane;
+        if (mg.L > 0)
+          xwg_store(mg.kscore + (int64_t)s * mg.P + at, __float_as_uint(ring_sc[(b % kFzRing) * kWave + lane]));
+      }
       nk += __popcll(kb);
 #pragma unroll
       for (int i = kFzNear - 1; i > 0; --i) kbh[i] = kbh[i - 1];
@@ -689,7 +764,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       }
       if (stop) break;
     }
-    if (lane == 0) kcounts[s] = nk;
+    if (lane == 0) xwg_store(reinterpret_cast<uint32_t*>(kcounts) + s, (uint32_t)nk);
+    if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status);
     return;
   }
   const uint32_t* sflags = flags + (int64_t)s * tri;
@@ -698,6 +774,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
     while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
     if (s_stop < p) break;
     const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
+    // merge: the block's row scores (the previous launch's output), in flight over the wait
+    const float rsc = mg.L > 0 ? mg.sel_scores[(int64_t)s * mg.P + min(p * 64 + lane, n_max - 1)] : 0.0f;
     if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
     if (!fz_wait_column(sflags + c0, p, lane, status, &s_stop)) {
       // stop the workgroup: s_stop < 0 first, then wake the resolver on this block's flag (LDS is
@@ -744,9 +822,11 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int i = 0; i < kFzNear; ++i) slot[(1 + i) * kWave] = nr[i];
     slot[(1 + kFzNear) * kWave] = d;
+    ring_sc[(p % kFzRing) * kWave + lane] = rsc;
     if (lane == 0) lds_flag(&ready[p % kFzRing], p + 1);
     if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
+  if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status);
 }
 
 // The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
@@ -797,26 +877,36 @@ bool nms_fused_fits(int32_t S, int32_t n_max) {
          S <= resident_capacity(reinterpret_cast<const void*>(nms_fused_kernel<false>), kFzThreads) / 4;
 }
 
+bool nms_merge_fits(int32_t L, int32_t n_max) { return (int64_t)(L - 1) * n_max <= kFzMergeFloats; }
+
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+ one spare)
   return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
 }
 
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
-                         uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps = nullptr) {
+                         uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps = nullptr,
+                         const NmsMerge* merge = nullptr) {
   FRH_REQUIRE(nms_fused_fits(S, n_max), "one-launch NMS: %d segments of %d boxes out of range", S, n_max);
   FRH_REQUIRE(status, "null status word");
+  NmsMerge mg{};
+  if (merge) {
+    mg = *merge;
+    FRH_REQUIRE(mg.L >= 1 && mg.L <= FRH_MAX_LEVELS && S % mg.L == 0 && mg.P == n_max &&
+                    (int64_t)(mg.L - 1) * mg.P <= kFzMergeFloats && mg.kscore && mg.img_bar,
+                "one-launch NMS merge: bad arguments");
+  }
   const int nbw = (n_max + 63) / 64;
   const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves;
   FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many mask tiles");
   if (stamps)
     hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, stamps);
+                       status, stamps, mg);
   else
     hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, nullptr);
+                       status, nullptr, mg);
   return check_launch("nms_fused");
 }
 

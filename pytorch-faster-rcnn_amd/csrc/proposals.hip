@@ -20,11 +20,12 @@ int32_t launch_nms_sorted(int32_t S, const float* boxes, int64_t seg_stride, con
                           uint64_t* mask, const int64_t* seg_base, hipStream_t st, int64_t* stamps = nullptr);
 size_t nms_mask_bytes(int32_t S, int32_t n_max);
 bool nms_fused_fits(int32_t S, int32_t n_max);
+bool nms_merge_fits(int32_t L, int32_t n_max);
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                          uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st,
-                         int64_t* stamps = nullptr);
+                         int64_t* stamps = nullptr, const NmsMerge* merge = nullptr);
 
 constexpr int kPropThreads = 1024;
 constexpr int kMaxSort = 16384;
@@ -802,11 +803,11 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
                            float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
                            void* workspace, size_t ws_bytes, void* stream, bool select_launches,
-                           int64_t* select_stamps = nullptr, bool nms_launches = false);
+                           int64_t* select_stamps = nullptr, bool nms_launches = false, bool merge_launch = false);
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, stage, cnt, keep, kcnt, mask, keys, mem, zero, nflags, zero_bytes, total;
+  size_t boxes, scores, idx, stage, cnt, keep, kcnt, kscore, mask, keys, mem, zero, nflags, nbar, zero_bytes, total;
   int64_t nmax, kld;
 };
 
@@ -834,14 +835,16 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
   z.cnt = z.stage + al(S * kRpnSelFused * sizeof(float4));
   z.keep = z.cnt + al(S * sizeof(int32_t));
   z.kcnt = z.keep + al(S * P * sizeof(int32_t));
-  z.mask = z.kcnt + al(S * sizeof(int32_t));
+  z.kscore = z.kcnt + al(S * sizeof(int32_t));
+  z.mask = z.kscore + al(S * P * sizeof(float));
   z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
   z.mem = z.keys + al(S * (size_t)z.kld * sizeof(uint32_t));
   z.zero = z.mem + al(S * (size_t)z.kld * sizeof(uint64_t));
-  // zeroed by one memset per call: the selection's histograms / state / barriers, then the
-  // one-launch NMS's tile flags
+  // zeroed by one memset per call: the selection's histograms / state / barriers, the
+  // one-launch NMS's tile flags, then its merge's per-image arrival counters
   z.nflags = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
-  z.zero_bytes = z.nflags - z.zero + nms_fused_flag_bytes((int32_t)S, P);
+  z.nbar = z.nflags + al(nms_fused_flag_bytes((int32_t)S, P));
+  z.zero_bytes = z.nbar - z.zero + (size_t)B * kBarWords * sizeof(int32_t);
   z.total = z.zero + al(z.zero_bytes);
   return z;
 }
@@ -925,7 +928,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
                                 int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes, void* stream,
-                                bool select_launches, int64_t* select_stamps, bool nms_launches) {
+                                bool select_launches, int64_t* select_stamps, bool nms_launches, bool merge_launch) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
@@ -1026,15 +1029,26 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   int32_t* keep = reinterpret_cast<int32_t*>(ws + z.keep);
   int32_t* kcnt = reinterpret_cast<int32_t*>(ws + z.kcnt);
   uint64_t* nmask = reinterpret_cast<uint64_t*>(ws + z.mask);
-  if (!nms_launches && nms_fused_fits(S, z.P))
+  const int64_t out_cap = max_num > 0 ? max_num : post * num_levels;
+  const bool nms_fused = !nms_launches && nms_fused_fits(S, z.P);
+  if (nms_fused && !merge_launch && nms_merge_fits(num_levels, z.P)) {
+    // 3. NMS + the cross-level merge in one launch (nms.hip fz_merge_tail)
+    const NmsMerge mg{num_levels, z.P, max_num, out_cap, p.sel_boxes, p.sel_scores,
+                      reinterpret_cast<uint32_t*>(ws + z.kscore), reinterpret_cast<int32_t*>(ws + z.nbar),
+                      out_boxes, out_scores, out_counts};
+    return launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
+                            (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask,
+                            reinterpret_cast<uint32_t*>(ws + z.nflags), status, st, nullptr, &mg);
+  }
+  if (nms_fused)
     r = launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou, (post_nms > 0) ? post_nms : -1,
                          keep, z.P, kcnt, nmask, reinterpret_cast<uint32_t*>(ws + z.nflags), status, st);
   else
     r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
                           (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask, nullptr, st);
   if (r) return r;
-  MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num,
-               (int64_t)(max_num > 0 ? max_num : post * num_levels), out_boxes, out_scores, out_counts};
+  MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num, out_cap, out_boxes, out_scores,
+               out_counts};
   const size_t merge_lds = (size_t)num_levels * z.P * sizeof(float);
   if (merge_lds <= 65536 - 256 && z.P <= kMergeThreads * kMergeOwn) {  // + the kernel's static counts
     hipLaunchKernelGGL(rpn_merge_lds_kernel, dim3((unsigned)num_levels, (unsigned)num_imgs), dim3(kMergeThreads),

@@ -17,6 +17,12 @@
   columns poll their flags in two loads), a post_nms cut that stops the scan early,
   tie-heavy and sparse score sets, 1, 2 and 4 images, three calls in a row (the flags are
   zeroed per call).  The two-launch NMS is pinned by test_gpu_parity.py's oracle cases.
+  Where (levels - 1) x P fits the scan's LDS (P <= 2048 at 5 levels) the one-launch NMS also
+  runs the cross-level merge (fz_merge_tail: the per-image arrival barrier, then each level's
+  ranks): the same comparison covers it -- the reference side runs rpn_merge_lds_kernel --
+  with a cut (the bench's call), without one (total <= max_num) and with post_nms stopping the
+  scans; P = 4000 / 8000 take the separate merge launch.  frh_rpn_proposals_merge_launch
+  (the one-launch NMS, then the merge launch) is compared too.
 * Device sampler: frh_sample_random's one-launch sampler (sampler_fused_kernel) against the
   tools library's keys + collect launches (frh_sample_random_launches): labels, selection
   sets and counts equal; the workspace's zero region is zero after every call.  The sampler's
@@ -122,9 +128,11 @@ def test_rpn_one_launch_selection_pre_nms_sizes(dev, pre, post, mx):
     ('near_half', 4, 2000, 2000, 4000),
     ('random_init', 1, 4000, 3000, 4000),   # 63 blocks (four-launch selection)
     ('random_init', 1, 8000, 2000, 2000),   # 125 blocks: column flags polled in two loads
+    ('sparse_high', 2, 300, 300, 4000),     # no cut: the merge keeps the level concatenation
 ])
-def test_rpn_one_launch_nms_equals_two_launches(dev, case, batch, pre, post, mx):
-    fused, ref = _run(dev, case, 1, True, batch, 0.0, pre, post, mx, 90 + batch, other='frh_rpn_proposals_nms2')
+@pytest.mark.parametrize('other', ['frh_rpn_proposals_nms2', 'frh_rpn_proposals_merge_launch'])
+def test_rpn_one_launch_nms_equals_two_launches(dev, case, batch, pre, post, mx, other):
+    fused, ref = _run(dev, case, 1, True, batch, 0.0, pre, post, mx, 90 + batch, other=other)
     rb, rs, rc = ref
     assert int(rc.min()) > 0
     for fb, fs, fc in fused:
