@@ -582,67 +582,156 @@ __device__ __forceinline__ bool fz_wait_column(const uint32_t* col_flags, int p,
 // resident, see above), then each ranks ITS level's survivors among the image's (score
 // descending, level order on ties -- the rank a stable sort of the level concatenation gives
 // them): a binary search per other level over that level's kept scores, staged in the
-// (now free) scan LDS, 8192 floats: the host folds the merge in only when (L - 1) * P fits.
+// (now free) scan LDS, 8192 floats: the host folds the merge in only when (L - 1) * P fits
+// and P <= kFzOwn * kFzThreads (own survivors held in registers).
 // Without a cut (total <= max_num) the rank is the concatenation position.  The kept scores
 // came from the ring (the loaders stage block p's 64 scores beside its tiles) and were
 // handed over with sc1 stores before the arrival (hand-off table row 1).
 constexpr int kFzMergeFloats = (kFzRing * kFzSlotWords + kFzMaxBlocks) * 2;
+constexpr int kFzOwn = 4;         // own survivors per thread: P <= kFzOwn * kFzThreads
+constexpr int kFzGatherPer = 16;  // other levels' scores per thread and batch (loads in flight together)
+constexpr int kFzSearch = 4;      // other levels searched together (16 chains per thread with kFzOwn = 4)
 
-__device__ void fz_merge_tail(const NmsMerge& m, int s, float* ms, const int32_t* kcounts, const int32_t* keep,
-                              int64_t kstride, int32_t* status) {
-  __shared__ int cnt_s[FRH_MAX_LEVELS];
-  const int L = m.L, b = s / L, l = s - b * L, t = threadIdx.x, nt = blockDim.x;
+// tst (timing build, else null): [0] barrier passed, [1] scores gathered, [2] ranks found, [3] done.
+// Latency shape: one round trip for the counts (one lane per level) with the own survivors'
+// keep indices and scores in flight beside it, one for the other levels' scores (16 loads per
+// thread in flight), then the searches in lock step (each step one LDS read per own survivor,
+// the kFzOwn chains overlapped), the boxes, the stores.  The code is kept compact (level loops
+// not unrolled): the tail runs once per launch, straight from a cold instruction cache, and an
+// unrolled form (8 levels x 16 gathers, twice inlined) measured 20 us for its searches alone.
+__device__ __forceinline__ void fz_merge_tail(NmsMerge m, int s, float* ms, const int32_t* kcounts,
+                                              const int32_t* keep, int64_t kstride, int32_t* status, int64_t* tst) {
+  __shared__ int cnt_s[FRH_MAX_LEVELS], beg_s[FRH_MAX_LEVELS];
+  const int L = m.L, b = s / L, l = s - b * L, t = threadIdx.x;
   if (!seg_barrier(m.img_bar + (int64_t)b * kBarWords, L, status, FRH_DEVERR_NMS_COLUMN)) return;
-  if (t < L) cnt_s[t] = min(max(xwg_load(kcounts + b * L + t), 0), m.P);
-  __syncthreads();
-  int total = 0, base = 0;
-  for (int q = 0; q < L; ++q) {
-    base += q < l ? cnt_s[q] : 0;
-    total += cnt_s[q];
+  if (tst && t == 0) tst[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  const int cv = t < L ? xwg_load(kcounts + b * L + t) : 0;
+  int own_pos[kFzOwn];
+  uint32_t own_sc[kFzOwn];
+#pragma unroll
+  for (int u = 0; u < kFzOwn; ++u) {  // the own count is not known yet: load up to P, mask later
+    const int j = min(t + u * kFzThreads, m.P - 1);
+    own_pos[u] = xwg_load(keep + (int64_t)s * kstride + j);
+    own_sc[u] = xwg_load(m.kscore + (int64_t)s * m.P + j);
   }
-  const bool cut = m.max_num > 0 && total > m.max_num;
-  if (l == 0 && t == 0) m.out_counts[b] = cut ? m.max_num : total;
-  if (cut) {  // the other levels' kept scores, packed in level order
+  if (t < L) cnt_s[t] = min(max(cv, 0), m.P);
+  __syncthreads();
+  if (t == 0) {
     int o = 0;
     for (int q = 0; q < L; ++q) {
-      if (q == l) continue;
-      const uint32_t* src = m.kscore + (int64_t)(b * L + q) * m.P;
-      for (int j = t; j < cnt_s[q]; j += nt) ms[o + j] = __uint_as_float(xwg_load(src + j));
-      o += cnt_s[q];
+      beg_s[q] = o;  // packed offset among the other levels
+      o += q == l ? 0 : cnt_s[q];
+    }
+  }
+  int total = 0, base = 0;
+#pragma unroll 1
+  for (int q = 0; q < L; ++q) {
+    const int c = cnt_s[q];
+    base += q < l ? c : 0;
+    total += c;
+  }
+  const int own_n = cnt_s[l];
+#pragma unroll
+  for (int u = 0; u < kFzOwn; ++u)
+    own_pos[u] = t + u * kFzThreads < own_n ? min(max(own_pos[u], 0), m.P - 1) : -1;
+  const bool cut = m.max_num > 0 && total > m.max_num;
+  if (l == 0 && t == 0) m.out_counts[b] = cut ? m.max_num : total;
+  __syncthreads();  // beg_s
+  if (cut) {  // the other levels' kept scores, packed in level order
+    const int n_other = total - own_n;
+    for (int e0 = 0; e0 < n_other; e0 += kFzThreads * kFzGatherPer) {
+      uint32_t v[kFzGatherPer];
+#pragma unroll
+      for (int u = 0; u < kFzGatherPer; ++u) {
+        const int e = e0 + u * kFzThreads + t;
+        int q = l == 0 ? 1 : 0;  // the level holding packed entry e
+#pragma unroll 1
+        for (int r = q + 1; r < L; ++r)
+          if (r != l && beg_s[r] <= e) q = r;
+        v[u] = e < n_other ? xwg_load(m.kscore + (uint32_t)((b * L + q) * m.P + (e - beg_s[q]))) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kFzGatherPer; ++u) {
+        const int e = e0 + u * kFzThreads + t;
+        if (e < n_other) ms[e] = __uint_as_float(v[u]);
+      }
     }
     __syncthreads();
   }
-  const int cnt = cnt_s[l];
-  float* ob = m.out_boxes + (int64_t)b * 4 * m.out_cap;
-  for (int j = t; j < cnt; j += nt) {
-    const int pos = min(max(xwg_load(keep + (int64_t)s * kstride + j), 0), m.P - 1);
-    const float sc = __uint_as_float(xwg_load(m.kscore + (int64_t)s * m.P + j));
-    const float4 bx = reinterpret_cast<const float4*>(m.sel_boxes)[(int64_t)s * m.P + pos];
-    int rank = base + j;
-    if (cut) {
-      rank = j;
-      int o = 0;
-      for (int q = 0; q < L; ++q) {
-        if (q == l) continue;
-        int lo = 0, hi = cnt_s[q];  // survivors of level q ordered before (sc, level l)
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          const float v = ms[o + mid];
-          if (q < l ? (v >= sc) : (v > sc))
-            lo = mid + 1;
-          else
-            hi = mid;
-        }
-        rank += lo;
-        o += cnt_s[q];
+  if (tst && t == 0) tst[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  int rank[kFzOwn];
+#pragma unroll
+  for (int u = 0; u < kFzOwn; ++u) rank[u] = (cut ? 0 : base) + t + u * kFzThreads;
+  if (cut) {
+    // up to kFzSearch other levels at once, every (own survivor, level) chain in lock step:
+    // kFzOwn * kFzSearch LDS reads in flight per step, [lo | hi << 16] packed (counts <= 2048)
+    for (int k0 = 0; k0 < L - 1; k0 += kFzSearch) {
+      int qv[kFzSearch], qb[kFzSearch], qc[kFzSearch];  // wave-uniform: scalar registers
+      int steps = 0;
+#pragma unroll
+      for (int i = 0; i < kFzSearch; ++i) {  // other level k = k0 + i is level k + (k >= l)
+        const int q = k0 + i + (k0 + i >= l ? 1 : 0);
+        qv[i] = q;
+        qc[i] = q < L ? __builtin_amdgcn_readfirstlane(cnt_s[q]) : 0;
+        qb[i] = q < L ? __builtin_amdgcn_readfirstlane(beg_s[q]) : 0;
+        steps = max(steps, 32 - __builtin_clz((uint32_t)qc[i] | 1u));
       }
-      if (rank >= m.max_num) continue;
+      uint32_t lh[kFzOwn][kFzSearch];
+#pragma unroll
+      for (int u = 0; u < kFzOwn; ++u)
+#pragma unroll
+        for (int i = 0; i < kFzSearch; ++i) lh[u][i] = (uint32_t)qc[i] << 16;
+#pragma unroll 1
+      for (int n = 0; n < steps; ++n) {
+        float v[kFzOwn][kFzSearch];
+#pragma unroll
+        for (int u = 0; u < kFzOwn; ++u)
+#pragma unroll
+          for (int i = 0; i < kFzSearch; ++i) {
+            const int mid = (int)(((lh[u][i] & 0xffffu) + (lh[u][i] >> 16)) >> 1);
+            v[u][i] = ms[qb[i] + min(mid, max(qc[i] - 1, 0))];
+          }
+#pragma unroll
+        for (int u = 0; u < kFzOwn; ++u) {
+          const float sc = __uint_as_float(own_sc[u]);
+#pragma unroll
+          for (int i = 0; i < kFzSearch; ++i) {
+            const uint32_t lo = lh[u][i] & 0xffffu, hi = lh[u][i] >> 16, mid = (lo + hi) >> 1;
+            const bool before = qv[i] < l ? (v[u][i] >= sc) : (v[u][i] > sc);
+            lh[u][i] = lo < hi ? (before ? (lh[u][i] & 0xffff0000u) | (mid + 1) : (mid << 16) | lo) : lh[u][i];
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kFzOwn; ++u)
+#pragma unroll
+        for (int i = 0; i < kFzSearch; ++i) rank[u] += qc[i] > 0 ? (int)(lh[u][i] & 0xffffu) : 0;
     }
-    ob[rank] = bx.x;
-    ob[m.out_cap + rank] = bx.y;
-    ob[2 * m.out_cap + rank] = bx.z;
-    ob[3 * m.out_cap + rank] = bx.w;
-    m.out_scores[(int64_t)b * m.out_cap + rank] = sc;
+  }
+  if (tst) {
+    __syncthreads();
+    if (t == 0) tst[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+  // the boxes after the searches (one more round trip, but no spills: 64 VGPRs at 8 waves / SIMD)
+  float4 own_bx[kFzOwn];
+#pragma unroll
+  for (int u = 0; u < kFzOwn; ++u)
+    if (own_pos[u] >= 0) own_bx[u] = reinterpret_cast<const float4*>(m.sel_boxes)[(int64_t)s * m.P + own_pos[u]];
+  float* ob = m.out_boxes + (int64_t)b * 4 * m.out_cap;
+#pragma unroll
+  for (int u = 0; u < kFzOwn; ++u) {
+    if (own_pos[u] < 0 || (cut && rank[u] >= m.max_num)) continue;
+    const int r = rank[u];
+    ob[r] = own_bx[u].x;
+    ob[m.out_cap + r] = own_bx[u].y;
+    ob[2 * m.out_cap + r] = own_bx[u].z;
+    ob[3 * m.out_cap + r] = own_bx[u].w;
+    m.out_scores[(int64_t)b * m.out_cap + r] = __uint_as_float(own_sc[u]);
+  }
+  if (tst) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) tst[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -765,68 +854,69 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       if (stop) break;
     }
     if (lane == 0) xwg_store(reinterpret_cast<uint32_t*>(kcounts) + s, (uint32_t)nk);
-    if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status);
-    return;
-  }
-  const uint32_t* sflags = flags + (int64_t)s * tri;
-  const uint64_t* smask = mask + (int64_t)s * tri * 64;
-  for (int p = wave - 1; p < nb; p += kFzLoaders) {
-    while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
-    if (s_stop < p) break;
-    const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
-    // merge: the block's row scores (the previous launch's output), in flight over the wait
-    const float rsc = mg.L > 0 ? mg.sel_scores[(int64_t)s * mg.P + min(p * 64 + lane, n_max - 1)] : 0.0f;
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    if (!fz_wait_column(sflags + c0, p, lane, status, &s_stop)) {
-      // stop the workgroup: s_stop < 0 first, then wake the resolver on this block's flag (LDS is
-      // served in order: the resolver sees s_stop once it sees the flag)
-      if (lane == 0) {
-        __hip_atomic_store(&s_stop, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");
-        lds_flag(&ready[p % kFzRing], p + 1);
+  } else {  // loaders
+    const uint32_t* sflags = flags + (int64_t)s * tri;
+    const uint64_t* smask = mask + (int64_t)s * tri * 64;
+    for (int p = wave - 1; p < nb; p += kFzLoaders) {
+      while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
+      if (s_stop < p) break;
+      const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
+      // merge: the block's row scores (the previous launch's output), in flight over the wait
+      const float rsc = mg.L > 0 ? mg.sel_scores[(int64_t)s * mg.P + min(p * 64 + lane, n_max - 1)] : 0.0f;
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      if (!fz_wait_column(sflags + c0, p, lane, status, &s_stop)) {
+        // stop the workgroup: s_stop < 0 first, then wake the resolver on this block's flag (LDS is
+        // served in order: the resolver sees s_stop once it sees the flag)
+        if (lane == 0) {
+          __hip_atomic_store(&s_stop, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          asm volatile("" ::: "memory");
+          lds_flag(&ready[p % kFzRing], p + 1);
+        }
+        break;
       }
-      break;
-    }
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    const uint64_t* col = smask + c0 * 64 + lane;
-    const uint64_t d = fz_tile(col + (int64_t)p * 64);
-    uint64_t nr[kFzNear];
-#pragma unroll
-    for (int i = 0; i < kFzNear; ++i) nr[i] = p > i ? fz_tile(col + (int64_t)(p - 1 - i) * 64) : 0ull;
-    // fold blocks j < jf = p - kFzNear (their kept sets appear as the resolver passes them)
-    // Batches of 16 tile words, branch-free (indices clamped to the last fold tile, extra
-    // words masked out): one memory round trip per 16 tiles.  (Eight per batch with the next
-    // batch prefetched needs 16 more VGPRs than the 64 that 8 waves per SIMD allow, so the
-    // compiler reused the registers and waited for each batch before issuing the next.)
-    const int jf = p - kFzNear;
-    uint64_t acc = 0;
-    if (jf > 0) {
-      const int jl = jf - 1;
-      for (int j0 = 0; j0 < jf; j0 += 16) {
-        uint64_t t[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) t[u] = fz_tile(col + (int64_t)min(j0 + u, jl) * 64);
-        const int need = min(j0 + 16, jf);
-        if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
-        if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const uint64_t k = kept[min(j0 + u, jl)];
-          acc |= (j0 + u < jf) ? (t[u] & k) : 0ull;
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      const uint64_t* col = smask + c0 * 64 + lane;
+      const uint64_t d = fz_tile(col + (int64_t)p * 64);
+      uint64_t nr[kFzNear];
+  #pragma unroll
+      for (int i = 0; i < kFzNear; ++i) nr[i] = p > i ? fz_tile(col + (int64_t)(p - 1 - i) * 64) : 0ull;
+      // fold blocks j < jf = p - kFzNear (their kept sets appear as the resolver passes them)
+      // Batches of 16 tile words, branch-free (indices clamped to the last fold tile, extra
+      // words masked out): one memory round trip per 16 tiles.  (Eight per batch with the next
+      // batch prefetched needs 16 more VGPRs than the 64 that 8 waves per SIMD allow, so the
+      // compiler reused the registers and waited for each batch before issuing the next.)
+      const int jf = p - kFzNear;
+      uint64_t acc = 0;
+      if (jf > 0) {
+        const int jl = jf - 1;
+        for (int j0 = 0; j0 < jf; j0 += 16) {
+          uint64_t t[16];
+  #pragma unroll
+          for (int u = 0; u < 16; ++u) t[u] = fz_tile(col + (int64_t)min(j0 + u, jl) * 64);
+          const int need = min(j0 + 16, jf);
+          if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          while (lds_poll(&s_resolved) < need) __builtin_amdgcn_s_sleep(1);
+          if (kStamp && lane == 0 && j0 + 16 >= jf) stamps[((int64_t)s * nbw + p) * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  #pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const uint64_t k = kept[min(j0 + u, jl)];
+            acc |= (j0 + u < jf) ? (t[u] & k) : 0ull;
+          }
         }
       }
+      uint64_t* slot = ring + (p % kFzRing) * kFzSlotWords + lane;
+      slot[0] = acc;
+  #pragma unroll
+      for (int i = 0; i < kFzNear; ++i) slot[(1 + i) * kWave] = nr[i];
+      slot[(1 + kFzNear) * kWave] = d;
+      ring_sc[(p % kFzRing) * kWave + lane] = rsc;
+      if (lane == 0) lds_flag(&ready[p % kFzRing], p + 1);
+      if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
     }
-    uint64_t* slot = ring + (p % kFzRing) * kFzSlotWords + lane;
-    slot[0] = acc;
-#pragma unroll
-    for (int i = 0; i < kFzNear; ++i) slot[(1 + i) * kWave] = nr[i];
-    slot[(1 + kFzNear) * kWave] = d;
-    ring_sc[(p % kFzRing) * kWave + lane] = rsc;
-    if (lane == 0) lds_flag(&ready[p % kFzRing], p + 1);
-    if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
-  if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status);
+  // the merge (RPN proposals): one call site, so the tail's code is in the kernel once
+  if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status,
+                                  kStamp ? stamps + (int64_t)S * nbw * 8 + (int64_t)S * tri + (int64_t)s * 4 : nullptr);
 }
 
 // The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
@@ -877,7 +967,9 @@ bool nms_fused_fits(int32_t S, int32_t n_max) {
          S <= resident_capacity(reinterpret_cast<const void*>(nms_fused_kernel<false>), kFzThreads) / 4;
 }
 
-bool nms_merge_fits(int32_t L, int32_t n_max) { return (int64_t)(L - 1) * n_max <= kFzMergeFloats; }
+bool nms_merge_fits(int32_t L, int32_t n_max) {
+  return n_max <= kFzOwn * kFzThreads && (int64_t)(L - 1) * n_max <= kFzMergeFloats;
+}
 
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+ one spare)
   return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
@@ -893,7 +985,7 @@ int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, cons
   if (merge) {
     mg = *merge;
     FRH_REQUIRE(mg.L >= 1 && mg.L <= FRH_MAX_LEVELS && S % mg.L == 0 && mg.P == n_max &&
-                    (int64_t)(mg.L - 1) * mg.P <= kFzMergeFloats && mg.kscore && mg.img_bar,
+                    nms_merge_fits(mg.L, mg.P) && mg.kscore && mg.img_bar,
                 "one-launch NMS merge: bad arguments");
   }
   const int nbw = (n_max + 63) / 64;

@@ -803,7 +803,8 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
                            float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
                            void* workspace, size_t ws_bytes, void* stream, bool select_launches,
-                           int64_t* select_stamps = nullptr, bool nms_launches = false, bool merge_launch = false);
+                           int64_t* select_stamps = nullptr, bool nms_launches = false, bool merge_launch = false,
+                           int64_t* nms_stamps = nullptr);
 
 struct PropLayout {
   int P;
@@ -928,7 +929,8 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
                                 int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes, void* stream,
-                                bool select_launches, int64_t* select_stamps, bool nms_launches, bool merge_launch) {
+                                bool select_launches, int64_t* select_stamps, bool nms_launches, bool merge_launch,
+                                int64_t* nms_stamps) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
   FRH_REQUIRE(num_levels >= 1 && num_levels <= FRH_MAX_LEVELS, "bad level count %d", num_levels);
@@ -1038,7 +1040,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                       out_boxes, out_scores, out_counts};
     return launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
                             (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask,
-                            reinterpret_cast<uint32_t*>(ws + z.nflags), status, st, nullptr, &mg);
+                            reinterpret_cast<uint32_t*>(ws + z.nflags), status, st, nms_stamps, &mg);
   }
   if (nms_fused)
     r = launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou, (post_nms > 0) ? post_nms : -1,

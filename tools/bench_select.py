@@ -102,6 +102,30 @@ def main():
     sa = stm.cpu().numpy()
     L = len(grids)
     nch0 = (3 * grids[0][0] * grids[0][1] + 4095) // 4096
+    # the one-launch NMS + folded merge: per segment, its scan's last resolved block and the
+    # merge tail's phases (barrier passed, scores gathered, ranks found, done), µs from the first stamp
+    S, P = 2 * len(grids), 2000
+    nbw = (P + 63) // 64
+    tri = nbw * (nbw + 1) // 2
+    nst = torch.zeros(S * nbw * 8 + S * tri + S * 4, dtype=torch.int64, device=dev)
+
+    def nstamped(*a):
+        a = list(a)
+        stream = a.pop()
+        return lib.frh_rpn_proposals_nms_stamped(*a, _lib.ptr(nst), stream)
+    ops.rpn_proposals(*argv, _entry=(nstamped, 'nms_stamped'))
+    torch.cuda.synchronize()
+    na = nst.cpu().numpy()
+    blk = na[:S * nbw * 8].reshape(S, nbw, 8)
+    tail = na[S * nbw * 8 + S * tri:].reshape(S, 4)
+    t0 = na[na > 0].min()
+    nms_tl = []
+    for sg in range(S):
+        r = blk[sg, :, 3]
+        nms_tl.append({'segment': sg, 'resolved_last_us': round(float((r[r > 0].max() - t0) / 100.0), 2)
+                       if (r > 0).any() else None,
+                       'tail_us': [round(float((v - t0) / 100.0), 2) if v > 0 else None for v in tail[sg]]})
+    res['nms_merge_timeline'] = nms_tl
     res['rpn_proposals'] = {'us_per_call_one_launch_select': round(one, 2),
                             'us_per_call_four_launch_select': round(four, 2),
                             'us_per_call_two_launch_nms': round(nms2, 2),

@@ -88,6 +88,17 @@ int32_t frh_rpn_proposals_stamped(int32_t num_imgs, int32_t num_levels, const fl
                                   int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
                                   float* out_scores, int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes,
                                   int64_t* stamps, void* stream);
+
+/* the one-launch NMS (+ folded merge) timing build: stamps = S*nbw*8 per-block + S*tri per-tile
+ * + S*4 merge-tail int64 (nms_fused_kernel<true>), zeroed by the caller. */
+int32_t frh_rpn_proposals_nms_stamped(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
+                                  const float* const* reg_ptrs, const int64_t* cls_strides,
+                                  const int64_t* reg_strides, const int32_t* grid_hw, int32_t num_anchors,
+                                  int32_t cls_channels, const float* anchors, int64_t anchor_ld, const float* means,
+                                  const float* stds, const float* img_hw, const float* min_size, int32_t pre_nms,
+                                  int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
+                                  float* out_scores, int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes,
+                                  int64_t* stamps, void* stream);
 int32_t frh_sample_random_stamped(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                   const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                                   uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts,

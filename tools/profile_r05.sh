@@ -22,8 +22,8 @@ for m in fwd train; do
   run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch_$m -o run --output-format csv -- python bench.py $A > $OUT/pmc_fetch_$m.log 2>&1 || exit 1
   run 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write_$m -o run --output-format csv -- python bench.py $A > $OUT/pmc_write_$m.log 2>&1 || exit 1
 done
-run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 41 > $OUT/pmc_calib_small.log 2>&1 || exit 1
-run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_band -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 41 > $OUT/pmc_calib_band.log 2>&1 || exit 1
+run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 50 > $OUT/pmc_calib_small.log 2>&1 || exit 1
+run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_band -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 50 > $OUT/pmc_calib_band.log 2>&1 || exit 1
 python tools/pmc_summary.py --fetch $OUT/pmc_fetch_fwd --write $OUT/pmc_write_fwd --kernel $K --calib-kernel roi_align_fwd_band_kernel \
   --calib-fetch $OUT/pmc_calib_small --calib-bytes 150994944 --out $OUT/roi_align_pmc.json || exit 1
 python tools/pmc_summary.py --fetch $OUT/pmc_fetch_train --write $OUT/pmc_write_train --kernel $K --calib-kernel roi_align_fwd_band_kernel \
