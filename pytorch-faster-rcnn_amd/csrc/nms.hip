@@ -577,164 +577,12 @@ __device__ __forceinline__ bool fz_wait_column(const uint32_t* col_flags, int p,
   return true;
 }
 
-// The RPN merge (m.L > 0, NmsMerge in seg_topk.h), after segment s's keep list: the scan
-// workgroups of image b meet on its arrival counter (seg_barrier: all S scan workgroups are
-// resident, see above), then each ranks ITS level's survivors among the image's (score
-// descending, level order on ties -- the rank a stable sort of the level concatenation gives
-// them): a binary search per other level over that level's kept scores, staged in the
-// (now free) scan LDS, 8192 floats: the host folds the merge in only when (L - 1) * P fits
-// and P <= kFzOwn * kFzThreads (own survivors held in registers).
-// Without a cut (total <= max_num) the rank is the concatenation position.  The kept scores
-// came from the ring (the loaders stage block p's 64 scores beside its tiles) and were
-// handed over with sc1 stores before the arrival (hand-off table row 1).
-constexpr int kFzMergeFloats = (kFzRing * kFzSlotWords + kFzMaxBlocks) * 2;
-constexpr int kFzOwn = 4;         // own survivors per thread: P <= kFzOwn * kFzThreads
-constexpr int kFzGatherPer = 16;  // other levels' scores per thread and batch (loads in flight together)
-constexpr int kFzSearch = 4;      // other levels searched together (16 chains per thread with kFzOwn = 4)
-
-// tst (timing build, else null): [0] barrier passed, [1] scores gathered, [2] ranks found, [3] done.
-// Latency shape: one round trip for the counts (one lane per level) with the own survivors'
-// keep indices and scores in flight beside it, one for the other levels' scores (16 loads per
-// thread in flight), then the searches in lock step (each step one LDS read per own survivor,
-// the kFzOwn chains overlapped), the boxes, the stores.  The code is kept compact (level loops
-// not unrolled): the tail runs once per launch, straight from a cold instruction cache, and an
-// unrolled form (8 levels x 16 gathers, twice inlined) measured 20 us for its searches alone.
-__device__ __forceinline__ void fz_merge_tail(NmsMerge m, int s, float* ms, const int32_t* kcounts,
-                                              const int32_t* keep, int64_t kstride, int32_t* status, int64_t* tst) {
-  __shared__ int cnt_s[FRH_MAX_LEVELS], beg_s[FRH_MAX_LEVELS];
-  const int L = m.L, b = s / L, l = s - b * L, t = threadIdx.x;
-  if (!seg_barrier(m.img_bar + (int64_t)b * kBarWords, L, status, FRH_DEVERR_NMS_COLUMN)) return;
-  if (tst && t == 0) tst[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  const int cv = t < L ? xwg_load(kcounts + b * L + t) : 0;
-  int own_pos[kFzOwn];
-  uint32_t own_sc[kFzOwn];
-#pragma unroll
-  for (int u = 0; u < kFzOwn; ++u) {  // the own count is not known yet: load up to P, mask later
-    const int j = min(t + u * kFzThreads, m.P - 1);
-    own_pos[u] = xwg_load(keep + (int64_t)s * kstride + j);
-    own_sc[u] = xwg_load(m.kscore + (int64_t)s * m.P + j);
-  }
-  if (t < L) cnt_s[t] = min(max(cv, 0), m.P);
-  __syncthreads();
-  if (t == 0) {
-    int o = 0;
-    for (int q = 0; q < L; ++q) {
-      beg_s[q] = o;  // packed offset among the other levels
-      o += q == l ? 0 : cnt_s[q];
-    }
-  }
-  int total = 0, base = 0;
-#pragma unroll 1
-  for (int q = 0; q < L; ++q) {
-    const int c = cnt_s[q];
-    base += q < l ? c : 0;
-    total += c;
-  }
-  const int own_n = cnt_s[l];
-#pragma unroll
-  for (int u = 0; u < kFzOwn; ++u)
-    own_pos[u] = t + u * kFzThreads < own_n ? min(max(own_pos[u], 0), m.P - 1) : -1;
-  const bool cut = m.max_num > 0 && total > m.max_num;
-  if (l == 0 && t == 0) m.out_counts[b] = cut ? m.max_num : total;
-  __syncthreads();  // beg_s
-  if (cut) {  // the other levels' kept scores, packed in level order
-    const int n_other = total - own_n;
-    for (int e0 = 0; e0 < n_other; e0 += kFzThreads * kFzGatherPer) {
-      uint32_t v[kFzGatherPer];
-#pragma unroll
-      for (int u = 0; u < kFzGatherPer; ++u) {
-        const int e = e0 + u * kFzThreads + t;
-        int q = l == 0 ? 1 : 0;  // the level holding packed entry e
-#pragma unroll 1
-        for (int r = q + 1; r < L; ++r)
-          if (r != l && beg_s[r] <= e) q = r;
-        v[u] = e < n_other ? xwg_load(m.kscore + (uint32_t)((b * L + q) * m.P + (e - beg_s[q]))) : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kFzGatherPer; ++u) {
-        const int e = e0 + u * kFzThreads + t;
-        if (e < n_other) ms[e] = __uint_as_float(v[u]);
-      }
-    }
-    __syncthreads();
-  }
-  if (tst && t == 0) tst[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  int rank[kFzOwn];
-#pragma unroll
-  for (int u = 0; u < kFzOwn; ++u) rank[u] = (cut ? 0 : base) + t + u * kFzThreads;
-  if (cut) {
-    // up to kFzSearch other levels at once, every (own survivor, level) chain in lock step:
-    // kFzOwn * kFzSearch LDS reads in flight per step, [lo | hi << 16] packed (counts <= 2048)
-    for (int k0 = 0; k0 < L - 1; k0 += kFzSearch) {
-      int qv[kFzSearch], qb[kFzSearch], qc[kFzSearch];  // wave-uniform: scalar registers
-      int steps = 0;
-#pragma unroll
-      for (int i = 0; i < kFzSearch; ++i) {  // other level k = k0 + i is level k + (k >= l)
-        const int q = k0 + i + (k0 + i >= l ? 1 : 0);
-        qv[i] = q;
-        qc[i] = q < L ? __builtin_amdgcn_readfirstlane(cnt_s[q]) : 0;
-        qb[i] = q < L ? __builtin_amdgcn_readfirstlane(beg_s[q]) : 0;
-        steps = max(steps, 32 - __builtin_clz((uint32_t)qc[i] | 1u));
-      }
-      uint32_t lh[kFzOwn][kFzSearch];
-#pragma unroll
-      for (int u = 0; u < kFzOwn; ++u)
-#pragma unroll
-        for (int i = 0; i < kFzSearch; ++i) lh[u][i] = (uint32_t)qc[i] << 16;
-#pragma unroll 1
-      for (int n = 0; n < steps; ++n) {
-        float v[kFzOwn][kFzSearch];
-#pragma unroll
-        for (int u = 0; u < kFzOwn; ++u)
-#pragma unroll
-          for (int i = 0; i < kFzSearch; ++i) {
-            const int mid = (int)(((lh[u][i] & 0xffffu) + (lh[u][i] >> 16)) >> 1);
-            v[u][i] = ms[qb[i] + min(mid, max(qc[i] - 1, 0))];
-          }
-#pragma unroll
-        for (int u = 0; u < kFzOwn; ++u) {
-          const float sc = __uint_as_float(own_sc[u]);
-#pragma unroll
-          for (int i = 0; i < kFzSearch; ++i) {
-            const uint32_t lo = lh[u][i] & 0xffffu, hi = lh[u][i] >> 16, mid = (lo + hi) >> 1;
-            const bool before = qv[i] < l ? (v[u][i] >= sc) : (v[u][i] > sc);
-            lh[u][i] = lo < hi ? (before ? (lh[u][i] & 0xffff0000u) | (mid + 1) : (mid << 16) | lo) : lh[u][i];
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kFzOwn; ++u)
-#pragma unroll
-        for (int i = 0; i < kFzSearch; ++i) rank[u] += qc[i] > 0 ? (int)(lh[u][i] & 0xffffu) : 0;
-    }
-  }
-  if (tst) {
-    __syncthreads();
-    if (t == 0) tst[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  }
-  // the boxes after the searches (one more round trip, but no spills: 64 VGPRs at 8 waves / SIMD)
-  float4 own_bx[kFzOwn];
-#pragma unroll
-  for (int u = 0; u < kFzOwn; ++u)
-    if (own_pos[u] >= 0) own_bx[u] = reinterpret_cast<const float4*>(m.sel_boxes)[(int64_t)s * m.P + own_pos[u]];
-  float* ob = m.out_boxes + (int64_t)b * 4 * m.out_cap;
-#pragma unroll
-  for (int u = 0; u < kFzOwn; ++u) {
-    if (own_pos[u] < 0 || (cut && rank[u] >= m.max_num)) continue;
-    const int r = rank[u];
-    ob[r] = own_bx[u].x;
-    ob[m.out_cap + r] = own_bx[u].y;
-    ob[2 * m.out_cap + r] = own_bx[u].z;
-    ob[3 * m.out_cap + r] = own_bx[u].w;
-    m.out_scores[(int64_t)b * m.out_cap + r] = __uint_as_float(own_sc[u]);
-  }
-  if (tst) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) tst[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  }
-}
-
+// kscore (RPN proposals, else null): the kept rows' scores, compact beside the keep list
+// ([s * n_max + j] = score of keep[j]), for the cross-level merge launch (proposals.hip
+// rpn_merge_wide_kernel: one round trip to gather them instead of keep index -> score).  The
+// loaders stage block p's 64 row scores in the LDS ring beside its tiles; the resolver stores
+// the kept ones.
+//
 // kStamp (tools-only timing build): s_memrealtime per (segment, block) at stamps +
 // (s * nbw + b) * 8: [0] loader starts b (slot free), [1] column b seen complete, [2] b
 // published, [3] b resolved, [4] / [5] the fold's last batch waits for / got the kept sets;
@@ -746,12 +594,13 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
                                                                uint32_t* flags, int max_keep,
                                                                int32_t* __restrict__ keep, int64_t kstride,
                                                                int32_t* __restrict__ kcounts, int32_t* status,
-                                                               int64_t* stamps, NmsMerge mg) {
+                                                               int64_t* stamps, const float* __restrict__ row_scores,
+                                                               uint32_t* __restrict__ kscore) {
   // scan: ring [kFzRing][kFzSlotWords] then kept[kFzMaxBlocks]; mask: per wave 64 row boxes + areas
   __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kFzMaxBlocks];
   __shared__ int ready[kFzRing];
   __shared__ int s_resolved, s_stop;
-  __shared__ float ring_sc[kFzRing * kWave];  // merge: block p's 64 row scores beside its tiles
+  __shared__ float ring_sc[kFzRing * kWave];  // kscore: block p's 64 row scores beside its tiles
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int64_t tri = tri_tiles(nbw);
@@ -836,8 +685,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       if ((kb >> lane) & 1ull) {
         const int at = nk + __popcll(kb & lanemask_lt());
         K[at] = b * 64 + lane;
-        if (mg.L > 0)
-          xwg_store(mg.kscore + (int64_t)s * mg.P + at, __float_as_uint(ring_sc[(b % kFzRing) * kWave + lane]));
+        if (kscore) kscore[(int64_t)s * n_max + at] = __float_as_uint(ring_sc[(b % kFzRing) * kWave + lane]);
       }
       nk += __popcll(kb);
 #pragma unroll
@@ -853,7 +701,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       }
       if (stop) break;
     }
-    if (lane == 0) xwg_store(reinterpret_cast<uint32_t*>(kcounts) + s, (uint32_t)nk);
+    if (lane == 0) kcounts[s] = nk;
   } else {  // loaders
     const uint32_t* sflags = flags + (int64_t)s * tri;
     const uint64_t* smask = mask + (int64_t)s * tri * 64;
@@ -861,8 +709,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       while (lds_poll(&s_resolved) < p - kFzRing + 1) __builtin_amdgcn_s_sleep(1);  // slot of p - kFzRing free
       if (s_stop < p) break;
       const int64_t c0 = (int64_t)p * (p + 1) / 2;  // tile (j, p) is tile c0 + j of the segment
-      // merge: the block's row scores (the previous launch's output), in flight over the wait
-      const float rsc = mg.L > 0 ? mg.sel_scores[(int64_t)s * mg.P + min(p * 64 + lane, n_max - 1)] : 0.0f;
+      // kscore: the block's row scores (the previous launch's output), in flight over the wait
+      const float rsc = kscore ? row_scores[(int64_t)s * n_max + min(p * 64 + lane, n_max - 1)] : 0.0f;
       if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (!fz_wait_column(sflags + c0, p, lane, status, &s_stop)) {
         // stop the workgroup: s_stop < 0 first, then wake the resolver on this block's flag (LDS is
@@ -914,9 +762,6 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       if (kStamp && lane == 0) stamps[((int64_t)s * nbw + p) * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
     }
   }
-  // the merge (RPN proposals): one call site, so the tail's code is in the kernel once
-  if (mg.L > 0) fz_merge_tail(mg, s, reinterpret_cast<float*>(fz_lds), kcounts, keep, kstride, status,
-                                  kStamp ? stamps + (int64_t)S * nbw * 8 + (int64_t)S * tri + (int64_t)s * 4 : nullptr);
 }
 
 // The scan's dynamic LDS (up to 128 KB) needs the per-device function attribute; it is
@@ -967,10 +812,6 @@ bool nms_fused_fits(int32_t S, int32_t n_max) {
          S <= resident_capacity(reinterpret_cast<const void*>(nms_fused_kernel<false>), kFzThreads) / 4;
 }
 
-bool nms_merge_fits(int32_t L, int32_t n_max) {
-  return n_max <= kFzOwn * kFzThreads && (int64_t)(L - 1) * n_max <= kFzMergeFloats;
-}
-
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+ one spare)
   return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
 }
@@ -978,27 +819,21 @@ size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                          uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps = nullptr,
-                         const NmsMerge* merge = nullptr) {
+                         const float* row_scores = nullptr, uint32_t* kscore = nullptr) {
   FRH_REQUIRE(nms_fused_fits(S, n_max), "one-launch NMS: %d segments of %d boxes out of range", S, n_max);
   FRH_REQUIRE(status, "null status word");
-  NmsMerge mg{};
-  if (merge) {
-    mg = *merge;
-    FRH_REQUIRE(mg.L >= 1 && mg.L <= FRH_MAX_LEVELS && S % mg.L == 0 && mg.P == n_max &&
-                    nms_merge_fits(mg.L, mg.P) && mg.kscore && mg.img_bar,
-                "one-launch NMS merge: bad arguments");
-  }
+  FRH_REQUIRE(!kscore || row_scores, "kept scores need the row scores");
   const int nbw = (n_max + 63) / 64;
   const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves;
   FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many mask tiles");
   if (stamps)
     hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, stamps, mg);
+                       status, stamps, row_scores, kscore);
   else
     hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, nullptr, mg);
+                       status, nullptr, row_scores, kscore);
   return check_launch("nms_fused");
 }
 

@@ -89,23 +89,6 @@ __device__ __forceinline__ int32_t xwg_load(const int32_t* p) {
   return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ------------------------------------------- RPN cross-level merge in the NMS launch
-// The RPN proposals' per-image merge of the per-level NMS survivors (reference
-// lib/heads/rpn_head.py get_bboxes_single: concatenate the levels, then the top max_num by
-// score), run by nms_fused_kernel's scan workgroups once their keep lists are done (nms.hip
-// fz_merge_tail).  L == 0: no merge.  Segment s = b * L + l (image b, level l).
-struct NmsMerge {
-  int L, P, max_num;
-  int64_t out_cap;
-  const float* sel_boxes;   // [S][P] float4, the NMS input rows
-  const float* sel_scores;  // [S][P] their scores
-  uint32_t* kscore;         // [S][P] the kept rows' scores, compact (written by the scan)
-  int32_t* img_bar;         // [B][kBarWords] per-image arrival counters, zero on entry
-  float* out_boxes;         // [B][4][out_cap]
-  float* out_scores;        // [B][out_cap]
-  int32_t* out_counts;      // [B]
-};
-
 // ------------------------------------------------------------ wave helpers
 // histogram add aggregated over the wave's most common bin (the first active
 // lane's): a concentrated key set costs one LDS atomic per wave, not 64

@@ -17,12 +17,12 @@
   columns poll their flags in two loads), a post_nms cut that stops the scan early,
   tie-heavy and sparse score sets, 1, 2 and 4 images, three calls in a row (the flags are
   zeroed per call).  The two-launch NMS is pinned by test_gpu_parity.py's oracle cases.
-  Where (levels - 1) x P fits the scan's LDS (P <= 2048 at 5 levels) the one-launch NMS also
-  runs the cross-level merge (fz_merge_tail: the per-image arrival barrier, then each level's
-  ranks): the same comparison covers it -- the reference side runs rpn_merge_lds_kernel --
-  with a cut (the bench's call), without one (total <= max_num) and with post_nms stopping the
-  scans; P = 4000 / 8000 take the separate merge launch.  frh_rpn_proposals_merge_launch
-  (the one-launch NMS, then the merge launch) is compared too.
+  After the one-launch NMS (which also writes the kept rows' scores compactly) the merge runs
+  as rpn_merge_wide_kernel (one survivor per thread, ~40 workgroups) where (levels - 1) x P
+  scores fit its LDS: the same comparison covers it -- the reference side runs the round-4
+  rpn_merge_lds_kernel -- with a cut (the bench's call), without one (total <= max_num) and
+  with post_nms stopping the scans; P = 8000 takes the old merge.  frh_rpn_proposals_merge_launch
+  (the one-launch NMS, then rpn_merge_lds_kernel) is compared too.
 * Device sampler: frh_sample_random's one-launch sampler (sampler_fused_kernel) against the
   tools library's keys + collect launches (frh_sample_random_launches): labels, selection
   sets and counts equal; the workspace's zero region is zero after every call.  The sampler's

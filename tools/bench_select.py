@@ -7,8 +7,8 @@ library stamps).
 RPN proposals: the bench's cfg2 RPN head outputs (random-init model, channels-last) through
 frh_rpn_proposals_strided (one-launch selection) and frh_rpn_proposals_launches (keys /
 refine / collect / rank) and through frh_rpn_proposals_nms2 (one-launch selection, two-launch
-NMS) and frh_rpn_proposals_merge_launch (the cross-level merge as its own launch, not folded
-into the one-launch NMS), back to back between one event pair, µs per call (everything included); then one stamped call: per workgroup, s_memrealtime at the kernel's
+NMS) and frh_rpn_proposals_merge_launch (the round-4 merge, rpn_merge_lds_kernel, after the
+one-launch NMS instead of rpn_merge_wide_kernel), back to back between one event pair, µs per call (everything included); then one stamped call: per workgroup, s_memrealtime at the kernel's
 phases, reported as medians relative to the workgroup's own start and to the launch's first
 start.  Device sampler: the cfg2 RPN call's shape (2 x 155 520 anchors, 256 / 128) on
 synthetic labels, the same three measurements.
@@ -102,12 +102,12 @@ def main():
     sa = stm.cpu().numpy()
     L = len(grids)
     nch0 = (3 * grids[0][0] * grids[0][1] + 4095) // 4096
-    # the one-launch NMS + folded merge: per segment, its scan's last resolved block and the
-    # merge tail's phases (barrier passed, scores gathered, ranks found, done), µs from the first stamp
+    # the one-launch NMS (timing build): per segment, when its scan resolved its last block,
+    # µs from the launch's first stamp
     S, P = 2 * len(grids), 2000
     nbw = (P + 63) // 64
     tri = nbw * (nbw + 1) // 2
-    nst = torch.zeros(S * nbw * 8 + S * tri + S * 4, dtype=torch.int64, device=dev)
+    nst = torch.zeros(S * nbw * 8 + S * tri, dtype=torch.int64, device=dev)
 
     def nstamped(*a):
         a = list(a)
@@ -117,19 +117,13 @@ def main():
     torch.cuda.synchronize()
     na = nst.cpu().numpy()
     blk = na[:S * nbw * 8].reshape(S, nbw, 8)
-    tail = na[S * nbw * 8 + S * tri:].reshape(S, 4)
     t0 = na[na > 0].min()
-    nms_tl = []
-    for sg in range(S):
-        r = blk[sg, :, 3]
-        nms_tl.append({'segment': sg, 'resolved_last_us': round(float((r[r > 0].max() - t0) / 100.0), 2)
-                       if (r > 0).any() else None,
-                       'tail_us': [round(float((v - t0) / 100.0), 2) if v > 0 else None for v in tail[sg]]})
-    res['nms_merge_timeline'] = nms_tl
+    res['nms_scan_resolved_last_us'] = [round(float((blk[sg, :, 3][blk[sg, :, 3] > 0].max() - t0) / 100.0), 2)
+                                        if (blk[sg, :, 3] > 0).any() else None for sg in range(S)]
     res['rpn_proposals'] = {'us_per_call_one_launch_select': round(one, 2),
                             'us_per_call_four_launch_select': round(four, 2),
                             'us_per_call_two_launch_nms': round(nms2, 2),
-                            'us_per_call_merge_own_launch': round(mlaunch, 2),
+                            'us_per_call_lds_merge': round(mlaunch, 2),
                             'timeline_one_launch_select': timeline(sa, RPN_PHASES),
                             'timeline_level0_key_workgroups': timeline(sa[0::L, :nch0], RPN_PHASES),
                             'timeline_level4': timeline(sa[L - 1::L], RPN_PHASES)}

@@ -60,8 +60,8 @@ int32_t frh_rpn_proposals_nms2(int32_t num_imgs, int32_t num_levels, const float
                                double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
                                int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
-/* frh_rpn_proposals_strided with the cross-level merge as its own launch (rpn_merge_lds_kernel)
- * after the one-launch NMS, instead of folded into it; same arguments and outputs. */
+/* frh_rpn_proposals_strided with the round-4 cross-level merge (rpn_merge_lds_kernel: one
+ * workgroup per level and image, keep-index indirection) instead of rpn_merge_wide_kernel. */
 int32_t frh_rpn_proposals_merge_launch(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                        const float* const* reg_ptrs, const int64_t* cls_strides,
                                        const int64_t* reg_strides, const int32_t* grid_hw, int32_t num_anchors,
@@ -89,8 +89,8 @@ int32_t frh_rpn_proposals_stamped(int32_t num_imgs, int32_t num_levels, const fl
                                   float* out_scores, int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes,
                                   int64_t* stamps, void* stream);
 
-/* the one-launch NMS (+ folded merge) timing build: stamps = S*nbw*8 per-block + S*tri per-tile
- * + S*4 merge-tail int64 (nms_fused_kernel<true>), zeroed by the caller. */
+/* the one-launch NMS timing build inside the proposals: stamps = S*nbw*8 per-block + S*tri
+ * per-tile int64 (nms_fused_kernel<true>), zeroed by the caller. */
 int32_t frh_rpn_proposals_nms_stamped(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                   const float* const* reg_ptrs, const int64_t* cls_strides,
                                   const int64_t* reg_strides, const int32_t* grid_hw, int32_t num_anchors,

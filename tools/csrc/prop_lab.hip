@@ -52,7 +52,7 @@ extern "C" int32_t frh_rpn_proposals_nms2(int32_t num_imgs, int32_t num_levels, 
                                  stream, false, nullptr, true);
 }
 
-// the one-launch NMS without the folded merge: the merge as its own launch (rpn_merge_lds_kernel)
+// the round-4 merge (rpn_merge_lds_kernel) after the one-launch NMS instead of rpn_merge_wide_kernel
 extern "C" int32_t frh_rpn_proposals_merge_launch(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                                   const float* const* reg_ptrs, const int64_t* cls_strides,
                                                   const int64_t* reg_strides, const int32_t* grid_hw,
@@ -68,8 +68,8 @@ extern "C" int32_t frh_rpn_proposals_merge_launch(int32_t num_imgs, int32_t num_
                                  stream, false, nullptr, false, true);
 }
 
-// the one-launch NMS (+ folded merge) with its stamps (nms_fused_kernel<true>: S * nbw * 8 per-block
-// + S * tri per-tile + S * 4 merge-tail int64, stamps zeroed by the caller)
+// the one-launch NMS with its stamps (nms_fused_kernel<true>: S * nbw * 8 per-block + S * tri
+// per-tile int64, stamps zeroed by the caller)
 extern "C" int32_t frh_rpn_proposals_nms_stamped(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
                                                  const float* const* reg_ptrs, const int64_t* cls_strides,
                                                  const int64_t* reg_strides, const int32_t* grid_hw,
