@@ -818,9 +818,7 @@ def main():
                 nbytes_nms = float(np.mean([ops.nms_bytes(o[1], o[6]) for o in nrep[1]]))
             lines['nms'] = line(per_group.get('nms'), nbytes_nms,
                                 '20*N + 16*N*ceil(N/64) + 8*K_keep per segment (SURVEY §8(d)); RPN call, {} '
-                                'segments; the one launch (nms_fused_kernel) also runs the cross-level merge '
-                                '(round 5: folded in, formerly rpn_merge_lds_kernel under proposals)'
-                                .format(nrecs[0][1].shape[0] if nrecs else 0))
+                                'segments'.format(nrecs[0][1].shape[0] if nrecs else 0))
             if nrep:  # frh_nms_sorted: the standalone two-launch NMS (the RPN's own is one launch)
                 lines['nms']['us_replay_warm_two_launch'] = nrep[0]
             if args.config in ('faster_rcnn_r50_fpn', 'cascade_rcnn_r50_fpn'):
