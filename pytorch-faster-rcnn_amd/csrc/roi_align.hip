@@ -226,6 +226,14 @@ extern "C" int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const flo
                  static_cast<hipEvent_t>(stop_event), reinterpret_cast<unsigned long long*>(span));
 }
 
+// channels-last gradient levels (unit channel stride), sampling 2, up to 8 x 8 bins: lane = channel
+static bool bwd_nhwc_ok(const RoiLevels& lv, int32_t sampling_ratio, int32_t ph, int32_t pw) {
+  if (sampling_ratio != 2 || ph > 8 || pw > 8 || 4 * ph > kSepEnt || 4 * pw > kSepEnt) return false;
+  for (int l = 0; l < lv.L; ++l)
+    if (lv.sc[l] != 1) return false;
+  return true;
+}
+
 extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats, const int32_t* feat_hw,
                                              const int64_t* strides, const float* scales, int32_t batch,
                                              int32_t channels, const float* rois, const int64_t* roi_levels,
@@ -241,7 +249,10 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   FRH_REQUIRE(grad_feats && grad_out, "null pointer argument");
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-  if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
+  if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w))
+    hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<false>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),
+                       dim3(kWave), 0, as_stream(stream), lv, c, grad_out);
+  else if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
     hipLaunchKernelGGL(roi_align_bwd_sep_kernel<false>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
                        grad_out);
   else if (sampling_ratio == 2 && pooled_h * pooled_w <= 64)
@@ -280,8 +291,13 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
   if (num_rois > 0) {
     FRH_REQUIRE(grad_out, "null grad_out");
     RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
-    dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
-    hipLaunchKernelGGL(roi_align_bwd_sep_kernel<true>, grid, dim3(kRoiThreads), 0, st, lv, c, grad_out);
+    if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w)) {
+      hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),
+                         dim3(kWave), 0, st, lv, c, grad_out);
+    } else {
+      dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
+      hipLaunchKernelGGL(roi_align_bwd_sep_kernel<true>, grid, dim3(kRoiThreads), 0, st, lv, c, grad_out);
+    }
   }
   for (int l = 0; l < num_levels; ++l) {
     const int64_t blocks = std::min<int64_t>((numel[l] + 255) / 256, 4096);

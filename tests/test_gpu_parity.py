@@ -792,14 +792,15 @@ def test_roi_align_module_and_strided_view(dev):
     np.testing.assert_array_equal(out, ref)
 
 
-@pytest.mark.parametrize('case', ['small', 'p2', 'p2_nhwc', 'adaptive', 'bins9x7'])
+@pytest.mark.parametrize('case', ['small', 'small_nhwc', 'p2', 'p2_nhwc', 'adaptive', 'bins9x7'])
 def test_roi_align_backward_vs_oracle(dev, case):
     """Backward against the oracle: the separable row-run kernel (sampling 2, up to 8x8
-    bins; NCHW and channels_last gradients), the LDS-window kernel (9x7 bins) and per-tap
-    atomics (adaptive sampling).  Float atomics reorder the sums, so the tolerance is
-    f32-accumulation level."""
+    bins, NCHW gradients), its lane = channel form for channels_last gradients
+    (roi_align_bwd_nhwc_kernel: 16 channels, and 80 = one full and one partial 64-channel
+    group), the LDS-window kernel (9x7 bins) and per-tap atomics (adaptive sampling).  Float
+    atomics reorder the sums, so the tolerance is f32-accumulation level."""
     from frcnn_amd import ops
-    if case == 'small' or case == 'adaptive':
+    if case in ('small', 'small_nhwc', 'adaptive'):
         grids, scales, C, K, L = [(38, 64), (19, 32)], [1 / 16, 1 / 32], 16, 120, 2
     else:
         grids, scales, C, K, L = [(152, 256), (76, 128)], [1 / 4, 1 / 8], 80, 300, 2
@@ -810,12 +811,12 @@ def test_roi_align_backward_vs_oracle(dev, case):
     levels = oracle.roi_level_map(rois, 56.0, L)
     g = np.random.default_rng(62).standard_normal((K, C, ph, pw)).astype(np.float32)
     ft = [T(f, dev) for f in feats]
-    if case == 'p2_nhwc':
+    if case.endswith('_nhwc'):
         ft = [f.contiguous(memory_format=torch.channels_last) for f in ft]
     ft = [f.requires_grad_(True) for f in ft]
     out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, (ph, pw), sr)
     out.backward(T(g, dev))
-    if case == 'p2_nhwc':
+    if case.endswith('_nhwc'):
         assert all(f.grad.stride(1) == 1 for f in ft)  # the gradient keeps the features' format
     ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, sr)
     for a, r in zip(ft, ref):
