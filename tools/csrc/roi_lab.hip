@@ -36,7 +36,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant >= 28 && variant <= 53) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+  if (variant >= 28 && variant <= 55) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
                                          // 31 256 cells, 32 208 cells at 4 waves per SIMD
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
@@ -113,6 +113,12 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                          0, st, lv, c, out);
     else if (variant == 53)  // as 50, the quad D = 4 stage off (bands below 232 cells are unreachable)
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 3, 0, 0, 3>), gq, dim3(kWave),
+                         0, st, lv, c, out);
+    else if (variant == 54)  // the product's paths on a 208-cell slab (13 KB: 12 waves per CU by LDS)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 3, 3, 4, 0, 2>), gq, dim3(kWave),
+                         0, st, lv, c, out);
+    else if (variant == 55)  // as 54, 4 waves per SIMD requested
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 208, false, 4, 3, 4, 0, 2>), gq, dim3(kWave),
                          0, st, lv, c, out);
     else  // 45: hybrid (D = 4), 232-cell slab, stamped
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
