@@ -1037,9 +1037,10 @@ struct BandLayout {
 // quads, the quad layout's [quad][cell] takes two), quads {0, 1} then {2, 3}.  G / P carry the
 // quad layout's 16-B tap offsets (pair_setup<16>); every lane evaluates every stage (no band
 // masking) and stores whole channel rows.  For windows of up to kSlabCells * 2 cells.
-template <int kStAux, int kSlabCells, int D = 2>
+template <int kStAux, int kSlabCells, int D = 2, bool kStamp = false>
 __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
-                                          float* __restrict__ out, int64_t k, int chunk, uint32_t sbase, int lane) {
+                                          float* __restrict__ out, int64_t k, int chunk, uint32_t sbase, int lane,
+                                          int64_t item = 0, int64_t t_start = 0) {
   constexpr int SR = 2;
   const int cw0 = chunk * 4 * kQuadWave;
   const int nquads = min(kQuadWave, (c.C - cw0) / 4);  // host: C % 4 == 0
@@ -1123,6 +1124,15 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if (kStamp && lane == 0) {  // tools timing build: [4] = -D marks this path
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + item * 8;
+    st[0] = t_start;
+    st[1] = st[2] = st[6] = 0;
+    st[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[4] = -D;
+    st[5] = ncell;
+    st[7] = blockIdx.x & 7;
+  }
 }
 
 // kHybrid = D > 0: windows that the quad kernel stages D quads at a time (at most
@@ -1150,13 +1160,13 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
     }
     if constexpr ((kIlv & 1) != 0) {  // up to kSlabCells cells: one whole-window stage of [cell][4 quads]
       if (!G.empty && G.R * G.Cs2 <= kSlabCells) {
-        ilv_body<kStAux, kSlabCells, 4>(G, P, c, out, k, chunk, sbase, lane);
+        ilv_body<kStAux, kSlabCells, 4, kStamp>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
         return;
       }
     }
     if constexpr ((kIlv & 2) != 0) {  // up to 2 * kSlabCells cells: two whole-window stages of [cell][2 quads]
       if (!G.empty && G.R * G.Cs2 <= 2 * kSlabCells) {
-        ilv_body<kStAux, kSlabCells, 2>(G, P, c, out, k, chunk, sbase, lane);
+        ilv_body<kStAux, kSlabCells, 2, kStamp>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
         return;
       }
     }
