@@ -1140,16 +1140,15 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
 // most small RoIs) take its path instead -- lane = cell, 64 cells and one address per DMA
 // instruction: fewer instructions where the window is small and the L2 request rate is not
 // the bound -- the rest the bands.
+// band_body: one item (RoI k, 16 channels from chunk) after its RoI setup (G, P of
+// pair_setup<16> when kHybrid or kIlv, else pair_setup<64>); P by value: the band path rescales it.
 template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0, int kHybridHi = 0,
           int kIlv = 0>
-__device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
-                                          int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
+__device__ __forceinline__ void band_body(const RoiCfg& c, float* __restrict__ out, int64_t k, int chunk,
+                                          int64_t item, uint32_t sbase, int64_t t_start, int lane, const PairGeom& G,
+                                          PairLane P) {
   constexpr int SR = 2;
   int64_t t_setup = 0, t_land = 0;
-  PairGeom G;
-  PairLane P;
-  const RoiRaw raw = roi_fetch(c, k);
-  pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, G, P);
   if constexpr (kHybrid > 0 || kIlv > 0) {
     if constexpr (kHybrid > 0) {
       if (!G.empty && G.R * G.Cs2 <= QuadLayout<kHybrid, kSlabCells * 16>::kCells) {
@@ -1343,17 +1342,59 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
   }
 }
 
+template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0, int kHybridHi = 0,
+          int kIlv = 0>
+__device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
+                                          int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
+  PairGeom G;
+  PairLane P;
+  const RoiRaw raw = roi_fetch(c, k);
+  pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, G, P);
+  band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, k, chunk, item, sbase, t_start, lane,
+                                                                        G, P);
+}
+
 // 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups; XCD x takes the x-th eighth of
 // the item list in chunk-pair-major order (quad kernel, kOrder 1: the two 16-channel chunks of
 // a 128-B line, adjacent, on one XCD).
+// kChunks 2: one wave per (RoI, chunk pair) -- both 16-channel chunks of a 128-B line, one after
+// the other on the SAME RoI fetch and setup (the record's first load and pair_setup were ~half of a
+// small item's life); the grid is then 8 * ceil(K * ceil(chunks / 2) / 8).
 template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
-          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0>
+          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0, int kChunks = 1>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   __shared__ __attribute__((aligned(16))) float slab[kSlabCells * 16];
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   const uint32_t G = (uint32_t)(c.C + kQuadChunk - 1) / (uint32_t)kQuadChunk, K32 = (uint32_t)c.K;
+  const int lane = threadIdx.x & (kWave - 1);
+  if constexpr (kChunks == 2) {
+    const uint32_t NP = (G + 1u) / 2u, total = K32 * NP, per = (total + 7u) / 8u;
+    const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
+    if (w >= wend) return;
+    const uint32_t p = w / K32, k = w - p * K32;
+    PairGeom Gm;
+    PairLane P;
+    const RoiRaw raw = roi_fetch(c, (int64_t)k);
+    pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, Gm, P);
+    const bool two = 2u * p + 1u < G;
+    const int64_t item0 = (int64_t)p * 2 * K32 + (two ? 2 * k : k);
+    band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, (int64_t)k, (int)(2u * p), item0,
+                                                                          sbase, t_start, lane, Gm, P);
+    if (two) {
+      // the first chunk's tap reads are complete (its evaluation waited on them) before the
+      // second chunk's DMA overwrites the slab
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, (int64_t)k, (int)(2u * p + 1u),
+                                                                            item0 + 1, sbase, t_start, lane, Gm, P);
+    }
+    if (kSpan && threadIdx.x == 0) record_span(c, t_start);
+    return;
+  }
   const uint32_t total = K32 * G, per = (total + 7u) / 8u;
   const uint32_t w = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
   const uint32_t wend = min((blockIdx.x & 7u) * per + per, total);
@@ -1368,8 +1409,7 @@ roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     ch0 = (int)(2u * p);
     k0 = (int64_t)r;
   }
-  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(lv, c, out, k0, ch0, w, sbase, t_start,
-                                                       threadIdx.x & (kWave - 1));
+  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(lv, c, out, k0, ch0, w, sbase, t_start, lane);
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 

@@ -25,7 +25,7 @@ import torch  # noqa: E402
 from frcnn_amd import ops, _lib  # noqa: E402
 
 SETS = {'bench': 'cfg2_rois.npz', 'voc': 'cfg2_rois_voc.npz', 'train': 'cfg2_rois_train.npz'}
-STAMPED = {9, 15, 27, 29, 39, 56}  # tools variants writing per-item phase stamps (s_memrealtime)
+STAMPED = {9, 15, 27, 29, 39, 56, 58}  # tools variants writing per-item phase stamps (s_memrealtime)
 R4_LIB = os.path.join(REPO, 'tools', 'lib', 'r4', 'libfrcnn_amd_r4.so')
 
 

@@ -36,7 +36,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant >= 28 && variant <= 56) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+  if (variant >= 28 && variant <= 58) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
                                          // 31 256 cells, 32 208 cells at 4 waves per SIMD
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
@@ -123,6 +123,16 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (variant == 56)  // the product kernel, stamped (8 int64 per item after the output)
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 3, 4, 0, 2>), gq, dim3(kWave),
                          0, st, lv, c, out);
+    else if (variant == 57 || variant == 58) {  // the product's paths, one wave per (RoI, chunk pair); 58 stamped
+      const int64_t tp = num_rois * (((channels + 4 * kQuadWave - 1) / (4 * kQuadWave) + 1) / 2);
+      const dim3 gp((unsigned)(8 * ((tp + 7) / 8)));
+      if (variant == 57)
+        hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 3, 4, 0, 2, 2>), gp,
+                           dim3(kWave), 0, st, lv, c, out);
+      else
+        hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 3, 4, 0, 2, 2>), gp,
+                           dim3(kWave), 0, st, lv, c, out);
+    }
     else  // 45: hybrid (D = 4), 232-cell slab, stamped
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
