@@ -52,7 +52,6 @@ const char* frh_last_error(void);
 #define FRH_DEVERR_SELECT_BARRIER 1   /* rpn_select_kernel: a segment barrier timed out */
 #define FRH_DEVERR_NMS_COLUMN 2       /* nms_fused_kernel: a mask column never completed */
 #define FRH_DEVERR_SAMPLER_BARRIER 4  /* sampler_fused_kernel: an image barrier timed out */
-#define FRH_DEVERR_NMS_MERGE 8        /* nms_fused_kernel: a merge workgroup's image never finished its scans */
 
 /* ---- a1: AnchorCreator.__call__ over all FPN levels in one launch ------------
  * Replaces lib/anchor.py:107-129 (called per level from

@@ -30,7 +30,6 @@
 
 #include "cdna.h"
 #include "seg_topk.h"
-#include "rpn_merge.h"
 
 namespace frh {
 
@@ -578,15 +577,6 @@ __device__ __forceinline__ bool fz_wait_column(const uint32_t* col_flags, int p,
   return true;
 }
 
-// RPN merge workgroups (mg.L > 0; round 5): after the mask workgroups, B * L * ceil(P / 512)
-// workgroups run the cross-level merge of rpn_merge.h (merge_wide_body: one survivor per thread)
-// inside this launch.  Each waits for its image's L scans on a per-image arrival counter
-// (img_bar; a scan's wave 0 arrives after its keep list, kept scores and count, all stored
-// write-through, have completed: vmcnt(0)); the merge reads them with sc1 loads (hand-off
-// table row 1).  No residency is needed: they have the highest workgroup ids, so every mask
-// workgroup is dispatched before any of them occupies a slot, and the scans they wait for
-// wait only for mask workgroups.  A wait that runs out ORs FRH_DEVERR_NMS_MERGE.
-//
 // kscore (RPN proposals, else null): the kept rows' scores, compact beside the keep list
 // ([s * n_max + j] = score of keep[j]), for the cross-level merge launch (proposals.hip
 // rpn_merge_wide_kernel: one round trip to gather them instead of keep index -> score).  The
@@ -605,8 +595,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
                                                                int32_t* __restrict__ keep, int64_t kstride,
                                                                int32_t* __restrict__ kcounts, int32_t* status,
                                                                int64_t* stamps, const float* __restrict__ row_scores,
-                                                               uint32_t* __restrict__ kscore, MergeArgs mg,
-                                                               int32_t* img_bar) {
+                                                               uint32_t* __restrict__ kscore) {
   // scan: ring [kFzRing][kFzSlotWords] then kept[kFzMaxBlocks]; mask: per wave 64 row boxes + areas
   __shared__ __attribute__((aligned(16))) uint64_t fz_lds[kFzRing * kFzSlotWords + kFzMaxBlocks];
   __shared__ int ready[kFzRing];
@@ -615,31 +604,6 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int64_t tri = tri_tiles(nbw);
-  const int64_t nmask_wgs = ((int64_t)S * tri + kFzWaves - 1) / kFzWaves;
-  if ((int64_t)blockIdx.x >= S + nmask_wgs) {
-    // ---------------- RPN merge: workgroup q = (image, level, chunk)
-    const int q = (int)((int64_t)blockIdx.x - S - nmask_wgs);
-    const int nch = (mg.P + kMwThreads - 1) / kMwThreads;
-    const int b = q / (mg.L * nch), rem = q - b * mg.L * nch, l = rem / nch, chunk = rem - l * nch;
-    __shared__ int s_go;
-    if (tid == 0) {
-      int ok = 1;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (xwg_load(img_bar + (int64_t)b * kBarWords) < mg.L) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-          atomicOr(status, FRH_DEVERR_NMS_MERGE);
-          ok = 0;
-          break;
-        }
-      }
-      s_go = ok;
-    }
-    __syncthreads();
-    if (!s_go) return;
-    merge_wide_body<true>(mg, kscore, chunk, l, b, reinterpret_cast<float*>(fz_lds));
-    return;
-  }
   if ((int)blockIdx.x >= S) {
     // ---------------- mask: one tile per wave
     const int64_t g = ((int64_t)blockIdx.x - S) * kFzWaves + wave;
@@ -720,14 +684,8 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       }
       if ((kb >> lane) & 1ull) {
         const int at = nk + __popcll(kb & lanemask_lt());
-        const uint32_t ksc = __float_as_uint(ring_sc[(b % kFzRing) * kWave + lane]);
-        if (img_bar) {  // merge workgroups of this launch read them: write-through
-          xwg_store(reinterpret_cast<uint32_t*>(K) + at, (uint32_t)(b * 64 + lane));
-          xwg_store(kscore + (int64_t)s * n_max + at, ksc);
-        } else {
-          K[at] = b * 64 + lane;
-          if (kscore) kscore[(int64_t)s * n_max + at] = ksc;
-        }
+        K[at] = b * 64 + lane;
+        if (kscore) kscore[(int64_t)s * n_max + at] = __float_as_uint(ring_sc[(b % kFzRing) * kWave + lane]);
       }
       nk += __popcll(kb);
 #pragma unroll
@@ -743,13 +701,7 @@ __global__ void __launch_bounds__(kFzThreads) __attribute__((amdgpu_waves_per_eu
       }
       if (stop) break;
     }
-    if (img_bar) {  // arrive on the image's counter once the keep list, scores and count have landed
-      if (lane == 0) xwg_store(reinterpret_cast<uint32_t*>(kcounts) + s, (uint32_t)nk);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) atomicAdd(img_bar + (int64_t)(s / mg.L) * kBarWords, 1);
-    } else if (lane == 0) {
-      kcounts[s] = nk;
-    }
+    if (lane == 0) kcounts[s] = nk;
   } else {  // loaders
     const uint32_t* sflags = flags + (int64_t)s * tri;
     const uint64_t* smask = mask + (int64_t)s * tri * 64;
@@ -860,11 +812,6 @@ bool nms_fused_fits(int32_t S, int32_t n_max) {
          S <= resident_capacity(reinterpret_cast<const void*>(nms_fused_kernel<false>), kFzThreads) / 4;
 }
 
-static_assert(kFzThreads == kMwThreads, "the merge workgroups run merge_wide_body at the scan's block size");
-
-// LDS the merge workgroups stage the other levels' scores in: the scan's ring + kept sets
-int nms_merge_lds_floats() { return (kFzRing * kFzSlotWords + kFzMaxBlocks) * 2; }
-
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+ one spare)
   return ((size_t)S * (size_t)tri_tiles((n_max + 63) / 64) + 1) * sizeof(uint32_t);
 }
@@ -872,34 +819,21 @@ size_t nms_fused_flag_bytes(int32_t S, int32_t n_max) {  // one word per tile (+
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                          uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps = nullptr,
-                         const float* row_scores = nullptr, uint32_t* kscore = nullptr,
-                         const MergeArgs* merge = nullptr, int32_t* img_bar = nullptr) {
+                         const float* row_scores = nullptr, uint32_t* kscore = nullptr) {
   FRH_REQUIRE(nms_fused_fits(S, n_max), "one-launch NMS: %d segments of %d boxes out of range", S, n_max);
   FRH_REQUIRE(status, "null status word");
   FRH_REQUIRE(!kscore || row_scores, "kept scores need the row scores");
-  MergeArgs mg{};
-  int64_t merge_wgs = 0;
-  if (merge) {  // the RPN merge in this launch (rpn_merge.h): needs the kept scores and the arrival counters
-    mg = *merge;
-    FRH_REQUIRE(kscore && img_bar && mg.L >= 1 && mg.L <= FRH_MAX_LEVELS && S % mg.L == 0 && mg.P == n_max &&
-                    mg.keep == keep && mg.keep_count == kcounts && kstride == n_max &&
-                    (int64_t)(mg.L - 1) * mg.P <= nms_merge_lds_floats(),
-                "one-launch NMS merge: bad arguments");
-    merge_wgs = (int64_t)S * ((mg.P + kMwThreads - 1) / kMwThreads);
-  } else {
-    img_bar = nullptr;
-  }
   const int nbw = (n_max + 63) / 64;
-  const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves + merge_wgs;
+  const int64_t grid = S + ((int64_t)S * tri_tiles(nbw) + kFzWaves - 1) / kFzWaves;
   FRH_REQUIRE(grid < ((int64_t)1 << 31), "too many mask tiles");
   if (stamps)
     hipLaunchKernelGGL(nms_fused_kernel<true>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, stamps, row_scores, kscore, mg, img_bar);
+                       status, stamps, row_scores, kscore);
   else
     hipLaunchKernelGGL(nms_fused_kernel<false>, dim3((unsigned)grid), dim3(kFzThreads), 0, st, (int)S, boxes,
                        seg_stride, counts, n_max, nbw, nms_thr(thr), mask, flags, max_keep, keep, kstride, kcounts,
-                       status, nullptr, row_scores, kscore, mg, img_bar);
+                       status, nullptr, row_scores, kscore);
   return check_launch("nms_fused");
 }
 

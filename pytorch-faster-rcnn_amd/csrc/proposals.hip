@@ -12,7 +12,6 @@
 //  3. merge   (1 block per image): concatenate the levels' survivors and, if
 //     more than max_num, keep the best max_num by (score desc, concat order).
 #include "seg_topk.h"
-#include "rpn_merge.h"
 
 namespace frh {
 
@@ -25,9 +24,7 @@ size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                          uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st,
-                         int64_t* stamps = nullptr, const float* row_scores = nullptr, uint32_t* kscore = nullptr,
-                         const MergeArgs* merge = nullptr, int32_t* img_bar = nullptr);
-int nms_merge_lds_floats();
+                         int64_t* stamps = nullptr, const float* row_scores = nullptr, uint32_t* kscore = nullptr);
 
 constexpr int kPropThreads = 1024;
 constexpr int kMaxSort = 16384;
@@ -633,6 +630,18 @@ static __global__ void __launch_bounds__(kPropThreads) rpn_sort_decode_kernel(Pr
   if (threadIdx.x == 0) p.sel_count[seg] = written;
 }
 
+struct MergeArgs {
+  const float* sel_boxes;
+  const float* sel_scores;
+  const int32_t* keep;
+  const int32_t* keep_count;
+  int L, P;
+  int max_num;  // <= 0: no cut
+  int64_t out_cap;
+  float* out_boxes;   // [B][4][out_cap]
+  float* out_scores;  // [B][out_cap]
+  int32_t* out_counts;
+};
 
 // Cross-level top-k as a merge: each level's survivors are already in
 // (score desc) order, so the rank of survivor j of level l among all levels
@@ -784,12 +793,111 @@ static __global__ void __launch_bounds__(256) rpn_merge_kernel(MergeArgs p) {
   merge_write(p, b, seg, pos, rank, s);
 }
 
-// The merge over the one-launch NMS's compact kept scores: rpn_merge.h (merge_wide_body), one
-// survivor per thread on a grid of (survivor chunks of kMwThreads, level, image).
+// The merge over the one-launch NMS's compact kept scores (nms.hip kscore: [seg][j] = the
+// score of keep[j]): grid (survivor chunks of kMwThreads, level, image), ONE survivor per
+// thread, so the image's ranks are spread over ~40 CUs instead of one workgroup per level
+// (rpn_merge_lds_kernel: the binary searches of 2 survivors per thread against 4 levels are
+// LDS-bound on 10 CUs -- as were the same searches run by the NMS launch's own scan
+// workgroups, a folded form measured and removed in round 5).  Each workgroup stages the
+// other levels' kept scores of its image (one round trip, kMwGather loads per thread in
+// flight; no keep-index indirection) and searches them with kMwSearch levels in lock step.
+constexpr int kMwThreads = 512;
+constexpr int kMwGather = 16;
+constexpr int kMwSearch = 4;
+
 static __global__ void __launch_bounds__(kMwThreads) rpn_merge_wide_kernel(MergeArgs p,
                                                                            const uint32_t* __restrict__ kscore) {
-  extern __shared__ float ms[];
-  merge_wide_body<false>(p, kscore, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, ms);
+  extern __shared__ float ms[];  // image b's other levels' kept scores, packed in level order
+  __shared__ int cnt_s[FRH_MAX_LEVELS], beg_s[FRH_MAX_LEVELS];
+  const int L = p.L, l = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int seg = b * L + l, j = blockIdx.x * kMwThreads + t, jc = min(j, p.P - 1);
+  const int cv = t < L ? p.keep_count[b * L + t] : 0;  // in flight together with the own survivor
+  const int pos_raw = p.keep[(int64_t)seg * p.P + jc];
+  const uint32_t scb = kscore[(int64_t)seg * p.P + jc];
+  if (t < L) cnt_s[t] = min(max(cv, 0), p.P);
+  __syncthreads();
+  if (t == 0) {
+    int o = 0;
+    for (int q = 0; q < L; ++q) {
+      beg_s[q] = o;
+      o += q == l ? 0 : cnt_s[q];
+    }
+  }
+  int total = 0, base = 0;
+  for (int q = 0; q < L; ++q) {
+    const int c = cnt_s[q];
+    base += q < l ? c : 0;
+    total += c;
+  }
+  const int own_n = cnt_s[l];
+  const bool cut = p.max_num > 0 && total > p.max_num;
+  if (blockIdx.x == 0 && l == 0 && t == 0) p.out_counts[b] = cut ? p.max_num : total;
+  if ((int)blockIdx.x * kMwThreads >= own_n) return;  // workgroup-uniform
+  const bool live = j < own_n;
+  const float4 bx = reinterpret_cast<const float4*>(p.sel_boxes)[(int64_t)seg * p.P + min(max(pos_raw, 0), p.P - 1)];
+  __syncthreads();  // beg_s
+  if (cut) {
+    const int n_other = total - own_n;
+    for (int e0 = 0; e0 < n_other; e0 += kMwThreads * kMwGather) {
+      uint32_t v[kMwGather];
+#pragma unroll
+      for (int u = 0; u < kMwGather; ++u) {
+        const int e = e0 + u * kMwThreads + t;
+        int q = l == 0 ? 1 : 0;  // the level holding packed entry e
+#pragma unroll 1
+        for (int r = q + 1; r < L; ++r)
+          if (r != l && beg_s[r] <= e) q = r;
+        v[u] = e < n_other ? kscore[(int64_t)(b * L + q) * p.P + (e - beg_s[q])] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kMwGather; ++u) {
+        const int e = e0 + u * kMwThreads + t;
+        if (e < n_other) ms[e] = __uint_as_float(v[u]);
+      }
+    }
+    __syncthreads();
+  }
+  const float sc = __uint_as_float(scb);
+  int rank = base + j;
+  if (cut) {
+    rank = j;
+    for (int k0 = 0; k0 < L - 1; k0 += kMwSearch) {
+      int qv[kMwSearch], qb[kMwSearch], qc[kMwSearch], lo[kMwSearch], hi[kMwSearch];
+      int steps = 0;
+#pragma unroll
+      for (int i = 0; i < kMwSearch; ++i) {  // other level k = k0 + i is level k + (k >= l)
+        const int q = k0 + i + (k0 + i >= l ? 1 : 0);
+        qv[i] = q;
+        qc[i] = q < L ? __builtin_amdgcn_readfirstlane(cnt_s[q]) : 0;
+        qb[i] = q < L ? __builtin_amdgcn_readfirstlane(beg_s[q]) : 0;
+        lo[i] = 0;
+        hi[i] = qc[i];
+        steps = max(steps, 32 - __builtin_clz((uint32_t)qc[i] | 1u));
+      }
+      for (int n = 0; n < steps; ++n) {  // survivors of level q ordered before (sc, level l)
+        float v[kMwSearch];
+#pragma unroll
+        for (int i = 0; i < kMwSearch; ++i) v[i] = ms[qb[i] + min((lo[i] + hi[i]) >> 1, max(qc[i] - 1, 0))];
+#pragma unroll
+        for (int i = 0; i < kMwSearch; ++i) {
+          const int mid = (lo[i] + hi[i]) >> 1;
+          const bool before = qv[i] < l ? (v[i] >= sc) : (v[i] > sc);
+          const bool act = lo[i] < hi[i];
+          lo[i] = act && before ? mid + 1 : lo[i];
+          hi[i] = act && !before ? mid : hi[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kMwSearch; ++i) rank += lo[i];
+    }
+  }
+  if (!live || (cut && rank >= p.max_num)) return;
+  float* ob = p.out_boxes + (int64_t)b * 4 * p.out_cap;
+  ob[rank] = bx.x;
+  ob[p.out_cap + rank] = bx.y;
+  ob[2 * p.out_cap + rank] = bx.z;
+  ob[3 * p.out_cap + rank] = bx.w;
+  p.out_scores[(int64_t)b * p.out_cap + rank] = sc;
 }
 
 static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -801,12 +909,12 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            const float* min_size, int32_t pre_nms, int32_t post_nms, int32_t max_num, double nms_iou,
                            float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
                            void* workspace, size_t ws_bytes, void* stream, bool select_launches,
-                           int64_t* select_stamps = nullptr, bool nms_launches = false, int merge_form = 0,
+                           int64_t* select_stamps = nullptr, bool nms_launches = false, bool merge_launch = false,
                            int64_t* nms_stamps = nullptr);
 
 struct PropLayout {
   int P;
-  size_t boxes, scores, idx, stage, cnt, keep, kcnt, kscore, mask, keys, mem, zero, nflags, nbar, zero_bytes, total;
+  size_t boxes, scores, idx, stage, cnt, keep, kcnt, kscore, mask, keys, mem, zero, nflags, zero_bytes, total;
   int64_t nmax, kld;
 };
 
@@ -839,11 +947,10 @@ static PropLayout prop_layout(int32_t B, int32_t L, const int32_t* grid_hw, int3
   z.keys = z.mask + al(nms_mask_bytes((int32_t)S, P));
   z.mem = z.keys + al(S * (size_t)z.kld * sizeof(uint32_t));
   z.zero = z.mem + al(S * (size_t)z.kld * sizeof(uint64_t));
-  // zeroed by one memset per call: the selection's histograms / state / barriers, the
-  // one-launch NMS's tile flags, then its merge workgroups' per-image arrival counters
+  // zeroed by one memset per call: the selection's histograms / state / barriers, then the
+  // one-launch NMS's tile flags
   z.nflags = z.zero + al(tk_zero_bytes((int)S, kRpnHistBits));
-  z.nbar = z.nflags + al(nms_fused_flag_bytes((int32_t)S, P));
-  z.zero_bytes = z.nbar - z.zero + (size_t)B * kBarWords * sizeof(int32_t);
+  z.zero_bytes = z.nflags - z.zero + nms_fused_flag_bytes((int32_t)S, P);
   z.total = z.zero + al(z.zero_bytes);
   return z;
 }
@@ -927,7 +1034,7 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
                                 const float* img_hw, const float* min_size, int32_t pre_nms, int32_t post_nms,
                                 int32_t max_num, double nms_iou, float* out_boxes, float* out_scores,
                                 int32_t* out_counts, int32_t* status, void* workspace, size_t ws_bytes, void* stream,
-                                bool select_launches, int64_t* select_stamps, bool nms_launches, int merge_form,
+                                bool select_launches, int64_t* select_stamps, bool nms_launches, bool merge_launch,
                                 int64_t* nms_stamps) {
   FRH_REQUIRE(cls_strides && reg_strides, "null stride arrays");
   FRH_REQUIRE(num_imgs >= 1 && num_imgs <= 64, "num_imgs %d must be in [1, 64]", num_imgs);
@@ -1031,25 +1138,20 @@ int32_t frh::rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const floa
   uint64_t* nmask = reinterpret_cast<uint64_t*>(ws + z.mask);
   const int64_t out_cap = max_num > 0 ? max_num : post * num_levels;
   const bool nms_fused = !nms_launches && nms_fused_fits(S, z.P);
-  MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num, out_cap, out_boxes, out_scores,
-               out_counts};
-  // 3 + 4. NMS and the cross-level merge.  merge_form 0: the merge workgroups of the one-launch
-  // NMS where the other levels' kept scores fit their LDS; 2 (or no room): the wide merge as its own
-  // launch; 1 (tools A/B) or the two-launch NMS: round 4's rpn_merge_lds_kernel.
+  // 4. the cross-level merge: the wide form over the one-launch NMS's compact kept scores
   const size_t wide_lds = (size_t)(num_levels - 1) * z.P * sizeof(float);
-  const bool in_nms = nms_fused && merge_form == 0 && (int64_t)(num_levels - 1) * z.P <= nms_merge_lds_floats();
-  const bool wide = nms_fused && !in_nms && merge_form != 1 && wide_lds <= 65536 - 256;
-  uint32_t* kscore = (in_nms || wide) ? reinterpret_cast<uint32_t*>(ws + z.kscore) : nullptr;
-  if (nms_fused)
+  const bool wide = nms_fused && !merge_launch && wide_lds <= 65536 - 256;
+  uint32_t* kscore = wide ? reinterpret_cast<uint32_t*>(ws + z.kscore) : nullptr;
+  if (nms_fused)  // 3. NMS
     r = launch_nms_fused(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou, (post_nms > 0) ? post_nms : -1,
                          keep, z.P, kcnt, nmask, reinterpret_cast<uint32_t*>(ws + z.nflags), status, st, nms_stamps,
-                         p.sel_scores, kscore, in_nms ? &mp : nullptr,
-                         in_nms ? reinterpret_cast<int32_t*>(ws + z.nbar) : nullptr);
+                         p.sel_scores, kscore);
   else
     r = launch_nms_sorted(S, p.sel_boxes, (int64_t)z.P * 4, p.sel_count, z.P, nms_iou,
                           (post_nms > 0) ? post_nms : -1, keep, z.P, kcnt, nmask, nullptr, st);
   if (r) return r;
-  if (in_nms) return FRH_OK;
+  MergeArgs mp{p.sel_boxes, p.sel_scores, keep, kcnt, num_levels, z.P, max_num, out_cap, out_boxes, out_scores,
+               out_counts};
   const size_t merge_lds = (size_t)num_levels * z.P * sizeof(float);
   if (wide) {
     const dim3 mg((unsigned)((post + kMwThreads - 1) / kMwThreads), (unsigned)num_levels, (unsigned)num_imgs);

@@ -42,8 +42,7 @@ def _drop_zero_workspaces():
 # call when FRCNN_AMD_DEBUG=1.
 DEVERR_BITS = {1: 'RPN selection segment barrier (rpn_select_kernel)',
                2: 'RPN NMS mask column wait (nms_fused_kernel)',
-               4: 'device sampler image barrier (sampler_fused_kernel)',
-               8: 'RPN merge wait for an image\'s NMS scans (nms_fused_kernel)'}
+               4: 'device sampler image barrier (sampler_fused_kernel)'}
 _STATUS = {}
 DEBUG = os.environ.get('FRCNN_AMD_DEBUG', '') not in ('', '0')
 

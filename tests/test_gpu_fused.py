@@ -17,13 +17,12 @@
   columns poll their flags in two loads), a post_nms cut that stops the scan early,
   tie-heavy and sparse score sets, 1, 2 and 4 images, three calls in a row (the flags are
   zeroed per call).  The two-launch NMS is pinned by test_gpu_parity.py's oracle cases.
-  The one-launch NMS also runs the cross-level merge where (levels - 1) x P scores fit its LDS:
-  merge workgroups after the mask workgroups wait on a per-image arrival counter for the scans
-  and rank one survivor per thread (rpn_merge.h).  The same comparison covers it -- the reference
-  side runs the round-4 rpn_merge_lds_kernel -- with a cut (the bench's call), without one
-  (total <= max_num) and with post_nms stopping the scans; P = 4000 / 8000 take a separate
-  merge launch.  frh_rpn_proposals_merge_launch (the one-launch NMS, then rpn_merge_lds_kernel)
-  and frh_rpn_proposals_merge_wide (then rpn_merge_wide_kernel) are compared too.
+  After the one-launch NMS (which also writes the kept rows' scores compactly) the merge runs
+  as rpn_merge_wide_kernel (one survivor per thread, ~40 workgroups) where (levels - 1) x P
+  scores fit its LDS: the same comparison covers it -- the reference side runs the round-4
+  rpn_merge_lds_kernel -- with a cut (the bench's call), without one (total <= max_num) and
+  with post_nms stopping the scans; P = 8000 takes the old merge.  frh_rpn_proposals_merge_launch
+  (the one-launch NMS, then rpn_merge_lds_kernel) is compared too.
 * Device sampler: frh_sample_random's one-launch sampler (sampler_fused_kernel) against the
   tools library's keys + collect launches (frh_sample_random_launches): labels, selection
   sets and counts equal; the workspace's zero region is zero after every call.  The sampler's
@@ -131,8 +130,7 @@ def test_rpn_one_launch_selection_pre_nms_sizes(dev, pre, post, mx):
     ('random_init', 1, 8000, 2000, 2000),   # 125 blocks: column flags polled in two loads
     ('sparse_high', 2, 300, 300, 4000),     # no cut: the merge keeps the level concatenation
 ])
-@pytest.mark.parametrize('other', ['frh_rpn_proposals_nms2', 'frh_rpn_proposals_merge_launch',
-                                   'frh_rpn_proposals_merge_wide'])
+@pytest.mark.parametrize('other', ['frh_rpn_proposals_nms2', 'frh_rpn_proposals_merge_launch'])
 def test_rpn_one_launch_nms_equals_two_launches(dev, case, batch, pre, post, mx, other):
     fused, ref = _run(dev, case, 1, True, batch, 0.0, pre, post, mx, 90 + batch, other=other)
     rb, rs, rc = ref

@@ -7,9 +7,8 @@ library stamps).
 RPN proposals: the bench's cfg2 RPN head outputs (random-init model, channels-last) through
 frh_rpn_proposals_strided (one-launch selection) and frh_rpn_proposals_launches (keys /
 refine / collect / rank) and through frh_rpn_proposals_nms2 (one-launch selection, two-launch
-NMS), frh_rpn_proposals_merge_launch (the round-4 merge, rpn_merge_lds_kernel, after the
-one-launch NMS) and frh_rpn_proposals_merge_wide (rpn_merge_wide_kernel as its own launch instead
-of the NMS launch's merge workgroups), back to back between one event pair, µs per call (everything included); then one stamped call: per workgroup, s_memrealtime at the kernel's
+NMS) and frh_rpn_proposals_merge_launch (the round-4 merge, rpn_merge_lds_kernel, after the
+one-launch NMS instead of rpn_merge_wide_kernel), back to back between one event pair, µs per call (everything included); then one stamped call: per workgroup, s_memrealtime at the kernel's
 phases, reported as medians relative to the workgroup's own start and to the launch's first
 start.  Device sampler: the cfg2 RPN call's shape (2 x 155 520 anchors, 256 / 128) on
 synthetic labels, the same three measurements.
@@ -91,8 +90,6 @@ def main():
     nms2 = time_calls(lambda: ops.rpn_proposals(*argv, _entry=(lib.frh_rpn_proposals_nms2, 'nms2')), args.iters)
     mlaunch = time_calls(lambda: ops.rpn_proposals(*argv, _entry=(lib.frh_rpn_proposals_merge_launch, 'merge_launch')),
                          args.iters)
-    mwide = time_calls(lambda: ops.rpn_proposals(*argv, _entry=(lib.frh_rpn_proposals_merge_wide, 'merge_wide')),
-                       args.iters)
     gx = max(max((3 * h * w + 4095) // 4096, (2000 + 63) // 64) for h, w in grids)
     stm = torch.zeros(2 * len(grids), gx, 16, dtype=torch.int64, device=dev)
 
@@ -127,7 +124,6 @@ def main():
                             'us_per_call_four_launch_select': round(four, 2),
                             'us_per_call_two_launch_nms': round(nms2, 2),
                             'us_per_call_lds_merge': round(mlaunch, 2),
-                            'us_per_call_wide_merge_launch': round(mwide, 2),
                             'timeline_one_launch_select': timeline(sa, RPN_PHASES),
                             'timeline_level0_key_workgroups': timeline(sa[0::L, :nch0], RPN_PHASES),
                             'timeline_level4': timeline(sa[L - 1::L], RPN_PHASES)}

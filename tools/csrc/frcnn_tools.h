@@ -71,17 +71,6 @@ int32_t frh_rpn_proposals_merge_launch(int32_t num_imgs, int32_t num_levels, con
                                        double nms_iou, float* out_boxes, float* out_scores, int32_t* out_counts,
                                        int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
-/* frh_rpn_proposals_strided with the wide merge (rpn_merge_wide_kernel) as its own launch instead
- * of the one-launch NMS's merge workgroups; same arguments and outputs. */
-int32_t frh_rpn_proposals_merge_wide(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
-                                     const float* const* reg_ptrs, const int64_t* cls_strides,
-                                     const int64_t* reg_strides, const int32_t* grid_hw, int32_t num_anchors,
-                                     int32_t cls_channels, const float* anchors, int64_t anchor_ld, const float* means,
-                                     const float* stds, const float* img_hw, const float* min_size, int32_t pre_nms,
-                                     int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                     float* out_scores, int32_t* out_counts, int32_t* status, void* workspace,
-                                     size_t ws_bytes, void* stream);
-
 /* frh_sample_random with the keys + collect launches instead of the one-launch sampler. */
 int32_t frh_sample_random_launches(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                                    const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,

@@ -20,14 +20,12 @@ extern "C" int32_t frh_nms_sorted_stamped(int32_t num_segs, const float* boxes, 
 }
 
 namespace frh {
-struct MergeArgs;
 bool nms_fused_fits(int32_t S, int32_t n_max);
 size_t nms_fused_flag_bytes(int32_t S, int32_t n_max);
 int32_t launch_nms_fused(int32_t S, const float* boxes, int64_t seg_stride, const int32_t* counts, int32_t n_max,
                          double thr, int32_t max_keep, int32_t* keep, int64_t kstride, int32_t* kcounts,
                          uint64_t* mask, uint32_t* flags, int32_t* status, hipStream_t st, int64_t* stamps,
-                         const float* row_scores = nullptr, uint32_t* kscore = nullptr,
-                         const struct MergeArgs* merge = nullptr, int32_t* img_bar = nullptr);
+                         const float* row_scores = nullptr, uint32_t* kscore = nullptr);
 }  // namespace frh
 
 // The RPN's one-launch NMS (nms_fused_kernel) on pre-sorted segments, tiles at s * tri(nbw):

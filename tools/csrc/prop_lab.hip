@@ -15,7 +15,7 @@ int32_t rpn_proposals_impl(int32_t num_imgs, int32_t num_levels, const float* co
                            float* out_boxes, float* out_scores, int32_t* out_counts, int32_t* status,
                            void* workspace, size_t ws_bytes, void* stream, bool select_launches,
                            int64_t* select_stamps = nullptr, bool nms_launches = false,
-                           int merge_form = 0, int64_t* nms_stamps = nullptr);
+                           bool merge_launch = false, int64_t* nms_stamps = nullptr);
 int32_t sample_random_impl(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,
                            const int32_t* num_boxes, int64_t max_boxes, int32_t max_num, int32_t pos_num,
                            uint64_t seed, int64_t* labels_out, int32_t* sel, int32_t* sel_counts, int32_t* status,
@@ -65,24 +65,7 @@ extern "C" int32_t frh_rpn_proposals_merge_launch(int32_t num_imgs, int32_t num_
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
                                  post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
-                                 stream, false, nullptr, false, 1);
-}
-
-// the wide merge (rpn_merge_wide_kernel) as its own launch after the one-launch NMS instead of
-// the NMS launch's merge workgroups
-extern "C" int32_t frh_rpn_proposals_merge_wide(int32_t num_imgs, int32_t num_levels, const float* const* cls_ptrs,
-                                                const float* const* reg_ptrs, const int64_t* cls_strides,
-                                                const int64_t* reg_strides, const int32_t* grid_hw,
-                                                int32_t num_anchors, int32_t cls_channels, const float* anchors,
-                                                int64_t anchor_ld, const float* means, const float* stds,
-                                                const float* img_hw, const float* min_size, int32_t pre_nms,
-                                                int32_t post_nms, int32_t max_num, double nms_iou, float* out_boxes,
-                                                float* out_scores, int32_t* out_counts, int32_t* status,
-                                                void* workspace, size_t ws_bytes, void* stream) {
-  return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
-                                 num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
-                                 post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
-                                 stream, false, nullptr, false, 2);
+                                 stream, false, nullptr, false, true);
 }
 
 // the one-launch NMS with its stamps (nms_fused_kernel<true>: S * nbw * 8 per-block + S * tri
@@ -99,7 +82,7 @@ extern "C" int32_t frh_rpn_proposals_nms_stamped(int32_t num_imgs, int32_t num_l
   return frh::rpn_proposals_impl(num_imgs, num_levels, cls_ptrs, reg_ptrs, cls_strides, reg_strides, grid_hw,
                                  num_anchors, cls_channels, anchors, anchor_ld, means, stds, img_hw, min_size, pre_nms,
                                  post_nms, max_num, nms_iou, out_boxes, out_scores, out_counts, status, workspace, ws_bytes,
-                                 stream, false, nullptr, false, 0, stamps);
+                                 stream, false, nullptr, false, false, stamps);
 }
 
 extern "C" int32_t frh_sample_random_launches(int32_t num_segs, const int64_t* labels_in, int64_t label_seg_stride,

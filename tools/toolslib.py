@@ -24,7 +24,6 @@ TOOL_SIGNATURES = {
     'frh_rpn_proposals_launches': _lib.SIGNATURES['frh_rpn_proposals_strided'],
     'frh_rpn_proposals_nms2': _lib.SIGNATURES['frh_rpn_proposals_strided'],
     'frh_rpn_proposals_merge_launch': _lib.SIGNATURES['frh_rpn_proposals_strided'],
-    'frh_rpn_proposals_merge_wide': _lib.SIGNATURES['frh_rpn_proposals_strided'],
     'frh_sample_random_launches': _lib.SIGNATURES['frh_sample_random'],
     'frh_rpn_proposals_stamped': (c_i32, _lib.SIGNATURES['frh_rpn_proposals_strided'][1][:-1] + [c_vp, c_vp]),
     'frh_rpn_proposals_nms_stamped': (c_i32, _lib.SIGNATURES['frh_rpn_proposals_strided'][1][:-1] + [c_vp, c_vp]),
