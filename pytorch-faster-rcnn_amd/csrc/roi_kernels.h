@@ -1361,7 +1361,7 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
 // the other on the SAME RoI fetch and setup (the record's first load and pair_setup were ~half of a
 // small item's life); the grid is then 8 * ceil(K * ceil(chunks / 2) / 8).
 template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
-          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0, int kChunks = 1>
+          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0, int kChunks = 1, int kOrder = 1>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -1402,7 +1402,10 @@ roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const uint32_t p = w / (2u * K32), r = w - p * 2u * K32;
   int ch0;
   int64_t k0;
-  if (2u * p + 1u < G) {
+  if (kOrder == 0) {  // chunk-major: XCD x walks its eighth of the (chunk, RoI) list
+    ch0 = (int)(w / K32);
+    k0 = (int64_t)(w - (uint32_t)ch0 * K32);
+  } else if (2u * p + 1u < G) {
     ch0 = (int)(2u * p + (r & 1u));
     k0 = (int64_t)(r >> 1);
   } else {  // odd chunk count: the last chunk alone
