@@ -1365,7 +1365,11 @@ template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool 
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  __shared__ __attribute__((aligned(16))) float slab[kSlabCells * 16];
+  // whole 1-KB DMA rounds: an LDS-DMA instruction writes 64 lanes x 16 B wherever its last cells
+  // fall, so the interleaved and band stages (up to ceil(cells / 32 or / 16) rounds from the
+  // slab start) may write up to 1 KB past kSlabCells * 64 B -- the slab holds that too
+  // (232 cells: 14.5 -> 15 KB, still 10 workgroups per CU by LDS)
+  __shared__ __attribute__((aligned(16))) float slab[(kSlabCells * 16 + 255) / 256 * 256];
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   const uint32_t G = (uint32_t)(c.C + kQuadChunk - 1) / (uint32_t)kQuadChunk, K32 = (uint32_t)c.K;
   const int lane = threadIdx.x & (kWave - 1);
