@@ -38,7 +38,7 @@ namespace frh {
 // this form 40.9 / 76.2 / 65.2 (stores per band: 40.9-42.9 / 77.2-79.0 / 67.2-69.3); bands
 // only 44.1-47.3 / 76-78 / 66-70; quad kernel (13 KB slab, pair order) 37.7-39.1 / 103-106 /
 // 96-98; round 4's 37.1-39.5 / 142 / 150.
-constexpr int kBandCells = 232;
+constexpr int kBandCells = 240;  // 15 KB: whole 1-KB DMA rounds, 10 workgroups per CU by LDS
 
 // region.py:256-264: floor(log2(sqrt(area) / finest + 1e-6)) clamped to [0, L-1]
 __device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, float y2, float finest, int L) {

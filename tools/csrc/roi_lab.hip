@@ -36,7 +36,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant >= 28 && variant <= 59) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+  if (variant >= 28 && variant <= 62) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
                                          // 31 256 cells, 32 208 cells at 4 waves per SIMD
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
@@ -136,6 +136,9 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (variant == 59)  // the product kernel with the chunk-major item order (round 4's quad kernel order)
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 232, false, 3, 3, 4, 0, 2, 1, 0>), gq,
                          dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 62)  // the product's paths on a 240-cell slab (15 KB: the same LDS as the declared 232-cell one)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2>), gq, dim3(kWave),
+                         0, st, lv, c, out);
     else  // 45: hybrid (D = 4), 232-cell slab, stamped
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
