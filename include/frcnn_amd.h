@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define FRH_ABI_VERSION 2
+#define FRH_ABI_VERSION 3
 
 #define FRH_OK 0
 #define FRH_EINVAL (-1)
@@ -47,8 +47,11 @@ const char* frh_last_error(void);
  * other kernels or on a partitioned GPU -- ORs one of these bits into the caller's device
  * int32 `status` word and ends that workgroup's work: the call's outputs are then undefined
  * and the workspace's zero region may be left dirty (re-zero it).  The library never reads
- * the word: the caller checks it where it synchronises anyway (frcnn_amd: the loss read, the
- * numpy sampler's count read, or after every call with FRCNN_AMD_DEBUG=1) and clears it. */
+ * the word except (ABI 3) the loss entries, which write NaN losses while it is nonzero, and
+ * frh_sample_random's one-launch form, which does nothing while it is nonzero (its zero region
+ * may be dirty): the step's own loss read carries a failure, and the caller checks the word
+ * where it synchronises anyway (frcnn_amd: every training step before the optimizer update,
+ * the numpy sampler's count read, or after every call with FRCNN_AMD_DEBUG=1) and clears it. */
 #define FRH_DEVERR_SELECT_BARRIER 1   /* rpn_select_kernel: a segment barrier timed out */
 #define FRH_DEVERR_NMS_COLUMN 2       /* nms_fused_kernel: a mask column never completed */
 #define FRH_DEVERR_SAMPLER_BARRIER 4  /* sampler_fused_kernel: an image barrier timed out */
@@ -416,19 +419,24 @@ int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* grad_feats,
                                   int32_t aligned, const float* grad_out, void* stream);
 
 /* Deterministic backward (parity runs; SURVEY §5 race detection): the gradient of
- * frh_roi_align_bwd_strided, accumulated in fixed point -- int64 in units of 2^-40, each
- * (RoI, row, column) partial sum rounded once and added with integer atomics, which are
- * associative -- so the result is bit-identical across runs whatever order the RoIs are
- * scheduled in (float atomics reorder sums).  acc_feats: per level an int64 buffer with the
- * element strides of grad_feats, zeroed by the caller; grad_feats (dense: every element is
- * written) = acc * 2^-40 rounded to f32.  |gradient element| < 2^23.  sampling_ratio 2 and
- * up to 8 x 8 bins (the reference configs' 7 x 7). */
+ * frh_roi_align_bwd_strided, accumulated in fixed point -- int64, each (RoI, row, column)
+ * partial sum rounded once and added with integer atomics, which are associative -- so the
+ * result is bit-identical across runs whatever order the RoIs are scheduled in (float atomics
+ * reorder sums).  The unit is set per call from the gradient's own magnitude (ABI 3; was a
+ * fixed 2^-40): 2^-(62 - hb - E) with max|grad_out| < 2^E and hb = ceil(log2(num_rois *
+ * pooled_h * pooled_w)) -- the most any cell can receive is max|grad_out| * num_rois * bins, so
+ * no accumulator can overflow, and the resolution is ~2^-(62 - hb) of the largest gradient
+ * element (about 2^-46 at cfg2) whatever its scale.  A non-finite grad_out makes every
+ * gradient element NaN.  acc_feats: per level an int64 buffer with the element strides of
+ * grad_feats, zeroed by the caller; grad_feats (dense: every element is written) = acc * unit
+ * rounded to f32.  scale_word: 4 bytes of caller-owned device memory (the call writes it: the
+ * bits of max|grad_out|).  sampling_ratio 2 and up to 8 x 8 bins (the reference configs' 7 x 7). */
 int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* grad_feats, int64_t* const* acc_feats,
                                 const int32_t* feat_hw, const int64_t* strides, const float* scales,
                                 int32_t batch, int32_t channels, const float* rois,
                                 const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
                                 int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                                const float* grad_out, void* stream);
+                                const float* grad_out, uint32_t* scale_word, void* stream);
 
 /* ---- RoIPool (torchvision.ops.RoIPool; C4 config configs/faster_rcnn_r50.py:26) --
  * feat [B, C, H, W] with element strides strides[0..3] = (b, c, y, x); rois
@@ -504,6 +512,7 @@ int32_t frh_bias_act_nhwc(float* y, const float* bias, int64_t rows, int32_t cha
  * value itself, int64 or, with target_is_float, f32), 2 = CrossEntropyLoss softmax
  * (losses.py:151-153, labels in [0, C)).  Logit (i, k) is x[i*sr + k*sc] (any strides,
  * so AnchorHead's [C, S] targets need no transpose copy); out is one f32 on the device.
+ * status (nullable, ABI 3): the device status word; while it is nonzero the forward writes NaN.
  * Backward writes grad_x (i, k) at grad_x[i*gsr + k*gsc] = grad_out[0] * dL/dx.  Rows with an
  * int64 label < 0 (padding rows of a fixed-capacity target buffer) add nothing, gradient 0.
  * Callers: AnchorHead.calc_loss (anchor_head.py:113-139), BBoxHead.calc_loss
@@ -514,7 +523,8 @@ int32_t frh_bias_act_nhwc(float* y, const float* bias, int64_t rows, int32_t cha
 size_t frh_loss_workspace(void);
 int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr,
                          int64_t sc, const void* target, int32_t target_is_float, float alpha,
-                         float gamma, float* out, void* workspace, size_t ws_bytes, void* stream);
+                         float gamma, const int32_t* status, float* out, void* workspace,
+                         size_t ws_bytes, void* stream);
 int32_t frh_cls_loss_bwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr,
                          int64_t sc, const void* target, int32_t target_is_float, float alpha,
                          float gamma, const float* grad_out, float* grad_x, int64_t gsr,
@@ -528,8 +538,8 @@ int32_t frh_cls_loss_bwd(int32_t kind, const float* x, int64_t n, int64_t c, int
  * grad_x (zero-filled by the caller). */
 int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l,
                           const float* y, int64_t ys_i, int64_t ys_j, const int64_t* label,
-                          int64_t n, int64_t m, int64_t n_sel, float beta, float* out,
-                          void* workspace, size_t ws_bytes, void* stream);
+                          int64_t n, int64_t m, int64_t n_sel, float beta, const int32_t* status,
+                          float* out, void* workspace, size_t ws_bytes, void* stream);
 int32_t frh_smooth_l1_bwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l,
                           const float* y, int64_t ys_i, int64_t ys_j, const int64_t* label,
                           int64_t n, int64_t m, int64_t n_sel, float beta,
@@ -549,8 +559,9 @@ int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
                          float cls_weight, float cls_div, const float* rx, int64_t xs_i,
                          int64_t xs_j, int64_t xs_l, const float* ry, int64_t ys_i, int64_t ys_j,
                          const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel, float beta,
-                         float reg_weight, float reg_div, const int32_t* div_count, float* out,
-                         void* workspace, size_t ws_bytes, void* stream);
+                         float reg_weight, float reg_div, const int32_t* div_count,
+                         const int32_t* status, float* out, void* workspace, size_t ws_bytes,
+                         void* stream);
 
 /* ---------------------------------------------------------------- f4: image pipeline
  * The train/test pipelines of configs/faster_rcnn_r50_fpn.py:120-139 (mmdet v1: Resize

@@ -48,6 +48,21 @@ int orc_set_threads(int n) {
 #endif
 }
 
+/* Reusable scratch (the timed CPU baseline calls these functions repeatedly: a fresh
+ * multi-MB malloc is an mmap whose pages are first-touched by every OpenMP thread at once,
+ * serialising on the kernel's page-fault path -- the 16-thread assignment measured slower than
+ * one thread).  Not reentrant: the oracle is called from one host thread. */
+static void* scratch(int slot, size_t bytes) {
+  static void* buf[4];
+  static size_t cap[4];
+  if (bytes > cap[slot]) {
+    free(buf[slot]);
+    buf[slot] = malloc(bytes);
+    cap[slot] = buf[slot] ? bytes : 0;
+  }
+  return buf[slot];
+}
+
 static float iou_p1(const float* a, int64_t lda, int64_t i, const float* b, int64_t ldb, int64_t j) {
   float ax1 = a[i], ay1 = a[lda + i], ax2 = a[2 * lda + i], ay2 = a[3 * lda + i];
   float bx1 = b[j], by1 = b[ldb + j], bx2 = b[2 * ldb + j], by2 = b[3 * ldb + j];
@@ -87,7 +102,7 @@ static void row_max(const float* v, int64_t n, int64_t stride, float* m, int64_t
 int orc_maxiou_assign(const float* boxes, int64_t ld, int64_t n, const float* gts, int64_t gld, int64_t g,
                       float pos_iou, float neg_iou, float min_pos_iou, int64_t* labels, float* max_iou) {
   if (g <= 0) return -1;
-  float* tab = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1) * (size_t)g);
+  float* tab = (float*)scratch(0, sizeof(float) * (size_t)(n > 0 ? n : 1) * (size_t)g);
   float* colmax = (float*)malloc(sizeof(float) * (size_t)g);
   if (!tab || !colmax) return -2;
   orc_iou_table(boxes, ld, n, gts, gld, g, tab);
@@ -136,7 +151,6 @@ int orc_maxiou_assign(const float* boxes, int64_t ld, int64_t n, const float* gt
     max_iou[i] = tab[i * g + arg];
     labels[i] = lab == 1 ? arg + 1 : lab;
   }
-  free(tab);
   free(colmax);
   return 0;
 }
@@ -252,11 +266,13 @@ int64_t orc_nms_sorted(const float* b, int64_t n, double thr, int64_t max_keep, 
 #endif
   if (threads > 1 && n >= 512) {
     const int64_t nw = (n + 63) / 64;
-    uint64_t* mask = (uint64_t*)calloc((size_t)n * (size_t)nw, sizeof(uint64_t));
+    uint64_t* mask = (uint64_t*)scratch(1, (size_t)n * (size_t)nw * sizeof(uint64_t));
 #pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t i = 0; i < n; ++i)
+    for (int64_t i = 0; i < n; ++i) {
+      for (int64_t w = 0; w < nw; ++w) mask[i * nw + w] = 0;
       for (int64_t j = i + 1; j < n; ++j)
         if (nms_above(b, area, i, j, thr)) mask[i * nw + j / 64] |= 1ull << (j % 64);
+    }
     uint64_t* removed = (uint64_t*)calloc((size_t)nw, sizeof(uint64_t));
     for (int64_t i = 0; i < n; ++i) {
       if (removed[i / 64] >> (i % 64) & 1ull) continue;
@@ -265,7 +281,6 @@ int64_t orc_nms_sorted(const float* b, int64_t n, double thr, int64_t max_keep, 
       for (int64_t w = i / 64; w < nw; ++w) removed[w] |= mask[i * nw + w];
     }
     free(removed);
-    free(mask);
     free(area);
     return nk;
   }

@@ -126,10 +126,18 @@ __device__ __forceinline__ float block_sum_f(float v, float* scratch) {
 }
 
 struct FanIn {
-  uint32_t* counter;  // zero between calls
-  float* partial;     // [gridDim.x]
+  uint32_t* counter;      // zero between calls
+  float* partial;         // [gridDim.x]
   float* out;
+  const int32_t* status;  // nullable: the caller's device status word; nonzero -> NaN loss
 };
+
+// A nonzero device status word (an in-launch wait of an earlier one-launch kernel ran out,
+// include/frcnn_amd.h FRH_DEVERR_*) makes the loss NaN: the outputs it was computed from are
+// undefined, and the step's own loss read carries the failure without an extra host sync.
+__device__ __forceinline__ bool status_set(const int32_t* status) {
+  return status && __hip_atomic_load(const_cast<int32_t*>(status), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 
 // Thread 0 holds the workgroup's partial sum.  The last workgroup to arrive sums
 // all partials in a fixed order (double accumulation: one slot per thread, then
@@ -155,7 +163,7 @@ __device__ void fan_in_finalize(float block_total, const FanIn& f) {
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    f.out[0] = (float)s[0];
+    f.out[0] = status_set(f.status) ? NAN : (float)s[0];
     __hip_atomic_store(f.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -302,8 +310,9 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_bwd_kernel(L1Args a, c
 // as torch does it: loss = (sum * loss_weight) / avg_factor in f32.
 struct DetScale {
   float wc, dc, wr, dr;
-  float* out;           // [2]: cls, reg
-  const int32_t* ndev;  // nullable: avg_factor = this device count for both (0 -> zero losses)
+  float* out;             // [2]: cls, reg
+  const int32_t* ndev;    // nullable: avg_factor = this device count for both (0 -> zero losses)
+  const int32_t* status;  // nullable: device status word; nonzero -> NaN losses
 };
 
 __device__ void det_fan_in(float pc, float pr, uint32_t* counter, float* partial, int nbc, int nbr,
@@ -346,6 +355,7 @@ __device__ void det_fan_in(float pc, float pr, uint32_t* counter, float* partial
       o.out[0] = (res[0] * o.wc) / o.dc;
       o.out[1] = (res[1] * o.wr) / o.dr;
     }
+    if (status_set(o.status)) o.out[0] = o.out[1] = NAN;
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -470,20 +480,20 @@ extern "C" {
 
 size_t frh_loss_workspace(void) { return kCounterBytes + 2 * kMaxPartials * sizeof(float); }
 
-static FanIn fan_in(void* workspace, float* out) {
+static FanIn fan_in(void* workspace, float* out, const int32_t* status) {
   char* w = static_cast<char*>(workspace);
-  return FanIn{reinterpret_cast<uint32_t*>(w), reinterpret_cast<float*>(w + kCounterBytes), out};
+  return FanIn{reinterpret_cast<uint32_t*>(w), reinterpret_cast<float*>(w + kCounterBytes), out, status};
 }
 
 int32_t frh_cls_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int64_t sr, int64_t sc,
-                         const void* target, int32_t target_is_float, float alpha, float gamma, float* out,
-                         void* workspace, size_t ws_bytes, void* stream) {
+                         const void* target, int32_t target_is_float, float alpha, float gamma,
+                         const int32_t* status, float* out, void* workspace, size_t ws_bytes, void* stream) {
   ClsArgs a = make_cls(x, n, c, sr, sc, target, target_is_float, alpha, gamma);
   int32_t st = check_cls(kind, a);
   if (st != FRH_OK) return st;
   FRH_REQUIRE(out, "cls loss: null output");
   FRH_REQUIRE(workspace && ws_bytes >= frh_loss_workspace(), "cls loss: workspace too small");
-  const FanIn f = fan_in(workspace, out);
+  const FanIn f = fan_in(workspace, out, status);
   int nb = grid_for(kind == kSoftmaxCe ? n : n * c);
   hipStream_t s = as_stream(stream);
   if (kind == kFocal)
@@ -518,7 +528,7 @@ int32_t frh_cls_loss_bwd(int32_t kind, const float* x, int64_t n, int64_t c, int
 
 int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs_l, const float* y, int64_t ys_i,
                           int64_t ys_j, const int64_t* label, int64_t n, int64_t m, int64_t n_sel, float beta,
-                          float* out, void* workspace, size_t ws_bytes, void* stream) {
+                          const int32_t* status, float* out, void* workspace, size_t ws_bytes, void* stream) {
   L1Args a = make_l1(x, xs_i, xs_j, xs_l, y, ys_i, ys_j, label, n, m, n_sel, beta);
   int32_t st = check_l1(a);
   if (st != FRH_OK) return st;
@@ -526,7 +536,7 @@ int32_t frh_smooth_l1_fwd(const float* x, int64_t xs_i, int64_t xs_j, int64_t xs
   FRH_REQUIRE(workspace && ws_bytes >= frh_loss_workspace(), "smooth l1: workspace too small");
   int nb = grid_for(n * m);
   hipLaunchKernelGGL(smooth_l1_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, as_stream(stream), a,
-                     fan_in(workspace, out));
+                     fan_in(workspace, out, status));
   return check_launch("frh_smooth_l1_fwd");
 }
 
@@ -534,8 +544,8 @@ int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
                          const void* target, int32_t target_is_float, float alpha, float gamma, float cls_weight,
                          float cls_div, const float* rx, int64_t xs_i, int64_t xs_j, int64_t xs_l, const float* ry,
                          int64_t ys_i, int64_t ys_j, const int64_t* label, int64_t rn, int64_t rm, int64_t n_sel,
-                         float beta, float reg_weight, float reg_div, const int32_t* div_count, float* out,
-                         void* workspace, size_t ws_bytes, void* stream) {
+                         float beta, float reg_weight, float reg_div, const int32_t* div_count,
+                         const int32_t* status, float* out, void* workspace, size_t ws_bytes, void* stream) {
   ClsArgs a = make_cls(x, n, c, sr, sc, target, target_is_float, alpha, gamma);
   int32_t st = check_cls(kind, a);
   if (st != FRH_OK) return st;
@@ -548,7 +558,7 @@ int32_t frh_det_loss_fwd(int32_t kind, const float* x, int64_t n, int64_t c, int
   char* w = static_cast<char*>(workspace);
   uint32_t* counter = reinterpret_cast<uint32_t*>(w);
   float* partial = reinterpret_cast<float*>(w + kCounterBytes);
-  const DetScale o{cls_weight, cls_div, reg_weight, reg_div, out, div_count};
+  const DetScale o{cls_weight, cls_div, reg_weight, reg_div, out, div_count, status};
   const dim3 g((unsigned)std::max(nbc, nbr));
   hipStream_t s = as_stream(stream);
   if (kind == kFocal)

@@ -267,10 +267,10 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
                                            int32_t batch, int32_t channels, const float* rois,
                                            const int64_t* roi_levels, int64_t num_rois, int32_t pooled_h,
                                            int32_t pooled_w, int32_t sampling_ratio, int32_t aligned,
-                                           const float* grad_out, void* stream) {
+                                           const float* grad_out, uint32_t* scale_word, void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, pooled_h, pooled_w, rois);
   if (r) return r;
-  FRH_REQUIRE(grad_feats && acc_feats, "null pointer argument");
+  FRH_REQUIRE(grad_feats && acc_feats && scale_word, "null pointer argument");
   FRH_REQUIRE(sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt,
               "the deterministic backward takes sampling_ratio 2 and up to %d x %d bins", kSepEnt / 4, kSepEnt / 4);
   RoiLevels lv;
@@ -288,9 +288,17 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
                 "level %d: the deterministic backward needs dense gradient buffers", l);
     numel[l] = n;
   }
+  // the call's fixed-point unit: max|grad_out| (one streaming pass), headroom for K * bins
+  int hb = 0;
+  while (hb < 62 && (int64_t(1) << hb) < num_rois * pooled_h * pooled_w) ++hb;
+  FRH_REQUIRE(hb <= 40, "too many RoIs x bins for the fixed-point backward");
+  if (hipMemsetAsync(scale_word, 0, sizeof(uint32_t), st) != hipSuccess) return check_launch("frh_roi_align_bwd_fixed");
   if (num_rois > 0) {
     FRH_REQUIRE(grad_out, "null grad_out");
-    RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
+    const int64_t ng = num_rois * channels * pooled_h * pooled_w;
+    const int64_t mb = std::min<int64_t>((ng / 4 + 255) / 256 + 1, 2048);
+    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)mb), dim3(256), 0, st, grad_out, ng, scale_word);
+    RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned, nullptr, scale_word, hb};
     if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w)) {
       hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),
                          dim3(kWave), 0, st, lv, c, grad_out);
@@ -302,7 +310,7 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
   for (int l = 0; l < num_levels; ++l) {
     const int64_t blocks = std::min<int64_t>((numel[l] + 255) / 256, 4096);
     hipLaunchKernelGGL(roi_bwd_fixed_to_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                       reinterpret_cast<const long long*>(acc_feats[l]), grad_feats[l], numel[l]);
+                       reinterpret_cast<const long long*>(acc_feats[l]), grad_feats[l], numel[l], scale_word, hb);
   }
   return check_launch("frh_roi_align_bwd_fixed");
 }

@@ -22,6 +22,8 @@ struct RoiCfg {
   int64_t K;
   int C, ph, pw, sampling, aligned;
   unsigned long long* span;  // measurement builds (kSpan): {min wave start, max wave end}, s_memrealtime
+  const uint32_t* fix_max;   // fixed-point backward: bits of max|grad_out| (the call's own pass)
+  int fix_hb;                // fixed-point backward: ceil(log2(K * ph * pw)), accumulation headroom
 };
 
 // kSpan kernels: the launch's span on the 100 MHz clock, first wave start to last wave end.

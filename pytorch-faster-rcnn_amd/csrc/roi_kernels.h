@@ -1611,9 +1611,36 @@ constexpr int kSepEnt = 32;  // tap entries per axis and wave half: 4 * ph, 4 * 
 
 // kFixed (deterministic backward, frh_roi_align_bwd_fixed): lv.grad[l] points at int64
 // accumulators with the gradient's element strides; each (RoI, row, column) sum is added as
-// rint(sum * 2^40) by an integer atomic -- integer adds are associative, so the total is the
+// rint(sum * scale) by an integer atomic -- integer adds are associative, so the total is the
 // same whatever order the RoIs arrive in (the float-atomic form's order is the scheduler's).
-constexpr double kBwdFixedScale = 1099511627776.0;  // 2^40: |gradient element| < 2^23 fits int64
+// scale = 2^(62 - hb - E), max|grad_out| < 2^E (the call's own max pass), hb = ceil(log2(K *
+// bins)): a cell receives at most max|grad_out| * K * bins, so |total * scale| < 2^62.  A
+// non-finite max gives scale -1: no atomics, and the conversion writes NaN.
+__device__ __forceinline__ double bwd_fixed_scale(const uint32_t* fix_max, int hb) {
+  const uint32_t m = __hip_atomic_load(const_cast<uint32_t*>(fix_max), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (m >= 0x7f800000u) return -1.0;
+  const int E = (int)(m >> 23) - 126;  // exponent field 0 (zero / subnormal): < 2^-126
+  return ldexp(1.0, 62 - hb - E);
+}
+
+// max |g| over n floats as the bits of |g| (monotonic for non-negative floats; NaN above inf),
+// one atomicMax per wave into *out (zeroed by the caller's memset)
+static __global__ void roi_bwd_absmax_kernel(const float* __restrict__ g, int64_t n, uint32_t* out) {
+  uint32_t m = 0u;
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(g) & 15) == 0 ? n / 4 : 0;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = g4[q];
+    m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                   max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+  }
+  for (int64_t q = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, __float_as_uint(g[q]) & 0x7fffffffu);
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0 && m) atomicMax(out, m);
+}
+
 template <bool kFixed = false>
 __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevels lv, RoiCfg c,
                                                                          const float* __restrict__ gout) {
@@ -1710,6 +1737,8 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevel
   const int64_t sy = lv.sy[l], sx = lv.sx[l], scs = lv.sc[l];
   const int64_t goff0 = (int64_t)g.b * lv.sb[l] + (int64_t)cw0 * scs;
   const float* go = gout + (k * c.C + cw0) * nbins;
+  const double fscale = kFixed ? bwd_fixed_scale(c.fix_max, c.fix_hb) : 0.0;
+  if (kFixed && fscale < 0.0) return;  // non-finite gradient: the conversion writes NaN
   for (int ch = 0; ch < nch; ch += 2) {
     // grad_out of channels ch, ch + 1 (a missing odd last channel reads 0 and is not written)
     for (int e = lane; e < 2 * nbins; e += kWave) {
@@ -1739,7 +1768,7 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevel
           const int64_t e = fo + (int64_t)row * sy + (int64_t)my_col * sx;
           if constexpr (kFixed)
             atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
-                      (unsigned long long)(long long)rint((double)sum * kBwdFixedScale));
+                      (unsigned long long)(long long)rint((double)sum * fscale));
           else
             atomicAdd(lv.grad[l] + e, sum);
         }
@@ -1816,6 +1845,8 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
   const int64_t base = (int64_t)g.b * lv.sb[l] + ch, sy = lv.sy[l], sx = lv.sx[l];
+  const double fscale = kFixed ? bwd_fixed_scale(c.fix_max, c.fix_hb) : 0.0;
+  if (kFixed && fscale < 0.0) return;  // non-finite gradient: the conversion writes NaN
   float R[kMaxP];
 #pragma unroll
   for (int px = 0; px < kMaxP; ++px) R[px] = 0.0f;
@@ -1840,7 +1871,7 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
       const int64_t e = base + (int64_t)row * sy + (int64_t)col * sx;
       if constexpr (kFixed)
         atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
-                  (unsigned long long)(long long)rint((double)v * kBwdFixedScale));
+                  (unsigned long long)(long long)rint((double)v * fscale));
       else
         atomicAdd(lv.grad[l] + e, v);
     }
@@ -1848,9 +1879,12 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
 }
 
 // the fixed-point accumulators to the f32 gradient, element by element (dense buffers)
-static __global__ void roi_bwd_fixed_to_f32_kernel(const long long* __restrict__ acc, float* __restrict__ grad, int64_t n) {
+static __global__ void roi_bwd_fixed_to_f32_kernel(const long long* __restrict__ acc, float* __restrict__ grad, int64_t n,
+                                                   const uint32_t* fix_max, int hb) {
+  const double s = bwd_fixed_scale(fix_max, hb);
+  const double inv = s > 0.0 ? 1.0 / s : (double)NAN;  // 1 / 2^k is exact
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
-    grad[q] = (float)((double)acc[q] * (1.0 / kBwdFixedScale));
+    grad[q] = (float)((double)acc[q] * inv);
 }
 
 // ---------------------------------------------------------------------------

@@ -298,6 +298,12 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   const int n = num[s];
   const int G = n > kTkChunk ? (n + kTkChunk - 1) / kTkChunk : 1;
   if (x >= G) return;
+  // A set status word means an earlier one-launch call (this kernel or the RPN's) ran out of a
+  // wait: this workspace's zero region may hold its counters, so a barrier here could pass on
+  // them early.  Do nothing; the word stays set (the loss entries turn it into NaN losses) until
+  // the host's check clears it and replaces the workspace.  (Loaded here, tested before the
+  // first zero-region access, so the load overlaps phase 1.)
+  const int32_t status0 = __hip_atomic_load(f.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto stamp = [&](int q) {
     if (f.stamps && t == 0)
       f.stamps[((int64_t)s * gridDim.x + x) * 16 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -346,6 +352,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   for (int i = t; i < 2 * kSampBins; i += kTkThreads)
     xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
   stamp(2);
+  if (status0 != 0) return;
   if (!seg_barrier(bar, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return;
   stamp(3);
 

@@ -90,7 +90,7 @@ SIGNATURES = {
     'frh_roi_align_bwd_strided': (c_i32, [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
                                           c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     'frh_roi_align_bwd_fixed': (c_i32, [c_i32, P(c_vp), P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp,
-                                        c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
+                                        c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     'frh_roi_pool_fwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_i32, c_i32, c_vp,
                                  c_vp, c_vp]),
     'frh_roi_pool_bwd': (c_i32, [c_vp, P(c_i64), c_i32, c_i32, c_i32, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp,
@@ -104,21 +104,21 @@ SIGNATURES = {
     'frh_image_preprocess': (c_i32, [c_vp, c_i32, P(c_i64), P(c_i32), P(c_i32), P(c_i32), P(c_f32), P(c_f32), c_i32,
                                      c_vp, c_i32, c_i32, c_vp]),
     'frh_cls_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,
-                                 c_size, c_vp]),
+                                 c_vp, c_size, c_vp]),
     'frh_cls_loss_bwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp,
                                  c_i64, c_i64, c_vp]),
     'frh_smooth_l1_fwd': (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
-                                  c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_smooth_l1_bwd': (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
                                   c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     'frh_det_loss_fwd': (c_i32, [c_i32, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32,
                                  c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32,
-                                 c_f32, c_f32, c_vp, c_vp, c_vp, c_size, c_vp]),
+                                 c_f32, c_f32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'frh_atss_assign': (c_i32, [c_i32, c_i32, P(c_i32), P(c_f32), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32,
                                 c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

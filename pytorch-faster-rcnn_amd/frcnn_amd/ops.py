@@ -8,6 +8,7 @@ these.  The torchvision drop-ins the reference imports (`nms`, `roi_align`,
 """
 import ctypes
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -47,9 +48,16 @@ _STATUS = {}
 DEBUG = os.environ.get('FRCNN_AMD_DEBUG', '') not in ('', '0')
 
 
+def _device_key(dev):
+    """Device index of `dev`; a bare 'cuda' device means the current device (both the word's
+    owner and its checker resolve it this way)."""
+    d = torch.device(dev)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
 def status_word(dev):
     """The device status word of `dev` (int32 [1], zero until a one-launch kernel flags)."""
-    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    key = _device_key(dev)
     w = _STATUS.get(key)
     if w is None:
         w = _STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device('cuda', key))
@@ -61,7 +69,7 @@ def check_device_status(dev=None):
     a timed-out in-launch wait since the last check.  Synchronises with the word's device.
     The word is cleared and the zero-contract workspaces are dropped (their counters may be
     left dirty by the aborted launch), so later calls start clean."""
-    keys = list(_STATUS) if dev is None else [torch.device(dev).index or 0]
+    keys = list(_STATUS) if dev is None else [_device_key(dev)]
     for k in keys:
         w = _STATUS.get(k)
         if w is None:
@@ -784,16 +792,30 @@ class _RoIAlignMulti(torch.autograd.Function):
         K, B, C = rois.shape[0], shapes[0][0], shapes[0][1]
         # the gradient keeps each feature map's memory format (NCHW or channels_last)
         if deterministic_backward() and int(sr) == 2 and ph <= 8 and pw <= 8:
-            # bit-identical across runs: fixed-point (int64, 2^-40) integer atomics, then one
+            # bit-identical across runs: fixed-point (int64, unit from max|grad|) integer atomics, then one
             # conversion pass that writes every gradient element (frh_roi_align_bwd_fixed)
             grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt)
                      for s, fmt in zip(shapes, ctx.formats)]
             accs = [torch.empty(s, dtype=torch.int64, device=grad.device, memory_format=fmt).zero_()
                     for s, fmt in zip(shapes, ctx.formats)]
             hw, st = _feat_desc(grads)
+            word = torch.empty(1, dtype=torch.int32, device=grad.device)  # the call's max|grad_out| bits
             call('frh_roi_align_bwd_fixed', len(grads), ptr_array(grads), ptr_array(accs), hw, st, f32_array(scales),
-                 B, C, ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), stream_of(grad))
+                 B, C, ptr(rois), ptr(levels), K, ph, pw, int(sr), int(bool(aligned)), ptr(grad), ptr(word),
+                 stream_of(grad))
             return (None, None, None, None, None, None) + tuple(grads)
+        if deterministic_backward():
+            # the fixed-point form covers sampling 2 with up to 8 x 8 bins (every config); the
+            # float-atomic form below is not deterministic, which torch's mode must hear about
+            msg = ('frcnn_amd roi_align backward: no deterministic form for sampling_ratio={}, '
+                   'output {}x{} (fixed point covers sampling 2 and up to 8x8 bins)'.format(sr, ph, pw))
+            if torch.are_deterministic_algorithms_enabled() and torch.is_deterministic_algorithms_warn_only_enabled() \
+                    and not _DETERMINISTIC['on']:
+                if not _DETERMINISTIC.get('warned'):
+                    _DETERMINISTIC['warned'] = True
+                    warnings.warn(msg)
+            else:
+                raise RuntimeError(msg)
         # cleared here and accumulated with float atomics (one per row run of a RoI's taps)
         grads = [torch.empty(s, dtype=torch.float32, device=grad.device, memory_format=fmt).zero_()
                  for s, fmt in zip(shapes, ctx.formats)]
@@ -1091,7 +1113,7 @@ class _ClsLoss(torch.autograd.Function):
         out = torch.empty((), dtype=torch.float32, device=x.device)
         ws = _loss_workspace(x)
         call('frh_cls_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
-             float(gamma), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+             float(gamma), ptr(status_word(x.device)), ptr(out), ptr(ws), ws.numel(), stream_of(x))
         ctx.save_for_backward(x, target)
         ctx.cfg = (kind, tfloat, alpha, gamma)
         return out
@@ -1129,7 +1151,7 @@ class _SmoothL1(torch.autograd.Function):
         out = torch.empty((), dtype=torch.float32, device=x.device)
         ws = _loss_workspace(x)
         call('frh_smooth_l1_fwd', ptr(x), xs[0], xs[1], xs[2], ptr(y), ys[0], ys[1], ptr(label), n, m, n_sel,
-             float(beta), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+             float(beta), ptr(status_word(x.device)), ptr(out), ptr(ws), ws.numel(), stream_of(x))
         ctx.save_for_backward(x, y, label)
         ctx.cfg = (xs, ys, n, m, n_sel, beta)
         return out
@@ -1201,7 +1223,8 @@ class _DetLoss(torch.autograd.Function):
         hdiv = 1.0 if dcount is not None else float(div)
         call('frh_det_loss_fwd', kind, ptr(x), n, c, x.stride(0), x.stride(1), ptr(target), tfloat, float(alpha),
              float(gamma), float(wc), hdiv, ptr(rx), xs[0], xs[1], xs[2], ptr(ry), ys[0], ys[1], ptr(rlabel), rn,
-             rm, n_sel, float(beta), float(wr), hdiv, ptr(dcount), ptr(out), ptr(ws), ws.numel(), stream_of(x))
+             rm, n_sel, float(beta), float(wr), hdiv, ptr(dcount), ptr(status_word(x.device)), ptr(out), ptr(ws),
+             ws.numel(), stream_of(x))
         if dcount is not None:
             # backward divides by the count as f32 (count 0: every row is padding, gradients 0)
             div = dcount.float()

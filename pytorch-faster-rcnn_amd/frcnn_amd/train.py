@@ -49,17 +49,30 @@ def build_optimizer(params, cfg):
 
 
 class TrainStep:
-    """Callable training iteration on this rank's batch; returns the (detached) local loss."""
+    """Callable training iteration on this rank's batch; returns the (detached) local loss.
+
+    The device status word (include/frcnn_amd.h FRH_DEVERR_*) is read every step, after
+    backward and before the optimizer update -- one 4-byte read where the reference's loop
+    reads every loss with `.item()` (`lib/trainer/trainer.py:110-119`) -- so a step whose
+    in-launch wait ran out raises before its update is applied (its losses are NaN already:
+    the loss kernels take the word).  `status_every=k` reads it every k-th step instead;
+    0 never (then a failed step's update lands, only its NaN losses carry the failure).
+
+    `force_ddp` wraps the detector in DistributedDataParallel even at world size 1 (the
+    RCCL readiness check on a one-GPU box: the bucketed all-reduce runs, over one rank)."""
 
     def __init__(self, detector, optimizer_cfg=None, grad_clip=None, world_size=1, device=None,
-                 bucket_mb=DEFAULT_BUCKET_MB, status_every=50):
+                 bucket_mb=DEFAULT_BUCKET_MB, status_every=1, force_ddp=False):
         self.detector = detector
-        self.device = device
-        self.status_every, self.steps = status_every, 0
         self.params = [p for p in detector.parameters() if p.requires_grad]
+        if device is None and self.params:
+            device = self.params[0].device
+        self.device = torch.device(device) if device is not None else None
+        self.status_every, self.steps = status_every, 0
         net = DetectorLoss(detector)
-        if world_size > 1:
-            ids = [device] if device is not None and device.type == 'cuda' else None
+        if world_size > 1 or force_ddp:
+            dev = self.device
+            ids = [dev] if dev is not None and dev.type == 'cuda' else None
             net = nn.parallel.DistributedDataParallel(net, device_ids=ids, bucket_cap_mb=bucket_mb,
                                                       gradient_as_bucket_view=True, broadcast_buffers=False)
         self.net = net
@@ -73,9 +86,9 @@ class TrainStep:
         if self.grad_clip:
             nn.utils.clip_grad_norm_(self.params, self.grad_clip['max_norm'],
                                      self.grad_clip.get('norm_type', 2))
-        self.optimizer.step()
         self.steps += 1
         if self.status_every and self.steps % self.status_every == 0 and self.device is not None and \
                 self.device.type == 'cuda':
-            ops.check_device_status(self.device)  # one synchronising 4-byte read per status_every steps
+            ops.check_device_status(self.device)  # raises before a failed step's update
+        self.optimizer.step()
         return loss.detach()

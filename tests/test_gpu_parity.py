@@ -823,12 +823,16 @@ def test_roi_align_backward_vs_oracle(dev, case):
         np.testing.assert_allclose(a.grad.cpu().numpy(), r, rtol=1e-4, atol=2e-5)
 
 
-@pytest.mark.parametrize('case', ['p2', 'p2_nhwc', 'voc_nhwc'])
-def test_roi_align_backward_deterministic(dev, case):
+@pytest.mark.parametrize('case,gscale', [('p2', 1.0), ('p2_nhwc', 1.0), ('voc_nhwc', 1.0), ('p2', 1e-8),
+                                         ('voc_nhwc', 1e-8), ('p2_nhwc', 3e4)])
+def test_roi_align_backward_deterministic(dev, case, gscale):
     """The deterministic backward (frh_roi_align_bwd_fixed: fixed-point integer atomics,
     SURVEY §5): within f32-accumulation tolerance of the oracle, bit-identical across runs AND
     under any permutation of the RoIs (the sum over RoIs is order-independent), where the
-    float-atomic form is not (reference: autograd of lib/region.py:276)."""
+    float-atomic form is not (reference: autograd of lib/region.py:276).  The fixed-point unit
+    follows the gradient's own magnitude (ABI 3): training-sized gradients (grad_out ~1e-8) keep
+    the same RELATIVE tolerance as unit-scale ones (a fixed 2^-40 unit would floor them at
+    ~1e-12 absolute), and large ones (3e4) do not overflow."""
     from frcnn_amd import ops
     if case == 'voc_nhwc':
         z = np.load(inputs.golden_path('cfg2_rois_voc.npz'))
@@ -840,7 +844,7 @@ def test_roi_align_backward_deterministic(dev, case):
         levels = oracle.roi_level_map(rois, 56.0, 2)
     K = rois.shape[0]
     feats = inputs.feature_maps(60, grids, C, 2)
-    g = np.random.default_rng(62).standard_normal((K, C, 7, 7)).astype(np.float32)
+    g = (np.random.default_rng(62).standard_normal((K, C, 7, 7)) * gscale).astype(np.float32)
     ref = oracle.roi_align_bwd([f.shape for f in feats], rois, levels, scales, g, 2)
 
     def run(order):
@@ -860,7 +864,30 @@ def test_roi_align_backward_deterministic(dev, case):
         ops.set_deterministic_backward(False)
     for x, y, z_, r in zip(a, b, c, ref):
         assert torch.equal(x, y) and torch.equal(x, z_)
-        np.testing.assert_allclose(x.cpu().numpy(), r, rtol=1e-4, atol=2e-5)
+        np.testing.assert_allclose(x.cpu().numpy(), r, rtol=1e-4, atol=2e-5 * gscale)
+
+
+def test_roi_align_backward_deterministic_nonfinite_and_unsupported(dev):
+    """A NaN in grad_out makes every element of the deterministic gradient NaN (no undefined
+    float -> int64 conversion); a shape the fixed-point form does not cover raises under
+    set_deterministic_backward instead of silently running the float atomics."""
+    from frcnn_amd import ops
+    grids, scales, C = [(38, 64)], [1 / 16], 16
+    feats = inputs.feature_maps(64, grids, C, 2)
+    rois = _rois(65, 40, 2)
+    g = np.random.default_rng(66).standard_normal((40, C, 7, 7)).astype(np.float32)
+    g[3, 2, 1, 1] = np.nan
+    ops.set_deterministic_backward(True)
+    try:
+        ft = [T(f, dev).requires_grad_(True) for f in feats]
+        ops.roi_align_multilevel(ft, T(rois, dev), None, scales, (7, 7), 2).backward(T(g, dev))
+        assert torch.isnan(ft[0].grad).all()
+        ft = [T(f, dev).requires_grad_(True) for f in feats]
+        out = ops.roi_align_multilevel(ft, T(rois, dev), None, scales, (7, 7), 0)  # adaptive sampling
+        with pytest.raises(RuntimeError, match='no deterministic form'):
+            out.backward(T(np.nan_to_num(g), dev))
+    finally:
+        ops.set_deterministic_backward(False)
 
 
 def test_roi_pool_vs_oracle(dev):

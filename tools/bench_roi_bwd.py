@@ -46,12 +46,14 @@ def main():
                       _lib.ptr(rois), _lib.ptr(levels), K, 7, 7, 2, 0, _lib.ptr(g), _lib.stream_of(g))
             return grads
 
+        word = torch.empty(1, dtype=torch.int32, device=dev)
+
         def fixed(r=rois, lv=levels, gg=g):
             grads = [torch.empty_like(f) for f in feats]
             accs = [torch.empty(f.shape, dtype=torch.int64, device=dev, memory_format=torch.channels_last).zero_()
                     for f in feats]
             _lib.call('frh_roi_align_bwd_fixed', len(grads), _lib.ptr_array(grads), _lib.ptr_array(accs), hw, st, sc,
-                      B, C, _lib.ptr(r), _lib.ptr(lv), K, 7, 7, 2, 0, _lib.ptr(gg), _lib.stream_of(gg))
+                      B, C, _lib.ptr(r), _lib.ptr(lv), K, 7, 7, 2, 0, _lib.ptr(gg), _lib.ptr(word), _lib.stream_of(gg))
             return grads
         res = {}
         for nm, fn in (('atomic', atomic), ('fixed', fixed)):
