@@ -588,6 +588,9 @@ def main():
     ap.add_argument('--config', default='faster_rcnn_r50_fpn', choices=sorted(CONFIG_NAMES),
                     help='model config (the BASELINE metric is faster_rcnn_r50_fpn; others are extra lines)')
     ap.add_argument('--bucket-mb', type=float, default=None, help='DDP all-reduce bucket size (train mode)')
+    ap.add_argument('--status-every', type=int, default=0,
+                    help='train mode: also read the device status word synchronously every k-th step before the '
+                         'update (TrainStep; 0 = only its sync-free guard: NaN losses, skipped update, lagged raise)')
     ap.add_argument('--force-ddp', action='store_true',
                     help='train mode at N = 1: initialise a world-size-1 process group on --backend (nccl = RCCL) '
                          'and wrap the detector in DDP anyway, so the bucketed all-reduce runs (RCCL readiness)')
@@ -648,7 +651,8 @@ def main():
         from frcnn_amd.train import TrainStep, DEFAULT_BUCKET_MB
         opt_cfg = cfg.get('optimizer_config', None) or {}
         train_step = TrainStep(model, cfg.get('optimizer', None), opt_cfg.get('grad_clip', None), world, dev,
-                               args.bucket_mb or DEFAULT_BUCKET_MB, force_ddp=force_ddp)
+                               args.bucket_mb or DEFAULT_BUCKET_MB, status_every=args.status_every,
+                               force_ddp=force_ddp)
 
         def step():
             return train_step(*batch)
@@ -794,7 +798,8 @@ def main():
                        'image': '600x1000 padded 608x1024', 'parallelism': 'dp{}'.format(world),
                        'backend': args.backend if world > 1 or force_ddp else None,
                        'ddp': world > 1 or force_ddp if args.mode == 'train' else None,
-                       'sampler': args.sampler, 'mode': args.mode},
+                       'sampler': args.sampler, 'mode': args.mode,
+                       'status_every': args.status_every if args.mode == 'train' else None},
         }
         if recs:
             out['roofline'] = {

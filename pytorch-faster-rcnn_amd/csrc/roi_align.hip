@@ -30,15 +30,19 @@
 
 namespace frh {
 
-// The band kernel's slab: 232 cells x 16 channels = 14.5 KB (11 waves per CU by LDS, 3 per
+// The band kernel's slab: 240 cells x 16 channels = 15 KB (10 waves per CU by LDS, 3 per
 // SIMD by registers): 8-row bands of the widest (29-column) windows, i.e. two bin rows of a
-// tap-list window per band.  Windows of <= 192 cells take the quad path (kHybrid = 4).
+// tap-list window per band; whole 1-KB LDS-DMA rounds (2 x 240 cells x 32 B of the interleaved
+// path and 15 rounds of 16 band cells both fill exactly 15 KB).  Windows of <= 192 cells take
+// the quad path (kHybrid = 4), <= 480 cells the two interleaved stages, larger ones the bands.
 // The bands' results are stored after the last band (kRot 3: whole channel rows per store).
 // Measured (tools/bench_roi_sets.py, MI355X, µs per launch, bench / VOC / train-step RoIs):
 // this form 40.9 / 76.2 / 65.2 (stores per band: 40.9-42.9 / 77.2-79.0 / 67.2-69.3); bands
 // only 44.1-47.3 / 76-78 / 66-70; quad kernel (13 KB slab, pair order) 37.7-39.1 / 103-106 /
 // 96-98; round 4's 37.1-39.5 / 142 / 150.
 constexpr int kBandCells = 240;  // 15 KB: whole 1-KB DMA rounds, 10 workgroups per CU by LDS
+static_assert(2 * kBandCells * 32 <= kBandCells * 64 && (kBandCells + 15) / 16 * 1024 <= kBandCells * 64,
+              "the interleaved stages and the band DMA rounds must fit the slab");
 
 // region.py:256-264: floor(log2(sqrt(area) / finest + 1e-6)) clamped to [0, L-1]
 __device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, float y2, float finest, int L) {
@@ -169,16 +173,19 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
   };
   if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
     // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels); tap
-    // windows of <= ~232 cells staged whole, 4 quads at a time ([quad][cell]); <= 464 cells
+    // windows of <= 192 cells staged whole, 4 quads at a time ([quad][cell]); <= 480 cells
     // whole in two stages of [cell][2 quads] (32 B per cell and request); larger in row bands
     // of [cell][16 channels], 64 B per cell and request
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
     const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
+    // kFwdTrim | kFwdIlvRot (round 6): no loads for lanes past the window and no empty DMA rounds;
+    // the interleaved path's two lanes of a cell read different quads at each step
+    constexpr int kOpt = kFwdTrim | kFwdIlvRot;
     if (span)
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true, 3, 3, 4, 0, 2>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, true, 3, 3, 4, 0, 2, 1, 1, kOpt>, grid, dim3(kWave));
     else
-      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, false, 3, 3, 4, 0, 2>, grid, dim3(kWave));
+      go(roi_align_fwd_band_kernel<kCpolNT, false, kBandCells, false, 3, 3, 4, 0, 2, 1, 1, kOpt>, grid, dim3(kWave));
   } else if (quad_ok(f, lv, channels, pooled_h, pooled_w)) {
     // channels-last, shapes the band kernel does not take: one quad per 16-B DMA lane
     const int64_t total = num_rois * ((channels + kQuadChunk - 1) / kQuadChunk);

@@ -788,7 +788,11 @@ __device__ __forceinline__ f32x4 quad_val(const float (&w)[4], const f32x4* x) {
 // kQW: channel quads per item (4: 16 channels).  kOut: 0 = per-channel 4-B stores of the
 // bin row (lane = bin), 1 = [channel][bin] staged in LDS (obuf), then 16-B stores of the
 // item's contiguous output block, 2 = no stores (tools-only diagnostic).
-template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, int kSlab = kQuadSlab, bool kOnly4 = false>
+// kOpt bit 1 (kFwdTrim): lanes past the window's cells load nothing (an out-of-range offset:
+// no memory request) and DMA rounds past the window are not issued.
+constexpr int kFwdTrim = 1, kFwdIlvRot = 2;
+template <int kStAux, bool kStamp, int kQW = kQuadWave, int kOut = 0, int kSlab = kQuadSlab, bool kOnly4 = false,
+          int kOpt = 0>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf);
@@ -806,7 +810,7 @@ __device__ __forceinline__ void quad_item(const RoiLevels& lv, const RoiCfg& c, 
 
 // the item after its setup (G, P): staging, evaluation, stores.  The host admits only
 // shapes whose largest tap grid fits one region (quad_ok: quad_max_cells <= kCells of D = 1).
-template <int kStAux, bool kStamp, int kQW, int kOut, int kSlab, bool kOnly4>
+template <int kStAux, bool kStamp, int kQW, int kOut, int kSlab, bool kOnly4, int kOpt>
 __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, int64_t item, uint32_t sbase,
                                           int64_t t_start, int lane, float* obuf) {
@@ -857,19 +861,23 @@ __device__ __forceinline__ void quad_body(const PairGeom& G, const PairLane& P, 
     // region 16-B unit j * 64 + lane of every quad  <-  that quad of cell j * 64 + lane
     auto goff_at = [&](int j) {
       int e = j * kWave + lane;
-      e = e < ncell ? e : 0;
+      const bool in = e < ncell;
+      e = in ? e : 0;
       const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
-      return (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave);
+      const int o = (dy && dx) ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(rsrc, r, kWave) + __shfl(csrc, col, kWave);
+      return ((kOpt & kFwdTrim) && !in) ? 0x40000000 : o;
     };
     int goff[RP];
 #pragma unroll
     for (int j = 0; j < RP; ++j) goff[j] = goff_at(j);
+    const int nr = (kOpt & kFwdTrim) ? (ncell + kWave - 1) / kWave : RP;  // rounds holding cells (uniform)
     auto issue = [&](int s) {  // quads past the last re-read it (their stores are dropped)
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int soff = (cw0 + 4 * min(s * D + d, nquads - 1)) * 4;
 #pragma unroll
-        for (int j = 0; j < RP; ++j) lds_dma_at<16, 0>(fr, sbase + 4u * (uint32_t)(d * RS + j * 256), goff[j], soff);
+        for (int j = 0; j < RP; ++j)
+          if (j < nr) lds_dma_at<16, 0>(fr, sbase + 4u * (uint32_t)(d * RS + j * 256), goff[j], soff);
       }
     };
     auto eval = [&](int s) {
@@ -1037,7 +1045,10 @@ struct BandLayout {
 // quads, the quad layout's [quad][cell] takes two), quads {0, 1} then {2, 3}.  G / P carry the
 // quad layout's 16-B tap offsets (pair_setup<16>); every lane evaluates every stage (no band
 // masking) and stores whole channel rows.  For windows of up to kSlabCells * 2 cells.
-template <int kStAux, int kSlabCells, int D = 2, bool kStamp = false>
+// kOpt bit 2 (kFwdIlvRot, D = 2): at step d lane l reads quad (d + l) & 1 of its cells, so the
+// 16 lanes of a ds_read_b128 group use both 16-B halves of the 32-B cells (16 bank slots
+// instead of 8); the two results are stored per channel after both steps.
+template <int kStAux, int kSlabCells, int D = 2, bool kStamp = false, int kOpt = 0>
 __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, const RoiCfg& c,
                                           float* __restrict__ out, int64_t k, int chunk, uint32_t sbase, int lane,
                                           int64_t item = 0, int64_t t_start = 0) {
@@ -1061,10 +1072,11 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
     const int dq = min(D * s + (lane & (D - 1)), nquads - 1);
     for (int j = 0; j < nj; ++j) {
       int e = (kWave / D) * j + (lane >> kLg);
-      e = e < ncell ? e : 0;
+      const bool in = e < ncell;
+      e = in ? e : 0;
       const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
       const int goff = dense ? ((y0 + r) * sy + (x0 + col) * sx) * 4 : __shfl(P.rsrc, r, kWave) + __shfl(P.csrc, col, kWave);
-      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, goff + dq * 16, soff);
+      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, ((kOpt & kFwdTrim) && !in) ? 0x40000000 : goff + dq * 16, soff);
     }
     wait_vmcnt<0>();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1087,14 +1099,17 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
     auto tap = [&](int iy, int ix, int q) -> uint32_t {
       return lb[iy][ix] + ((q & 1) ? ldq[ix] : 0u) + ((q & 2) ? ldr[iy] : 0u);
     };
+    constexpr bool kRotI = (kOpt & kFwdIlvRot) != 0 && D == 2;
+    f32x4 rr0 = {}, rr1 = {};  // kRotI: the results of steps 0 / 1
     static_for<0, D>([&](auto dd) {
       constexpr int d = decltype(dd)::value;
+      const uint32_t qo = kRotI ? 16u * (uint32_t)((d + lane) & 1) : 0u;  // kRotI: this lane's quad at step d
       auto load = [&](auto hh) {
         constexpr int iy = decltype(hh)::value;
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[iy][ix * 4 + q] = lds_read_b128<16 * d>(tap(iy, ix, q));
+          for (int q = 0; q < 4; ++q) v[iy][ix * 4 + q] = lds_read_b128<kRotI ? 0 : 16 * d>(tap(iy, ix, q) + qo);
       };
       load(std::integral_constant<int, 0>{});
       load(std::integral_constant<int, 1>{});
@@ -1112,13 +1127,31 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
         acc = acc + quad_val(w, &v[1][ix * 4]);
       }
       const f32x4 r4 = acc * 0.25f;  // count 4: / 4 == * 0.25
-      const int Q = D * s + d;
-      const int vo = Q < nquads ? ovoff : 0x40000000;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, vo, (4 * Q) * ostep, kStAux);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, vo, (4 * Q + 1) * ostep, kStAux);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, vo, (4 * Q + 2) * ostep, kStAux);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, vo, (4 * Q + 3) * ostep, kStAux);
+      if constexpr (kRotI) {
+        if constexpr (d == 0) rr0 = r4;
+        else rr1 = r4;
+      } else {
+        const int Q = D * s + d;
+        const int vo = Q < nquads ? ovoff : 0x40000000;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, vo, (4 * Q) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, vo, (4 * Q + 1) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, vo, (4 * Q + 2) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, vo, (4 * Q + 3) * ostep, kStAux);
+      }
     });
+    if constexpr (kRotI) {  // quad q of the stage was computed at step (q - lane) & 1
+      const bool sw = (lane & 1) != 0;  // odd lanes: step 0 read quad 1
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 r4 = (q == 0) != sw ? rr0 : rr1;
+        const int Q = 2 * s + q;
+        const int vo = Q < nquads ? ovoff : 0x40000000;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.x), orr, vo, (4 * Q) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.y), orr, vo, (4 * Q + 1) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.z), orr, vo, (4 * Q + 2) * ostep, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4.w), orr, vo, (4 * Q + 3) * ostep, kStAux);
+      }
+    }
     // this stage's tap reads are complete (lds_wait4<0>) before the next stage's DMA
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1143,7 +1176,7 @@ __device__ __forceinline__ void ilv_body(const PairGeom& G, const PairLane& P, c
 // band_body: one item (RoI k, 16 channels from chunk) after its RoI setup (G, P of
 // pair_setup<16> when kHybrid or kIlv, else pair_setup<64>); P by value: the band path rescales it.
 template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0, int kHybridHi = 0,
-          int kIlv = 0>
+          int kIlv = 0, int kOpt = 0>
 __device__ __forceinline__ void band_body(const RoiCfg& c, float* __restrict__ out, int64_t k, int chunk,
                                           int64_t item, uint32_t sbase, int64_t t_start, int lane, const PairGeom& G,
                                           PairLane P) {
@@ -1152,27 +1185,27 @@ __device__ __forceinline__ void band_body(const RoiCfg& c, float* __restrict__ o
   if constexpr (kHybrid > 0 || kIlv > 0) {
     if constexpr (kHybrid > 0) {
       if (!G.empty && G.R * G.Cs2 <= QuadLayout<kHybrid, kSlabCells * 16>::kCells) {
-        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, kHybrid == 4>(G, P, c, out, k, chunk, item, sbase,
-                                                                              t_start, lane, nullptr);
+        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, kHybrid == 4, kOpt>(G, P, c, out, k, chunk, item,
+                                                                                    sbase, t_start, lane, nullptr);
         return;
       }
     }
     if constexpr ((kIlv & 1) != 0) {  // up to kSlabCells cells: one whole-window stage of [cell][4 quads]
       if (!G.empty && G.R * G.Cs2 <= kSlabCells) {
-        ilv_body<kStAux, kSlabCells, 4, kStamp>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
+        ilv_body<kStAux, kSlabCells, 4, kStamp, kOpt>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
         return;
       }
     }
     if constexpr ((kIlv & 2) != 0) {  // up to 2 * kSlabCells cells: two whole-window stages of [cell][2 quads]
       if (!G.empty && G.R * G.Cs2 <= 2 * kSlabCells) {
-        ilv_body<kStAux, kSlabCells, 2, kStamp>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
+        ilv_body<kStAux, kSlabCells, 2, kStamp, kOpt>(G, P, c, out, k, chunk, sbase, lane, item, t_start);
         return;
       }
     }
     if constexpr (kHybridHi > 0) {  // windows of many bands: the quad kernel's D = 2 / 1 stages instead
       if (!G.empty && G.R * G.Cs2 > kHybridHi) {
-        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, false>(G, P, c, out, k, chunk, item, sbase,
-                                                                       t_start, lane, nullptr);
+        quad_body<kStAux, kStamp, kQuadWave, 0, kSlabCells * 16, false, kOpt>(G, P, c, out, k, chunk, item, sbase,
+                                                                             t_start, lane, nullptr);
         return;
       }
     }
@@ -1222,11 +1255,13 @@ __device__ __forceinline__ void band_body(const RoiCfg& c, float* __restrict__ o
     // stage rows [rs, re): instruction j, lane -> cell 16 j + (lane >> 2) of the band, quad dq
     for (int j = 0; j < nj; ++j) {
       int e = 16 * j + (lane >> 2);
-      e = e < nb ? e : 0;
+      const bool inb = e < nb;
+      e = inb ? e : 0;
       const int r = (int)(((uint32_t)e * inv) >> 16), col = min(e - r * Cs2, Cs - 1);
       const int goff = dense ? ((y0 + rs + r) * sy + (x0 + col) * sx) * 4
                              : __shfl(P.rsrc, rs + r, kWave) + __shfl(P.csrc, col, kWave);
-      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, goff + dq * 16, soff);
+      lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)j, ((kOpt & kFwdTrim) && !inb) ? 0x40000000 : goff + dq * 16,
+                        soff);
     }
     wait_vmcnt<0>();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1343,15 +1378,15 @@ __device__ __forceinline__ void band_body(const RoiCfg& c, float* __restrict__ o
 }
 
 template <int kStAux, bool kStamp, int kSlabCells, int kRot = 1, int kHybrid = 0, int kHybridHi = 0,
-          int kIlv = 0>
+          int kIlv = 0, int kOpt = 0>
 __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, float* __restrict__ out, int64_t k,
                                           int chunk, int64_t item, uint32_t sbase, int64_t t_start, int lane) {
   PairGeom G;
   PairLane P;
   const RoiRaw raw = roi_fetch(c, k);
   pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, G, P);
-  band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, k, chunk, item, sbase, t_start, lane,
-                                                                        G, P);
+  band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv, kOpt>(c, out, k, chunk, item, sbase, t_start,
+                                                                              lane, G, P);
 }
 
 // 1-D grid of 8 * ceil(K * chunks / 8) single-wave workgroups; XCD x takes the x-th eighth of
@@ -1361,14 +1396,14 @@ __device__ __forceinline__ void band_item(const RoiLevels& lv, const RoiCfg& c, 
 // the other on the SAME RoI fetch and setup (the record's first load and pair_setup were ~half of a
 // small item's life); the grid is then 8 * ceil(K * ceil(chunks / 2) / 8).
 template <int kStAux = kCpolNT, bool kStamp = false, int kSlabCells = 208, bool kSpan = false, int kWpe = 3,
-          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0, int kChunks = 1, int kOrder = 1>
+          int kRot = 1, int kHybrid = 0, int kHybridHi = 0, int kIlv = 0, int kChunks = 1, int kOrder = 1, int kOpt = 0>
 __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWpe)))
 roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int64_t t_start = (kStamp || kSpan) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   // whole 1-KB DMA rounds: an LDS-DMA instruction writes 64 lanes x 16 B wherever its last cells
   // fall, so the interleaved and band stages (up to ceil(cells / 32 or / 16) rounds from the
-  // slab start) may write up to 1 KB past kSlabCells * 64 B -- the slab holds that too
-  // (232 cells: 14.5 -> 15 KB, still 10 workgroups per CU by LDS)
+  // slab start) write whole KB; the slab is rounded up to whole KB (the product's 240 cells:
+  // exactly 15 KB, 10 workgroups per CU by LDS)
   __shared__ __attribute__((aligned(16))) float slab[(kSlabCells * 16 + 255) / 256 * 256];
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
   const uint32_t G = (uint32_t)(c.C + kQuadChunk - 1) / (uint32_t)kQuadChunk, K32 = (uint32_t)c.K;
@@ -1385,16 +1420,17 @@ roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     pair_setup<(kHybrid || kIlv) ? 16 : 64>(lv, c, raw, lane, Gm, P);
     const bool two = 2u * p + 1u < G;
     const int64_t item0 = (int64_t)p * 2 * K32 + (two ? 2 * k : k);
-    band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, (int64_t)k, (int)(2u * p), item0,
-                                                                          sbase, t_start, lane, Gm, P);
+    band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv, kOpt>(c, out, (int64_t)k, (int)(2u * p),
+                                                                                item0, sbase, t_start, lane, Gm, P);
     if (two) {
       // the first chunk's tap reads are complete (its evaluation waited on them) before the
       // second chunk's DMA overwrites the slab
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(c, out, (int64_t)k, (int)(2u * p + 1u),
-                                                                            item0 + 1, sbase, t_start, lane, Gm, P);
+      band_body<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv, kOpt>(c, out, (int64_t)k,
+                                                                                  (int)(2u * p + 1u), item0 + 1, sbase,
+                                                                                  t_start, lane, Gm, P);
     }
     if (kSpan && threadIdx.x == 0) record_span(c, t_start);
     return;
@@ -1416,7 +1452,8 @@ roi_align_fwd_band_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     ch0 = (int)(2u * p);
     k0 = (int64_t)r;
   }
-  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv>(lv, c, out, k0, ch0, w, sbase, t_start, lane);
+  band_item<kStAux, kStamp, kSlabCells, kRot, kHybrid, kHybridHi, kIlv, kOpt>(lv, c, out, k0, ch0, w, sbase, t_start,
+                                                                              lane);
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
 

@@ -270,6 +270,46 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
 // device's resident capacity of the kernel (CU count x occupancy: 4 per CU by LDS on a whole
 // MI355X, so 512), else the keys + collect launches.
 
+// Block-wide sums of four ints (all threads get them).  scratch: 4 * nw ints.
+__device__ __forceinline__ int4 block_sum4(int4 v, int* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v.x += __shfl_xor(v.x, o, kWave);
+    v.y += __shfl_xor(v.y, o, kWave);
+    v.z += __shfl_xor(v.z, o, kWave);
+    v.w += __shfl_xor(v.w, o, kWave);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane_id() == 0) scratch[4 * w] = v.x, scratch[4 * w + 1] = v.y, scratch[4 * w + 2] = v.z, scratch[4 * w + 3] = v.w;
+  __syncthreads();
+  int4 t = make_int4(0, 0, 0, 0);
+  for (int i = 0; i < nw; ++i) t.x += scratch[4 * i], t.y += scratch[4 * i + 1], t.z += scratch[4 * i + 2], t.w += scratch[4 * i + 3];
+  __syncthreads();
+  return t;
+}
+
+// This thread's first (selection, candidate) slots in list 0 (.x, .y) and list 1 (.z, .w): the
+// workgroup's bases plus the exclusive prefix of the counts in thread order (per workgroup each
+// count < 65536: packed pairs, one scan per list).  Block-uniform call; part: 2 * nw ints.
+__device__ __forceinline__ int4 block_offsets4(int nsel0, int ncand0, int nsel1, int ncand1, int4 base, int* part) {
+  const int t = threadIdx.x, w = t / kWave, nw = (int)blockDim.x / kWave;
+  __syncthreads();  // part free
+  const int a = nsel0 | (ncand0 << 16), b = nsel1 | (ncand1 << 16);
+  int ia = a, ib = b;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+    if (lane_id() >= o) ia += xa, ib += xb;
+  }
+  if (lane_id() == kWave - 1) part[w] = ia, part[nw + w] = ib;
+  __syncthreads();
+  int pa = 0, pb = 0;
+  for (int i = 0; i < w; ++i) pa += part[i], pb += part[nw + i];
+  __syncthreads();  // part reused after
+  const int ea = pa + ia - a, eb = pb + ib - b;
+  return make_int4(base.x + (ea & 0xffff), base.y + (ea >> 16), base.z + (eb & 0xffff), base.w + (eb >> 16));
+}
+
 struct SampFused {
   uint32_t* part_hist;   // [S][2][nchunk][kSampBins] per-chunk histograms (sc1 stores, every call)
   int32_t* part_count;   // [S][2][nchunk] per-chunk class counts
@@ -357,9 +397,10 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   stamp(3);
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
-  // the count loads (threads < G) and the first 2 x 32 chunk-histogram loads are issued together
-  int sp0 = 0, sn0 = 0;
-  uint32_t hp = 0u, hn = 0u;
+  // the count loads (threads < G) and the first 2 x 32 chunk-histogram loads are issued together;
+  // the sums over the chunks BEFORE this one (_lt) give this workgroup's list slots (phase 3)
+  int sp0 = 0, sn0 = 0, sp_lt = 0, sn_lt = 0;
+  uint32_t hp = 0u, hn = 0u, hp_lt = 0u, hn_lt = 0u;
   for (int c0 = 0; c0 < G; c0 += 32) {
     uint32_t a[32], b[32];
     const int cc = c0 + t;
@@ -370,8 +411,12 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
       b[c] = c0 + c < G ? xwg_load(ph + ((int64_t)f.nchunk + c0 + c) * kSampBins + t) : 0u;
     }
     sp0 += cpv, sn0 += cnv;
+    if (cc < x) sp_lt += cpv, sn_lt += cnv;
 #pragma unroll
-    for (int c = 0; c < 32; ++c) hp += a[c], hn += b[c];
+    for (int c = 0; c < 32; ++c) {
+      hp += a[c], hn += b[c];
+      if (c0 + c < x) hp_lt += a[c], hn_lt += b[c];
+    }
   }
   const int npos = block_sum(sp0, sm.part), nneg = block_sum(sn0, sm.part);
   hc[t] = hp;
@@ -396,9 +441,23 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     take |= (live && (all || pre > P)) ? 1u << r : 0u;
     tie |= (live && !all && pre == P) ? 1u << r : 0u;
   }
-  // both classes' (selection, candidate) slots in one round trip
-  const int4 sl4 = block_reserve4(__popc(take & posm), __popc(tie & posm), __popc(take & negm), __popc(tie & negm),
-                                  st + TK_OUT, st + TK_WORDS + TK_OUT, sm.part, sm.res4);
+  // both classes' (selection, candidate) slots without atomics: the chunks before this one take
+  // their class count (plan `all`), or their keys in bins above P (and list their bin-P keys as
+  // ties) -- sums of the phase-2 loads over t > P / t == P -- then this workgroup's own keys in
+  // thread order.  (One contended atomic per workgroup on the image's counters, 38 workgroups
+  // on one word at cfg2, cost more than these block sums.)  The lists come out in box order.
+  int4 lbase;
+  {
+    const bool lp = pl[0].kv > 0, ln = pl[1].kv > 0;
+    const int P0 = (int)pl[0].P, P1 = (int)pl[1].P;
+    lbase = block_sum4(make_int4(!lp ? 0 : pl[0].all ? sp_lt : (t > P0 ? (int)hp_lt : 0),
+                                (lp && !pl[0].all && t == P0) ? (int)hp_lt : 0,
+                                !ln ? 0 : pl[1].all ? sn_lt : (t > P1 ? (int)hn_lt : 0),
+                                (ln && !pl[1].all && t == P1) ? (int)hn_lt : 0),
+                      sm.fb.wave_tot);
+  }
+  const int4 sl4 = block_offsets4(__popc(take & posm), __popc(tie & posm), __popc(take & negm), __popc(tie & negm),
+                                  lbase, sm.part);
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const uint32_t m = c ? negm : posm;
@@ -439,7 +498,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
       const int k2 = pl[c].k2, nabove = kv - k2;
       int32_t* sl = f.sel ? f.sel + (int64_t)v * f.sel_ld : nullptr;
       const uint64_t* cl = f.cand + (int64_t)v * f.ld;
-      const int ncand = xwg_load(st + c * TK_WORDS + TK_CAND);
+      const int ncand = (int)hc[c * kSampBins + (int)pl[c].P];  // every key of the class in bin P
       if (ncand <= kTkCandCap) {
         // the k2 largest (key, ~box) of the prefix ties by radix passes over the key's
         // next bits (its top kSampHistBits are the plan's prefix): no sort

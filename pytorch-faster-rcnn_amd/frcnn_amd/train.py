@@ -40,29 +40,37 @@ class DetectorLoss(nn.Module):
 
 
 def build_optimizer(params, cfg):
-    """The reference's optimizer dict (type SGD) -> torch optimizer."""
+    """The reference's optimizer dict (type SGD) -> torch optimizer.  HIP parameters take the
+    fused SGD kernel (one launch; it also honours a device `found_inf` flag, which TrainStep uses
+    to skip a failed step's update without a host sync)."""
     cfg = dict(cfg or dict(type='SGD', lr=0.0025, momentum=0.9, weight_decay=0.0001))
     kind = cfg.pop('type')
     if kind != 'SGD':
         raise ValueError('unsupported optimizer type {}'.format(kind))
+    params = list(params)
+    if params and all(p.is_cuda for p in params):
+        cfg.setdefault('fused', True)
     return torch.optim.SGD(params, **cfg)
 
 
 class TrainStep:
     """Callable training iteration on this rank's batch; returns the (detached) local loss.
 
-    The device status word (include/frcnn_amd.h FRH_DEVERR_*) is read every step, after
-    backward and before the optimizer update -- one 4-byte read where the reference's loop
-    reads every loss with `.item()` (`lib/trainer/trainer.py:110-119`) -- so a step whose
-    in-launch wait ran out raises before its update is applied (its losses are NaN already:
-    the loss kernels take the word).  `status_every=k` reads it every k-th step instead;
-    0 never (then a failed step's update lands, only its NaN losses carry the failure).
+    Device status word (include/frcnn_amd.h FRH_DEVERR_*), with no host synchronisation:
+      * the loss kernels read it, so a step whose in-launch wait ran out returns NaN losses
+        (the reference's loop reads every loss each iteration, `lib/trainer/trainer.py:110-119`);
+      * the fused SGD step takes `found_inf` = (word != 0), so that step's update is skipped on
+        the device (momentum buffers are zero-initialised, so even a skipped first step leaves
+        them defined);
+      * the word is copied to pinned host memory after each step and the NEXT call raises
+        (ops.check_device_status) once that copy has landed -- a finished event query, not a wait.
+    `status_every=k` adds a synchronous check every k-th step before the update (0: never).
 
-    `force_ddp` wraps the detector in DistributedDataParallel even at world size 1 (the
-    RCCL readiness check on a one-GPU box: the bucketed all-reduce runs, over one rank)."""
+    `force_ddp` wraps the detector in DistributedDataParallel even at world size 1 (the RCCL
+    readiness check on a one-GPU box: the bucketed all-reduce runs, over one rank)."""
 
     def __init__(self, detector, optimizer_cfg=None, grad_clip=None, world_size=1, device=None,
-                 bucket_mb=DEFAULT_BUCKET_MB, status_every=1, force_ddp=False):
+                 bucket_mb=DEFAULT_BUCKET_MB, status_every=0, force_ddp=False):
         self.detector = detector
         self.params = [p for p in detector.parameters() if p.requires_grad]
         if device is None and self.params:
@@ -78,8 +86,29 @@ class TrainStep:
         self.net = net
         self.optimizer = build_optimizer(self.params, optimizer_cfg)
         self.grad_clip = dict(grad_clip) if grad_clip else None
+        self._hip = self.device is not None and self.device.type == 'cuda'
+        self._guard = self._hip and all(g.get('fused') for g in self.optimizer.param_groups)
+        if self._guard:
+            for g in self.optimizer.param_groups:
+                if g.get('momentum', 0) != 0:
+                    for p in g['params']:
+                        self.optimizer.state[p]['momentum_buffer'] = torch.zeros_like(p)
+            self._found = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self.optimizer.found_inf = self._found
+        self._host_status = torch.zeros(1, dtype=torch.int32).pin_memory() if self._hip else None
+        self._status_event = None
+
+    def _lagged_check(self):
+        """Raise if the previous step's status copy has landed and is nonzero (no wait)."""
+        ev = self._status_event
+        if ev is not None and ev.query():
+            self._status_event = None
+            if int(self._host_status[0]):
+                ops.check_device_status(self.device)  # the word is still set: raises, clears it
 
     def __call__(self, img, gt_bboxes, gt_labels, img_metas):
+        if self._hip:
+            self._lagged_check()
         self.optimizer.zero_grad(set_to_none=True)
         loss = self.net(img, gt_bboxes, gt_labels, img_metas)
         loss.backward()
@@ -87,8 +116,13 @@ class TrainStep:
             nn.utils.clip_grad_norm_(self.params, self.grad_clip['max_norm'],
                                      self.grad_clip.get('norm_type', 2))
         self.steps += 1
-        if self.status_every and self.steps % self.status_every == 0 and self.device is not None and \
-                self.device.type == 'cuda':
-            ops.check_device_status(self.device)  # raises before a failed step's update
+        if self.status_every and self.steps % self.status_every == 0 and self._hip:
+            ops.check_device_status(self.device)  # synchronous: raises before a failed step's update
+        if self._guard:
+            self._found.copy_(ops.status_word(self.device).ne(0))  # device-side: no sync
         self.optimizer.step()
+        if self._hip:
+            self._host_status.copy_(ops.status_word(self.device), non_blocking=True)
+            self._status_event = torch.cuda.Event()
+            self._status_event.record()
         return loss.detach()

@@ -72,7 +72,9 @@ def _reference_step(model, cfg, batch, world, seed):
     off = 0
     for p in params:
         n = p.numel()
-        p.grad = flat[off:off + n].view_as(p).to(p.device)
+        # the averaged gradient in the parameter's own layout (channels-last conv weights keep
+        # their strides: the gradient layout contract, which the fused SGD step requires)
+        p.grad = torch.empty_like(p).copy_(flat[off:off + n].view(p.shape))
         off += n
     clip = cfg.optimizer_config.get('grad_clip')
     if clip:

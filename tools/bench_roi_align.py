@@ -63,6 +63,9 @@ def stamps_report(stm):
     pc = lambda a: np.percentile(a / 100.0, [50, 90, 99]).round(2).tolist()  # noqa: E731
     for D in sorted(set(stm[:, 4].tolist())):
         x = stm[stm[:, 4] == D]
+        if D < 0:  # the interleaved path (ilv_body) records only start and end: its phases are not stamped
+            print('  D={} waves {:5d}: (phases not stamped) life {}'.format(D, len(x), pc(x[:, 3] - x[:, 0])))
+            continue
         print('  D={} waves {:5d}: fetch {} taps {} land {} eval+rest {} life {}'.format(
             D, len(x), pc(x[:, 6] - x[:, 0]), pc(x[:, 1] - x[:, 6]), pc(x[:, 2] - x[:, 1]), pc(x[:, 3] - x[:, 2]),
             pc(x[:, 3] - x[:, 0])))

@@ -31,7 +31,22 @@ def main():
         rois, levels, shapes, scales, feats = s
         K, C = rois.shape[0], shapes[0][1]
         cells = tap_cells(rois, levels, shapes, scales)
-        orders = {'own': np.arange(K), 'desc': np.argsort(-cells, kind='stable'), 'asc': np.argsort(cells, kind='stable')}
+        r5 = rois.cpu().numpy()
+        lvn = levels.cpu().numpy()
+        sc_l = np.array(scales, np.float64)[lvn]
+        cy = ((r5[:, 2] + r5[:, 4]) * 0.5 * sc_l).astype(np.int64)
+        cx = ((r5[:, 1] + r5[:, 3]) * 0.5 * sc_l).astype(np.int64)
+
+        def morton(y, x):
+            z = np.zeros_like(y)
+            for b in range(10):
+                z |= ((y >> b) & 1) << (2 * b + 1) | ((x >> b) & 1) << (2 * b)
+            return z
+        img = r5[:, 0].astype(np.int64)
+        orders = {'own': np.arange(K), 'desc': np.argsort(-cells, kind='stable'), 'asc': np.argsort(cells, kind='stable'),
+                  'img_level': np.lexsort((np.arange(K), lvn, img)),
+                  'morton': np.lexsort((morton(cy // 2, cx // 2), lvn, img)),
+                  'raster8': np.lexsort((cx, cy // 8, lvn, img))}
         hw, st = ops._feat_desc(feats)
         sc = _lib.f32_array(scales)
         fp = _lib.ptr_array(feats)

@@ -36,7 +36,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL((roi_align_fwd_quadp_kernel<kCpolNT>), gq, dim3(kWave), 0, st, lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
-  if (variant >= 28 && variant <= 62) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
+  if (variant >= 28 && variant <= 70) {  // band kernel: 28 product (208 cells), 29 stamped, 30 176 cells,
                                          // 31 256 cells, 32 208 cells at 4 waves per SIMD
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, 160),
@@ -139,6 +139,15 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (variant == 62)  // the product's paths on a 240-cell slab (15 KB: the same LDS as the declared 232-cell one)
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2>), gq, dim3(kWave),
                          0, st, lv, c, out);
+    else if (variant == 63)  // round 6: the product + kFwdTrim (no loads for lanes past the window, no empty rounds)
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1, kFwdTrim>), gq,
+                         dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 64)  // round 6: the product + the interleaved path's quad rotation
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1, kFwdIlvRot>), gq,
+                         dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 65)  // round 6: trim + rotation
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1,
+                                                    kFwdTrim | kFwdIlvRot>), gq, dim3(kWave), 0, st, lv, c, out);
     else  // 45: hybrid (D = 4), 232-cell slab, stamped
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, true, 232, false, 3, 0, 4>), gq, dim3(kWave), 0, st,
                          lv, c, out);
