@@ -772,8 +772,17 @@ def main():
         # passes over `bench.py` and `bench.py --mode train`)
         pmc = os.path.join(REPO, 'profiles', 'roi_align_pmc.json' if args.mode == 'fwd' else
                            'roi_align_pmc_train.json')
+        traffic_note = None
         if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+            pj = json.load(open(pmc))
+            names = [kernel_short(n) for n in pj.get('kernel_names', [])]
+            if roi_kernel and roi_kernel in names:
+                traffic = pj.get('hbm_bytes_per_launch')
+                traffic_note = 'PMC of this same kernel instantiation, {} ({})'.format(
+                    os.path.relpath(pmc, REPO), pj.get('measured'))
+            else:  # the profile is of another kernel (or the trace gave no name): stale, not reported
+                traffic_note = 'stale: {} profiles {} but this run dispatched {}'.format(
+                    os.path.relpath(pmc, REPO), names or pj.get('kernel'), roi_kernel)
 
         imgs_total = world * args.batch * args.steps
         out = {
@@ -831,7 +840,8 @@ def main():
                            'replay_cold = '
                            'each launch after a 768 MB read (L2 + Infinity Cache evicted)'.format(steps_traced)) +
                           '; traffic = PMC FETCH_SIZE (x2 calibrated) + WRITE_SIZE per launch, '
-                          'profiles/roi_align_pmc.json'}
+                          'profiles/roi_align_pmc.json',
+                'traffic_source': traffic_note}
             out['roofline_voc_rois'] = roi_set_line(recs[-1], 'cfg2_rois_voc.npz', dev)
             out['roofline_train_rois'] = roi_set_line(recs[-1], 'cfg2_rois_train.npz', dev)
         else:

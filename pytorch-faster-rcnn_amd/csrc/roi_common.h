@@ -24,6 +24,8 @@ struct RoiCfg {
   unsigned long long* span;  // measurement builds (kSpan): {min wave start, max wave end}, s_memrealtime
   const uint32_t* fix_max;   // fixed-point backward: bits of max|grad_out| (the call's own pass)
   int fix_hb;                // fixed-point backward: ceil(log2(K * ph * pw)), accumulation headroom
+  const int32_t* rec;        // forward, kFwdSorted: RoI records in processing order, 8 words each:
+                             // (x5 as written, level, original index, 0) -- roi_sort_kernel
 };
 
 // kSpan kernels: the launch's span on the 100 MHz clock, first wave start to last wave end.
@@ -129,6 +131,24 @@ __device__ __forceinline__ RoiRaw roi_fetch(const RoiCfg& c, int64_t k) {
       : "s"(c.rois + k * 5), "s"(roi_level_ptr(c, k))
       : "memory");
   return roi_raw(c, q, r4, l);
+}
+
+// record j of c.rec (kFwdSorted): the RoI and, in *ko, the output row it belongs to
+typedef uint32_t roi_u32x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ RoiRaw roi_fetch_rec(const RoiCfg& c, int64_t j, int64_t* ko) {
+  roi_u32x8_t q;
+  const uint64_t a = reinterpret_cast<uint64_t>(c.rec + j * 8);  // wave-uniform: made scalar
+  const uint64_t as = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  asm volatile(
+      "s_load_dwordx8 %0, %1, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=s"(q)
+      : "s"(reinterpret_cast<const int32_t*>(as))
+      : "memory");
+  *ko = (int64_t)q[6];
+  return RoiRaw{__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), __uint_as_float(q[3]),
+                __uint_as_float(q[4]), (int)q[5]};
 }
 
 __device__ __forceinline__ void roi_fetch2(const RoiCfg& c, int64_t k0, int64_t k1, RoiRaw* a, RoiRaw* b) {

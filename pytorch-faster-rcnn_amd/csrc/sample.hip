@@ -257,18 +257,20 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_collect_kernel(cons
 //      their top 8 bits and the class counts, stored per chunk;         barrier
 //   2. every workgroup sums the image's chunk counts and histograms: kp, kn
 //      (region.py:43-57) and both two-level plans (tk_plan_direct);
-//   3. its boxes above each plan's prefix are taken: output label and list slot
-//      (one reservation per class); its prefix ties go to the class's candidate
-//      list; every other box gets label -1;                              barrier
+//   3. its boxes above each plan's prefix are taken: output label and list slot (round 6:
+//      slots from the phase-2 loads -- what the chunks before it take, a block sum, plus its
+//      own prefix in thread order; no atomics, lists in box order); its prefix ties go to
+//      the class's candidate list (slots likewise); every other box gets label -1;  barrier
 //      (only when a class has ties)
-//   4. workgroup 0 orders each class's ties by (key desc, box asc) and takes the
-//      first k2 (labels of all tied boxes, list slots of the taken ones);
+//   4. workgroup 0 (positives) / 1 (negatives) orders the class's ties by (key desc, box
+//      asc) and takes the first k2 (labels of all tied boxes, list slots of the taken ones);
 // then the last workgroup to leave zeroes the image's state words, which is the
 // workspace contract (frh_sample_zero_bytes: zero before, zero after).
 // The selected set is exactly the two-launch path's.
 // The grid's live workgroups must be resident together: the host admits at most half the
-// device's resident capacity of the kernel (CU count x occupancy: 4 per CU by LDS on a whole
-// MI355X, so 512), else the keys + collect launches.
+// device's resident capacity of the kernel (CU count x occupancy, queried per device: 2 per CU
+// by registers on a whole MI355X since round 6's 48-chunk batches, so 256 admitted), else the
+// keys + collect launches.
 
 // Block-wide sums of four ints (all threads get them).  scratch: 4 * nw ints.
 __device__ __forceinline__ int4 block_sum4(int4 v, int* scratch) {
@@ -309,6 +311,8 @@ __device__ __forceinline__ int4 block_offsets4(int nsel0, int ncand0, int nsel1,
   const int ea = pa + ia - a, eb = pb + ib - b;
   return make_int4(base.x + (ea & 0xffff), base.y + (ea >> 16), base.z + (eb & 0xffff), base.w + (eb >> 16));
 }
+
+constexpr int kSampBatch = 48;  // chunk histograms per thread and class in flight (phase 2)
 
 struct SampFused {
   uint32_t* part_hist;   // [S][2][nchunk][kSampBins] per-chunk histograms (sc1 stores, every call)
@@ -397,23 +401,24 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   stamp(3);
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
-  // the count loads (threads < G) and the first 2 x 32 chunk-histogram loads are issued together;
+  // the count loads (threads < G) and the first 2 x kSampBatch chunk-histogram loads are issued
+  // together (48: one round trip for the cfg2 RPN's 38 chunks per image);
   // the sums over the chunks BEFORE this one (_lt) give this workgroup's list slots (phase 3)
   int sp0 = 0, sn0 = 0, sp_lt = 0, sn_lt = 0;
   uint32_t hp = 0u, hn = 0u, hp_lt = 0u, hn_lt = 0u;
-  for (int c0 = 0; c0 < G; c0 += 32) {
-    uint32_t a[32], b[32];
+  for (int c0 = 0; c0 < G; c0 += kSampBatch) {
+    uint32_t a[kSampBatch], b[kSampBatch];
     const int cc = c0 + t;
-    const int32_t cpv = cc < G && t < 32 ? xwg_load(pc + cc) : 0, cnv = cc < G && t < 32 ? xwg_load(pc + f.nchunk + cc) : 0;
+    const int32_t cpv = cc < G && t < kSampBatch ? xwg_load(pc + cc) : 0, cnv = cc < G && t < kSampBatch ? xwg_load(pc + f.nchunk + cc) : 0;
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
+    for (int c = 0; c < kSampBatch; ++c) {
       a[c] = c0 + c < G ? xwg_load(ph + (int64_t)(c0 + c) * kSampBins + t) : 0u;
       b[c] = c0 + c < G ? xwg_load(ph + ((int64_t)f.nchunk + c0 + c) * kSampBins + t) : 0u;
     }
     sp0 += cpv, sn0 += cnv;
     if (cc < x) sp_lt += cpv, sn_lt += cnv;
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
+    for (int c = 0; c < kSampBatch; ++c) {
       hp += a[c], hn += b[c];
       if (c0 + c < x) hp_lt += a[c], hn_lt += b[c];
     }

@@ -27,6 +27,8 @@ def main():
     ap.add_argument('--sets', default='bench,voc,train')
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--json')
+    ap.add_argument('--variants', default='', help='tools backward variants (frh_roi_align_bwd_variant) beside the '
+                    'product: 0 nhwc float, 1 register-resident float, 2 nhwc fixed, 3 register-resident fixed')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     out = {}
@@ -55,8 +57,27 @@ def main():
             _lib.call('frh_roi_align_bwd_fixed', len(grads), _lib.ptr_array(grads), _lib.ptr_array(accs), hw, st, sc,
                       B, C, _lib.ptr(r), _lib.ptr(lv), K, 7, 7, 2, 0, _lib.ptr(gg), _lib.ptr(word), _lib.stream_of(gg))
             return grads
+        fns = [('atomic', atomic), ('fixed', fixed)]
+        tools = None
+        for v in [int(x) for x in args.variants.split(',') if x]:
+            if tools is None:
+                import toolslib
+                tools = toolslib.load()
+
+            def var(v=v):
+                grads = [torch.zeros_like(f) if v < 2 else torch.empty_like(f) for f in feats]
+                accs = [torch.empty(f.shape, dtype=torch.int64, device=dev, memory_format=torch.channels_last).zero_()
+                        for f in feats] if v >= 2 else grads
+                rc = tools.frh_roi_align_bwd_variant(v, len(grads), _lib.ptr_array(grads), _lib.ptr_array(accs), hw, st,
+                                                     sc, B, C, _lib.ptr(rois), _lib.ptr(levels), K, _lib.ptr(g),
+                                                     _lib.ptr(word), _lib.stream_of(g))
+                assert rc == 0, tools.frh_last_error()
+                return grads
+            fns.append(('v{}'.format(v), var))
         res = {}
-        for nm, fn in (('atomic', atomic), ('fixed', fixed)):
+        outs = {}
+        for nm, fn in fns:
+            outs[nm] = fn()
             for _ in range(2):
                 fn()
             torch.cuda.synchronize()
@@ -74,7 +95,14 @@ def main():
         diff = max(float((x - y).abs().max()) for x, y in zip(a, at))
         used = torch.unique(rois[:, 0].long() * 64 + levels).cpu().tolist()
         nbytes = 4 * C * (K * 49 + 2 * sum(shapes[u % 64][2] * shapes[u % 64][3] for u in used))
+        for nm in res:
+            if nm.startswith('v'):
+                ref = outs['fixed' if int(nm[1:]) >= 2 else 'atomic']
+                d = max(float((x - y).abs().max()) for x, y in zip(outs[nm], ref))
+                print('  {}: {:.1f} us, max |diff| to the product form {:.3g}{}'.format(
+                    nm, res[nm], d, ' (bit-identical)' if d == 0 else ''), flush=True)
         out[name] = {'atomic_us': res['atomic'], 'fixed_us': res['fixed'], 'fixed_bit_identical_permuted': same,
+                     'variants_us': {k: v for k, v in res.items() if k.startswith('v')},
                      'max_abs_diff_fixed_vs_atomic': diff, 'algorithmic_bytes': nbytes}
         print('set {}: atomic {:.1f} us, deterministic {:.1f} us; deterministic bit-identical under a RoI '
               'permutation: {}; max |fixed - atomic| {:.3g}'.format(name, res['atomic'], res['fixed'], same, diff),

@@ -13,6 +13,12 @@ extern "C" {
 /* variant 0: frh_roi_align_fwd_strided's pair kernel; 1: the same with per-item stamps (8
  * int64 per item after the output).  Arguments as frh_roi_align_fwd_strided, plus a
  * workspace of frh_roi_align_workspace bytes (unused by these two). */
+/* round-6 backward A/B: 0 nhwc float, 1 register-resident float, 2 / 3 the same in fixed point */
+int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels, float* const* grad_feats,
+                                  int64_t* const* acc_feats, const int32_t* feat_hw, const int64_t* strides,
+                                  const float* scales, int32_t batch, int32_t channels, const float* rois,
+                                  const int64_t* roi_levels, int64_t num_rois, const float* grad_out,
+                                  uint32_t* scale_word, void* stream);
 int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels, const float* const* feats,
                                   const int32_t* feat_hw, const int64_t* strides, const float* scales,
                                   int32_t batch, int32_t channels, const float* rois, const int64_t* roi_levels,

@@ -145,6 +145,21 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
     else if (variant == 64)  // round 6: the product + the interleaved path's quad rotation
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1, kFwdIlvRot>), gq,
                          dim3(kWave), 0, st, lv, c, out);
+    else if (variant == 66) {  // round 6: the product (trim + rotation) on spatially sorted RoI records
+      FRH_REQUIRE(workspace && ws_bytes >= (size_t)num_rois * 32, "workspace too small");
+      RoiCfg cs = c;
+      cs.rec = reinterpret_cast<const int32_t*>(workspace);
+      hipLaunchKernelGGL(roi_sort_kernel, dim3(1), dim3(kSortThreads), 0, st, lv, c,
+                         reinterpret_cast<int32_t*>(workspace));
+      hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1,
+                                                    kFwdTrim | kFwdIlvRot | kFwdSorted>), gq, dim3(kWave), 0, st, lv,
+                         cs, out);
+    }
+    else if (variant == 67) {  // the sort kernel alone (its cost in the variant-66 sum)
+      FRH_REQUIRE(workspace && ws_bytes >= (size_t)num_rois * 32, "workspace too small");
+      hipLaunchKernelGGL(roi_sort_kernel, dim3(1), dim3(kSortThreads), 0, st, lv, c,
+                         reinterpret_cast<int32_t*>(workspace));
+    }
     else if (variant == 65)  // round 6: trim + rotation
       hipLaunchKernelGGL((roi_align_fwd_band_kernel<kCpolNT, false, 240, false, 3, 3, 4, 0, 2, 1, 1,
                                                     kFwdTrim | kFwdIlvRot>), gq, dim3(kWave), 0, st, lv, c, out);
@@ -249,4 +264,53 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   else
     FRH_REQUIRE(false, "roi_align variant %d unknown", variant);
   return check_launch("frh_roi_align_fwd_variant");
+}
+
+// Round-6 backward A/B (channels-last gradients, sampling 2, 7 x 7 bins): 0 = the product's
+// roi_align_bwd_nhwc_kernel (float atomics), 1 = roi_align_bwd_nhwc_reg_kernel (grad_out in
+// registers, float atomics), 2 / 3 = the same two in fixed point (absmax pass + conversion, as
+// frh_roi_align_bwd_fixed; accs zeroed by the caller).  grads zeroed by the caller for 0 / 1.
+extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels, float* const* grad_feats,
+                                             int64_t* const* acc_feats, const int32_t* feat_hw, const int64_t* strides,
+                                             const float* scales, int32_t batch, int32_t channels, const float* rois,
+                                             const int64_t* roi_levels, int64_t num_rois, const float* grad_out,
+                                             uint32_t* scale_word, void* stream) {
+  int32_t r = roi_common_checks(batch, channels, num_rois, 7, 7, rois);
+  if (r) return r;
+  const bool fixed = variant >= 2;
+  RoiLevels lv;
+  r = make_levels(num_levels, nullptr, fixed ? reinterpret_cast<float* const*>(acc_feats) : grad_feats, feat_hw,
+                  strides, scales, &lv);
+  if (r) return r;
+  for (int l = 0; l < lv.L; ++l) FRH_REQUIRE(lv.sc[l] == 1, "channels-last gradients only");
+  hipStream_t st = as_stream(stream);
+  int hb = 0;
+  while (hb < 62 && (int64_t(1) << hb) < num_rois * 49) ++hb;
+  RoiCfg c{rois, roi_levels, num_rois, channels, 7, 7, 2, 0, nullptr, scale_word, hb};
+  const dim3 grid((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave));
+  if (fixed) {
+    FRH_HIP(hipMemsetAsync(scale_word, 0, 4, st));
+    const int64_t ng = num_rois * channels * 49;
+    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)std::min<int64_t>((ng / 4 + 255) / 256 + 1, 2048)),
+                       dim3(256), 0, st, grad_out, ng, scale_word);
+  }
+  if (variant == 0)
+    hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<false>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 1)
+    hipLaunchKernelGGL(roi_align_bwd_nhwc_reg_kernel<false>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 2)
+    hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 3)
+    hipLaunchKernelGGL(roi_align_bwd_nhwc_reg_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else
+    FRH_REQUIRE(false, "backward variant %d unknown", variant);
+  if (fixed) {
+    for (int l = 0; l < lv.L; ++l) {
+      const int64_t n = (int64_t)batch * channels * lv.h[l] * lv.w[l];
+      hipLaunchKernelGGL(roi_bwd_fixed_to_f32_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
+                         dim3(256), 0, st, reinterpret_cast<const long long*>(acc_feats[l]), grad_feats[l], n,
+                         scale_word, hb);
+    }
+  }
+  return check_launch("frh_roi_align_bwd_variant");
 }

@@ -259,4 +259,68 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2)))
   }
 }
 
+// ---------------------------------------------------------------------------
+// Processing order for the forward (kFwdSorted): the RoIs' records grouped by (image, level,
+// 8 x 8-cell tile of the RoI centre, tiles row-major), so the waves a XCD runs together stage
+// overlapping windows while they are still in its L2.  One 1024-thread workgroup: a counting sort
+// over at most kSortBins bins (more tiles fold modulo kSortBins: still grouped), records written
+// 8 words each (the RoI's 5 words as given, its level, its index, 0).  Order inside a bin is
+// arbitrary: every output row is its own RoI's, whatever the order.
+constexpr int kSortThreads = 1024, kSortBins = 4096, kSortTile = 8;
+__device__ __forceinline__ int roi_sort_bin(const RoiLevels& lv, const RoiCfg& c, int64_t k) {
+  const float* r = c.rois + k * 5;
+  const int b = (int)r[0];
+  const int l = c.levels ? (int)c.levels[k] : 0;
+  int tb = 0, T = 0;
+  for (int i = 0; i < lv.L; ++i) {
+    const int n = ((lv.h[i] + kSortTile - 1) / kSortTile) * ((lv.w[i] + kSortTile - 1) / kSortTile);
+    tb += i < l ? n : 0;
+    T += n;
+  }
+  const int th = (lv.h[l] + kSortTile - 1) / kSortTile, tw = (lv.w[l] + kSortTile - 1) / kSortTile;
+  const float sc = lv.scale[l];
+  const int ty = min(max((int)(0.5f * (r[2] + r[4]) * sc) / kSortTile, 0), th - 1);
+  const int tx = min(max((int)(0.5f * (r[1] + r[3]) * sc) / kSortTile, 0), tw - 1);
+  return (int)(((int64_t)max(b, 0) * T + tb + ty * tw + tx) % kSortBins);
+}
+
+static __global__ void __launch_bounds__(kSortThreads) roi_sort_kernel(RoiLevels lv, RoiCfg c, int32_t* rec) {
+  __shared__ uint32_t h[kSortBins];
+  __shared__ uint32_t part[kSortThreads / kWave];
+  const int t = threadIdx.x;
+  for (int i = t; i < kSortBins; i += kSortThreads) h[i] = 0u;
+  __syncthreads();
+  for (int64_t k = t; k < c.K; k += kSortThreads) atomicAdd(&h[roi_sort_bin(lv, c, k)], 1u);
+  __syncthreads();
+  // exclusive scan of the bins: thread t owns bins 4t .. 4t + 3
+  constexpr int kPer = kSortBins / kSortThreads;
+  uint32_t v[kPer], sum = 0u;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) sum += (v[i] = h[kPer * t + i]);
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o, kWave);
+    if (lane_id() >= o) incl += x;
+  }
+  if (lane_id() == kWave - 1) part[t / kWave] = incl;
+  __syncthreads();
+  uint32_t pre = 0u;
+  for (int i = 0; i < t / kWave; ++i) pre += part[i];
+  uint32_t run = pre + incl - sum;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    h[kPer * t + i] = run;
+    run += v[i];
+  }
+  __syncthreads();
+  for (int64_t k = t; k < c.K; k += kSortThreads) {
+    const uint32_t pos = atomicAdd(&h[roi_sort_bin(lv, c, k)], 1u);
+    const int32_t* r = reinterpret_cast<const int32_t*>(c.rois + k * 5);
+    int4* o = reinterpret_cast<int4*>(rec + (int64_t)pos * 8);
+    o[0] = make_int4(r[0], r[1], r[2], r[3]);
+    o[1] = make_int4(r[4], c.levels ? (int)c.levels[k] : 0, (int)k, 0);
+  }
+}
+
 }  // namespace frh

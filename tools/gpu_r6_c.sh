@@ -20,7 +20,7 @@ for k,v in s['timeline_one_launch'].items(): print('  ', k, v['rel_launch_us_med
 "
 run 300 python -u tools/bench_roi_order.py --sets bench,voc,train --rounds 5 > $OUT/roi_order.log 2>&1 || { tail -20 $OUT/roi_order.log; exit 1; }
 grep -v amdgpu.ids $OUT/roi_order.log
-run 300 python -u tools/bench_roi_sets.py --sets bench,voc,train --variants 62 --rounds 7 --json $OUT/roi_sets.json > $OUT/roi_sets.log 2>&1 || { tail -20 $OUT/roi_sets.log; exit 1; }
+run 300 python -u tools/bench_roi_sets.py --sets bench,voc,train --variants 62,66,67 --rounds 7 --json $OUT/roi_sets.json > $OUT/roi_sets.log 2>&1 || { tail -20 $OUT/roi_sets.log; exit 1; }
 grep -v amdgpu.ids $OUT/roi_sets.log
 for se in 0 1 0; do
   run 300 python bench.py --mode train --status-every $se --steps 20 --warmup 3 --trace-steps 0 --no-cpu-baseline >> $OUT/train_status.jsonl 2> $OUT/train_status.err || { tail -20 $OUT/train_status.err; exit 1; }

@@ -38,8 +38,13 @@ def main():
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
     fkb, nf = per_launch(a.fetch, 'FETCH_SIZE', a.kernel)
+    # the full dispatched name (template arguments included): bench.py uses this figure only
+    # while the kernel it dispatches is this same instantiation
+    names = sorted({r['Kernel_Name'] for r in counter_rows(a.fetch, 'FETCH_SIZE') if a.kernel in r['Kernel_Name']})
     wkb, nw = per_launch(a.write, 'WRITE_SIZE', a.kernel)
-    res = {'kernel': a.kernel, 'fetch_kib_per_launch': fkb, 'write_kib_per_launch': wkb,
+    import datetime
+    res = {'kernel': a.kernel, 'kernel_names': names, 'measured': datetime.datetime.now().isoformat(timespec='seconds'),
+           'fetch_kib_per_launch': fkb, 'write_kib_per_launch': wkb,
            'launches_fetch_pass': nf, 'launches_write_pass': nw}
     scale, how = 1.0, 'raw FETCH_SIZE (uncalibrated access width)'
     if a.calib_fetch:

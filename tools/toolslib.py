@@ -15,6 +15,8 @@ P, c_i32, c_i64, c_f32, c_vp, c_size = ctypes.POINTER, _lib.c_i32, _lib.c_i64, _
 _RA = [c_i32, P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32]
 TOOL_SIGNATURES = {
     'frh_roi_align_fwd_variant': (c_i32, [c_i32] + _RA + [c_vp, c_vp, c_size, c_vp]),
+    'frh_roi_align_bwd_variant': (c_i32, [c_i32, c_i32, P(c_vp), P(c_vp), P(c_i32), P(c_i64), P(c_f32), c_i32, c_i32,
+                                          c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     'frh_roi_align_workspace': (c_size, [c_i64]),
     'frh_nms_sorted_stamped': (c_i32, [c_i32, c_vp, c_i64, c_vp, c_i32, ctypes.c_double, c_i32, c_vp, c_i64, c_vp,
                                        c_vp, c_size, c_vp, c_vp]),
