@@ -303,8 +303,9 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
   if (num_rois > 0) {
     FRH_REQUIRE(grad_out, "null grad_out");
     const int64_t ng = num_rois * channels * pooled_h * pooled_w;
-    const int64_t mb = std::min<int64_t>((ng / 4 + 255) / 256 + 1, 2048);
-    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)mb), dim3(256), 0, st, grad_out, ng, scale_word);
+    const int64_t mb = std::min<int64_t>((ng / 4 + kAbsmaxThreads - 1) / kAbsmaxThreads + 1, kAbsmaxBlocks);
+    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)mb), dim3(kAbsmaxThreads), 0, st, grad_out, ng,
+                       scale_word);
     RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned, nullptr, scale_word, hb};
     if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w)) {
       hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),

@@ -291,8 +291,8 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
   if (fixed) {
     FRH_HIP(hipMemsetAsync(scale_word, 0, 4, st));
     const int64_t ng = num_rois * channels * 49;
-    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)std::min<int64_t>((ng / 4 + 255) / 256 + 1, 2048)),
-                       dim3(256), 0, st, grad_out, ng, scale_word);
+    hipLaunchKernelGGL(roi_bwd_absmax_kernel, dim3((unsigned)std::min<int64_t>((ng / 4 + 255) / 256 + 1, kAbsmaxBlocks)),
+                       dim3(kAbsmaxThreads), 0, st, grad_out, ng, scale_word);
   }
   if (variant == 0)
     hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<false>, grid, dim3(kWave), 0, st, lv, c, grad_out);

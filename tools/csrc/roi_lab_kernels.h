@@ -323,4 +323,97 @@ static __global__ void __launch_bounds__(kSortThreads) roi_sort_kernel(RoiLevels
   }
 }
 
+// Round-6 experiment (tools only; measured slower: the backward is bound by its atomics, not by
+// the 8 waves per CU its LDS staging allows -- DESIGN §4).  The channels-last backward with 7 x 7 bins and the wave's grad_out held in registers (49 per lane:
+// its channel's bins) instead of LDS: the kernel's LDS is the four tap-entry tables (< 0.5 KB),
+// so residency is set by registers (~20 waves per CU against 8 with the 18.9-KB LDS staging).
+// The bin row and column of a tap entry are wave-uniform, so the register operand is chosen by a
+// uniform switch (static indices).  Same operation order as roi_align_bwd_nhwc_kernel: the same
+// per-(RoI, row, column) sums, bit for bit.
+template <bool kFixed = false>
+__global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_reg_kernel(RoiLevels lv, RoiCfg c,
+                                                                     const float* __restrict__ gout) {
+  constexpr int P = 7, NB = P * P;
+  __shared__ int ye[kSepEnt], xe[kSepEnt];  // sorted tap entries: position << 16 | bin index
+  __shared__ float yws[kSepEnt], xws[kSepEnt];
+  const int64_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int c0 = blockIdx.y * kWave, ch = c0 + lane;
+  const bool live = ch < c.C;
+  float gr[NB];  // grad_out of this lane's channel, bin py * 7 + px
+  {
+    const float* go = gout + (k * c.C + (live ? ch : c0)) * NB;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gr[b] = live ? go[b] : 0.0f;
+  }
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl, H = lv.h[l], W = lv.w[l];
+  constexpr int nye = 4 * P, nxe = 4 * P;
+  auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
+    const Tap t = make_tap(start + (float)(e >> 2) * bin + ((float)((e >> 1) & 1) + 0.5f) * bin * 0.5f, size);
+    *pos = t.valid ? ((e & 1) ? t.hi : t.lo) : -1;
+    *w = (e & 1) ? t.l : t.h;
+  };
+  int yp = -1, xp = -1;
+  float ywv = 0.0f, xwv = 0.0f;
+  if (lane < nye) entry(lane, g.start_h, g.bin_h, H, &yp, &ywv);
+  if (lane < nxe) entry(lane, g.start_w, g.bin_w, W, &xp, &xwv);
+  const int ypm = yp < 0 ? (1 << 20) : yp, xpm = xp < 0 ? (1 << 20) : xp;
+  int yr = 0, xr = 0;  // rank by (position, entry)
+  for (int e = 0; e < nye; ++e) {
+    const int pe = __shfl(ypm, e, kWave);
+    yr += (pe < ypm || (pe == ypm && e < lane)) ? 1 : 0;
+  }
+  for (int e = 0; e < nxe; ++e) {
+    const int pe = __shfl(xpm, e, kWave);
+    xr += (pe < xpm || (pe == xpm && e < lane)) ? 1 : 0;
+  }
+  if (yp >= 0) ye[yr] = (yp << 16) | (lane >> 2), yws[yr] = ywv;
+  if (xp >= 0) xe[xr] = (xp << 16) | (lane >> 2), xws[xr] = xwv;
+  const int nyv = __popcll(__ballot(yp >= 0)), nxv = __popcll(__ballot(xp >= 0));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  const int64_t base = (int64_t)g.b * lv.sb[l] + ch, sy = lv.sy[l], sx = lv.sx[l];
+  const double fscale = kFixed ? bwd_fixed_scale(c.fix_max, c.fix_hb) : 0.0;
+  if (kFixed && fscale < 0.0) return;  // non-finite gradient: the conversion writes NaN
+  float R[P];
+#pragma unroll
+  for (int px = 0; px < P; ++px) R[px] = 0.0f;
+  for (int i = 0; i < nyv; ++i) {
+    const int yv = __builtin_amdgcn_readfirstlane(ye[i]), row = yv >> 16, py = yv & 0xffff;
+    const float wy = yws[i];
+    switch (py) {  // wave-uniform: static register operands
+#define FRH_ROW_CASE(Q)                                                       \
+  case Q:                                                                     \
+    _Pragma("unroll") for (int px = 0; px < P; ++px) R[px] = R[px] + wy * gr[Q * P + px]; \
+    break;
+      FRH_ROW_CASE(0) FRH_ROW_CASE(1) FRH_ROW_CASE(2) FRH_ROW_CASE(3) FRH_ROW_CASE(4) FRH_ROW_CASE(5) FRH_ROW_CASE(6)
+#undef FRH_ROW_CASE
+      default: break;
+    }
+    if (i + 1 < nyv && (ye[i + 1] >> 16) == row) continue;  // the row continues (uniform)
+    float acc = 0.0f;
+    for (int jx = 0; jx < nxv; ++jx) {
+      const int xv = __builtin_amdgcn_readfirstlane(xe[jx]), col = xv >> 16, px = xv & 0xffff;
+      const float rv = px == 0 ? R[0] : px == 1 ? R[1] : px == 2 ? R[2] : px == 3 ? R[3] : px == 4 ? R[4]
+                                                                                             : px == 5 ? R[5] : R[6];
+      acc = acc + xws[jx] * rv;
+      if (jx + 1 < nxv && (xe[jx + 1] >> 16) == col) continue;
+      const float v = acc * 0.25f;  // / count (4 samples)
+      acc = 0.0f;
+      if (!live || v == 0.0f) continue;
+      const int64_t e = base + (int64_t)row * sy + (int64_t)col * sx;
+      if constexpr (kFixed)
+        atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
+                  (unsigned long long)(long long)rint((double)v * fscale));
+      else
+        atomicAdd(lv.grad[l] + e, v);
+    }
+#pragma unroll
+    for (int px = 0; px < P; ++px) R[px] = 0.0f;
+  }
+}
+
 }  // namespace frh
