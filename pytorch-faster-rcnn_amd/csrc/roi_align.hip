@@ -6,6 +6,10 @@
 //
 // Forward (all bit-identical: -ffp-contract=off, reference op order; kernels in
 // roi_kernels.h):
+//  * roi_align_fwd_cg_kernel -- channels-last features with C % 64 == 0 (the product trunk's
+//    FPN levels): one 4-wave workgroup per (RoI, 64 channels), the tap window staged once as
+//    [cell][64 channels] (256-B requests), lane = (bin, channel quad): bank-conflict-free
+//    ds_read_b128 taps; windows above the 36-KB slab in bands of bin rows.
 //  * roi_align_fwd_band_kernel -- channels-last features (unit channel stride, C % 4
 //    == 0, sampling 2, 7x7 bins and smaller): small windows as the quad kernel (16-B
 //    LDS-DMA staging, lane = cell, one ds_read_b128 per tap for 4 channels), larger ones
@@ -41,6 +45,12 @@ namespace frh {
 // only 44.1-47.3 / 76-78 / 66-70; quad kernel (13 KB slab, pair order) 37.7-39.1 / 103-106 /
 // 96-98; round 4's 37.1-39.5 / 142 / 150.
 constexpr int kBandCells = 240;  // 15 KB: whole 1-KB DMA rounds, 10 workgroups per CU by LDS
+// The channel-group kernel's slab (round 6): 144 cells x 64 channels = 36 KB, 4 workgroups of 4
+// waves per CU (by LDS and by its 107 VGPRs alike); a 120-cell slab at 5 per CU needs <= 96 VGPRs
+// (spills: slower), 160 / 192 cells allow 3 per CU (slower).  Measured (tools/bench_roi_sets.py,
+// variants 80-93, µs per launch, bench / VOC / train RoIs): 32.4-34.3 / 56.6-58.6 / 51.0-53.0 vs
+// the band kernel's 38.7-39.2 / 67.4-68.3 / 58.2-59.6 on the same boxes, bit-identical.
+constexpr int kCgCells = 144;
 static_assert(2 * kBandCells * 32 <= kBandCells * 64 && (kBandCells + 15) / 16 * 1024 <= kBandCells * 64,
               "the interleaved stages and the band DMA rounds must fit the slab");
 
@@ -171,7 +181,17 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     else
       hipLaunchKernelGGL(kern, grid, block, 0, st, lv, c, out);
   };
-  if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
+  if (quad_ok(f, lv, channels, pooled_h, pooled_w) && cg_ok(channels, pooled_h, pooled_w, kCgCells)) {
+    // channels-last features, C % 64 == 0 (the FPN's NHWC levels, round 6): one 4-wave workgroup
+    // per (RoI, 64 channels), the window staged once as [cell][64 channels], conflict-free taps
+    const int64_t total = num_rois * (channels / kCgChan);
+    FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
+    const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
+    if (span)
+      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, true>, grid, dim3(4 * kWave));
+    else
+      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, false>, grid, dim3(4 * kWave));
+  } else if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
     // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels); tap
     // windows of <= 192 cells staged whole, 4 quads at a time ([quad][cell]); <= 480 cells
     // whole in two stages of [cell][2 quads] (32 B per cell and request); larger in row bands

@@ -782,6 +782,38 @@ def test_roi_align_multilevel_vs_oracle(dev, layout, sampling):
     np.testing.assert_array_equal(out, ref)  # every forward kernel keeps the oracle's operation order
 
 
+def _pathological_rois(batch):
+    """RoIs whose dense tap windows defeat row bands: far larger than a 10 x 30 level, so one bin
+    row's two samples lie 3.6 rows apart with every row between them inside the window (the
+    channel-group kernel stages such a bin row as its 4 tap-list rows), plus RoIs hanging off
+    every edge, tiny and degenerate ones."""
+    r = np.array([[0, 0, 0, 400, 200], [1, -50, -40, 380, 230], [0, 3, 2, 900, 60], [1, 100, 0, 119.5, 300],
+                  [0, -500, -500, 600, 600], [1, 0, 30, 119, 36], [0, 60, 10, 61, 11], [1, 119, 39, 119, 39],
+                  [0, -30, -30, -1, -1], [1, 10, -10, 110, 45], [0, 0, 0, 1000, 200]], np.float32)
+    r[:, 0] %= batch
+    return r
+
+
+@pytest.mark.parametrize('pooled,C', [((7, 7), 64), ((7, 7), 192), ((4, 5), 128), ((8, 8), 64), ((1, 1), 64)])
+def test_roi_align_channel_group_kernel_vs_oracle(dev, pooled, C):
+    """The channel-group forward (roi_align_fwd_cg_kernel: channels-last levels with C % 64 == 0,
+    one 4-wave workgroup per (RoI, 64 channels), 144-cell slab, bands of bin rows, list-row bands
+    for bin rows spanning more rows than the slab holds) against the oracle, bit-identical: random
+    RoIs over four levels (windows from 1 cell to 28 x 28, single- and multi-band), pathological
+    RoIs on a 10 x 30 level, pooled sizes 1x1 .. 8x8."""
+    from frcnn_amd import ops
+    grids = [(76, 128), (38, 64), (19, 32), (10, 30)]
+    feats = inputs.feature_maps(60, grids, C, 2)
+    rois = np.concatenate([_rois(61, 300, 2), _pathological_rois(2)], 0)
+    levels = oracle.roi_level_map(rois, 56.0, 4)
+    levels[-11:] = 3  # the pathological RoIs on the 10 x 30 level
+    scales = [1 / 8, 1 / 16, 1 / 32, 1 / 4]
+    ref = oracle.roi_align(feats, rois, levels, scales, pooled, 2)
+    ft = [T(f, dev).contiguous(memory_format=torch.channels_last) for f in feats]
+    out = ops.roi_align_multilevel(ft, T(rois, dev), T(levels, dev), scales, pooled, 2).cpu().numpy()
+    np.testing.assert_array_equal(out, ref)
+
+
 def test_roi_align_module_and_strided_view(dev):
     from frcnn_amd.ops import RoIAlign
     f = inputs.feature_maps(50, [(40, 60)], 32, 2)[0]

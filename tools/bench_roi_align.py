@@ -23,7 +23,7 @@ import toolslib  # noqa: E402
 
 STAMPED = {1, 9, 15}
 STAMPED_NHWC = {6}  # channels-last stamped build: 8 int64 per 64-channel item
-NHWC = set(range(2, 71))  # channels-last kernels: run on channels_last copies of the same features
+NHWC = set(range(2, 71)) | set(range(80, 100))  # channels-last kernels: run on channels_last copies of the same features
 
 
 def calibrate(variants, dev, small=False):

@@ -168,6 +168,48 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                          lv, c, out);
     return check_launch("frh_roi_align_fwd_variant");
   }
+  if (variant >= 80 && variant <= 99) {  // round 6: channel-group kernel, one workgroup per (RoI, 64 channels)
+    // 80: 4 waves, 144-cell slab (36 KB); 81: 8 waves, 144; 82: 4 waves, 192 cells; 83: 2 waves, 144;
+    // 84: 8 waves, 192; 85: 4 waves, 160
+    const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
+    FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w) && cg_ok(channels, pooled_h, pooled_w, 112),
+                "the channel-group kernel does not take this shape");
+    const int64_t tg = num_rois * (channels / kCgChan);
+    const dim3 gg((unsigned)(8 * ((tg + 7) / 8)));
+    if (variant == 80)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 144>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 81)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<8, 144>), gg, dim3(8 * kWave), 0, st, lv, c, out);
+    else if (variant == 82)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 192>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 83)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<2, 144>), gg, dim3(2 * kWave), 0, st, lv, c, out);
+    else if (variant == 84)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<8, 192>), gg, dim3(8 * kWave), 0, st, lv, c, out);
+    else if (variant == 85)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 160>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 86)  // 120-cell slab (30 KB: 5 workgroups per CU by LDS), <= 96 VGPRs (5 waves per SIMD)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 120, kCpolNT, false, 5>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 87)  // 120-cell slab, registers as compiled (4 waves per SIMD)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 120>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 88)  // 112-cell slab (28 KB), 5 waves per SIMD
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 112, kCpolNT, false, 5>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 89)  // 120 cells, 5 waves per SIMD, one sample row's taps in flight
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 120, kCpolNT, false, 5, false>), gg, dim3(4 * kWave), 0, st, lv,
+                         c, out);
+    else if (variant == 90)  // 144 cells, one sample row's taps in flight
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 144, kCpolNT, false, 0, false>), gg, dim3(4 * kWave), 0, st, lv,
+                         c, out);
+    else if (variant == 92)  // as 90, RoI-major item order
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 144, kCpolNT, false, 0, false, 1>), gg, dim3(4 * kWave), 0, st,
+                         lv, c, out);
+    else if (variant == 93)  // as 90, default store policy
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 144, 0, false, 0, false>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else  // 91: 8 waves, 144 cells, one sample row's taps in flight, 4 waves per SIMD (2 workgroups per CU)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<8, 120, kCpolNT, false, 5, false>), gg, dim3(8 * kWave), 0, st, lv,
+                         c, out);
+    return check_launch("frh_roi_align_fwd_variant");
+  }
   if (variant == 26 || variant == 27) {  // quad kernel, chunk-pair-major item order (27: + stamps)
     const FwdCaps fq = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
     FRH_REQUIRE(quad_ok(fq, lv, channels, pooled_h, pooled_w), "the quad kernel does not take this shape");

@@ -7,7 +7,7 @@
 #   bash tools/profile_r06.sh <outdir under gpurun_out>
 set -o pipefail
 OUT=${1:-gpurun_out/r6_prof}
-K=roi_align_fwd_band_kernel
+K=roi_align_fwd_cg_kernel
 mkdir -p $OUT
 export TMPDIR=/tmp
 run() { timeout -k 10 "$@"; }
@@ -22,11 +22,11 @@ for m in fwd train; do
   run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch_$m -o run --output-format csv -- python bench.py $A > $OUT/pmc_fetch_$m.log 2>&1 || exit 1
   run 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write_$m -o run --output-format csv -- python bench.py $A > $OUT/pmc_write_$m.log 2>&1 || exit 1
 done
-run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 65 > $OUT/pmc_calib_small.log 2>&1 || exit 1
-run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_band -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 65 > $OUT/pmc_calib_band.log 2>&1 || exit 1
-python tools/pmc_summary.py --fetch $OUT/pmc_fetch_fwd --write $OUT/pmc_write_fwd --kernel $K --calib-kernel roi_align_fwd_band_kernel \
+run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_small -o run --output-format csv -- python tools/bench_roi_align.py --calib --calib-small --variants 80 > $OUT/pmc_calib_small.log 2>&1 || exit 1
+run 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_calib_band -o run --output-format csv -- python tools/bench_roi_align.py --calib --variants 80 > $OUT/pmc_calib_band.log 2>&1 || exit 1
+python tools/pmc_summary.py --fetch $OUT/pmc_fetch_fwd --write $OUT/pmc_write_fwd --kernel $K --calib-kernel roi_align_fwd_cg_kernel \
   --calib-fetch $OUT/pmc_calib_small --calib-bytes 150994944 --out $OUT/roi_align_pmc.json || exit 1
-python tools/pmc_summary.py --fetch $OUT/pmc_fetch_train --write $OUT/pmc_write_train --kernel $K --calib-kernel roi_align_fwd_band_kernel \
+python tools/pmc_summary.py --fetch $OUT/pmc_fetch_train --write $OUT/pmc_write_train --kernel $K --calib-kernel roi_align_fwd_cg_kernel \
   --calib-fetch $OUT/pmc_calib_band --calib-bytes 205520896 --out $OUT/roi_align_pmc_train.json || exit 1
 run 300 rocprofv3 --pmc OccupancyPercent MeanOccupancyPerCU --kernel-trace -d $OUT/pmc_occ -o run --output-format csv -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline --trace-steps 0 > $OUT/pmc_occ.log 2>&1 || exit 1
 python tools/pmc_table.py $OUT/pmc_occ frh:: > $OUT/occupancy.txt
@@ -37,7 +37,7 @@ for set in bench voc train; do
              "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
     mkdir -p $OUT/stall_$set
-    run 120 rocprofv3 --pmc $grp --kernel-trace -d $OUT/stall_$set/p$i -o run --output-format csv -- python tools/bench_roi_sets.py --sets $set --variants 26 --rounds 1 --iters 3 > $OUT/stall_$set/p$i.log 2>&1 || { echo "stall pass $set $i failed"; exit 1; }
+    run 120 rocprofv3 --pmc $grp --kernel-trace -d $OUT/stall_$set/p$i -o run --output-format csv -- python tools/bench_roi_sets.py --sets $set --variants 65 --rounds 1 --iters 3 > $OUT/stall_$set/p$i.log 2>&1 || { echo "stall pass $set $i failed"; exit 1; }
   done
   python tools/pmc_table.py $OUT/stall_$set roi_align_fwd > $OUT/roi_align_counters_$set.txt || true
   rm -rf $OUT/stall_$set
