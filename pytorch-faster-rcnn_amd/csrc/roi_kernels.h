@@ -1492,8 +1492,11 @@ constexpr int kCgChan = 64;  // channels per item
 // first row's sums: 32 VGPRs fewer)
 // kOrder 0: XCD x walks the x-th eighth of the group-major (group, RoI) list (each XCD's L2 holds
 // one 64-channel slice); 1: RoI-major (RoI, group) -- the 4 groups of a RoI adjacent.
+// kStamp (tools-only timing builds): thread 0 writes 16 int64 per item after the output --
+// s_memrealtime at start / setup done / first band landed / end, bands, window cells, RoI record
+// landed, evaluation done, taps made, window extents, tables written.
 template <int kNW, int kSlabCells, int kStAux = kCpolNT, bool kSpan = false, int kWpe = 0, bool kLd2 = true,
-          int kOrder = 0>
+          int kOrder = 0, bool kStamp = false>
 __global__ void __launch_bounds__(kNW * kWave) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
 roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   constexpr int SR = 2;
@@ -1501,7 +1504,9 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   static_assert(kNW == 2 || kNW == 4 || kNW == 8, "waves per workgroup");
   static_assert(kSlabCells >= 64 && kSlabCells % 4 == 0, "the output block [64][<= 64 bins] leaves through the slab");
   static_assert((kSlabCells + 3) / 4 <= 63 * kNW, "vmcnt is 6 bits");
-  const int64_t t_start = kSpan ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  const int64_t t_start = (kSpan || kStamp) ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  int64_t t_rec = 0, t_setup = 0, t_land = 0, t_eval = 0, t_tap = 0, t_ext = 0, t_tab = 0;
+  int n_bands = 0;
   __shared__ __attribute__((aligned(16))) float slab[kSlabCells * kCgChan];
   __shared__ __attribute__((aligned(16))) float4 tab[32];  // y samples [0, 16), x samples [16, 32)
   const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
@@ -1519,6 +1524,7 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int nq = nbins * kCgChan / 4;  // 16-B units of the item's output block
   const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + (int64_t)grp * kCgChan) * nbins, (int64_t)nq * 16);
   const RoiRaw raw = roi_fetch(c, k);
+  if (kStamp) t_rec = (int64_t)__builtin_amdgcn_s_memrealtime();
   const RoiGeom g = roi_geom_raw(c, lv, raw);
   const int l = g.lvl;
   const int H = lv.h[l], W = lv.w[l];
@@ -1536,16 +1542,24 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     const Tap t = make_tap(v, isx ? W : H);
     if (t.valid) trow = (e & 1) ? t.hi : t.lo, tlo = t.lo, thi = t.hi, tl = t.l, th = t.h;
   }
-  const int y0 = __builtin_amdgcn_readfirstlane(wave_min_i32(isx ? 0x7fffffff : tlo));
-  const int y1 = __builtin_amdgcn_readfirstlane(wave_max_i32(isx ? -1 : thi));
-  const int x0 = __builtin_amdgcn_readfirstlane(wave_min_i32(isx ? tlo : 0x7fffffff));
-  const int x1 = __builtin_amdgcn_readfirstlane(wave_max_i32(isx ? thi : -1));
-  if (!(y1 >= y0 && x1 >= x0)) {  // no valid sample: every bin 0
+  // the window: the sample positions increase along each axis (start + p bin + (i + 0.5) bin / 2,
+  // bin >= 1 / ph) and make_tap is monotonic, so the valid samples are one run of lanes whose first
+  // lo and last hi bound it: a ballot and two readlanes per axis (round 5's DPP min / max chains
+  // were ~0.4 us of the item's setup latency)
+  if (kStamp) t_tap = (int64_t)__builtin_amdgcn_s_memrealtime();
+  const uint64_t vm = __ballot(trow >= 0);
+  const uint32_t vy = (uint32_t)vm, vx = (uint32_t)(vm >> 32);
+  if (!vy || !vx) {  // no valid sample: every bin 0
     for (int u = (int)threadIdx.x; u < nq; u += kNW * kWave)
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, orr, u * 16, 0, kStAux);
     if (kSpan && threadIdx.x == 0) record_span(c, t_start);
     return;
   }
+  const int y0 = __builtin_amdgcn_readlane(tlo, __builtin_ctz(vy));
+  const int y1 = __builtin_amdgcn_readlane(thi, 31 - __builtin_clz(vy));
+  const int x0 = __builtin_amdgcn_readlane(tlo, 32 + __builtin_ctz(vx));
+  const int x1 = __builtin_amdgcn_readlane(thi, 63 - __builtin_clz(vx));
+  if (kStamp) t_ext = (int64_t)__builtin_amdgcn_s_memrealtime();
   const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
   const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;  // dense window, else the tap-list entries
   const int R = dy ? y1 - y0 + 1 : nly, Cs = dx ? x1 - x0 + 1 : nlx;
@@ -1560,17 +1574,24 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int r0 = tv ? (dax ? tlo - org : e) : 0, dr = tv ? (dax ? thi - tlo : 1) : 0;
   if (wave == 0 && (e & 1) == 0 && e < 32)
     tab[(isx ? 16 : 0) + (e >> 1)] = float4{__int_as_float(r0), __int_as_float(dr), tv ? tl : 0.f, tv ? th : 0.f};
-  // bin row p's slab rows: [lo, hi] of its valid samples 2 p, 2 p + 1 (y lanes 4 p, 4 p + 2); lane p holds them
-  const int rl = tv ? r0 : 0x7fffffff, rh = tv ? r0 + dr : -1;
-  const int pr = min(lane, 15);
-  const int brl = min(__shfl(rl, 4 * pr, kWave), __shfl(rl, 4 * pr + 2, kWave));
-  const int brh = max(__shfl(rh, 4 * pr, kWave), __shfl(rh, 4 * pr + 2, kWave));
+  // windows above the slab: bin row p's slab rows [lo, hi] of its valid samples 2 p, 2 p + 1 (y lanes
+  // 4 p, 4 p + 2), held by lane p; rows_cap = slab rows of the window's width
+  if (kStamp) t_tab = (int64_t)__builtin_amdgcn_s_memrealtime();
+  const bool multi = R * Cs > kSlabCells;
+  const float rcs = __builtin_amdgcn_rcpf((float)Cs);  // (e + 0.5) * rcs: e / Cs within 3e-4 of a value
+                                                       // >= 0.5 / Cs from an integer, for e < 1100
+  int brl = 0, brh = -1, rows_cap = kSlabCells;
+  if (multi) {
+    const int rl = tv ? r0 : 0x7fffffff, rh = tv ? r0 + dr : -1;
+    const int pr = min(lane, 15);
+    brl = min(__shfl(rl, 4 * pr, kWave), __shfl(rl, 4 * pr + 2, kWave));
+    brh = max(__shfl(rh, 4 * pr, kWave), __shfl(rh, 4 * pr + 2, kWave));
+    rows_cap = (int)(((float)kSlabCells + 0.5f) * rcs);
+  }
   const __amdgpu_buffer_rsrc_t fr =
       uniform_rsrc(lv.feat[l] + (int64_t)g.b * lv.sb[l],
                    ((int64_t)(c.C - 1) + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4);
   const int soff = (int)grp * kCgChan * 4;
-  const uint32_t inv = (65536u + (uint32_t)Cs - 1u) / (uint32_t)Cs;  // e / Cs == (e * inv) >> 16 for e < 1100
-  const int rows_cap = kSlabCells / Cs;
   const int q = lane & 15, b4 = lane >> 4;
   f32x4 res[kJ];
 #pragma unroll
@@ -1579,7 +1600,7 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   while (pb < c.ph) {
     // the band: bin rows [pb, pe) whose valid samples' rows fit rows_cap slab rows
     int rs = 0x7fffffff, re = -1, pe = pb;
-    if (R * Cs <= kSlabCells) {
+    if (!multi) {
       rs = 0, re = R - 1, pe = c.ph;
     } else {
       while (pe < c.ph) {
@@ -1596,21 +1617,24 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     // a dense window whose single bin row spans more rows than the slab holds (samples far apart
     // with the rows between them clamped or outside: a RoI much larger than its level) is staged
     // as that bin row's 4 tap-list entries instead (cg_ok: 4 rows of the widest window fit)
-    const bool lst = dy && re - rs + 1 > rows_cap;
+    const bool lst = multi && dy && re - rs + 1 > rows_cap;
     if (lst) rs = 4 * pb, re = 4 * pb + 3, pe = pb + 1;
     const int nb = (re - rs + 1) * Cs;
     const int nj = (nb + 3) >> 2;
+    if (kStamp && n_bands == 0) t_setup = (int64_t)__builtin_amdgcn_s_memrealtime();
     // stage: instruction J (waves take J = wave, wave + kNW, ...): cells 4 J .. 4 J + 3, 16 lanes per cell
     for (int J = wave; J < nj; J += kNW) {
       int cell = 4 * J + b4;
       const bool in = cell < nb;
       cell = in ? cell : 0;
-      const int r = (int)(((uint32_t)cell * inv) >> 16), cc = cell - r * Cs;
+      const int r = (int)(((float)cell + 0.5f) * rcs), cc = cell - r * Cs;
       const int voff = __shfl(lst ? srcl : src, rs + r, kWave) + __shfl(src, 32 + cc, kWave) + q * 16;
       lds_dma_at<16, 0>(fr, sbase + 1024u * (uint32_t)J, in ? voff : 0x40000000, soff);
     }
     wait_vmcnt<0>();
     __syncthreads();  // every wave's DMA (and wave 0's tables) landed
+    if (kStamp && n_bands == 0) t_land = (int64_t)__builtin_amdgcn_s_memrealtime();
+    ++n_bands;
     // evaluate the 4-bin steps holding bins of bin rows [pb, pe)
     const int bin_lo = pb * c.pw, bin_hi = min(pe * c.pw, nbins);
     const int rsb = rs;
@@ -1664,6 +1688,7 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
         acc = acc + quad_val(wq, &v[0][ix * 4]);
       }
       if constexpr (!kLd2) {
+        asm volatile("" : "+v"(acc));  // the first row's sums before the second row's reads: v[0] dies here
         load(std::integral_constant<int, 1>{});
       }
       lds_wait4<0>(v[1]);
@@ -1677,6 +1702,7 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     __syncthreads();  // the band's tap reads are done before the next band (or the outputs) overwrite the slab
     pb = pe;
   }
+  if (kStamp) t_eval = (int64_t)__builtin_amdgcn_s_memrealtime();
   // outputs: [channel][bin] through the slab, then the contiguous block in 16-B stores
   float* ob = slab;
 #pragma unroll
@@ -1696,6 +1722,309 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
     __builtin_amdgcn_raw_buffer_store_b128(
         u32x4{__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z), __float_as_uint(v4.w)}, orr,
         u * 16, 0, kStAux);
+  }
+  if (kSpan && threadIdx.x == 0) record_span(c, t_start);
+  if (kStamp && threadIdx.x == 0) {
+    int64_t* st = reinterpret_cast<int64_t*>(out + c.K * c.C * nbins) + (int64_t)w * 16;  // 16 per item
+    st[0] = t_start;
+    st[1] = t_setup;
+    st[2] = t_land;
+    st[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[4] = n_bands;
+    st[5] = R * Cs;
+    st[6] = t_rec;
+    st[7] = t_eval;
+    st[8] = t_tap;
+    st[9] = t_ext;
+    st[10] = t_tab;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The channel-group forward with kItems items per workgroup, software-pipelined (round 6): the
+// next item's RoI record, window and sample tables (the ~1.5-2 us setup chain: scalar loads, tap
+// math, tables) are computed while the current item's window DMA is in flight, and the slab is
+// never idle during a setup.  Tables double-buffered; barriers wait for LDS only (the output
+// stores drain in the background).  Item j of workgroup r of XCD x: x * per + r + j * nwx (per
+// items per XCD, nwx workgroups per XCD), so the resident workgroups of an XCD stay on nearby
+// RoIs of one channel group.  Same evaluation as roi_align_fwd_cg_kernel: bit-identical.
+__device__ __forceinline__ void lds_only_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+struct CgItem {  // wave-uniform (SGPRs); the per-lane tables live in LDS (CgTab)
+  const float* base;  // image b of the RoI's level
+  uint32_t extent;    // feature bytes addressable from base
+  int k, grp, state;  // state 0: none, 1: no valid sample (zeros), 2: staged and evaluated
+  int R, Cs, dy, multi, rows_cap;
+  float rcs;
+};
+
+// An item's LDS tables (written by wave 0 in cg_setup): the sample tables (y samples [0, 16), x
+// [16, 32): slab row / column of the lo tap, hi - lo, l, h), the source byte offsets of the window
+// rows (dense or tap-list) and columns, the tap-list rows (list bands), bin-row row spans.
+struct CgTab {
+  float4 smp[32];
+  int rsrc[32], rsrcl[32], csrc[32];
+  int brl[8], brh[8];
+};
+
+template <int kSlabCells>
+__device__ __forceinline__ void cg_setup(const RoiLevels& lv, const RoiCfg& c, uint32_t w, uint32_t wend, CgTab* tb,
+                                         int lane, int wave, CgItem& it) {
+  constexpr int SR = 2;
+  if (w >= wend) {
+    it.state = 0;
+    return;
+  }
+  const uint32_t K32 = (uint32_t)c.K;
+  it.grp = (int)(w / K32);
+  it.k = (int)(w - (uint32_t)it.grp * K32);
+  const RoiRaw raw = roi_fetch(c, (int64_t)it.k);
+  const RoiGeom g = roi_geom_raw(c, lv, raw);
+  const int l = g.lvl;
+  const int H = lv.h[l], W = lv.w[l];
+  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l];
+  const bool isx = lane >= 32;
+  const int e = lane & 31;
+  const int nl = isx ? 2 * SR * c.pw : 2 * SR * c.ph;
+  int trow = -1, tlo = 0x7fffffff, thi = -1;
+  float tl = 0.f, th = 0.f;
+  if (e < nl) {
+    const int s = e >> 1, p = s >> 1, i = s & 1;
+    const float v = isx ? g.start_w + (float)p * g.bin_w + ((float)i + 0.5f) * g.bin_w * 0.5f
+                        : g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h * 0.5f;
+    const Tap t = make_tap(v, isx ? W : H);
+    if (t.valid) trow = (e & 1) ? t.hi : t.lo, tlo = t.lo, thi = t.hi, tl = t.l, th = t.h;
+  }
+  const uint64_t vm = __ballot(trow >= 0);
+  const uint32_t vy = (uint32_t)vm, vx = (uint32_t)(vm >> 32);
+  if (!vy || !vx) {
+    it.state = 1;
+    return;
+  }
+  it.state = 2;
+  const int y0 = __builtin_amdgcn_readlane(tlo, __builtin_ctz(vy));
+  const int y1 = __builtin_amdgcn_readlane(thi, 31 - __builtin_clz(vy));
+  const int x0 = __builtin_amdgcn_readlane(tlo, 32 + __builtin_ctz(vx));
+  const int x1 = __builtin_amdgcn_readlane(thi, 63 - __builtin_clz(vx));
+  const int nly = 2 * SR * c.ph, nlx = 2 * SR * c.pw;
+  const bool dy = y1 - y0 + 1 <= nly, dx = x1 - x0 + 1 <= nlx;
+  it.dy = dy;
+  it.R = dy ? y1 - y0 + 1 : nly;
+  it.Cs = dx ? x1 - x0 + 1 : nlx;
+  it.multi = it.R * it.Cs > kSlabCells;
+  it.rcs = __builtin_amdgcn_rcpf((float)it.Cs);
+  it.rows_cap = it.multi ? (int)(((float)kSlabCells + 0.5f) * it.rcs) : kSlabCells;
+  it.base = lv.feat[l] + (int64_t)g.b * lv.sb[l];
+  it.extent = (uint32_t)(((int64_t)(c.C - 1) + (int64_t)(H - 1) * sy + (int64_t)(W - 1) * sx + 1) * 4);
+  if (wave == 0) {
+    const bool dax = isx ? dx : dy;
+    const int org = isx ? x0 : y0;
+    const int src = (dax ? org + min(e, (isx ? it.Cs : it.R) - 1) : (trow >= 0 ? trow : org)) * (isx ? sx : sy) * 4;
+    if (isx) {
+      tb->csrc[e] = src;
+    } else {
+      tb->rsrc[e] = src;
+      tb->rsrcl[e] = (trow >= 0 ? trow : org) * sy * 4;
+    }
+    const bool tv = e < nl && trow >= 0 && (e & 1) == 0;
+    const int r0 = tv ? (dax ? tlo - org : e) : 0, dr = tv ? (dax ? thi - tlo : 1) : 0;
+    if ((e & 1) == 0)
+      tb->smp[(isx ? 16 : 0) + (e >> 1)] = float4{__int_as_float(r0), __int_as_float(dr), tv ? tl : 0.f, tv ? th : 0.f};
+    if (it.multi) {
+      const int rl = tv ? r0 : 0x7fffffff, rh = tv ? r0 + dr : -1;
+      const int pr = min(lane, 15);
+      const int a = min(__shfl(rl, 4 * pr, kWave), __shfl(rl, 4 * pr + 2, kWave));
+      const int b = max(__shfl(rh, 4 * pr, kWave), __shfl(rh, 4 * pr + 2, kWave));
+      if (lane < 8) tb->brl[lane] = a, tb->brh[lane] = b;
+    }
+  }
+}
+
+// one item: its bands (staging, evaluation), the output block; hook() runs once, right after
+// the first band's DMA is issued (or at once for an item without a valid sample)
+template <int kNW, int kSlabCells, int kStAux, bool kLd2, typename Hook>
+__device__ __forceinline__ void cg_body(const RoiCfg& c, const CgItem& it, float* __restrict__ out, float* slab,
+                                        uint32_t sbase, const CgTab* tb, int lane, int wave, Hook&& hook) {
+  const uint32_t tbase = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const float4*)reinterpret_cast<const float4*>(tb->smp));
+  constexpr int SR = 2;
+  constexpr int kJ = 16 / kNW;
+  const int nbins = c.ph * c.pw;
+  const int nq = nbins * kCgChan / 4;
+  if (it.state == 1) {
+    const __amdgpu_buffer_rsrc_t orr =
+        uniform_rsrc(out + ((int64_t)it.k * c.C + (int64_t)it.grp * kCgChan) * nbins, (int64_t)nq * 16);
+    for (int u = (int)threadIdx.x; u < nq; u += kNW * kWave)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, orr, u * 16, 0, kStAux);
+    hook();
+    return;
+  }
+  const int R = it.R, Cs = it.Cs;
+  const float rcs = it.rcs;
+  const int soff = it.grp * kCgChan * 4;
+  const int q = lane & 15, b4 = lane >> 4;
+  f32x4 res[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) res[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int pb = 0;
+  bool first = true;
+  while (pb < c.ph) {
+    int rs = 0x7fffffff, re = -1, pe = pb;
+    if (!it.multi) {
+      rs = 0, re = R - 1, pe = c.ph;
+    } else {
+      while (pe < c.ph) {
+        const int lo = __builtin_amdgcn_readfirstlane(tb->brl[pe]), hi = __builtin_amdgcn_readfirstlane(tb->brh[pe]);
+        if (hi >= 0) {
+          const int nrs = min(rs, lo), nre = max(re, hi);
+          if (pe > pb && nre - nrs + 1 > it.rows_cap) break;
+          rs = nrs, re = nre;
+        }
+        ++pe;
+      }
+      if (re < 0) rs = re = 0;
+    }
+    const bool lst = it.multi && it.dy && re - rs + 1 > it.rows_cap;
+    if (lst) rs = 4 * pb, re = 4 * pb + 3, pe = pb + 1;
+    const int nb = (re - rs + 1) * Cs;
+    const int nj = (nb + 3) >> 2;
+    for (int J = wave; J < nj; J += kNW) {
+      int cell = 4 * J + b4;
+      const bool in = cell < nb;
+      cell = in ? cell : 0;
+      const int r = (int)(((float)cell + 0.5f) * rcs), cc = cell - r * Cs;
+      const int voff = (lst ? tb->rsrcl[rs + r] : tb->rsrc[rs + r]) + tb->csrc[cc] + q * 16;
+      lds_dma_at<16, 0>(uniform_rsrc(it.base, (int64_t)it.extent), sbase + 1024u * (uint32_t)J,
+                        in ? voff : 0x40000000, soff);
+    }
+    if (first) {
+      hook();  // the next item's setup while this DMA is in flight
+      first = false;
+    }
+    wait_vmcnt<0>();
+    lds_only_barrier();  // every wave's DMA (and the tables) landed
+    const int bin_lo = pb * c.pw, bin_hi = min(pe * c.pw, nbins);
+    const int rsb = rs;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      const int t = wave + kNW * j;
+      if (4 * t + 3 < bin_lo || 4 * t >= bin_hi) continue;
+      int b4o = b4;
+      asm volatile("" : "+v"(b4o));
+      const int bin = 4 * t + b4o;
+      const bool act = bin >= bin_lo && bin < bin_hi;
+      const int bq = act ? bin : bin_lo;
+      const int py = (int)(((uint32_t)bq * ((65536u + (uint32_t)c.pw - 1u) / (uint32_t)c.pw)) >> 16), px = bq - py * c.pw;
+      f32x4 Y[2], X[2];
+      Y[0] = lds_read_b128<0>(tbase + 32u * (uint32_t)py);
+      Y[1] = lds_read_b128<16>(tbase + 32u * (uint32_t)py);
+      X[0] = lds_read_b128<256>(tbase + 32u * (uint32_t)px);
+      X[1] = lds_read_b128<272>(tbase + 32u * (uint32_t)px);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Y[0]), "+v"(Y[1]), "+v"(X[0]), "+v"(X[1]) : : "memory");
+      uint32_t ra[SR], rd[SR], ca[SR], cd[SR];
+#pragma unroll
+      for (int i = 0; i < SR; ++i) {
+        const int ry = lst ? 4 * py + 2 * i - rsb : max(__float_as_int(Y[i].x) - rsb, 0);
+        ra[i] = (uint32_t)(ry * Cs) * 256u;
+        rd[i] = (uint32_t)((lst ? 1 : __float_as_int(Y[i].y)) * Cs) * 256u;
+        ca[i] = (uint32_t)__float_as_int(X[i].x) * 256u;
+        cd[i] = (uint32_t)__float_as_int(X[i].y) * 256u;
+      }
+      const uint32_t qb = sbase + 16u * (uint32_t)q;
+      f32x4 v[2][8];
+      auto load = [&](auto hh) {
+        constexpr int iy = decltype(hh)::value;
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+          const uint32_t a = qb + ra[iy] + ca[ix];
+          v[iy][ix * 4 + 0] = lds_read_b128<0>(a);
+          v[iy][ix * 4 + 1] = lds_read_b128<0>(a + cd[ix]);
+          v[iy][ix * 4 + 2] = lds_read_b128<0>(a + rd[iy]);
+          v[iy][ix * 4 + 3] = lds_read_b128<0>(a + rd[iy] + cd[ix]);
+        }
+      };
+      load(std::integral_constant<int, 0>{});
+      if constexpr (kLd2) load(std::integral_constant<int, 1>{});
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (kLd2) lds_wait4<8>(v[0]);
+      else lds_wait4<0>(v[0]);
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const float wq[4] = {Y[0].w * X[ix].w, Y[0].w * X[ix].z, Y[0].z * X[ix].w, Y[0].z * X[ix].z};
+        acc = acc + quad_val(wq, &v[0][ix * 4]);
+      }
+      if constexpr (!kLd2) {
+        asm volatile("" : "+v"(acc));
+        load(std::integral_constant<int, 1>{});
+      }
+      lds_wait4<0>(v[1]);
+#pragma unroll
+      for (int ix = 0; ix < SR; ++ix) {
+        const float wq[4] = {Y[1].w * X[ix].w, Y[1].w * X[ix].z, Y[1].z * X[ix].w, Y[1].z * X[ix].z};
+        acc = acc + quad_val(wq, &v[1][ix * 4]);
+      }
+      if (act) res[j] = acc * 0.25f;
+    }
+    lds_only_barrier();  // the band's tap reads are done before the next band (or the outputs) overwrite the slab
+    pb = pe;
+  }
+  float* ob = slab;
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const int bin = 4 * (wave + kNW * j) + b4;
+    if (bin < nbins) {
+      ob[(4 * q + 0) * nbins + bin] = res[j].x;
+      ob[(4 * q + 1) * nbins + bin] = res[j].y;
+      ob[(4 * q + 2) * nbins + bin] = res[j].z;
+      ob[(4 * q + 3) * nbins + bin] = res[j].w;
+    }
+  }
+  lds_only_barrier();
+  const __amdgpu_buffer_rsrc_t orr =
+      uniform_rsrc(out + ((int64_t)it.k * c.C + (int64_t)it.grp * kCgChan) * nbins, (int64_t)nq * 16);
+  const float4* o4 = reinterpret_cast<const float4*>(slab);
+  for (int u = (int)threadIdx.x; u < nq; u += kNW * kWave) {
+    const float4 v4 = o4[u];
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u32x4{__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z), __float_as_uint(v4.w)}, orr,
+        u * 16, 0, kStAux);
+  }
+  lds_only_barrier();  // the output block's reads are done before the next item's DMA overwrites the slab
+}
+
+template <int kNW, int kSlabCells, int kItems, int kStAux = kCpolNT, bool kSpan = false, int kWpe = 0,
+          bool kLd2 = false>
+__global__ void __launch_bounds__(kNW * kWave) __attribute__((amdgpu_waves_per_eu(kWpe > 0 ? kWpe : 1)))
+roi_align_fwd_cgp_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
+  static_assert(kNW == 2 || kNW == 4 || kNW == 8, "waves per workgroup");
+  static_assert(kSlabCells >= 64 && kSlabCells % 4 == 0, "the output block [64][<= 64 bins] leaves through the slab");
+  static_assert((kSlabCells + 3) / 4 <= 63 * kNW, "vmcnt is 6 bits");
+  const int64_t t_start = kSpan ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) float slab[kSlabCells * kCgChan];
+  __shared__ CgTab tab[2];  // double-buffered item tables
+  const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)slab);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const uint32_t total = (uint32_t)c.K * ((uint32_t)c.C / kCgChan), per = (total + 7u) / 8u;
+  const uint32_t nwx = (per + kItems - 1u) / kItems;  // workgroups per XCD
+  const uint32_t x = blockIdx.x & 7u, r = blockIdx.x >> 3;
+  const uint32_t wend = min(x * per + per, total);
+  uint32_t w = x * per + r;
+  CgItem cur, nxt;
+  cg_setup<kSlabCells>(lv, c, w, wend, &tab[0], lane, wave, cur);
+  lds_only_barrier();  // the first item's tables
+  int b = 0;
+  for (int j = 0; j < kItems && cur.state; ++j) {
+    const uint32_t wn = j + 1 < kItems ? w + nwx : wend;
+    nxt.state = 0;
+    cg_body<kNW, kSlabCells, kStAux, kLd2>(c, cur, out, slab, sbase, &tab[b], lane, wave, [&] {
+      cg_setup<kSlabCells>(lv, c, wn, wend, &tab[b ^ 1], lane, wave, nxt);
+    });
+    cur = nxt;
+    w = wn;
+    b ^= 1;
   }
   if (kSpan && threadIdx.x == 0) record_span(c, t_start);
 }
@@ -2167,6 +2496,104 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
       else
         atomicAdd(lv.grad[l] + e, v);
     }
+  }
+}
+
+// The channels-last backward with the tap lists in registers (round 6): the sorted y / x tap
+// entries sit one per lane and are read by v_readlane with the wave-uniform loop index (a
+// scalar, no LDS round trip), the row sums R[px] stay in registers and the column loop picks
+// R[px] by a uniform select -- the round-5 kernel read each x entry, its weight and R[px]
+// from LDS in a dependent chain (two LDS round trips per (row, column) pair: ~50 us of serial
+// latency per wave on VOC-sized windows).  Same sums in the same order: each cell's
+// contribution is bit-identical to roi_align_bwd_nhwc_kernel's.
+template <bool kFixed = false>
+__global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv, RoiCfg c,
+                                                                  const float* __restrict__ gout) {
+  constexpr int kMaxP = 8;
+  __shared__ float gs[kMaxP * kMaxP * kWave];  // grad_out of the wave's channels, [bin][lane]
+  __shared__ int ye[kSepEnt], xe[kSepEnt];     // sorted tap entries: position << 16 | bin index
+  __shared__ float yws[kSepEnt], xws[kSepEnt];
+  const int64_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int c0 = blockIdx.y * kWave, ch = c0 + lane;
+  const bool live = ch < c.C;
+  const RoiGeom g = roi_geom(c, lv, k);
+  const int l = g.lvl, H = lv.h[l], W = lv.w[l];
+  const int ph = c.ph, pw = c.pw, nbins = ph * pw, nye = 4 * ph, nxe = 4 * pw;
+  {  // [K][C][bins] -> LDS [bin][lane]: the wave's 64 channels are one contiguous run
+    const float* go = gout + (k * c.C + c0) * nbins;
+    const int nvalid = min(kWave, c.C - c0) * nbins;
+    for (int e = lane; e < kWave * nbins; e += kWave) {
+      const int cl = e / nbins, bin = e - cl * nbins;
+      gs[bin * kWave + cl] = e < nvalid ? go[e] : 0.0f;
+    }
+  }
+  auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
+    const Tap t = make_tap(start + (float)(e >> 2) * bin + ((float)((e >> 1) & 1) + 0.5f) * bin * 0.5f, size);
+    *pos = t.valid ? ((e & 1) ? t.hi : t.lo) : -1;
+    *w = (e & 1) ? t.l : t.h;
+  };
+  int yp = -1, xp = -1;
+  float ywv = 0.0f, xwv = 0.0f;
+  if (lane < nye) entry(lane, g.start_h, g.bin_h, H, &yp, &ywv);
+  if (lane < nxe) entry(lane, g.start_w, g.bin_w, W, &xp, &xwv);
+  if (lane >= nye) yp = -1;
+  if (lane >= nxe) xp = -1;
+  const int ypm = yp < 0 ? (1 << 20) : yp, xpm = xp < 0 ? (1 << 20) : xp;
+  int yr = 0, xr = 0;  // rank by (position, entry)
+  for (int e = 0; e < nye; ++e) {
+    const int pe = __shfl(ypm, e, kWave);
+    yr += (pe < ypm || (pe == ypm && e < lane)) ? 1 : 0;
+  }
+  for (int e = 0; e < nxe; ++e) {
+    const int pe = __shfl(xpm, e, kWave);
+    xr += (pe < xpm || (pe == xpm && e < lane)) ? 1 : 0;
+  }
+  if (yp >= 0) ye[yr] = (yp << 16) | (lane >> 2), yws[yr] = ywv;
+  if (xp >= 0) xe[xr] = (xp << 16) | (lane >> 2), xws[xr] = xwv;
+  const int nyv = __popcll(__ballot(yp >= 0)), nxv = __popcll(__ballot(xp >= 0));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  // lane i holds sorted entry i of each axis (read by v_readlane below)
+  const int ye_l = lane < kSepEnt ? ye[lane] : 0, xe_l = lane < kSepEnt ? xe[lane] : 0;
+  const float yw_l = lane < kSepEnt ? yws[lane] : 0.0f, xw_l = lane < kSepEnt ? xws[lane] : 0.0f;
+  const int64_t base = (int64_t)g.b * lv.sb[l] + ch, sy = lv.sy[l], sx = lv.sx[l];
+  const double fscale = kFixed ? bwd_fixed_scale(c.fix_max, c.fix_hb) : 0.0;
+  if (kFixed && fscale < 0.0) return;  // non-finite gradient: the conversion writes NaN
+  float R[kMaxP];
+#pragma unroll
+  for (int px = 0; px < kMaxP; ++px) R[px] = 0.0f;
+  for (int i = 0; i < nyv; ++i) {
+    const int yv = __builtin_amdgcn_readlane(ye_l, i), row = yv >> 16, py = yv & 0xffff;
+    const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yw_l), i));
+    const float* gr = gs + py * pw * kWave + lane;
+#pragma unroll
+    for (int px = 0; px < kMaxP; ++px)
+      if (px < pw) R[px] = R[px] + wy * gr[px * kWave];
+    if (i + 1 < nyv && (__builtin_amdgcn_readlane(ye_l, i + 1) >> 16) == row) continue;  // the row continues
+    float acc = 0.0f;
+    for (int jx = 0; jx < nxv; ++jx) {
+      const int xv = __builtin_amdgcn_readlane(xe_l, jx), col = xv >> 16, px = xv & 0xffff;
+      const float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xw_l), jx));
+      float r = R[0];
+#pragma unroll
+      for (int q = 1; q < kMaxP; ++q) r = px == q ? R[q] : r;  // uniform select
+      acc = acc + wx * r;
+      if (jx + 1 < nxv && (__builtin_amdgcn_readlane(xe_l, jx + 1) >> 16) == col) continue;
+      const float v = acc * 0.25f;  // / count (4 samples)
+      acc = 0.0f;
+      if (!live || v == 0.0f) continue;
+      const int64_t e = base + (int64_t)row * sy + (int64_t)col * sx;
+      if constexpr (kFixed)
+        atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
+                  (unsigned long long)(long long)rint((double)v * fscale));
+      else
+        atomicAdd(lv.grad[l] + e, v);
+    }
+#pragma unroll
+    for (int px = 0; px < kMaxP; ++px) R[px] = 0.0f;
   }
 }
 

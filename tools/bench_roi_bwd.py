@@ -28,7 +28,8 @@ def main():
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--json')
     ap.add_argument('--variants', default='', help='tools backward variants (frh_roi_align_bwd_variant) beside the '
-                    'product: 0 nhwc float, 1 register-resident float, 2 nhwc fixed, 3 register-resident fixed')
+                    'product: 0 nhwc float, 1 register-resident float, 2 nhwc fixed, 3 register-resident fixed, 4 / 5 '
+                    'readlane tap lists float / fixed')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     out = {}
@@ -65,9 +66,10 @@ def main():
                 tools = toolslib.load()
 
             def var(v=v):
-                grads = [torch.zeros_like(f) if v < 2 else torch.empty_like(f) for f in feats]
+                fx = v in (2, 3, 5)
+                grads = [torch.zeros_like(f) if not fx else torch.empty_like(f) for f in feats]
                 accs = [torch.empty(f.shape, dtype=torch.int64, device=dev, memory_format=torch.channels_last).zero_()
-                        for f in feats] if v >= 2 else grads
+                        for f in feats] if fx else grads
                 rc = tools.frh_roi_align_bwd_variant(v, len(grads), _lib.ptr_array(grads), _lib.ptr_array(accs), hw, st,
                                                      sc, B, C, _lib.ptr(rois), _lib.ptr(levels), K, _lib.ptr(g),
                                                      _lib.ptr(word), _lib.stream_of(g))
@@ -97,7 +99,7 @@ def main():
         nbytes = 4 * C * (K * 49 + 2 * sum(shapes[u % 64][2] * shapes[u % 64][3] for u in used))
         for nm in res:
             if nm.startswith('v'):
-                ref = outs['fixed' if int(nm[1:]) >= 2 else 'atomic']
+                ref = outs['fixed' if int(nm[1:]) in (2, 3, 5) else 'atomic']
                 d = max(float((x - y).abs().max()) for x, y in zip(outs[nm], ref))
                 print('  {}: {:.1f} us, max |diff| to the product form {:.3g}{}'.format(
                     nm, res[nm], d, ' (bit-identical)' if d == 0 else ''), flush=True)

@@ -25,7 +25,8 @@ import torch  # noqa: E402
 from frcnn_amd import ops, _lib  # noqa: E402
 
 SETS = {'bench': 'cfg2_rois.npz', 'voc': 'cfg2_rois_voc.npz', 'train': 'cfg2_rois_train.npz'}
-STAMPED = {9, 15, 27, 29, 39, 56, 58}  # tools variants writing per-item phase stamps (s_memrealtime)
+STAMPED = {9, 15, 27, 29, 39, 56, 58, 94}  # tools variants writing per-item phase stamps (s_memrealtime)
+STAMPED_CG = {94}  # channel-group kernel stamps: [start, setup, land, end, bands, cells, record, eval done]
 R4_LIB = os.path.join(REPO, 'tools', 'lib', 'r4', 'libfrcnn_amd_r4.so')
 
 
@@ -69,6 +70,31 @@ def tap_cells(rois, levels, shapes, scales):
         rw, rh = max(x2 * s - x1 * s, 1), max(y2 * s - y1 * s, 1)
         out.append(span(y1 * s, rh, H) * (span(x1 * s, rw, W) | 1))
     return np.array(out)
+
+
+def cg_stamps_report(stm):
+    stm = stm.reshape(-1, 16)  # 16 int64 per item
+    """Per-item phases of the channel-group kernel (µs, 100 MHz clock): record landed, window /
+    tables computed, first band landed (DMA + barrier), evaluation done (all bands), end (output
+    block stored); by band count."""
+    stm = stm[stm[:, 0] > 0]
+    t0 = stm[:, 0].min()
+    span = (stm[:, 3].max() - t0) / 100.0
+    pc = lambda a: np.percentile(a / 100.0, [50, 90]).round(2).tolist()  # noqa: E731
+    print('  {} items; span {:.1f} us'.format(len(stm), span))
+    for nb in sorted(set(stm[:, 4].tolist())):
+        x = stm[stm[:, 4] == nb]
+        print('  bands={} items {:5d} cells p50 {:4.0f}: record {} setup {} land {} eval {} out {} life {}'.format(
+            nb, len(x), np.median(x[:, 5]), pc(x[:, 6] - x[:, 0]), pc(x[:, 1] - x[:, 6]), pc(x[:, 2] - x[:, 1]),
+            pc(x[:, 7] - x[:, 2]), pc(x[:, 3] - x[:, 7]), pc(x[:, 3] - x[:, 0])))
+        print('      setup: geometry + taps {} window {} tables {} bands {}'.format(
+            pc(x[:, 8] - x[:, 6]), pc(x[:, 9] - x[:, 8]), pc(x[:, 10] - x[:, 9]), pc(x[:, 1] - x[:, 10])))
+    alive = np.zeros(int(span) + 1)
+    for a, b in zip((stm[:, 0] - t0) / 100.0, (stm[:, 3] - t0) / 100.0):
+        alive[int(a):int(b) + 1] += 1
+    print('  items alive per CU by us: ' + ' '.join('%.1f' % (v / 256) for v in alive))
+    print('  start-time percentiles 0/50/100:', np.percentile((stm[:, 0] - t0) / 100.0, [0, 50, 100]).round(1).tolist(),
+          'end 50/90/100:', np.percentile((stm[:, 3] - t0) / 100.0, [50, 90, 100]).round(1).tolist(), flush=True)
 
 
 def main():
@@ -159,7 +185,9 @@ def main():
             frac = nbytes / (us * 1e-6) / 8e12
             summary[name]['kernels'][k] = {'us': us, 'frac': frac, 'bit_identical_to_product': same}
             print('  {:8s} {:8.2f} us  frac {:.3f}  bit-identical to product: {}'.format(k, us, frac, same), flush=True)
-            if k in stamps:
+            if k in stamps and int(k[1:]) in STAMPED_CG:
+                cg_stamps_report(stamps[k].cpu().numpy())
+            elif k in stamps:
                 from bench_roi_align import stamps_report
                 stamps_report(stamps[k].cpu().numpy())
     if args.json:

@@ -205,6 +205,27 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
                          lv, c, out);
     else if (variant == 93)  // as 90, default store policy
       hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 144, 0, false, 0, false>), gg, dim3(4 * kWave), 0, st, lv, c, out);
+    else if (variant == 94)  // variant 89 (120 cells, 5 waves per SIMD, one sample row in flight), stamped (8 int64 per item after the output)
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 120, kCpolNT, false, 5, false, 0, true>), gg, dim3(4 * kWave), 0,
+                         st, lv, c, out);
+    else if (variant == 95)  // 124 cells (31 KB: 5 workgroups per CU), 5 waves per SIMD, one sample row in flight
+      hipLaunchKernelGGL((roi_align_fwd_cg_kernel<4, 124, kCpolNT, false, 5, false>), gg, dim3(4 * kWave), 0, st, lv,
+                         c, out);
+    else if (variant >= 96 && variant <= 99) {  // software-pipelined, kItems items per workgroup:
+                                                 // 96 / 97 / 98: 2 / 3 / 4 items at 144 cells; 99: 2 at 116 cells
+      const int ki = variant == 96 || variant == 99 ? 2 : variant == 97 ? 3 : 4;
+      const int64_t per = (tg + 7) / 8, nwx = (per + ki - 1) / ki;
+      const dim3 gp((unsigned)(8 * nwx));
+      if (variant == 96)
+        hipLaunchKernelGGL((roi_align_fwd_cgp_kernel<4, 144, 2>), gp, dim3(4 * kWave), 0, st, lv, c, out);
+      else if (variant == 97)
+        hipLaunchKernelGGL((roi_align_fwd_cgp_kernel<4, 144, 3>), gp, dim3(4 * kWave), 0, st, lv, c, out);
+      else if (variant == 98)
+        hipLaunchKernelGGL((roi_align_fwd_cgp_kernel<4, 144, 4>), gp, dim3(4 * kWave), 0, st, lv, c, out);
+      else
+        hipLaunchKernelGGL((roi_align_fwd_cgp_kernel<4, 116, 2, kCpolNT, false, 5>), gp, dim3(4 * kWave), 0, st, lv, c,
+                           out);
+    }
     else  // 91: 8 waves, 144 cells, one sample row's taps in flight, 4 waves per SIMD (2 workgroups per CU)
       hipLaunchKernelGGL((roi_align_fwd_cg_kernel<8, 120, kCpolNT, false, 5, false>), gg, dim3(8 * kWave), 0, st, lv,
                          c, out);
@@ -319,7 +340,7 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
                                              uint32_t* scale_word, void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, 7, 7, rois);
   if (r) return r;
-  const bool fixed = variant >= 2;
+  const bool fixed = variant == 2 || variant == 3 || variant == 5;
   RoiLevels lv;
   r = make_levels(num_levels, nullptr, fixed ? reinterpret_cast<float* const*>(acc_feats) : grad_feats, feat_hw,
                   strides, scales, &lv);
@@ -344,6 +365,10 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
   else if (variant == 3)
     hipLaunchKernelGGL(roi_align_bwd_nhwc_reg_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 4)  // round 6: tap lists read by v_readlane, row sums in registers
+    hipLaunchKernelGGL(roi_align_bwd_nhwc2_kernel<false>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 5)
+    hipLaunchKernelGGL(roi_align_bwd_nhwc2_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
   else
     FRH_REQUIRE(false, "backward variant %d unknown", variant);
   if (fixed) {
