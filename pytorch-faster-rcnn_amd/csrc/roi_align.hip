@@ -9,7 +9,7 @@
 //  * roi_align_fwd_cg_kernel -- channels-last features with C % 64 == 0 (the product trunk's
 //    FPN levels): one 4-wave workgroup per (RoI, 64 channels), the tap window staged once as
 //    [cell][64 channels] (256-B requests), lane = (bin, channel quad): bank-conflict-free
-//    ds_read_b128 taps; windows above the 36-KB slab in bands of bin rows.
+//    ds_read_b128 taps; windows above the 30-KB slab in bands of bin rows.
 //  * roi_align_fwd_band_kernel -- channels-last features (unit channel stride, C % 4
 //    == 0, sampling 2, 7x7 bins and smaller): small windows as the quad kernel (16-B
 //    LDS-DMA staging, lane = cell, one ds_read_b128 per tap for 4 channels), larger ones
@@ -45,12 +45,14 @@ namespace frh {
 // only 44.1-47.3 / 76-78 / 66-70; quad kernel (13 KB slab, pair order) 37.7-39.1 / 103-106 /
 // 96-98; round 4's 37.1-39.5 / 142 / 150.
 constexpr int kBandCells = 240;  // 15 KB: whole 1-KB DMA rounds, 10 workgroups per CU by LDS
-// The channel-group kernel's slab (round 6): 144 cells x 64 channels = 36 KB, 4 workgroups of 4
-// waves per CU (by LDS and by its 107 VGPRs alike); a 120-cell slab at 5 per CU needs <= 96 VGPRs
-// (spills: slower), 160 / 192 cells allow 3 per CU (slower).  Measured (tools/bench_roi_sets.py,
-// variants 80-93, µs per launch, bench / VOC / train RoIs): 32.4-34.3 / 56.6-58.6 / 51.0-53.0 vs
-// the band kernel's 38.7-39.2 / 67.4-68.3 / 58.2-59.6 on the same boxes, bit-identical.
-constexpr int kCgCells = 144;
+// The channel-group kernel's slab (round 6): 120 cells x 64 channels = 30 KB + the sample tables,
+// 5 workgroups of 4 waves per CU (by LDS, and by its 82 VGPRs at waves_per_eu 5: one sample row's
+// 8 tap reads in flight at a time).  Measured (tools/bench_roi_sets.py, lab variants 80-99, µs per
+// launch, bench / VOC / train RoIs, bit-identical): this form (variant 89) 32.5-34.3 / 56.6-58.5 /
+// 50.4-52.5; 144 cells at 4 per CU with both rows' reads in flight (variant 80, the first product
+// form) 33.5-35.5 / 58.9-61.5 / 53.3-55.2; the round-5 band kernel 38.7-42.1 / 67.4-72.7 /
+// 58.2-61.4.  120 cells hold the 4 tap-list rows of a 28-column window (cg_ok: 7 x 7 bins at most).
+constexpr int kCgCells = 120;
 static_assert(2 * kBandCells * 32 <= kBandCells * 64 && (kBandCells + 15) / 16 * 1024 <= kBandCells * 64,
               "the interleaved stages and the band DMA rounds must fit the slab");
 
@@ -188,9 +190,9 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
     FRH_REQUIRE(total <= (int64_t)0x7fffffff - 7, "too many RoIs");
     const dim3 grid((unsigned)(8 * ((total + 7) / 8)));
     if (span)
-      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, true>, grid, dim3(4 * kWave));
+      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, true, 5, false>, grid, dim3(4 * kWave));
     else
-      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, false>, grid, dim3(4 * kWave));
+      go(roi_align_fwd_cg_kernel<4, kCgCells, kCpolNT, false, 5, false>, grid, dim3(4 * kWave));
   } else if (quad_ok(f, lv, channels, pooled_h, pooled_w) && band_fits(pooled_h, pooled_w, kBandCells)) {
     // channels-last features (the FPN's NHWC levels): one wave per (RoI, 16 channels); tap
     // windows of <= 192 cells staged whole, 4 quads at a time ([quad][cell]); <= 480 cells
@@ -253,6 +255,12 @@ extern "C" int32_t frh_roi_align_fwd_strided_timed(int32_t num_levels, const flo
                  static_cast<hipEvent_t>(stop_event), reinterpret_cast<unsigned long long*>(span));
 }
 
+// The channels-last backward: 4 waves per (RoI, 64 channels), the RoI's tap rows split between
+// them (round 6; tools/bench_roi_bwd.py variants 9-12, µs per call incl. the clear, bench / voc /
+// train RoIs: one wave 236 / 500 / 400, 2 waves 177 / 438 / 365, 4 waves 153 / 401 / 338, 8 waves
+// 148 / 408 / 337; fixed point 390 -> 321 / 799 -> 721 / 702 -> 637)
+constexpr int kBwdWaves = 4;
+
 // channels-last gradient levels (unit channel stride), sampling 2, up to 8 x 8 bins: lane = channel
 static bool bwd_nhwc_ok(const RoiLevels& lv, int32_t sampling_ratio, int32_t ph, int32_t pw) {
   if (sampling_ratio != 2 || ph > 8 || pw > 8 || 4 * ph > kSepEnt || 4 * pw > kSepEnt) return false;
@@ -277,8 +285,9 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
   if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w))
-    hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<false>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),
-                       dim3(kWave), 0, as_stream(stream), lv, c, grad_out);
+    hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<false, kBwdWaves>),
+                       dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)), dim3(kBwdWaves * kWave), 0,
+                       as_stream(stream), lv, c, grad_out);
   else if (sampling_ratio == 2 && 4 * pooled_h <= kSepEnt && 4 * pooled_w <= kSepEnt)
     hipLaunchKernelGGL(roi_align_bwd_sep_kernel<false>, grid, dim3(kRoiThreads), 0, as_stream(stream), lv, c,
                        grad_out);
@@ -328,8 +337,9 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
                        scale_word);
     RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned, nullptr, scale_word, hb};
     if (bwd_nhwc_ok(lv, sampling_ratio, pooled_h, pooled_w)) {
-      hipLaunchKernelGGL(roi_align_bwd_nhwc_kernel<true>, dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)),
-                         dim3(kWave), 0, st, lv, c, grad_out);
+      hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<true, kBwdWaves>),
+                         dim3((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave)), dim3(kBwdWaves * kWave),
+                         0, st, lv, c, grad_out);
     } else {
       dim3 grid((unsigned)num_rois, (unsigned)((channels + kRoiChanChunk - 1) / kRoiChanChunk));
       hipLaunchKernelGGL(roi_align_bwd_sep_kernel<true>, grid, dim3(kRoiThreads), 0, st, lv, c, grad_out);

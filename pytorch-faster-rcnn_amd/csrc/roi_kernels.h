@@ -2413,27 +2413,38 @@ __global__ void __launch_bounds__(kRoiThreads) roi_align_bwd_sep_kernel(RoiLevel
 // the row's y entries, then per column cell = 0.25 * sum of wx * R[px] over the column's x
 // entries -- mathematically the reference's sum of g * (wy * wx) / count, in another order
 // (float atomics are run-order dependent anyway; the fixed-point form is order-independent).
-template <bool kFixed = false>
-__global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv, RoiCfg c,
-                                                                 const float* __restrict__ gout) {
+// kNW (round 6): a workgroup of kNW waves per (RoI, 64 channels) sharing the staged grad_out and
+// the sorted tap lists; wave w takes the RoI's distinct tap rows w, w + kNW, ... (the row loop was
+// one wave's serial chain -- 28 rows x 28 column entries on VOC-sized windows).  Each cell's sum
+// is the same as with one wave (same entries, same order): bit-identical per cell.
+template <bool kFixed = false, int kNW = 1>
+__global__ void __launch_bounds__(kNW * kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv, RoiCfg c,
+                                                                       const float* __restrict__ gout) {
   constexpr int kMaxP = 8;
-  __shared__ float gs[kMaxP * kMaxP * kWave];  // grad_out of the wave's channels, [bin][lane]
-  __shared__ float rs[kMaxP * kWave];          // the current row's sums, [px][lane]
-  __shared__ int ye[kSepEnt], xe[kSepEnt];     // sorted tap entries: position << 16 | bin index
+  __shared__ __attribute__((aligned(16))) float gs[kMaxP * kMaxP * kWave];  // grad_out of the 64 channels, [lane][bin]
+  __shared__ float rs_all[kNW][kMaxP * kWave];  // each wave's current row sums, [px][lane]
+  __shared__ int ye[kSepEnt], xe[kSepEnt];      // sorted tap entries: position << 16 | bin index
   __shared__ float yws[kSepEnt], xws[kSepEnt];
   const int64_t k = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = kNW == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  float* rs = rs_all[wave];
   const int c0 = blockIdx.y * kWave, ch = c0 + lane;
   const bool live = ch < c.C;
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl, H = lv.h[l], W = lv.w[l];
   const int ph = c.ph, pw = c.pw, nbins = ph * pw, nye = 4 * ph, nxe = 4 * pw;
-  {  // [K][C][bins] -> LDS [bin][lane]: the wave's 64 channels are one contiguous run
+  {  // [K][C][bins]: the 64 channels are one contiguous run, staged as it lies ([lane][bin]) by
+     // LDS-DMA, 256 B per instruction, every instruction in flight together (round 6: a load ->
+     // LDS-store loop left one global round trip per bin in series); channels past C read 0
     const float* go = gout + (k * c.C + c0) * nbins;
     const int nvalid = min(kWave, c.C - c0) * nbins;
-    for (int e = lane; e < kWave * nbins; e += kWave) {
-      const int cl = e / nbins, bin = e - cl * nbins;
-      gs[bin * kWave + cl] = e < nvalid ? go[e] : 0.0f;
+    const __amdgpu_buffer_rsrc_t gr = uniform_rsrc(go, (int64_t)nvalid * 4);
+    const uint32_t gsb = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)gs);
+    for (int i0 = wave; i0 < nbins; i0 += 32 * kNW) {
+      for (int i = i0; i < min(nbins, i0 + 32 * kNW); i += kNW)
+        lds_dma_at<4, 0>(gr, gsb + 256u * (uint32_t)i, lane * 4, i * 256);
+      wait_vmcnt<0>();
     }
   }
   // tap entry e of an axis: sample e / 2 (bin e / 4, sub-sample (e / 2) & 1), lo (e even) or hi
@@ -2448,36 +2459,48 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
   if (lane < nxe) entry(lane, g.start_w, g.bin_w, W, &xp, &xwv);
   if (lane >= nye) yp = -1;
   if (lane >= nxe) xp = -1;
-  const int ypm = yp < 0 ? (1 << 20) : yp, xpm = xp < 0 ? (1 << 20) : xp;
-  int yr = 0, xr = 0;  // rank by (position, entry)
-  for (int e = 0; e < nye; ++e) {
-    const int pe = __shfl(ypm, e, kWave);
-    yr += (pe < ypm || (pe == ypm && e < lane)) ? 1 : 0;
-  }
-  for (int e = 0; e < nxe; ++e) {
-    const int pe = __shfl(xpm, e, kWave);
-    xr += (pe < xpm || (pe == xpm && e < lane)) ? 1 : 0;
-  }
-  if (yp >= 0) ye[yr] = (yp << 16) | (lane >> 2), yws[yr] = ywv;
-  if (xp >= 0) xe[xr] = (xp << 16) | (lane >> 2), xws[xr] = xwv;
   const int nyv = __popcll(__ballot(yp >= 0)), nxv = __popcll(__ballot(xp >= 0));
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  if (wave == 0) {
+    const int ypm = yp < 0 ? (1 << 20) : yp, xpm = xp < 0 ? (1 << 20) : xp;
+    int yr = 0, xr = 0;  // rank by (position, entry)
+    for (int e = 0; e < nye; ++e) {
+      const int pe = __shfl(ypm, e, kWave);
+      yr += (pe < ypm || (pe == ypm && e < lane)) ? 1 : 0;
+    }
+    for (int e = 0; e < nxe; ++e) {
+      const int pe = __shfl(xpm, e, kWave);
+      xr += (pe < xpm || (pe == xpm && e < lane)) ? 1 : 0;
+    }
+    if (yp >= 0) ye[yr] = (yp << 16) | (lane >> 2), yws[yr] = ywv;
+    if (xp >= 0) xe[xr] = (xp << 16) | (lane >> 2), xws[xr] = xwv;
+  }
+  if constexpr (kNW > 1) {
+    __syncthreads();  // the staged grad_out (every wave's DMA) and wave 0's sorted lists
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient (uniform over the workgroup)
   const int64_t base = (int64_t)g.b * lv.sb[l] + ch, sy = lv.sy[l], sx = lv.sx[l];
   const double fscale = kFixed ? bwd_fixed_scale(c.fix_max, c.fix_hb) : 0.0;
   if (kFixed && fscale < 0.0) return;  // non-finite gradient: the conversion writes NaN
   float R[kMaxP];
 #pragma unroll
   for (int px = 0; px < kMaxP; ++px) R[px] = 0.0f;
+  int ro = 0;  // ordinal of the current distinct row: this wave's rows are ro % kNW == wave
   for (int i = 0; i < nyv; ++i) {
     const int yv = ye[i], row = yv >> 16, py = yv & 0xffff;
-    const float wy = yws[i];
+    const bool mine = kNW == 1 || ro % kNW == wave;
+    if (mine) {
+      const float wy = yws[i];
 #pragma unroll
-    for (int px = 0; px < kMaxP; ++px)
-      if (px < pw) R[px] = R[px] + wy * gs[(py * pw + px) * kWave + lane];
+      for (int px = 0; px < kMaxP; ++px)
+        if (px < pw) R[px] = R[px] + wy * gs[lane * nbins + py * pw + px];
+    }
     if (i + 1 < nyv && (ye[i + 1] >> 16) == row) continue;  // the row continues (uniform)
+    ++ro;
+    if (!mine) continue;
 #pragma unroll
     for (int px = 0; px < kMaxP; ++px)  // the lane's own slots: no wave sync needed
       if (px < pw) rs[px * kWave + lane] = R[px], R[px] = 0.0f;
@@ -2506,11 +2529,14 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc_kernel(RoiLevels lv,
 // from LDS in a dependent chain (two LDS round trips per (row, column) pair: ~50 us of serial
 // latency per wave on VOC-sized windows).  Same sums in the same order: each cell's
 // contribution is bit-identical to roi_align_bwd_nhwc_kernel's.
-template <bool kFixed = false>
+// kStore (tools-only diagnostic): plain stores instead of the atomics (wrong sums): the kernel's
+// time without the atomic traffic; kDiag (tools-only): 1 = no column loop (the row sums stored),
+// 2 = return after the tap-entry setup
+template <bool kFixed = false, bool kStore = false, int kDiag = 0>
 __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv, RoiCfg c,
                                                                   const float* __restrict__ gout) {
   constexpr int kMaxP = 8;
-  __shared__ float gs[kMaxP * kMaxP * kWave];  // grad_out of the wave's channels, [bin][lane]
+  __shared__ __attribute__((aligned(16))) float gs[kMaxP * kMaxP * kWave];  // grad_out, [lane][bin]
   __shared__ int ye[kSepEnt], xe[kSepEnt];     // sorted tap entries: position << 16 | bin index
   __shared__ float yws[kSepEnt], xws[kSepEnt];
   const int64_t k = blockIdx.x;
@@ -2520,12 +2546,15 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv
   const RoiGeom g = roi_geom(c, lv, k);
   const int l = g.lvl, H = lv.h[l], W = lv.w[l];
   const int ph = c.ph, pw = c.pw, nbins = ph * pw, nye = 4 * ph, nxe = 4 * pw;
-  {  // [K][C][bins] -> LDS [bin][lane]: the wave's 64 channels are one contiguous run
+  {  // the wave's contiguous [64][bins] grad_out block by LDS-DMA (as roi_align_bwd_nhwc_kernel)
     const float* go = gout + (k * c.C + c0) * nbins;
     const int nvalid = min(kWave, c.C - c0) * nbins;
-    for (int e = lane; e < kWave * nbins; e += kWave) {
-      const int cl = e / nbins, bin = e - cl * nbins;
-      gs[bin * kWave + cl] = e < nvalid ? go[e] : 0.0f;
+    const __amdgpu_buffer_rsrc_t gr = uniform_rsrc(go, (int64_t)nvalid * 4);
+    const uint32_t gsb = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)gs);
+    for (int i0 = 0; i0 < nbins; i0 += 32) {
+      const int i1 = min(nbins, i0 + 32);
+      for (int i = i0; i < i1; ++i) lds_dma_at<4, 0>(gr, gsb + 256u * (uint32_t)i, lane * 4, i * 256);
+      wait_vmcnt<0>();
     }
   }
   auto entry = [&](int e, float start, float bin, int size, int* pos, float* w) {
@@ -2556,6 +2585,10 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (nyv == 0 || nxv == 0) return;  // no valid tap: no gradient
+  if (kDiag == 2) {
+    if (ye[0] == 0x7fffffff) lv.grad[l][lane] = 1.0f;  // keep the setup alive
+    return;
+  }
   // lane i holds sorted entry i of each axis (read by v_readlane below)
   const int ye_l = lane < kSepEnt ? ye[lane] : 0, xe_l = lane < kSepEnt ? xe[lane] : 0;
   const float yw_l = lane < kSepEnt ? yws[lane] : 0.0f, xw_l = lane < kSepEnt ? xws[lane] : 0.0f;
@@ -2568,11 +2601,18 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv
   for (int i = 0; i < nyv; ++i) {
     const int yv = __builtin_amdgcn_readlane(ye_l, i), row = yv >> 16, py = yv & 0xffff;
     const float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yw_l), i));
-    const float* gr = gs + py * pw * kWave + lane;
+    const float* gr = gs + lane * nbins + py * pw;
 #pragma unroll
     for (int px = 0; px < kMaxP; ++px)
-      if (px < pw) R[px] = R[px] + wy * gr[px * kWave];
+      if (px < pw) R[px] = R[px] + wy * gr[px];
     if (i + 1 < nyv && (__builtin_amdgcn_readlane(ye_l, i + 1) >> 16) == row) continue;  // the row continues
+    if (kDiag == 1) {
+      float t = 0.0f;
+#pragma unroll
+      for (int px = 0; px < kMaxP; ++px) t = t + R[px], R[px] = 0.0f;
+      if (live) __builtin_nontemporal_store(t, lv.grad[l] + base + (int64_t)row * sy);
+      continue;
+    }
     float acc = 0.0f;
     for (int jx = 0; jx < nxv; ++jx) {
       const int xv = __builtin_amdgcn_readlane(xe_l, jx), col = xv >> 16, px = xv & 0xffff;
@@ -2586,7 +2626,9 @@ __global__ void __launch_bounds__(kWave) roi_align_bwd_nhwc2_kernel(RoiLevels lv
       acc = 0.0f;
       if (!live || v == 0.0f) continue;
       const int64_t e = base + (int64_t)row * sy + (int64_t)col * sx;
-      if constexpr (kFixed)
+      if constexpr (kStore)
+        __builtin_nontemporal_store(v, lv.grad[l] + e);
+      else if constexpr (kFixed)
         atomicAdd(reinterpret_cast<unsigned long long*>(lv.grad[l]) + e,
                   (unsigned long long)(long long)rint((double)v * fscale));
       else

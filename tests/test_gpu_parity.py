@@ -797,10 +797,10 @@ def _pathological_rois(batch):
 @pytest.mark.parametrize('pooled,C', [((7, 7), 64), ((7, 7), 192), ((4, 5), 128), ((8, 8), 64), ((1, 1), 64)])
 def test_roi_align_channel_group_kernel_vs_oracle(dev, pooled, C):
     """The channel-group forward (roi_align_fwd_cg_kernel: channels-last levels with C % 64 == 0,
-    one 4-wave workgroup per (RoI, 64 channels), 144-cell slab, bands of bin rows, list-row bands
+    one 4-wave workgroup per (RoI, 64 channels), 120-cell slab, bands of bin rows, list-row bands
     for bin rows spanning more rows than the slab holds) against the oracle, bit-identical: random
     RoIs over four levels (windows from 1 cell to 28 x 28, single- and multi-band), pathological
-    RoIs on a 10 x 30 level, pooled sizes 1x1 .. 8x8."""
+    RoIs on a 10 x 30 level, pooled sizes 1x1 .. 7x7 (8x8: the band kernel, cg_ok)."""
     from frcnn_amd import ops
     grids = [(76, 128), (38, 64), (19, 32), (10, 30)]
     feats = inputs.feature_maps(60, grids, C, 2)

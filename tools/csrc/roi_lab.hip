@@ -340,7 +340,7 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
                                              uint32_t* scale_word, void* stream) {
   int32_t r = roi_common_checks(batch, channels, num_rois, 7, 7, rois);
   if (r) return r;
-  const bool fixed = variant == 2 || variant == 3 || variant == 5;
+  const bool fixed = variant == 2 || variant == 3 || variant == 5 || variant == 12;
   RoiLevels lv;
   r = make_levels(num_levels, nullptr, fixed ? reinterpret_cast<float* const*>(acc_feats) : grad_feats, feat_hw,
                   strides, scales, &lv);
@@ -369,6 +369,23 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
     hipLaunchKernelGGL(roi_align_bwd_nhwc2_kernel<false>, grid, dim3(kWave), 0, st, lv, c, grad_out);
   else if (variant == 5)
     hipLaunchKernelGGL(roi_align_bwd_nhwc2_kernel<true>, grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 6)  // diagnostic: variant 4 with plain stores instead of atomics (wrong sums)
+    hipLaunchKernelGGL((roi_align_bwd_nhwc2_kernel<false, true>), grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 9 || variant == 10 || variant == 11 || variant == 12) {  // product kernel, kNW waves per RoI
+    const dim3 gw((unsigned)num_rois, (unsigned)((channels + kWave - 1) / kWave));
+    if (variant == 9)
+      hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<false, 2>), gw, dim3(2 * kWave), 0, st, lv, c, grad_out);
+    else if (variant == 10)
+      hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<false, 4>), gw, dim3(4 * kWave), 0, st, lv, c, grad_out);
+    else if (variant == 11)
+      hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<false, 8>), gw, dim3(8 * kWave), 0, st, lv, c, grad_out);
+    else
+      hipLaunchKernelGGL((roi_align_bwd_nhwc_kernel<true, 4>), gw, dim3(4 * kWave), 0, st, lv, c, grad_out);
+  }
+  else if (variant == 7)  // diagnostic: no column loop (row sums stored)
+    hipLaunchKernelGGL((roi_align_bwd_nhwc2_kernel<false, true, 1>), grid, dim3(kWave), 0, st, lv, c, grad_out);
+  else if (variant == 8)  // diagnostic: setup only (grad_out staging, tap entries, ranks)
+    hipLaunchKernelGGL((roi_align_bwd_nhwc2_kernel<false, true, 2>), grid, dim3(kWave), 0, st, lv, c, grad_out);
   else
     FRH_REQUIRE(false, "backward variant %d unknown", variant);
   if (fixed) {
