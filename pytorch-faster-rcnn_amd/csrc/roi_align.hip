@@ -65,7 +65,7 @@ __device__ __forceinline__ int64_t roi_level_of(float x1, float y1, float x2, fl
   float lg = (float)log2((double)v);
   float fl = floorf(lg);
   float hi = (float)(L - 1);
-  fl = fl < 0.0f ? 0.0f : (fl > hi ? hi : fl);
+  fl = !(fl >= 0.0f) ? 0.0f : (fl > hi ? hi : fl);  // NaN (NaN coordinates): level 0
   return (int64_t)fl;
 }
 
@@ -172,6 +172,7 @@ static int32_t roi_fwd(int32_t num_levels, const float* const* feats, const int3
   RoiLevels lv;
   r = make_levels(num_levels, feats, nullptr, feat_hw, strides, scales, &lv);
   if (r) return r;
+  lv.B = batch;
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned, span};
   const FwdCaps f = fwd_caps(lv, channels, pooled_h, pooled_w, sampling_ratio);
@@ -280,6 +281,7 @@ extern "C" int32_t frh_roi_align_bwd_strided(int32_t num_levels, float* const* g
   RoiLevels lv;
   r = make_levels(num_levels, nullptr, grad_feats, feat_hw, strides, scales, &lv);
   if (r) return r;
+  lv.B = batch;
   if (num_rois == 0) return FRH_OK;
   FRH_REQUIRE(grad_feats && grad_out, "null pointer argument");
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
@@ -313,6 +315,7 @@ extern "C" int32_t frh_roi_align_bwd_fixed(int32_t num_levels, float* const* gra
   // the kernel adds into the accumulators through lv.grad (same element strides)
   r = make_levels(num_levels, nullptr, reinterpret_cast<float* const*>(acc_feats), feat_hw, strides, scales, &lv);
   if (r) return r;
+  lv.B = batch;
   hipStream_t st = as_stream(stream);
   int64_t numel[FRH_MAX_LEVELS];
   for (int l = 0; l < num_levels; ++l) {

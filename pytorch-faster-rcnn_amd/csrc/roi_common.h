@@ -14,7 +14,19 @@ struct RoiLevels {
   int64_t sb[FRH_MAX_LEVELS], sc[FRH_MAX_LEVELS], sy[FRH_MAX_LEVELS], sx[FRH_MAX_LEVELS];
   float scale[FRH_MAX_LEVELS];
   int L;
+  int B;  // images in the batch (make_levels: no limit until the entry sets it)
 };
+
+// A RoI's image and level as indices the feature descriptors can address whatever the RoI rows
+// hold: a batch index outside [0, B) or NaN and a level outside [0, L) are clamped (the reference
+// would raise an IndexError; a C-ABI kernel must not address outside its tensors -- e.g. the rows
+// of an aborted proposal call, NaN coordinates, reach here with garbage in them).
+__device__ __forceinline__ int roi_image(const RoiLevels& lv, float b) {
+  return b >= 0.0f ? (b < (float)lv.B ? (int)b : lv.B - 1) : 0;  // NaN: 0
+}
+__device__ __forceinline__ int roi_level(const RoiLevels& lv, int64_t l) {
+  return l < 0 ? 0 : (l >= lv.L ? lv.L - 1 : (int)l);
+}
 
 struct RoiCfg {
   const float* rois;         // [K, 5]
@@ -78,8 +90,8 @@ struct RoiGeom {
 __device__ __forceinline__ RoiGeom roi_geom(const RoiCfg& c, const RoiLevels& lv, int64_t k) {
   RoiGeom g;
   const float* r = c.rois + k * 5;
-  g.b = (int)r[0];
-  g.lvl = c.levels ? (int)c.levels[k] : 0;
+  g.b = roi_image(lv, r[0]);
+  g.lvl = c.levels ? roi_level(lv, c.levels[k]) : 0;
   const float sc = lv.scale[g.lvl];
   const float off = c.aligned ? 0.5f : 0.0f;
   float sw = r[1] * sc - off, sh = r[2] * sc - off;
@@ -172,8 +184,8 @@ __device__ __forceinline__ void roi_fetch2(const RoiCfg& c, int64_t k0, int64_t 
 // roi_geom from a fetched RoI
 __device__ __forceinline__ RoiGeom roi_geom_raw(const RoiCfg& c, const RoiLevels& lv, const RoiRaw& rr) {
   RoiGeom g;
-  g.b = (int)rr.r0;
-  g.lvl = rr.lvl;
+  g.b = roi_image(lv, rr.r0);
+  g.lvl = roi_level(lv, rr.lvl);
   const float sc = lv.scale[g.lvl];
   const float off = c.aligned ? 0.5f : 0.0f;
   float sw = rr.r1 * sc - off, sh = rr.r2 * sc - off;

@@ -2844,6 +2844,7 @@ static inline int32_t make_levels(int32_t L, const float* const* feats, float* c
   FRH_REQUIRE(L >= 1 && L <= FRH_MAX_LEVELS, "num_levels %d out of range", L);
   FRH_REQUIRE(feat_hw && scales && strides, "null pointer argument");
   lv->L = L;
+  lv->B = 0x7fffffff;  // the entry points set the batch size (roi_image)
   for (int l = 0; l < L; ++l) {
     lv->feat[l] = feats ? feats[l] : nullptr;
     lv->grad[l] = grads ? grads[l] : nullptr;

@@ -21,6 +21,7 @@ extern "C" int32_t frh_roi_align_fwd_variant(int32_t variant, int32_t num_levels
   RoiLevels lv;
   r = make_levels(num_levels, feats, nullptr, feat_hw, strides, scales, &lv);
   if (r) return r;
+  lv.B = batch;
   if (num_rois == 0) return FRH_OK;
   RoiCfg c{rois, roi_levels, num_rois, channels, pooled_h, pooled_w, sampling_ratio, aligned};
   hipStream_t st = as_stream(stream);
@@ -345,6 +346,7 @@ extern "C" int32_t frh_roi_align_bwd_variant(int32_t variant, int32_t num_levels
   r = make_levels(num_levels, nullptr, fixed ? reinterpret_cast<float* const*>(acc_feats) : grad_feats, feat_hw,
                   strides, scales, &lv);
   if (r) return r;
+  lv.B = batch;
   for (int l = 0; l < lv.L; ++l) FRH_REQUIRE(lv.sc[l] == 1, "channels-last gradients only");
   hipStream_t st = as_stream(stream);
   int hb = 0;
