@@ -61,6 +61,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # in-step kernel groups of the detection path (substrings of the dispatched kernel names)
 KERNEL_GROUPS = [
     ('roi_align_fwd', ('roi_align_fwd',)),
+    ('roi_align_bwd', ('roi_align_bwd', 'roi_bwd_')),
     ('nms', ('nms_fused_kernel', 'nms_mask_kernel', 'nms_scan_kernel')),
     ('proposals', ('rpn_select', 'rpn_keys', 'rpn_refine', 'rpn_collect', 'rpn_rank', 'rpn_merge')),
     ('assign', ('assign_',)),
@@ -117,6 +118,19 @@ def roi_align_bytes(rec):
     used = torch.unique(bidx * 64 + lv).cpu().tolist()
     feat_elems = sum(shapes[u % 64][2] * shapes[u % 64][3] for u in used)
     return 4 * C * (K * ph * pw + feat_elems) + 20 * K
+
+
+def roi_align_bwd_bytes(rec):
+    """Algorithmic bytes of one RoIAlign backward kernel: the grad_out read
+    4*C*sum_K ph*pw plus one accumulated write per feature cell of the levels holding RoIs,
+    4*C*sum H_l*W_l (the gradient clear before it is a separate fill; tools/bench_roi_bwd.py, which
+    times the call with its clear, counts that write twice)."""
+    _, _, rois, levels, shapes, (ph, pw) = rec[:6]
+    K, C = rois.shape[0], shapes[0][1]
+    bidx = rois[:, 0].long()
+    lv = levels if levels is not None else torch.zeros_like(bidx)
+    used = torch.unique(bidx * 64 + lv).cpu().tolist()
+    return 4 * C * (K * ph * pw + sum(shapes[u % 64][2] * shapes[u % 64][3] for u in used))
 
 
 # ------------------------------------------------------------------ in-step kernel trace
@@ -895,6 +909,12 @@ def main():
                 for g in ('sampler', 'targets', 'losses'):
                     lines[g] = {'us_per_step': per_group.get(g)}
             lines['roi_align_fwd'] = {'us_per_step': per_group.get('roi_align_fwd')}
+            if args.mode == 'train':  # the backward launch of the step (channels-last: 4 waves per RoI)
+                lines['roi_align_bwd'] = line(
+                    per_group.get('roi_align_bwd'),
+                    float(np.mean([roi_align_bwd_bytes(r) for r in recs])) if recs else None,
+                    '4*C*sum_K*ph*pw grad_out read + 4*C*sum H_l*W_l (one accumulated write per level cell); the '
+                    'kernel only (the clear is a separate fill); float atomics')
             out['kernels'] = {'per_step': lines, 'detection_path_us_per_step': det_us,
                               'device_timeline': TRACE_TIMELINE,
                               'detection_path_kernels_us_per_step': det_kernels, 'dispatched': group_names,
