@@ -206,6 +206,31 @@ __device__ __forceinline__ RoiGeom roi_geom_raw(const RoiCfg& c, const RoiLevels
   return g;
 }
 
+// roi_geom_raw with the level and its scale already picked (same arithmetic)
+__device__ __forceinline__ RoiGeom roi_geom_scaled(const RoiCfg& c, const RoiLevels& lv, const RoiRaw& rr, int lvl,
+                                                  float sc) {
+  RoiGeom g;
+  g.b = roi_image(lv, rr.r0);
+  g.lvl = lvl;
+  const float off = c.aligned ? 0.5f : 0.0f;
+  float sw = rr.r1 * sc - off, sh = rr.r2 * sc - off;
+  float ew = rr.r3 * sc - off, eh = rr.r4 * sc - off;
+  float rw = ew - sw, rh = eh - sh;
+  if (!c.aligned) {
+    rw = fmaxf(rw, 1.0f);
+    rh = fmaxf(rh, 1.0f);
+  }
+  g.start_w = sw;
+  g.start_h = sh;
+  g.bin_h = rh / (float)c.ph;
+  g.bin_w = rw / (float)c.pw;
+  g.gh = c.sampling > 0 ? c.sampling : (int)ceilf(rh / (float)c.ph);
+  g.gw = c.sampling > 0 ? c.sampling : (int)ceilf(rw / (float)c.pw);
+  int cnt = g.gh * g.gw;
+  g.count = (float)(cnt > 1 ? cnt : 1);
+  return g;
+}
+
 // fill the separable sample tables: rows [ph*gh], cols [pw*gw]
 __device__ __forceinline__ float sample_y(const RoiGeom& g, int p, int i) {
   return g.start_h + (float)p * g.bin_h + ((float)i + 0.5f) * g.bin_h / (float)g.gh;

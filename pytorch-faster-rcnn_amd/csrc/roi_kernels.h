@@ -1523,12 +1523,26 @@ roi_align_fwd_cg_kernel(RoiLevels lv, RoiCfg c, float* __restrict__ out) {
   const int nbins = c.ph * c.pw;
   const int nq = nbins * kCgChan / 4;  // 16-B units of the item's output block
   const __amdgpu_buffer_rsrc_t orr = uniform_rsrc(out + (k * c.C + (int64_t)grp * kCgChan) * nbins, (int64_t)nq * 16);
+  // levels 0-3's parameters at constant offsets: loaded with the kernel's other arguments, in
+  // flight together with the RoI record, then picked by the RoI's level (a uniform select) --
+  // indexed by the level, they were a second scalar round trip after the record's
+  float sc4[4];
+  int h4[4], w4[4], sy4[4], sx4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    sc4[q] = lv.scale[q], h4[q] = lv.h[q], w4[q] = lv.w[q], sy4[q] = (int)lv.sy[q], sx4[q] = (int)lv.sx[q];
   const RoiRaw raw = roi_fetch(c, k);
   if (kStamp) t_rec = (int64_t)__builtin_amdgcn_s_memrealtime();
-  const RoiGeom g = roi_geom_raw(c, lv, raw);
-  const int l = g.lvl;
-  const int H = lv.h[l], W = lv.w[l];
-  const int sy = (int)lv.sy[l], sx = (int)lv.sx[l];
+  const int l = roi_level(lv, raw.lvl);
+  float scl;
+  int H, W, sy, sx;
+  if (l < 4) {
+    auto pk = [&](const auto (&a)[4]) { return l == 0 ? a[0] : l == 1 ? a[1] : l == 2 ? a[2] : a[3]; };
+    scl = pk(sc4), H = pk(h4), W = pk(w4), sy = pk(sy4), sx = pk(sx4);
+  } else {
+    scl = lv.scale[l], H = lv.h[l], W = lv.w[l], sy = (int)lv.sy[l], sx = (int)lv.sx[l];
+  }
+  const RoiGeom g = roi_geom_scaled(c, lv, raw, l, scl);
   // tap-list entries: lanes [0, 32) along y, [32, 64) along x; entry e = tap (e & 1 ? hi : lo) of sample e / 2
   const bool isx = lane >= 32;
   const int e = lane & 31;

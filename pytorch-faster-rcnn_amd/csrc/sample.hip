@@ -688,6 +688,7 @@ __global__ void __launch_bounds__(kSsThreads) sampler_small_kernel(const int64_t
     } else {  // the first pl.k tied keys by ascending box (box = r * kSsThreads + t)
       int before = 0;
       for (int r = 0; r < kSsPer; ++r) {
+        if (r * kSsThreads >= n) break;  // uniform: rounds past the image's boxes hold no key
         int tot;
         const bool f = (tie >> r) & 1u;
         const int rk = block_rank(f, part, &tot);
@@ -700,6 +701,7 @@ __global__ void __launch_bounds__(kSsThreads) sampler_small_kernel(const int64_t
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kSsPer; ++r) {
+    if (r * kSsThreads >= n) break;  // uniform (the RCNN stage's ~2000 rows: 2 of 16 rounds)
     const int i = r * kSsThreads + t;
     const bool tk = (take >> r) & 1u;
     const bool mine = w == 0 ? lab[r] != 0 : lab[r] == 0;  // positives + ignored, or negatives
