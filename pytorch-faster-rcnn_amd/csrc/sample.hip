@@ -326,7 +326,19 @@ struct SampFused {
   int32_t* sel_cnt;  // [S][2]
   int64_t* stamps;   // tools timing only (null in the product): 16 int64 per workgroup
   int32_t* status;   // the caller's device status word (FRH_DEVERR_SAMPLER_BARRIER)
+  uint64_t* spec;      // [S][2][nchunk][kSpecCap] the chunk's window records: key << 32 | ~box
+  int32_t* part_spec;  // [S][nchunk] the chunk's negatives in the key window
 };
+
+// Window records (round 6): every positive and every negative whose key has its top kSpecBits
+// bits set (1/64 of the uniform keys) is written, per chunk, as (key << 32 | ~box) to the
+// chunk's own record row.  After the first barrier, when the window holds the whole selection
+// -- at least kn negatives in it (or all of them), every positive listed, no chunk row and no
+// class above the LDS capacity -- the k largest records of each class are exactly the
+// selection, and two workgroups finish the call from the records alone (fast path); otherwise
+// every workgroup goes on with the histogram phases 2-4.
+constexpr int kSpecBits = 6;
+constexpr int kSpecCap = 256;  // records per chunk row and class
 
 __device__ __forceinline__ uint32_t samp_key(uint64_t seed, int v, int i, bool cand) {
   return cand ? ((~hash_u32(seed, (uint32_t)v, (uint32_t)i)) | 1u) : 0u;
@@ -383,8 +395,35 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     cn += neg;
   }
   stamp(1);
-  cp = block_sum(cp, sm.part);
-  cn = block_sum(cn, sm.part);
+  uint32_t specm = posm;
+#pragma unroll
+  for (int r = 0; r < kTkPerThread; ++r)
+    specm |= (((negm >> r) & 1u) && (key[r] >> (32 - kSpecBits)) == (1u << kSpecBits) - 1u) ? 1u << r : 0u;
+  const int4 c4 = block_sum4(make_int4(cp, cn, __popc(specm & negm), 0), sm.fb.wave_tot);
+  cp = c4.x;
+  cn = c4.y;
+  {
+    // this chunk's window records, in thread order (rows past kSpecCap are not written: such a
+    // chunk sends the call to the histogram phases)
+    const int4 o = block_offsets4(__popc(posm), __popc(specm & negm), 0, 0, make_int4(0, 0, 0, 0), sm.part);
+    uint64_t* rp = f.spec + ((int64_t)(2 * s) * f.nchunk + x) * kSpecCap;
+    uint64_t* rn = rp + (int64_t)f.nchunk * kSpecCap;
+    int qp = o.x, qn = o.y;
+#pragma unroll
+    for (int r = 0; r < kTkPerThread; ++r) {
+      if (!((specm >> r) & 1u)) continue;
+      const int i = base + r * kTkThreads + t;
+      const uint64_t rec = ((uint64_t)key[r] << 32) | (uint32_t)~(uint32_t)i;
+      if ((posm >> r) & 1u) {
+        if (qp < kSpecCap) xwg_store(rp + qp, rec);
+        ++qp;
+      } else {
+        if (qn < kSpecCap) xwg_store(rn + qn, rec);
+        ++qn;
+      }
+    }
+    if (t == 0) xwg_store(reinterpret_cast<uint32_t*>(f.part_spec) + (int64_t)s * f.nchunk + x, (uint32_t)c4.z);
+  }
   // this chunk's histograms and counts, write-through (one store per bin: no atomics on
   // the 256 hot bins of an image, which every chunk's uniform keys fill)
   uint32_t* ph = f.part_hist + (int64_t)(2 * s) * f.nchunk * kSampBins;  // [2][nchunk][bins]
@@ -396,9 +435,103 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   for (int i = t; i < 2 * kSampBins; i += kTkThreads)
     xwg_store(ph + ((int64_t)(i / kSampBins) * f.nchunk + x) * kSampBins + (i % kSampBins), hc[i]);
   stamp(2);
-  if (status0 != 0) return;
-  if (!seg_barrier(bar, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return;
+  // a call that cannot finish leaves defined (memory-safe) outputs all the same: the boxes of
+  // `m` get label -1, and workgroup 0 lists nothing
+  auto bail = [&](uint32_t m) {
+    if (lo) {
+#pragma unroll
+      for (int r = 0; r < kTkPerThread; ++r) {
+        const int i = base + r * kTkThreads + t;
+        if (i < n && ((m >> r) & 1u)) lo[i] = -1;
+      }
+    }
+    if (x == 0 && f.sel_cnt && t < 2) f.sel_cnt[2 * s + t] = 0;
+  };
+  if (status0 != 0) return bail(~0u);
+  if (!seg_barrier(bar, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return bail(~0u);
   stamp(3);
+  // the last workgroup out leaves the image's zero region zero
+  auto leave = [&]() {
+    stamp(7);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
+    __syncthreads();
+    if (sm.last && t < 2 * TK_WORDS) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
+    if (sm.last && t < 2) xwg_store(reinterpret_cast<uint32_t*>(bar) + t, 0u);
+    stamp(8);
+  };
+
+  // ---- fast path: the window records hold the selection (G <= kTkThreads: the host admits at
+  // most 256 workgroups)
+  {
+    const int32_t* psn = f.part_spec + (int64_t)s * f.nchunk;
+    const int cpv = t < G ? xwg_load(pc + t) : 0, cnv = t < G ? xwg_load(pc + f.nchunk + t) : 0;
+    const int snv = t < G ? xwg_load(psn + t) : 0;
+    const int4 tot = block_sum4(make_int4(cpv, cnv, snv, (cpv > kSpecCap || snv > kSpecCap) ? 1 : 0), sm.fb.wave_tot);
+    const int npos = tot.x, nneg = tot.y, nspec = tot.z;
+    const int kp = npos < pos_num ? npos : pos_num;
+    const int kn = nneg < max_num - kp ? nneg : max_num - kp;
+    const bool okp = npos <= kTkCandCap;
+    const bool okn = kn <= 0 || (nspec <= kTkCandCap && (kn < nneg ? nspec >= kn : nspec == nneg));
+    if (G <= kTkThreads && tot.w == 0 && okp && okn) {
+      stamp(9);
+      if (lo) {  // boxes outside the window: never selected
+#pragma unroll
+        for (int r = 0; r < kTkPerThread; ++r) {
+          const int i = base + r * kTkThreads + t;
+          if (i < n && !((specm >> r) & 1u)) lo[i] = -1;
+        }
+      }
+      for (int c = 0; c < 2; ++c) {
+        if (x != (c < G ? c : 0)) continue;
+        const int v = 2 * s + c, kv = c ? kn : kp, nc = c ? nspec : npos;
+        if (f.sel_cnt && t == 0) f.sel_cnt[v] = kv > 0 ? kv : 0;
+        if (nc == 0) continue;
+        // the class's records from every chunk row into LDS (row offsets: an exclusive scan of the
+        // row counts, then a binary search per record)
+        const int4 o = block_offsets4(c ? snv : cpv, 0, 0, 0, make_int4(0, 0, 0, 0), sm.part);
+        if (t < G) hc[t] = (uint32_t)o.x;
+        __syncthreads();
+        const uint64_t* rows = f.spec + (int64_t)v * f.nchunk * kSpecCap;
+        uint64_t rec[kTkPerThread];
+#pragma unroll
+        for (int r = 0; r < kTkPerThread; ++r) {
+          const int q = r * kTkThreads + t;
+          int lo_j = 0, hi_j = G - 1;
+          while (lo_j < hi_j) {
+            const int mid = (lo_j + hi_j + 1) >> 1;
+            if ((int)hc[mid] <= q) lo_j = mid; else hi_j = mid - 1;
+          }
+          rec[r] = q < nc ? xwg_load(rows + (int64_t)lo_j * kSpecCap + (q - (int)hc[lo_j])) : 0ull;
+        }
+#pragma unroll
+        for (int r = 0; r < kTkPerThread; ++r) {
+          const int q = r * kTkThreads + t;
+          if (q < nc) sm.cand[q] = rec[r];
+        }
+        __syncthreads();
+        const bool all = kv >= nc;
+        LdsCut cut{0ull, 0};
+        if (kv > 0 && !all)
+          cut = c ? lds_topk_cut(sm.cand, nc, kv, 64 - kSpecBits, ((1ull << kSpecBits) - 1ull) << (64 - kSpecBits), sm)
+                  : lds_topk_cut(sm.cand, nc, kv, 64, 0ull, sm);
+        if (t == 0) sm.fb.cnt_gt = 0;
+        __syncthreads();
+        int32_t* sl = f.sel ? f.sel + (int64_t)v * f.sel_ld : nullptr;
+        for (int q = t; q < nc; q += kTkThreads) {
+          const uint64_t e = sm.cand[q];
+          const int i = (int)~(uint32_t)e;
+          const bool tk = kv > 0 && (all || (e >> cut.sh) >= (cut.P >> cut.sh));
+          if (lo) lo[i] = tk ? (c ? (int64_t)0 : li[i]) : (int64_t)-1;
+          if (sl && tk) sl[atomicAdd(&sm.fb.cnt_gt, 1)] = i;
+        }
+        __syncthreads();  // sm.cand, hc reused by the other class
+      }
+      leave();
+      return;
+    }
+  }
 
   // ---- phase 2: the image's counts and histograms, summed over its chunks (bin t per thread)
   // the count loads (threads < G) and the first 2 x kSampBatch chunk-histogram loads are issued
@@ -490,7 +623,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
   }
   const bool ties = (pl[0].kv > 0 && !pl[0].all) || (pl[1].kv > 0 && !pl[1].all);
   stamp(5);
-  if (ties && !seg_barrier(bar + 1, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return;
+  if (ties && !seg_barrier(bar + 1, G, f.status, FRH_DEVERR_SAMPLER_BARRIER)) return bail(tie);
   stamp(6);
 
   // ---- phase 4: the prefix ties, positives by workgroup 0, negatives by workgroup 1 (0 if alone)
@@ -553,15 +686,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
     }
   }
 
-  // ---- exit: the last workgroup out leaves the image's zero region zero
-  stamp(7);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) sm.last = atomicAdd(st + TK_DONE1, 1) == G - 1;
-  __syncthreads();
-  if (sm.last && t < 2 * TK_WORDS) xwg_store(reinterpret_cast<uint32_t*>(st) + t, 0u);
-  if (sm.last && t < 2) xwg_store(reinterpret_cast<uint32_t*>(bar) + t, 0u);
-  stamp(8);
+  leave();
 }
 
 // Small images (num_boxes <= kSsMax, e.g. the RCNN stage's ~2000 proposal rows): the whole
@@ -744,7 +869,7 @@ using namespace frh;
 static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct SampLayout {
-  size_t keys, cand, state, phist, pcount, total;
+  size_t keys, cand, state, phist, pcount, spec, pspec, total;
   int64_t kld;
   int nchunk;
 };
@@ -769,7 +894,9 @@ static SampLayout samp_layout(int32_t S, int64_t max_boxes) {
   z.state = z.cand + al256((size_t)V * n * sizeof(uint64_t));
   z.phist = z.state + al256((size_t)V * TK_WORDS * sizeof(int32_t));
   z.pcount = z.phist + al256((size_t)V * z.nchunk * kSampBins * sizeof(uint32_t));
-  z.total = z.pcount + al256((size_t)V * z.nchunk * sizeof(int32_t));
+  z.spec = z.pcount + al256((size_t)V * z.nchunk * sizeof(int32_t));
+  z.pspec = z.spec + al256((size_t)V * z.nchunk * kSpecCap * sizeof(uint64_t));
+  z.total = z.pspec + al256((size_t)S * z.nchunk * sizeof(int32_t));
   return z;
 }
 
@@ -862,7 +989,8 @@ int32_t frh::sample_random_impl(int32_t num_segs, const int64_t* labels_in, int6
       (int64_t)num_segs * z.nchunk <= resident_capacity(reinterpret_cast<const void*>(sampler_fused_kernel), kTkThreads) / 2) {
     SampFused f{reinterpret_cast<uint32_t*>(ws + z.phist), reinterpret_cast<int32_t*>(ws + z.pcount), z.nchunk,
                 reinterpret_cast<int32_t*>(ws), reinterpret_cast<uint64_t*>(ws + z.cand), z.kld, sel,
-                (int64_t)(max_num > 0 ? max_num : 1), sel_counts, stamps, status};
+                (int64_t)(max_num > 0 ? max_num : 1), sel_counts, stamps, status,
+                reinterpret_cast<uint64_t*>(ws + z.spec), reinterpret_cast<int32_t*>(ws + z.pspec)};
     hipLaunchKernelGGL(sampler_fused_kernel, dim3((unsigned)z.nchunk, (unsigned)num_segs), dim3(kTkThreads), 0, st,
                        labels_in, label_seg_stride, num_boxes, max_num, pos_num, seed, f, labels_out);
     return check_launch("frh_sample_random");

@@ -346,7 +346,7 @@ __device__ __forceinline__ bool seg_barrier(int32_t* counter, int target, int32_
 
 // ------------------------------------------------- top-k of a small LDS list
 // The k largest (1 <= k <= n) of n DISTINCT u64 values v[0..n) in LDS whose bits above
-// `top` all equal those of P0: radix passes of 8 bits downwards from `top`, each an LDS
+// `top` (<= 64) all equal those of P0: radix passes of 8 bits downwards from `top`, each an LDS
 // histogram (sm.fb.hist) of the values still matching the prefix + tk_find, stopping as soon
 // as the bin holding the k-th value is taken whole.  v is taken iff (v >> sh) >= (P >> sh).
 // No sort: a few passes where a bitonic network over n takes log2(n)^2 / 2 barriers.
@@ -364,7 +364,7 @@ __device__ LdsCut lds_topk_cut(const uint64_t* v, int n, int k, int top, uint64_
     __syncthreads();
     for (int j = t; j < n; j += nt) {
       const uint64_t x = v[j];
-      if ((x >> (sh + 8)) == (P >> (sh + 8))) atomicAdd(&sm.fb.hist[(x >> sh) & 255u], 1u);
+      if (sh + 8 >= 64 || (x >> (sh + 8)) == (P >> (sh + 8))) atomicAdd(&sm.fb.hist[(x >> sh) & 255u], 1u);
     }
     __syncthreads();
     tk_find(sm, 256, krem, [&](int i) { return sm.fb.hist[i]; });

@@ -190,12 +190,18 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
   __syncthreads();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= cnt) return;
-  const int32_t x = min(max(su[j], 0), (int32_t)(lim > 0 ? lim - 1 : 0));
+  // rank among the listed values, equal values by list position: a permutation of [0, cnt)
+  // whatever the lists hold (a valid selection lists distinct boxes; the lists of an aborted
+  // call -- status word set -- may repeat values, and every output row must still be written)
+  const int32_t raw = su[j];
+  const int32_t x = min(max(raw, 0), (int32_t)(lim > 0 ? lim - 1 : 0));
   int rank = 0;
   const int4* s4 = reinterpret_cast<const int4*>(su);
   for (int q = 0; q < cnt4 / 4; ++q) {
     const int4 v = s4[q];
-    rank += (v.x < x) + (v.y < x) + (v.z < x) + (v.w < x);
+    const int e = 4 * q;
+    rank += (v.x < raw) + (v.y < raw) + (v.z < raw) + (v.w < raw);
+    rank += (v.x == raw && e < j) + (v.y == raw && e + 1 < j) + (v.z == raw && e + 2 < j) + (v.w == raw && e + 3 < j);
   }
   item(s, (int64_t)x, off + rank);
 }

@@ -214,3 +214,45 @@ def test_sampler_workspace_reuse_across_num_segs_and_paths(dev):
     ops.check_device_status(dev)
     assert torch.equal(fresh, reused)
     ops.set_sampler_mode('numpy')
+
+
+@pytest.mark.parametrize('n,max_num,pos_num,p,fast', [
+    (155520, 256, 128, [0.30, 0.68, 0.01, 0.005, 0.005], True),    # cfg2 RPN: positives cut in the window
+    (155520, 256, 128, [0.30, 0.6999, 0.0001, 0.0, 0.0], True),   # few positives: all taken
+    (40000, 512, 128, [0.3, 0.6, 0.04, 0.03, 0.03], False),       # > 256 positives in a chunk row
+    (20000, 256, 128, [0.999, 0.0005, 0.0005, 0.0, 0.0], False),  # every negative taken, few in the window
+])
+def test_sampler_window_fast_path(dev, n, max_num, pos_num, p, fast):
+    """The one-launch sampler's window-record path (round 6) is the one taken when the window
+    holds the selection, and the histogram phases otherwise (stamp 9 of every workgroup of the
+    tools timing build); either way the result equals the keys + collect launches."""
+    from frcnn_amd import ops, _lib
+    lib = _tools()
+    S = 2
+    rng = np.random.default_rng(n + max_num)
+    lab = torch.from_numpy(_labels(rng, S, n, p)).to(dev)
+    num = torch.full((S,), n, dtype=torch.int32, device=dev)
+    sst = torch.zeros(S, (n + 4095) // 4096, 16, dtype=torch.int64, device=dev)
+
+    def stamped(*a):
+        a = list(a)
+        stream = a.pop()
+        return lib.frh_sample_random_stamped(*a, _lib.ptr(sst), stream)
+    res = []
+    for entry in ((stamped, 'stamped'), (lib.frh_sample_random_launches, 'frh_sample_random_launches')):
+        for lists in (False, True):
+            ops.set_sampler_mode('device', seed=77)
+            res.append(ops.sample_labels(lab, num, n, max_num, pos_num, mode='device', lists=lists, _entry=entry))
+    a_lab, a_sl, b_lab, b_sl = res
+    torch.cuda.synchronize()
+    ops.check_device_status(dev)
+    st = sst.cpu().numpy()
+    assert (st[:, :, 0] > 0).all()
+    assert bool((st[:, :, 9] > 0).all()) == fast and bool((st[:, :, 9] > 0).any()) == fast
+    assert torch.equal(a_lab, b_lab)
+    assert torch.equal(a_sl.sel_counts, b_sl.sel_counts)
+    for s in range(S):
+        for c in range(2):
+            k = int(a_sl.sel_counts[s, c])
+            assert torch.equal(torch.sort(a_sl.sel[s, c, :k])[0], torch.sort(b_sl.sel[s, c, :k])[0]), (s, c)
+    ops.set_sampler_mode('numpy')
