@@ -399,16 +399,37 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
 #pragma unroll
   for (int r = 0; r < kTkPerThread; ++r)
     specm |= (((negm >> r) & 1u) && (key[r] >> (32 - kSpecBits)) == (1u << kSpecBits) - 1u) ? 1u << r : 0u;
-  const int4 c4 = block_sum4(make_int4(cp, cn, __popc(specm & negm), 0), sm.fb.wave_tot);
-  cp = c4.x;
-  cn = c4.y;
+  // one block scan gives the class counts and this thread's record slots: (positives | window
+  // negatives << 16) and negatives per thread, packed (per workgroup each < 65536)
+  int qp, qn, spec_n;
+  {
+    const int pa = cp | (__popc(specm & negm) << 16);
+    int ia = pa, ib = cn;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+      if (lane_id() >= o) ia += xa, ib += xb;
+    }
+    const int w = t / kWave;
+    if (lane_id() == kWave - 1) sm.part[w] = ia, sm.part[kTkThreads / kWave + w] = ib;
+    __syncthreads();
+    int ea = 0, ta = 0, tb = 0;
+#pragma unroll
+    for (int i = 0; i < kTkThreads / kWave; ++i) {
+      const int va = sm.part[i];
+      ea += i < w ? va : 0;
+      ta += va;
+      tb += sm.part[kTkThreads / kWave + i];
+    }
+    ea += ia - pa;
+    qp = ea & 0xffff, qn = ea >> 16;
+    cp = ta & 0xffff, spec_n = ta >> 16, cn = tb;
+  }
   {
     // this chunk's window records, in thread order (rows past kSpecCap are not written: such a
     // chunk sends the call to the histogram phases)
-    const int4 o = block_offsets4(__popc(posm), __popc(specm & negm), 0, 0, make_int4(0, 0, 0, 0), sm.part);
     uint64_t* rp = f.spec + ((int64_t)(2 * s) * f.nchunk + x) * kSpecCap;
     uint64_t* rn = rp + (int64_t)f.nchunk * kSpecCap;
-    int qp = o.x, qn = o.y;
 #pragma unroll
     for (int r = 0; r < kTkPerThread; ++r) {
       if (!((specm >> r) & 1u)) continue;
@@ -422,7 +443,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
         ++qn;
       }
     }
-    if (t == 0) xwg_store(reinterpret_cast<uint32_t*>(f.part_spec) + (int64_t)s * f.nchunk + x, (uint32_t)c4.z);
+    if (t == 0) xwg_store(reinterpret_cast<uint32_t*>(f.part_spec) + (int64_t)s * f.nchunk + x, (uint32_t)spec_n);
   }
   // this chunk's histograms and counts, write-through (one store per bin: no atomics on
   // the 256 hot bins of an image, which every chunk's uniform keys fill)
@@ -488,29 +509,32 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
         const int v = 2 * s + c, kv = c ? kn : kp, nc = c ? nspec : npos;
         if (f.sel_cnt && t == 0) f.sel_cnt[v] = kv > 0 ? kv : 0;
         if (nc == 0) continue;
-        // the class's records from every chunk row into LDS (row offsets: an exclusive scan of the
-        // row counts, then a binary search per record)
+        // the class's records from every chunk row into LDS at the row's offset (an exclusive scan
+        // of the row counts): wave w copies rows w, w + 4, ..., 64 records of 16 rows in flight
+        stamp(4);
         const int4 o = block_offsets4(c ? snv : cpv, 0, 0, 0, make_int4(0, 0, 0, 0), sm.part);
-        if (t < G) hc[t] = (uint32_t)o.x;
+        if (t < G) hc[t] = (uint32_t)o.x, hc[kSampBins + t] = (uint32_t)(c ? snv : cpv);
         __syncthreads();
         const uint64_t* rows = f.spec + (int64_t)v * f.nchunk * kSpecCap;
-        uint64_t rec[kTkPerThread];
+        const int w = t / kWave, ln = lane_id();
+        constexpr int kRowsPerWave = 16;
+        uint64_t rec[kRowsPerWave];
 #pragma unroll
-        for (int r = 0; r < kTkPerThread; ++r) {
-          const int q = r * kTkThreads + t;
-          int lo_j = 0, hi_j = G - 1;
-          while (lo_j < hi_j) {
-            const int mid = (lo_j + hi_j + 1) >> 1;
-            if ((int)hc[mid] <= q) lo_j = mid; else hi_j = mid - 1;
-          }
-          rec[r] = q < nc ? xwg_load(rows + (int64_t)lo_j * kSpecCap + (q - (int)hc[lo_j])) : 0ull;
+        for (int u = 0; u < kRowsPerWave; ++u) {
+          const int j = w + u * (kTkThreads / kWave);
+          rec[u] = j < G && ln < (int)hc[kSampBins + j] ? xwg_load(rows + (int64_t)j * kSpecCap + ln) : 0ull;
         }
 #pragma unroll
-        for (int r = 0; r < kTkPerThread; ++r) {
-          const int q = r * kTkThreads + t;
-          if (q < nc) sm.cand[q] = rec[r];
+        for (int u = 0; u < kRowsPerWave; ++u) {
+          const int j = w + u * (kTkThreads / kWave);
+          if (j < G && ln < (int)hc[kSampBins + j]) sm.cand[hc[j] + ln] = rec[u];
         }
+        // rows beyond 64 records, rows of chunks >= 64 (rare: one at a time)
+        for (int j = w; j < G; j += kTkThreads / kWave)
+          for (int l = (j < kRowsPerWave * (kTkThreads / kWave) ? kWave : 0) + ln; l < (int)hc[kSampBins + j]; l += kWave)
+            sm.cand[hc[j] + l] = xwg_load(rows + (int64_t)j * kSpecCap + l);
         __syncthreads();
+        stamp(5);
         const bool all = kv >= nc;
         LdsCut cut{0ull, 0};
         if (kv > 0 && !all)
@@ -518,6 +542,7 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
                   : lds_topk_cut(sm.cand, nc, kv, 64, 0ull, sm);
         if (t == 0) sm.fb.cnt_gt = 0;
         __syncthreads();
+        stamp(6);
         int32_t* sl = f.sel ? f.sel + (int64_t)v * f.sel_ld : nullptr;
         for (int q = t; q < nc; q += kTkThreads) {
           const uint64_t e = sm.cand[q];

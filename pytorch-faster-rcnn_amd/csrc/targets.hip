@@ -197,11 +197,20 @@ __device__ __forceinline__ void ranked_selection(const int32_t* sel, const int32
   const int32_t x = min(max(raw, 0), (int32_t)(lim > 0 ? lim - 1 : 0));
   int rank = 0;
   const int4* s4 = reinterpret_cast<const int4*>(su);
-  for (int q = 0; q < cnt4 / 4; ++q) {
+  // (one comparison per value: <= before position j, < from it on)
+  const int jq = j >> 2, jr = j & 3;
+  for (int q = 0; q < jq; ++q) {
     const int4 v = s4[q];
-    const int e = 4 * q;
+    rank += (v.x <= raw) + (v.y <= raw) + (v.z <= raw) + (v.w <= raw);
+  }
+  {
+    const int4 v = s4[jq];
+    rank += (jr > 0 ? v.x <= raw : v.x < raw) + (jr > 1 ? v.y <= raw : v.y < raw) + (jr > 2 ? v.z <= raw : v.z < raw) +
+            (v.w < raw);
+  }
+  for (int q = jq + 1; q < cnt4 / 4; ++q) {
+    const int4 v = s4[q];
     rank += (v.x < raw) + (v.y < raw) + (v.z < raw) + (v.w < raw);
-    rank += (v.x == raw && e < j) + (v.y == raw && e + 1 < j) + (v.z == raw && e + 2 < j) + (v.w == raw && e + 3 < j);
   }
   item(s, (int64_t)x, off + rank);
 }
