@@ -512,8 +512,21 @@ static __global__ void __launch_bounds__(kTkThreads) sampler_fused_kernel(const 
         // the class's records from every chunk row into LDS at the row's offset (an exclusive scan
         // of the row counts): wave w copies rows w, w + 4, ..., 64 records of 16 rows in flight
         stamp(4);
-        const int4 o = block_offsets4(c ? snv : cpv, 0, 0, 0, make_int4(0, 0, 0, 0), sm.part);
-        if (t < G) hc[t] = (uint32_t)o.x, hc[kSampBins + t] = (uint32_t)(c ? snv : cpv);
+        const int rc = c ? snv : cpv;
+        if (G <= kWave) {  // every row count is in wave 0: its own scan, one barrier
+          if (t < kWave) {
+            int inc = rc;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+              const int y = __shfl_up(inc, o, kWave);
+              if (lane_id() >= o) inc += y;
+            }
+            if (t < G) hc[t] = (uint32_t)(inc - rc), hc[kSampBins + t] = (uint32_t)rc;
+          }
+        } else {
+          const int4 o = block_offsets4(rc, 0, 0, 0, make_int4(0, 0, 0, 0), sm.part);
+          if (t < G) hc[t] = (uint32_t)o.x, hc[kSampBins + t] = (uint32_t)rc;
+        }
         __syncthreads();
         const uint64_t* rows = f.spec + (int64_t)v * f.nchunk * kSpecCap;
         const int w = t / kWave, ln = lane_id();
