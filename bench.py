@@ -638,6 +638,11 @@ def main():
                     help='replay backbone + neck + RPN head convs as one captured hipGraph (frcnn_amd.graphs) '
                          'after the warmup.  auto = on for fwd with a two-stage detector, off for train')
     args = ap.parse_args()
+    if args.mode == 'train' and 'MIOPEN_USER_DB_PATH' not in os.environ:
+        # MIOpen's per-user database as a fresh box has it: after a forward-mode bench in the same
+        # account, the train step's timed steps ran MIOpen's naive convolutions
+        import tempfile
+        os.environ['MIOPEN_USER_DB_PATH'] = tempfile.mkdtemp(prefix='frcnn_miopen_train_')
 
     if 'WORLD_SIZE' in os.environ:  # torchrun (or launch_ranks) started this rank
         if args.gpus is not None and args.gpus != int(os.environ['WORLD_SIZE']):
