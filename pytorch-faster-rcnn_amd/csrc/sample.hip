@@ -331,13 +331,13 @@ struct SampFused {
 };
 
 // Window records (round 6): every positive and every negative whose key has its top kSpecBits
-// bits set (1/64 of the uniform keys) is written, per chunk, as (key << 32 | ~box) to the
+// bits set (1/128 of the uniform keys) is written, per chunk, as (key << 32 | ~box) to the
 // chunk's own record row.  After the first barrier, when the window holds the whole selection
 // -- at least kn negatives in it (or all of them), every positive listed, no chunk row and no
 // class above the LDS capacity -- the k largest records of each class are exactly the
 // selection, and two workgroups finish the call from the records alone (fast path); otherwise
 // every workgroup goes on with the histogram phases 2-4.
-constexpr int kSpecBits = 6;
+constexpr int kSpecBits = 7;
 constexpr int kSpecCap = 256;  // records per chunk row and class
 
 __device__ __forceinline__ uint32_t samp_key(uint64_t seed, int v, int i, bool cand) {
